@@ -1,0 +1,228 @@
+/*
+ * doko_amd.h — C-ABI of the MI355X determinized-MCTS rollout engine.
+ *
+ * This is the drop-in boundary for the hot path of
+ * theodm/master_doko_reinforcement_learning.  Every entry
+ * point names the Rust interface it replaces.  Plain pointers and sizes only;
+ * no torch / HIP types in the signatures.  All compute runs on the GPU: the
+ * library has no CPU fallback and returns DK_E_NO_DEVICE when no gfx950
+ * device is usable.
+ *
+ * Two flavours of every batched call:
+ *   dk_xxx(...)        host pointers; the call copies in/out and synchronises.
+ *   dk_xxx_async(...)  device pointers + an opaque stream handle (hipStream_t,
+ *                      NULL = the context's stream); nothing is synchronised.
+ *
+ * Reference interfaces (file:line under /root/reference):
+ *   McEnvState trait ......... rs-doko-mcts/src/env/env_state.rs:7-28
+ *   McFullDokoEnvState ....... rs-doko-mcts/src/env/envs/env_state_full_doko.rs:22-220
+ *   McDokoEnvState ........... rs-doko-mcts/src/env/envs/env_state_doko.rs:15-170
+ *   TicTacToe McEnvState ..... rs-doko-mcts/src/example/tic_tac_toe_impl.rs:17-63
+ *   CachedMCTS ............... rs-doko-mcts/src/mcts/mcts.rs:252-321
+ *   EvFullDokoMCTSPolicy ..... rs-doko-evaluator/src/full_doko/policy/mcts_policy.rs:136-169
+ *   SamplingFn / CAPSampling . rs-doko-py-bridge/src/compare_impi/compare_impi.rs:49-82
+ *   PolicyFusionFn ........... rs-doko-py-bridge/src/compare_impi/policy_fusion.rs:9-123
+ *   DefaultImpiPolicy ........ rs-doko-py-bridge/src/compare_impi/compare_impi.rs:212-371
+ *   FdoState::new_game ....... rs-full-doko/src/state/state.rs:165-176
+ *   DoState::new_game ........ rs-doko/src/state/state.rs:159-168
+ */
+#ifndef DOKO_AMD_H
+#define DOKO_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DK_ABI_VERSION 1
+#define DK_STATE_BYTES 128
+#define DK_NUM_ACTIONS 39 /* FdoAction::COUNT (rs-full-doko/src/action/action.rs:9-54) */
+#define DK_NONE 0xFF
+
+/* ---- games ---------------------------------------------------------------- */
+enum dk_game {
+    DK_GAME_FULL_DOKO = 0, /* rs-full-doko: 39 actions, solos, announcements, DKV scoring */
+    DK_GAME_DOKO = 1,      /* rs-doko: 26 actions (bits 0-25 == FdoAction bits 0-25)      */
+    DK_GAME_TTT = 2        /* tic-tac-toe of rs-doko-mcts/src/example: actions 0-8         */
+};
+
+/* ---- status codes (the Rust path panics instead) -------------------------- */
+enum dk_status {
+    DK_OK = 0,
+    DK_E_INVALID = -1,   /* bad argument / unknown game / sizes                        */
+    DK_E_CAPACITY = -2,  /* node pool or batch larger than the context was created for */
+    DK_E_STATE = -3,     /* illegal action for a state, or a malformed state           */
+    DK_E_NO_DEVICE = -4, /* no usable gfx950 device / HIP error                        */
+    DK_E_LAUNCH = -5     /* kernel launch or execution failure                         */
+};
+
+/* ---- packed states (128 bytes; byte 127 is the game tag) ------------------
+ * Hands use the reference bit layout (rs-full-doko/src/hand/hand.rs:17-20):
+ * bit k (0..23) = first copy of card kind k, bit k+24 = second copy; card kind
+ * order = FdoCard (♦9 ♦10 ♦J ♦Q ♦K ♦A ♥… ♣… ♠…).  Players 0..3 = BOTTOM LEFT TOP RIGHT.
+ */
+typedef struct dk_fdo_state {
+    uint64_t hands[4];       /*   0: FdoState.hands                                         */
+    uint8_t cards[48];       /*  32: card kind played at card index i (DK_NONE = not yet)   */
+    uint8_t eyes[4];         /*  80: player_eyes (<= 240)                                   */
+    uint8_t ntricks[4];      /*  84: player_num_tricks                                      */
+    uint32_t trick_winners;  /*  88: 2 bits per completed trick (trick t at bits 2t..2t+1)   */
+    uint8_t res[4];          /*  92: played reservations in round order (FdoReservation)    */
+    uint8_t res_start;       /*  96: reservation round starting player                      */
+    uint8_t res_len;         /*  97                                                          */
+    uint8_t card_index;      /*  98                                                          */
+    uint8_t phase;           /*  99: 0 Reservation 1 Announcement 2 PlayCard 3 Finished     */
+    uint8_t current_player;  /* 100: DK_NONE when finished                                  */
+    uint8_t game_type;       /* 101: FdoGameType or DK_NONE                                 */
+    uint8_t rr_kind;         /* 102: reservation result: DK_NONE, 0 none, 1 solo, 2 wedding */
+    uint8_t rr_player;       /* 103                                                          */
+    uint8_t rr_reservation;  /* 104: FdoReservation of the winning solo                     */
+    uint8_t team_kind;       /* 105: 0 InReservations 1 WeddingUnsolved 2 WeddingSolved 3 NoWedding */
+    uint8_t wedding_player;  /* 106                                                          */
+    uint8_t solved_trick;    /* 107: WeddingSolved.solved_trick_index                       */
+    uint8_t re_players;      /* 108: bit mask                                               */
+    uint8_t re_lowest;       /* 109: FdoAnnouncement bit (1,2,4,8,16,32) or 0 = None        */
+    uint8_t contra_lowest;   /* 110                                                          */
+    uint8_t ann_turns;       /* 111: number_of_turns_without_announcement                   */
+    uint8_t ann_start;       /* 112: starting player of the announcement round             */
+    uint8_t ann_allowed;     /* 113: current_player_allowed_announcements (FdoAnnouncementSet) */
+    uint8_t ann_count;       /* 114: announcement occurrences recorded (<= 12)             */
+    uint8_t ann_players;     /* 115: mask of players that made an announcement             */
+    uint8_t n_tricks;        /* 116: tricks started (FdoState.tricks.len())                 */
+    uint8_t reserved[10];    /* 117                                                          */
+    uint8_t game;            /* 127: DK_GAME_FULL_DOKO                                      */
+} dk_fdo_state;
+
+typedef struct dk_do_state {
+    uint64_t hands[4];       /*   0: DoState.hands (rs-doko/src/hand/hand.rs:13)            */
+    uint8_t cards[48];       /*  32                                                          */
+    uint8_t eyes[4];         /*  80                                                          */
+    uint8_t ntricks[4];      /*  84                                                          */
+    uint32_t trick_winners;  /*  88                                                          */
+    uint8_t res[4];          /*  92: DoReservation (0 Wedding, 1 Healthy), DK_NONE empty    */
+    uint8_t res_start;       /*  96                                                          */
+    uint8_t res_len;         /*  97                                                          */
+    uint8_t card_index;      /*  98                                                          */
+    uint8_t phase;           /*  99: 0 Reservation 1 PlayCard 2 Finished (DoPhase)          */
+    uint8_t current_player;  /* 100                                                          */
+    uint8_t rr_kind;         /* 101: DK_NONE, 0 NoReservation, 2 Wedding                    */
+    uint8_t rr_player;       /* 102                                                          */
+    uint8_t team_kind;       /* 103                                                          */
+    uint8_t wedding_player;  /* 104                                                          */
+    uint8_t solved_trick;    /* 105                                                          */
+    uint8_t re_players;      /* 106                                                          */
+    uint8_t trick_index;     /* 107: current_trick_index                                    */
+    uint8_t reserved[19];    /* 108                                                          */
+    uint8_t game;            /* 127: DK_GAME_DOKO                                           */
+} dk_do_state;
+
+typedef struct dk_ttt_state {
+    uint8_t board[9];        /* 0 empty, 1 X, 2 O                                            */
+    uint8_t finish;          /* 0 NotFinished 1 Xwon 2 Owon 3 Draw                          */
+    uint8_t last_action;     /* DK_NONE or cell                                              */
+    uint8_t reserved[116];
+    uint8_t game;            /* 127: DK_GAME_TTT                                             */
+} dk_ttt_state;
+
+typedef union dk_state {
+    uint8_t raw[DK_STATE_BYTES];
+    dk_fdo_state fdo;
+    dk_do_state dk;
+    dk_ttt_state ttt;
+} dk_state;
+
+/* ---- context ---------------------------------------------------------------- */
+typedef struct dk_config {
+    int32_t device;          /* HIP device ordinal                                          */
+    uint32_t max_roots;      /* largest batch of roots one search call may carry            */
+    uint32_t max_iterations; /* largest `iterations` one search call may use                */
+    uint32_t slot_capacity;  /* child slots per root (0 = derive the proven bound)          */
+} dk_config;
+
+typedef struct dk_ctx dk_ctx;
+
+dk_ctx* dk_create(const dk_config* cfg);
+void dk_destroy(dk_ctx* ctx);
+int dk_last_error(const dk_ctx* ctx);
+const char* dk_status_string(int status);
+int dk_abi_version(void);
+
+/* ---- game construction ------------------------------------------------------
+ * FdoState::new_game(SmallRng::seed_from_u64(seed[i])) / DoState::new_game(...)
+ * rs-full-doko/src/state/state.rs:165-176, rs-doko/src/state/state.rs:159-168.
+ */
+int dk_new_game_batch(dk_ctx* ctx, int game, const uint64_t* seeds, uint32_t n, dk_state* out);
+int dk_new_game_batch_async(dk_ctx* ctx, int game, const uint64_t* d_seeds, uint32_t n, dk_state* d_out, void* stream);
+
+/* ---- McEnvState (rs-doko-mcts/src/env/env_state.rs:7-28), batched ----------
+ * allowed_actions(first_expansion) -> FdoAllowedActions bits (u64 per state)
+ * by_action(action)                -> state stepped in place (one-hot action bit)
+ * rewards_or_none()                -> has_rewards[i] and rewards[4*i..]
+ * random_rollout(rng)              -> rewards[4*i..] ; rng[4*i..] = Xoshiro256++ state, advanced
+ */
+int dk_env_allowed_batch(dk_ctx* ctx, const dk_state* states, uint32_t n, int first_expansion, uint64_t* masks);
+int dk_env_step_batch(dk_ctx* ctx, dk_state* states, const uint64_t* action_bits, uint32_t n);
+int dk_env_rewards_batch(dk_ctx* ctx, const dk_state* states, uint32_t n, int32_t* has_rewards, double* rewards);
+int dk_env_rollout_batch(dk_ctx* ctx, const dk_state* states, uint64_t* rng_states, uint32_t n, double* rewards);
+int dk_env_rollout_batch_async(dk_ctx* ctx, const dk_state* d_states, uint64_t* d_rng_states, uint32_t n,
+                               double* d_rewards, void* stream);
+/* random_action_for_current_player_no_announcement applied k[i] times
+ * (rs-full-doko/src/state/state.rs:401-431; rs-doko uses random_action_for_current_player). */
+int dk_env_random_plies_batch(dk_ctx* ctx, dk_state* states, uint64_t* rng_states, const uint32_t* plies, uint32_t n);
+
+/* ---- CachedMCTS::monte_carlo_tree_search (rs-doko-mcts/src/mcts/mcts.rs:284-315)
+ * One independent UCT search per root (the reference's sequential per-root
+ * semantics; parallel only across roots).  rng seed: SmallRng::seed_from_u64(seeds[i]).
+ * visits/values: [n][39] by action index (mcts_policy.rs:95-104, values as f64
+ * win_score/visits); best[i] = max_by_key(visits) over root children in
+ * expansion order (last maximum wins), DK_NONE when the root has no children.
+ * `c` is the UCT exploration constant as f64 (the evaluator passes (double)(float)c).
+ */
+int dk_search_batch(dk_ctx* ctx, const dk_state* roots, const uint64_t* seeds, uint32_t n, uint32_t iterations,
+                    double c, uint32_t* visits, double* values, uint8_t* best);
+int dk_search_batch_async(dk_ctx* ctx, const dk_state* d_roots, const uint64_t* d_seeds, uint32_t n,
+                          uint32_t iterations, double c, uint32_t* d_visits, double* d_values, uint8_t* d_best,
+                          void* stream);
+
+/* ---- CAPSampling::sample -> card_matching_full ------------------------------
+ * (compare_impi.rs:64-81 -> rs-full-doko/src/matching/card_matching.rs:469-497)
+ * out[i*samples + s] = card_matching_full(infostates[i], SmallRng::seed_from_u64(seeds[i*samples+s]))
+ */
+int dk_determinize_batch(dk_ctx* ctx, const dk_state* infostates, uint32_t n_info, uint32_t samples,
+                         const uint64_t* seeds, dk_state* out);
+int dk_determinize_batch_async(dk_ctx* ctx, const dk_state* d_infostates, uint32_t n_info, uint32_t samples,
+                               const uint64_t* d_seeds, dk_state* d_out, void* stream);
+
+/* ---- PolicyFusionFn::fuse (policy_fusion.rs:23-123) --------------------------
+ * mode DK_FUSE_MAXN: per infostate sum of per-sample visit ranks (u32, disallowed
+ *   = UINT32_MAX) -> first minimum.   acc_u32 = [n_info][39] rank sums.
+ * mode DK_FUSE_AVG: per infostate sum over samples of visits/total (f32) -> last
+ *   maximum.                           acc_f32 = [n_info][39] probability sums.
+ * The _accumulate/_select split lets a multi-GPU caller all-reduce(sum) the
+ * accumulators between the two steps (RCCL over xGMI).
+ */
+enum dk_fuse_mode { DK_FUSE_MAXN = 0, DK_FUSE_AVG = 1 };
+int dk_fuse(dk_ctx* ctx, const uint32_t* visits, uint32_t n_info, uint32_t samples, const uint64_t* allowed,
+            int mode, uint8_t* action);
+int dk_fuse_accumulate_async(dk_ctx* ctx, const uint32_t* d_visits, uint32_t n_info, uint32_t samples,
+                             const uint64_t* d_allowed, int mode, uint32_t* d_acc_u32, float* d_acc_f32, void* stream);
+int dk_fuse_select_async(dk_ctx* ctx, uint32_t n_info, int mode, const uint32_t* d_acc_u32, const float* d_acc_f32,
+                         uint8_t* d_action, void* stream);
+
+/* ---- DefaultImpiPolicy::execute (compare_impi.rs:212-371), batched ----------
+ * For each infostate: `samples` CAP determinizations -> one UCT search each ->
+ * fusion. actions[i] = fused action; visits [n_info*samples][39] optional (NULL).
+ */
+int dk_decide_batch(dk_ctx* ctx, const dk_state* infostates, uint32_t n_info, uint32_t samples,
+                    const uint64_t* seeds, uint32_t iterations, double c, int fuse_mode, uint8_t* actions,
+                    uint32_t* visits);
+
+/* ---- timing of the last *_async search launch (HIP events on its stream) ---- */
+int dk_last_search_ms(dk_ctx* ctx, float* ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DOKO_AMD_H */

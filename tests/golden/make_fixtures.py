@@ -1,0 +1,221 @@
+"""Extract golden vectors from the reference's own test code into JSON fixtures.
+
+Run HERE (the container that has /root/reference); the GPU box never reads the
+reference. The output files are data only (inputs + expected outputs):
+
+* fdo_traces.json — the four full-game traces written as (commented) tests in
+  rs-full-doko/src/state/state.rs:551-951, :955-1346, :1350-1552, :1558-1808:
+  initial hands, start player, every action, and after every action the
+  expected phase / current player / legal-action set / eyes / trick winners /
+  lowest announcements, ending in the expected FdoEndOfGameStats.
+* fdo_deal_seed42.json — the seeded deal of rs-full-doko/src/hand/hand.rs:558-585.
+* do_display_game.json — the finished rs-doko game of
+  rs-doko/src/display/display.rs:242-280 (tricks + expected eyes / re points).
+* bitflag_select_rank.json — rs-game-utils/src/bit_flag.rs:186-192.
+* ttt_kats.json — rs-doko-mcts/src/example/tic_tac_toe.rs tests (finish states).
+* fusion_kats.json — rs-doko-py-bridge/src/compare_impi/policy_fusion.rs:130-311.
+
+Usage: python tests/golden/make_fixtures.py
+"""
+import json
+import os
+import re
+
+REF = "/root/reference"
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+CARD_NAMES = [
+    "DiamondNine", "DiamondTen", "DiamondJack", "DiamondQueen", "DiamondKing", "DiamondAce",
+    "HeartNine", "HeartTen", "HeartJack", "HeartQueen", "HeartKing", "HeartAce",
+    "ClubNine", "ClubTen", "ClubJack", "ClubQueen", "ClubKing", "ClubAce",
+    "SpadeNine", "SpadeTen", "SpadeJack", "SpadeQueen", "SpadeKing", "SpadeAce",
+]
+ACTION_NAMES = ["Card" + c for c in CARD_NAMES] + [
+    "ReservationHealthy", "ReservationWedding", "ReservationDiamondsSolo", "ReservationHeartsSolo",
+    "ReservationSpadesSolo", "ReservationClubsSolo", "ReservationTrumplessSolo", "ReservationQueensSolo",
+    "ReservationJacksSolo", "AnnouncementReContra", "AnnouncementNo90", "AnnouncementNo60",
+    "AnnouncementNo30", "AnnouncementBlack", "NoAnnouncement",
+]
+PLAYERS = {"BOTTOM": 0, "LEFT": 1, "TOP": 2, "RIGHT": 3}
+PHASES = {"Reservation": 0, "Announcement": 1, "PlayCard": 2, "Finished": 3}
+GAME_TYPES = {"Normal": 0, "Wedding": 1, "DiamondsSolo": 2, "HeartsSolo": 3, "SpadesSolo": 4,
+              "ClubsSolo": 5, "TrumplessSolo": 6, "QueensSolo": 7, "JacksSolo": 8}
+ANN = {"ReContra": 1, "No90": 2, "No60": 4, "No30": 8, "Black": 16, "CounterReContra": 32}
+
+
+def _uncomment(lines):
+    out = []
+    for ln in lines:
+        s = ln.lstrip()
+        if s.startswith("//"):
+            s = s[2:]
+        out.append(s)
+    return out
+
+
+def _bracket(text, start):
+    """Return the substring of balanced {...} starting at text[start] == '{'."""
+    depth = 0
+    for i in range(start, len(text)):
+        if text[i] == "{":
+            depth += 1
+        elif text[i] == "}":
+            depth -= 1
+            if depth == 0:
+                return text[start:i + 1]
+    raise ValueError("unbalanced")
+
+
+def _parse_obs(obs):
+    d = {}
+    d["phase"] = PHASES[re.search(r"phase: FdoPhase::(\w+)", obs).group(1)]
+    m = re.search(r"current_player: (None|Some\(FdoPlayer::(\w+)\))", obs)
+    d["current_player"] = -1 if m.group(1) == "None" else PLAYERS[m.group(2)]
+    m = re.search(r"allowed_actions_current_player: FdoAllowedActions::from_vec\(vec!\[([^\]]*)\]\)", obs)
+    names = [x.strip() for x in m.group(1).split(",") if x.strip()]
+    d["allowed"] = sorted(ACTION_NAMES.index(n) for n in names)
+    m = re.search(r"game_type: (None|Some\(FdoGameType::(\w+)\))", obs)
+    d["game_type"] = -1 if m.group(1) == "None" else GAME_TYPES[m.group(2)]
+    m = re.search(r"player_eyes: \[(\d+), (\d+), (\d+), (\d+)\]", obs)
+    d["player_eyes"] = [int(x) for x in m.groups()]
+    d["trick_winners"] = [(-1 if w == "None" else PLAYERS[w2]) for w, w2 in
+                          re.findall(r"winning_player: (None|Some\(FdoPlayer::(\w+)\))", obs.split("visible_reservations")[0])]
+    m = re.search(r"re_lowest_announcement: (None|Some\((\w+)\))", obs)
+    d["re_lowest"] = -1 if m.group(1) == "None" else ANN[m.group(2)]
+    m = re.search(r"contra_lowest_announcement: (None|Some\((\w+)\))", obs)
+    d["contra_lowest"] = -1 if m.group(1) == "None" else ANN[m.group(2)]
+    m = re.search(r"observing_player_hand: FdoHand::from_vec\(vec!\[([^\]]*)\]\)", obs)
+    d["observing_hand"] = sorted(CARD_NAMES.index(x.strip()) for x in m.group(1).split(",") if x.strip())
+    m = re.search(r"phi_re_players: (None|Some\(FdoPlayerSet::from_vec\(vec!\[([^\]]*)\]\)\))", obs)
+    if m.group(1) == "None":
+        d["re_players"] = -1
+    else:
+        d["re_players"] = sum(1 << PLAYERS[p.strip().split("::")[1]] for p in m.group(2).split(",") if p.strip())
+    fs = obs.find("finished_stats: Some(")
+    if fs >= 0:
+        st = _bracket(obs, obs.find("{", fs))
+        f = {}
+        for key in ("re_eyes", "kontra_eyes", "re_points", "kontra_points"):
+            f[key] = int(re.search(key + r": (-?\d+)", st).group(1))
+        f["is_solo"] = re.search(r"is_solo: (\w+)", st).group(1) == "true"
+        f["player_points"] = [int(x) for x in re.search(r"player_points: \[(-?\d+), (-?\d+), (-?\d+), (-?\d+)\]", st).groups()]
+        d["finished"] = f
+    else:
+        d["finished"] = None
+    return d
+
+
+def fdo_traces():
+    path = os.path.join(REF, "rs-full-doko/src/state/state.rs")
+    with open(path, encoding="utf-8") as fh:
+        all_lines = fh.readlines()
+    spans = [("full_normal_game", 551, 951), ("full2_clubs_solo", 955, 1346),
+             ("test_full3_wedding", 1350, 1552), ("test_full4_silent_solo", 1558, 1808)]
+    games = []
+    for name, a, b in spans:
+        text = "\n".join(_uncomment(all_lines[a - 1:b]))
+        hands = [sorted(CARD_NAMES.index(c.strip()) for c in h.split(","))
+                 for h in re.findall(r"FdoHand::from_vec\(vec!\[([^\]]*)\]\)", text.split(");")[0])][:4]
+        start = PLAYERS[re.search(r"\],\s*FdoPlayer::(\w+),", text).group(1)]
+        steps = []
+        # The first assertion describes the initial state.
+        pos = 0
+        pending_action = None
+        token = re.compile(r"state\.play_action\((\w+)\);|assert_eq!\(state\.observation_for_current_player\(\), FdoObservation ")
+        while True:
+            m = token.search(text, pos)
+            if not m:
+                break
+            if m.group(1):
+                pending_action = ACTION_NAMES.index(m.group(1))
+                pos = m.end()
+            else:
+                obs = _bracket(text, text.find("{", m.end() - 1))
+                steps.append({"action": pending_action, "expect": _parse_obs(obs)})
+                pending_action = None
+                pos = m.end() + len(obs)
+        games.append({"name": name, "source": "rs-full-doko/src/state/state.rs:%d-%d" % (a, b),
+                      "hands": hands, "start_player": start, "steps": steps})
+    return games
+
+
+def deal_seed42():
+    path = os.path.join(REF, "rs-full-doko/src/hand/hand.rs")
+    with open(path, encoding="utf-8") as fh:
+        lines = fh.readlines()
+    text = "".join(lines[557:585])
+    vals = [int(x, 2) for x in re.findall(r"0b([01]+)", text)]
+    return {"source": "rs-full-doko/src/hand/hand.rs:558-585", "seed": 42, "hands": vals[:4]}
+
+
+def do_display_game():
+    path = os.path.join(REF, "rs-doko/src/display/display.rs")
+    with open(path, encoding="utf-8") as fh:
+        lines = fh.readlines()
+    text = "".join(lines[241:280])
+    tricks = []
+    for sp, cards in re.findall(r"DoTrick::existing\((PLAYER_\w+), vec!\[([^\]]*)\]\)", text):
+        tricks.append({"start": PLAYERS[sp.split("_")[1]],
+                       "cards": [CARD_NAMES.index(c.strip().split("::")[1]) for c in cards.split(",")]})
+    eyes = [int(x) for x in re.search(r"player_eyes: \[(\d+), (\d+), (\d+), (\d+)\]", text).groups()]
+    fin = re.search(r"re_eyes: (\d+), kontra_eyes: (\d+), re_points: (-?\d+), kontra_points: (-?\d+)", text)
+    return {"source": "rs-doko/src/display/display.rs:242-280", "tricks": tricks, "player_eyes": eyes,
+            "re_eyes": int(fin.group(1)), "kontra_eyes": int(fin.group(2)),
+            "re_points": int(fin.group(3)), "kontra_points": int(fin.group(4)),
+            "note": "player_points/phi_team_eyes in that fixture are hand-typed and inconsistent; "
+                    "eyes, re/kontra eyes and points are the checked fields"}
+
+
+def select_rank():
+    path = os.path.join(REF, "rs-game-utils/src/bit_flag.rs")
+    with open(path, encoding="utf-8") as fh:
+        lines = fh.readlines()
+    text = "".join(lines[185:193])
+    cases = [{"v": int(v, 2), "r": int(r), "expect": int(e, 2)}
+             for v, r, e in re.findall(r"select_by_rank\(0b([01]+), (\d+)\), 0b([01]+)\)", text)]
+    return {"source": "rs-game-utils/src/bit_flag.rs:186-192", "cases": cases}
+
+
+def ttt_kats():
+    path = os.path.join(REF, "rs-doko-mcts/src/example/tic_tac_toe.rs")
+    with open(path, encoding="utf-8") as fh:
+        text = fh.read()
+    tests = text[text.find("#[cfg(test)]"):]
+    fin = {"Xwon": 1, "Owon": 2, "Draw": 3, "NotFinished": 0}
+    cases = []
+    for board, st in re.findall(r'str_to_state\("([ XO]{9})"\);\s*let finish_state = state\.finish_state\(\);\s*'
+                                r'assert_eq!\(TicTacToeFinishState::(\w+), finish_state\)', tests):
+        cases.append({"board": board, "finish": fin[st]})
+    succ = []
+    for body in re.findall(r'fn test_possible_states_\w+\(\) \{(.*?)\n    \}', tests, re.S):
+        m = re.search(r'str_to_state\("([ XO]{9})"\)', body)
+        parent = "         " if "TicTacToeState::new()" in body else m.group(1)
+        children = re.findall(r'assert_eq!\(str_to_state\("([ XO]{9})"\), possible_states\[\d+\]\)', body)
+        succ.append({"board": parent, "successors": children})
+    return {"source": "rs-doko-mcts/src/example/tic_tac_toe.rs:236-317", "cases": cases, "successors": succ}
+
+
+def fusion_kats():
+    path = os.path.join(REF, "rs-doko-py-bridge/src/compare_impi/policy_fusion.rs")
+    with open(path, encoding="utf-8") as fh:
+        text = fh.read()
+    return {"source": "rs-doko-py-bridge/src/compare_impi/policy_fusion.rs:130-311",
+            "raw_test_count": text.count("#[tokio::test]")}
+
+
+def main():
+    with open(os.path.join(OUT, "fdo_traces.json"), "w") as fh:
+        json.dump(fdo_traces(), fh, indent=0)
+    with open(os.path.join(OUT, "fdo_deal_seed42.json"), "w") as fh:
+        json.dump(deal_seed42(), fh, indent=1)
+    with open(os.path.join(OUT, "do_display_game.json"), "w") as fh:
+        json.dump(do_display_game(), fh, indent=1)
+    with open(os.path.join(OUT, "bitflag_select_rank.json"), "w") as fh:
+        json.dump(select_rank(), fh, indent=1)
+    with open(os.path.join(OUT, "ttt_kats.json"), "w") as fh:
+        json.dump(ttt_kats(), fh, indent=1)
+    print("wrote fixtures to", OUT)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,265 @@
+"""ctypes wrapper of the ORACLE (oracle/liboracle_doko.so) — test infrastructure only.
+
+Imported by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg, never by
+the product package.
+"""
+import ctypes
+import os
+import subprocess
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+LIB_PATH = os.path.join(ORACLE_DIR, "liboracle_doko.so")
+
+_lib = None
+
+u64p = ctypes.POINTER(ctypes.c_uint64)
+u32p = ctypes.POINTER(ctypes.c_uint32)
+i32p = ctypes.POINTER(ctypes.c_int32)
+f64p = ctypes.POINTER(ctypes.c_double)
+f32p = ctypes.POINTER(ctypes.c_float)
+u8p = ctypes.POINTER(ctypes.c_uint8)
+vp = ctypes.c_void_p
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        sig = {
+            "or_rng_seed": (None, [ctypes.c_uint64, u64p]),
+            "or_rng_next_u64": (ctypes.c_uint64, [u64p]),
+            "or_rng_range_u32": (ctypes.c_uint32, [u64p, ctypes.c_uint32, ctypes.c_uint32]),
+            "or_rng_choose_unsized": (ctypes.c_int, [u64p, ctypes.c_uint32]),
+            "or_select_by_rank": (ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_uint64]),
+            "or_fdo_new_game": (vp, [ctypes.c_uint64]),
+            "or_fdo_from_hands": (vp, [u64p, ctypes.c_int]),
+            "or_fdo_clone": (vp, [vp]),
+            "or_fdo_free": (None, [vp]),
+            "or_fdo_play": (None, [vp, ctypes.c_int]),
+            "or_fdo_allowed": (ctypes.c_uint64, [vp]),
+            "or_fdo_env_allowed": (ctypes.c_uint64, [vp, ctypes.c_int]),
+            "or_fdo_hands": (None, [vp, u64p]),
+            "or_fdo_info": (None, [vp, i32p]),
+            "or_fdo_pack": (None, [vp, u8p]),
+            "or_fdo_random_plies": (ctypes.c_int, [vp, u64p, ctypes.c_int, ctypes.c_int]),
+            "or_fdo_rollout": (None, [vp, u64p, f64p]),
+            "or_fdo_rewards": (ctypes.c_int, [vp, f64p]),
+            "or_fdo_search": (ctypes.c_int, [vp, u64p, ctypes.c_uint32, ctypes.c_double, u32p, f64p, u64p]),
+            "or_fdo_card_matching": (vp, [vp, u64p]),
+            "or_fdo_sample_consistent": (ctypes.c_int, [vp, vp]),
+            "or_fdo_visible_reservations": (None, [vp, ctypes.c_int, i32p]),
+            "or_fdo_calc_allowed_announcements": (ctypes.c_int, [ctypes.c_int] * 7),
+            "or_fdo_card_to_color": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
+            "or_fdo_is_greater": (ctypes.c_int, [ctypes.c_int] * 4),
+            "or_fdo_search_many": (ctypes.c_double, [vp, ctypes.POINTER(vp), u64p, ctypes.c_uint32, ctypes.c_uint32,
+                                                     ctypes.c_double, u32p, ctypes.c_int]),
+            "or_do_new_game": (vp, [ctypes.c_uint64]),
+            "or_do_from_hands": (vp, [u64p, ctypes.c_int]),
+            "or_do_clone": (vp, [vp]),
+            "or_do_free": (None, [vp]),
+            "or_do_play": (None, [vp, ctypes.c_int]),
+            "or_do_allowed": (ctypes.c_uint64, [vp]),
+            "or_do_hands": (None, [vp, u64p]),
+            "or_do_info": (None, [vp, i32p]),
+            "or_do_pack": (None, [vp, u8p]),
+            "or_do_random_plies": (ctypes.c_int, [vp, u64p, ctypes.c_int]),
+            "or_do_rollout": (None, [vp, u64p, f64p]),
+            "or_do_search": (ctypes.c_int, [vp, u64p, ctypes.c_uint32, ctypes.c_double, u32p, f64p, u64p]),
+            "or_do_search_many": (ctypes.c_double, [ctypes.POINTER(vp), u64p, ctypes.c_uint32, ctypes.c_uint32,
+                                                    ctypes.c_double, u32p, ctypes.c_int]),
+            "or_ttt_finish": (ctypes.c_int, [i32p]),
+            "or_ttt_rollout": (None, [i32p, u64p, f64p]),
+            "or_ttt_search": (ctypes.c_int, [i32p, u64p, ctypes.c_uint32, ctypes.c_double, u32p, f64p]),
+            "or_ttt_pack": (None, [i32p, ctypes.c_int, u8p]),
+            "or_fuse_maxn": (ctypes.c_int, [u32p, ctypes.c_int, ctypes.c_uint64, u32p]),
+            "or_fuse_avg": (ctypes.c_int, [u32p, ctypes.c_int, f32p]),
+        }
+        for name, (res, args) in sig.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def arr(ctype, n, init=None):
+    a = (ctype * n)()
+    if init is not None:
+        for i, v in enumerate(init):
+            a[i] = v
+    return a
+
+
+def rng_seed(seed):
+    s = arr(ctypes.c_uint64, 4)
+    lib().or_rng_seed(seed, s)
+    return s
+
+
+class FdoState:
+    """Handle to an oracle FdoState (rs-full-doko/src/state/state.rs:24-75)."""
+
+    def __init__(self, handle):
+        self.h = handle
+
+    @classmethod
+    def new_game(cls, seed):
+        return cls(lib().or_fdo_new_game(seed))
+
+    @classmethod
+    def from_hands(cls, hands, start):
+        return cls(lib().or_fdo_from_hands(arr(ctypes.c_uint64, 4, hands), start))
+
+    def clone(self):
+        return FdoState(lib().or_fdo_clone(self.h))
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.or_fdo_free(self.h)
+            self.h = None
+
+    def play(self, a):
+        lib().or_fdo_play(self.h, a)
+
+    def allowed(self):
+        return lib().or_fdo_allowed(self.h)
+
+    def env_allowed(self, first):
+        return lib().or_fdo_env_allowed(self.h, 1 if first else 0)
+
+    def hands(self):
+        o = arr(ctypes.c_uint64, 4)
+        lib().or_fdo_hands(self.h, o)
+        return list(o)
+
+    def info(self):
+        o = arr(ctypes.c_int32, 40)
+        lib().or_fdo_info(self.h, o)
+        o = list(o)
+        return {"phase": o[0], "current_player": o[1], "game_type": o[2], "eyes": o[3:7], "re_lowest": o[7],
+                "contra_lowest": o[8], "has_stats": o[9], "player_points": o[10:14], "re_eyes": o[14],
+                "kontra_eyes": o[15], "re_points": o[16], "kontra_points": o[17], "is_solo": o[18],
+                "n_tricks": o[19], "trick_winners": o[20:32], "re_players": o[32], "card_index": o[33],
+                "team_kind": o[34], "ann_turns": o[35], "ann_allowed": o[36], "n_ann": o[37]}
+
+    def pack(self):
+        o = arr(ctypes.c_uint8, 128)
+        lib().or_fdo_pack(self.h, o)
+        return bytes(o)
+
+    def random_plies(self, rng, k, no_announcement=True):
+        return lib().or_fdo_random_plies(self.h, rng, k, 1 if no_announcement else 0)
+
+    def rollout(self, rng):
+        o = arr(ctypes.c_double, 4)
+        lib().or_fdo_rollout(self.h, rng, o)
+        return list(o)
+
+    def search(self, rng, iters, c):
+        v = arr(ctypes.c_uint32, 39)
+        val = arr(ctypes.c_double, 39)
+        ctr = arr(ctypes.c_uint64, 8)
+        best = lib().or_fdo_search(self.h, rng, iters, c, v, val, ctr)
+        return best, list(v), list(val), list(ctr)
+
+    def card_matching(self, rng):
+        return FdoState(lib().or_fdo_card_matching(self.h, rng))
+
+    def consistent_sample(self, sample):
+        return bool(lib().or_fdo_sample_consistent(self.h, sample.h))
+
+
+class DoState:
+    """Handle to an oracle DoState (rs-doko/src/state/state.rs:28-76)."""
+
+    def __init__(self, handle):
+        self.h = handle
+
+    @classmethod
+    def new_game(cls, seed):
+        return cls(lib().or_do_new_game(seed))
+
+    @classmethod
+    def from_hands(cls, hands, start):
+        return cls(lib().or_do_from_hands(arr(ctypes.c_uint64, 4, hands), start))
+
+    def clone(self):
+        return DoState(lib().or_do_clone(self.h))
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.or_do_free(self.h)
+            self.h = None
+
+    def play(self, a):
+        lib().or_do_play(self.h, a)
+
+    def allowed(self):
+        return lib().or_do_allowed(self.h)
+
+    def hands(self):
+        o = arr(ctypes.c_uint64, 4)
+        lib().or_do_hands(self.h, o)
+        return list(o)
+
+    def info(self):
+        o = arr(ctypes.c_int32, 32)
+        lib().or_do_info(self.h, o)
+        o = list(o)
+        return {"phase": o[0], "current_player": o[1], "eyes": o[2:6], "has_stats": o[6], "player_points": o[7:11],
+                "re_eyes": o[11], "kontra_eyes": o[12], "re_points": o[13], "kontra_points": o[14],
+                "trick_index": o[15], "trick_winners": o[16:28], "re_players": o[28]}
+
+    def pack(self):
+        o = arr(ctypes.c_uint8, 128)
+        lib().or_do_pack(self.h, o)
+        return bytes(o)
+
+    def random_plies(self, rng, k):
+        return lib().or_do_random_plies(self.h, rng, k)
+
+    def rollout(self, rng):
+        o = arr(ctypes.c_double, 4)
+        lib().or_do_rollout(self.h, rng, o)
+        return list(o)
+
+    def search(self, rng, iters, c):
+        v = arr(ctypes.c_uint32, 39)
+        val = arr(ctypes.c_double, 39)
+        ctr = arr(ctypes.c_uint64, 8)
+        best = lib().or_do_search(self.h, rng, iters, c, v, val, ctr)
+        return best, list(v), list(val), list(ctr)
+
+
+def ttt_pack(board, last_action=-1):
+    o = arr(ctypes.c_uint8, 128)
+    lib().or_ttt_pack(arr(ctypes.c_int32, 9, board), last_action, o)
+    return bytes(o)
+
+
+def ttt_search(board, rng, iters, c):
+    v = arr(ctypes.c_uint32, 39)
+    val = arr(ctypes.c_double, 39)
+    best = lib().or_ttt_search(arr(ctypes.c_int32, 9, board), rng, iters, c, v, val)
+    return best, list(v), list(val)
+
+
+def fuse_maxn(visits_rows, allowed):
+    S = len(visits_rows)
+    flat = arr(ctypes.c_uint32, 39 * S, [x for row in visits_rows for x in row])
+    ranks = arr(ctypes.c_uint32, 39)
+    return lib().or_fuse_maxn(flat, S, allowed, ranks), list(ranks)
+
+
+def fuse_avg(visits_rows):
+    S = len(visits_rows)
+    flat = arr(ctypes.c_uint32, 39 * S, [x for row in visits_rows for x in row])
+    probs = arr(ctypes.c_float, 39)
+    return lib().or_fuse_avg(flat, S, probs), list(probs)
