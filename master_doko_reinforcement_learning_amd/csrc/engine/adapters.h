@@ -1,0 +1,51 @@
+// Engine adapters: the McEnvState surface (rs-doko-mcts/src/env/env_state.rs:7-28)
+// of each game as static functions for search_core.h and the env kernels.
+#pragma once
+#include "do_engine.h"
+#include "fdo_engine.h"
+
+namespace dk {
+
+struct FdoE {
+    using Work = fdo::Work;
+    using Packed = dk_fdo_state;
+    static constexpr int GAME = DK_GAME_FULL_DOKO;
+    DK_HD static void load(const dk_state& s, Work& w) { fdo::unpack(s.fdo, w); }
+    DK_HD static uint64_t allowed(const Work& w, bool first) { return fdo::env_allowed(w, first); }
+    DK_HD static int current_player(const Work& w) { return fdo::env_current_player(w); }
+    DK_HD static bool terminal(const Work& w) { return fdo::is_terminal(w); }
+    DK_HD static void step(Work& w, int a) { fdo::play_action(w, a); }
+    DK_HD static int rollout(const Work& w, Rng& rng, int r[4]) { return fdo::rollout(w, rng, r); }
+    DK_HD static void rewards(const Work& w, int r[4]) { fdo::score(w, r); }
+    DK_HD static void step_packed(dk_state& s, int a) { fdo::step_packed(s.fdo, a); }
+};
+
+struct DoE {
+    using Work = dko::Work;
+    using Packed = dk_do_state;
+    static constexpr int GAME = DK_GAME_DOKO;
+    DK_HD static void load(const dk_state& s, Work& w) { dko::unpack(s.dk, w); }
+    DK_HD static uint64_t allowed(const Work& w, bool first) { return dko::env_allowed(w, first); }
+    DK_HD static int current_player(const Work& w) { return dko::env_current_player(w); }
+    DK_HD static bool terminal(const Work& w) { return dko::is_terminal(w); }
+    DK_HD static void step(Work& w, int a) { dko::play_action(w, a); }
+    DK_HD static int rollout(const Work& w, Rng& rng, int r[4]) { return dko::rollout(w, rng, r); }
+    DK_HD static void rewards(const Work& w, int r[4]) { dko::score(w, r); }
+    DK_HD static void step_packed(dk_state& s, int a) { dko::step_packed(s.dk, a); }
+};
+
+struct TttE {
+    using Work = ttt::Work;
+    using Packed = dk_ttt_state;
+    static constexpr int GAME = DK_GAME_TTT;
+    DK_HD static void load(const dk_state& s, Work& w) { ttt::unpack(s.ttt, w); }
+    DK_HD static uint64_t allowed(const Work& w, bool first) { return ttt::env_allowed(w, first); }
+    DK_HD static int current_player(const Work& w) { return ttt::env_current_player(w); }
+    DK_HD static bool terminal(const Work& w) { return ttt::is_terminal(w); }
+    DK_HD static void step(Work& w, int a) { ttt::play_action(w, a); }
+    DK_HD static int rollout(const Work& w, Rng& rng, int r[4]) { return ttt::rollout(w, rng, r); }
+    DK_HD static void rewards(const Work& w, int r[4]) { ttt::score(w, r); }
+    DK_HD static void step_packed(dk_state& s, int a) { ttt::step_packed(s.ttt, a); }
+};
+
+}  // namespace dk

@@ -1,0 +1,247 @@
+// rs-doko (simplified Doppelkopf: normal game, wedding, silent solo; no
+// announcements) as a register-resident state machine.
+// Reference: rs-doko/src/state/state.rs:159-334, action/allowed_actions.rs:131-198,
+// trick/trick_winning_player_logic.rs:11-34, teams/team_logic.rs:69-143,
+// stats/stats.rs:25-135, hand/hand.rs:38-46 (removes the FIRST copy),
+// env adapter rs-doko-mcts/src/env/envs/env_state_doko.rs (allowed_actions /
+// by_action are todo!() there; DoAction bits 0-25 == FdoAction bits 0-25).
+#pragma once
+#include "../../../include/doko_amd.h"
+#include "common.h"
+#include "fdo_engine.h"
+#include "rng.h"
+
+namespace dk {
+namespace dko {
+
+enum : uint32_t { PH_RESERVATION = 0, PH_PLAYCARD = 1, PH_FINISHED = 2 };
+enum : uint32_t { RES_WEDDING = 0, RES_HEALTHY = 1 };
+
+struct Work {
+    uint64_t h[4];
+    uint32_t trick_cards, trick_winners, eyes, ntricks, res;
+    uint8_t trick_len, trick_start, trick_index, card_index;
+    uint8_t phase, cur, res_len, res_start;
+    uint8_t rr_wedding, team_kind, wedding_player, solved_trick;  // rr_wedding: 0xFF = NoReservation
+    uint8_t re_players, pad0, pad1, pad2;
+};
+
+DK_HD uint64_t legal_actions(const Work& w) {
+    const uint64_t h = sel4(w.h, w.cur);
+    if (w.phase == PH_RESERVATION) {
+        uint64_t a = 1ULL << 24;
+        if ((h >> 15 & 1) && (h >> 39 & 1)) a |= 1ULL << 25;
+        return a;
+    }
+    if (w.phase != PH_PLAYCARD) return 0;
+    const uint64_t single = (h | (h >> 24)) & 0xFFFFFFULL;
+    if (w.trick_len == 0) return single;
+    const uint32_t tc = fdo::card_color((int)(w.trick_cards & 0xFF), fdo::GT_NORMAL);
+    const uint64_t follow = single & fdo::color_mask(tc, fdo::GT_NORMAL);
+    return follow ? follow : single;
+}
+
+DK_HD void finish_reservations(Work& w) {
+    int wi = -1;
+    for (int i = 0; i < 4; ++i) if (byte_get(w.res, i) == RES_WEDDING) wi = i;
+    w.rr_wedding = wi < 0 ? 0xFF : (uint8_t)((wi + w.res_start) & 3);
+    if (wi < 0) {
+        uint8_t re = 0;
+        for (int p = 0; p < 4; ++p) { const uint64_t h = sel4(w.h, p); if ((h >> 15 & 1) || (h >> 39 & 1)) re |= (uint8_t)(1u << p); }
+        w.team_kind = fdo::TK_NOWEDDING; w.re_players = re;
+    } else {
+        w.team_kind = fdo::TK_WED_UNSOLVED; w.wedding_player = w.rr_wedding; w.re_players = 0;
+    }
+}
+
+DK_HD int complete_trick(Work& w) {
+    const uint32_t tc = fdo::card_color((int)(w.trick_cards & 0xFF), fdo::GT_NORMAL);
+    int best_key = -2, best_i = 0; uint32_t e = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int c = (int)((w.trick_cards >> (8 * i)) & 0xFF);
+        const int k = fdo::trick_key(c, tc, fdo::GT_NORMAL);
+        const bool better = k > best_key;
+        best_key = better ? k : best_key; best_i = better ? i : best_i;
+        e += fdo::card_eyes(c);
+    }
+    const int winner = (w.trick_start + best_i) & 3;
+    const int t = w.trick_index;
+    w.trick_winners |= (uint32_t)winner << (2 * t);
+    w.eyes = byte_add(w.eyes, winner, e);
+    w.ntricks = byte_add(w.ntricks, winner, 1);
+    if (w.team_kind == fdo::TK_WED_UNSOLVED && t < 3) {
+        if (winner != w.wedding_player) {
+            w.team_kind = fdo::TK_WED_SOLVED; w.solved_trick = (uint8_t)t;
+            w.re_players = (uint8_t)((1u << w.wedding_player) | (1u << winner));
+        } else if (t == 2) {
+            w.team_kind = fdo::TK_WED_SOLVED; w.solved_trick = 2; w.re_players = (uint8_t)(1u << w.wedding_player);
+        }
+    }
+    return winner;
+}
+
+// DoState::play_action (state.rs:189-309)
+DK_HD void play_action(Work& w, int a) {
+    const int cp = w.cur;
+    if (a <= 23) {
+        const uint64_t h = sel4(w.h, cp);
+        const uint64_t lo = 1ULL << a;
+        set4(w.h, cp, (h & lo) ? (h & ~lo) : (h & ~(1ULL << (a + 24))));
+        w.trick_cards |= (uint32_t)a << (8 * w.trick_len);
+        w.trick_len += 1; w.card_index += 1;
+        if (w.trick_len == 4) {
+            const int winner = complete_trick(w);
+            w.trick_index += 1;
+            if (w.trick_index == 12) { w.phase = PH_FINISHED; w.cur = 0xFF; return; }
+            w.trick_cards = 0; w.trick_len = 0; w.trick_start = (uint8_t)winner; w.cur = (uint8_t)winner;
+            return;
+        }
+        w.cur = (uint8_t)((cp + 1) & 3);
+    } else {
+        w.res = byte_set(w.res, w.res_len, a == 25 ? RES_WEDDING : RES_HEALTHY);
+        w.res_len += 1;
+        w.cur = (uint8_t)((cp + 1) & 3);
+        if (w.res_len == 4) {
+            w.phase = PH_PLAYCARD;
+            w.trick_index = 0; w.trick_cards = 0; w.trick_len = 0; w.trick_start = w.cur;
+            finish_reservations(w);
+        }
+    }
+}
+
+// stats.rs:25-135 -> player points (env_state_doko.rs:36-97 rewards)
+DK_HD void score(const Work& w, int pts[4]) {
+    uint32_t re_e = 0, ko_e = 0, re_t = 0, ko_t = 0;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        const bool r = (w.re_players >> p) & 1;
+        re_e += r ? byte_get(w.eyes, p) : 0; ko_e += r ? 0 : byte_get(w.eyes, p);
+        re_t += r ? byte_get(w.ntricks, p) : 0; ko_t += r ? 0 : byte_get(w.ntricks, p);
+    }
+    const bool re_wins = re_e > ko_e;
+    const uint32_t we = re_wins ? re_e : ko_e, wt = re_wins ? re_t : ko_t;
+    const int v = (we >= 120) + (we >= 150) + (we >= 180) + (we >= 210) + (wt == 12);
+    int rp = re_wins ? v : -v;
+    const int kp = re_wins ? -v : v;
+    if (popc32(w.re_players) == 1) rp *= 3;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) pts[p] = ((w.re_players >> p) & 1) ? rp : kp;
+}
+
+DK_HD int rollout(Work w, Rng& rng, int pts[4]) {
+    int plies = 0;
+    while (w.phase != PH_FINISHED) {
+        const uint64_t a = legal_actions(w);
+        play_action(w, ctz64(random_single(a, rng)));
+        plies++;
+    }
+    score(w, pts);
+    return plies;
+}
+
+DK_HD void unpack(const dk_do_state& s, Work& w) {
+    for (int p = 0; p < 4; ++p) w.h[p] = s.hands[p];
+    w.eyes = (uint32_t)s.eyes[0] | (uint32_t)s.eyes[1] << 8 | (uint32_t)s.eyes[2] << 16 | (uint32_t)s.eyes[3] << 24;
+    w.ntricks = (uint32_t)s.ntricks[0] | (uint32_t)s.ntricks[1] << 8 | (uint32_t)s.ntricks[2] << 16 | (uint32_t)s.ntricks[3] << 24;
+    w.trick_winners = s.trick_winners;
+    w.res = 0;
+    for (int i = 0; i < 4; ++i) if (i < s.res_len) w.res = byte_set(w.res, i, s.res[i]);
+    w.res_len = s.res_len; w.res_start = s.res_start; w.card_index = s.card_index; w.phase = s.phase;
+    w.cur = s.current_player; w.trick_index = s.trick_index;
+    w.rr_wedding = s.rr_kind == 2 ? s.rr_player : (uint8_t)0xFF;
+    w.team_kind = s.team_kind; w.wedding_player = s.wedding_player; w.solved_trick = s.solved_trick; w.re_players = s.re_players;
+    w.pad0 = w.pad1 = w.pad2 = 0;
+    w.trick_cards = 0; w.trick_len = 0;
+    const int completed = s.card_index / 4;
+    w.trick_start = (uint8_t)(completed == 0 ? s.res_start : (int)((s.trick_winners >> (2 * (completed - 1))) & 3));
+    if (s.phase == PH_PLAYCARD) {
+        const int in_trick = s.card_index - 4 * completed;
+        for (int i = 0; i < in_trick; ++i) w.trick_cards |= (uint32_t)s.cards[4 * completed + i] << (8 * i);
+        w.trick_len = (uint8_t)in_trick;
+    }
+}
+
+DK_HD void pack_fields(const Work& w, dk_do_state& s) {
+    for (int p = 0; p < 4; ++p) { s.hands[p] = w.h[p]; s.eyes[p] = (uint8_t)byte_get(w.eyes, p); s.ntricks[p] = (uint8_t)byte_get(w.ntricks, p); }
+    s.trick_winners = w.trick_winners;
+    for (int i = 0; i < 4; ++i) s.res[i] = i < w.res_len ? (uint8_t)byte_get(w.res, i) : (uint8_t)DK_NONE;
+    s.res_start = w.res_start; s.res_len = w.res_len; s.card_index = w.card_index; s.phase = w.phase;
+    s.current_player = w.phase == PH_FINISHED ? (uint8_t)DK_NONE : w.cur;
+    s.rr_kind = w.res_len < 4 ? (uint8_t)DK_NONE : (w.rr_wedding == 0xFF ? (uint8_t)0 : (uint8_t)2);
+    s.rr_player = w.rr_wedding == 0xFF ? 0 : w.rr_wedding;
+    s.team_kind = w.team_kind; s.wedding_player = w.wedding_player; s.solved_trick = w.solved_trick; s.re_players = w.re_players;
+    s.trick_index = w.trick_index; s.game = DK_GAME_DOKO;
+}
+
+DK_HD void step_packed(dk_do_state& s, int a) {
+    Work w; unpack(s, w);
+    const uint8_t ci = w.card_index;
+    play_action(w, a);
+    if (a <= 23) s.cards[ci] = (uint8_t)a;
+    pack_fields(w, s);
+}
+
+DK_HD bool is_terminal(const Work& w) { return w.phase == PH_FINISHED; }
+DK_HD int env_current_player(const Work& w) { return w.phase == PH_FINISHED ? 0 : (int)w.cur; }
+DK_HD uint64_t env_allowed(const Work& w, bool) { return legal_actions(w); }
+
+}  // namespace dko
+
+// ---------------------------------------------------------------------------
+// Tic-tac-toe (rs-doko-mcts/src/example/tic_tac_toe.rs:29-193): X and O as
+// 9-bit masks.
+namespace ttt {
+
+struct Work { uint32_t x, o; uint8_t finish, last, pad0, pad1; };
+
+DK_HD uint32_t finish_state(uint32_t x, uint32_t o) {
+    const uint32_t L[8] = {0x007, 0x038, 0x1C0, 0x049, 0x092, 0x124, 0x111, 0x054};
+    for (int i = 0; i < 8; ++i) {
+        if ((x & L[i]) == L[i]) return 1;
+        if ((o & L[i]) == L[i]) return 2;
+    }
+    return ((x | o) == 0x1FF) ? 3u : 0u;
+}
+DK_HD int current_player(const Work& w) { return popc32(w.x) == popc32(w.o) ? 0 : 1; }
+DK_HD uint64_t env_allowed(const Work& w, bool) { return w.finish ? 0ULL : (uint64_t)(~(w.x | w.o) & 0x1FFu); }
+DK_HD void play_action(Work& w, int a) {
+    if (current_player(w) == 0) w.x |= 1u << a; else w.o |= 1u << a;
+    w.finish = (uint8_t)finish_state(w.x, w.o);
+    w.last = (uint8_t)a;
+}
+DK_HD void score(const Work& w, int pts[4]) {
+    pts[0] = w.finish == 1 ? 1 : (w.finish == 2 ? -1 : 0);
+    pts[1] = -pts[0]; pts[2] = 0; pts[3] = 0;
+}
+// random_state: gen_range(0..empties) over the empty cells in ascending order
+DK_HD int rollout(Work w, Rng& rng, int pts[4]) {
+    int plies = 0;
+    while (w.finish == 0) {
+        const uint32_t empt = ~(w.x | w.o) & 0x1FFu;
+        const uint32_t n = (uint32_t)popc32(empt);
+        const uint32_t r = rng.range_u32(n);
+        const uint64_t bit = select_msb_rank((uint64_t)empt, n - 1u - r);  // r-th from the LSB
+        const int cell = ctz64(bit);
+        if (current_player(w) == 0) w.x |= 1u << cell; else w.o |= 1u << cell;
+        w.finish = (uint8_t)finish_state(w.x, w.o);
+        plies++;
+    }
+    score(w, pts);
+    return plies;
+}
+DK_HD void unpack(const dk_ttt_state& s, Work& w) {
+    w.x = 0; w.o = 0;
+    for (int i = 0; i < 9; ++i) { if (s.board[i] == 1) w.x |= 1u << i; if (s.board[i] == 2) w.o |= 1u << i; }
+    w.finish = (uint8_t)finish_state(w.x, w.o); w.last = s.last_action; w.pad0 = w.pad1 = 0;
+}
+DK_HD void pack_fields(const Work& w, dk_ttt_state& s) {
+    for (int i = 0; i < 9; ++i) s.board[i] = (w.x >> i & 1) ? 1 : ((w.o >> i & 1) ? 2 : 0);
+    s.finish = w.finish; s.last_action = w.last; s.game = DK_GAME_TTT;
+}
+DK_HD void step_packed(dk_ttt_state& s, int a) { Work w; unpack(s, w); play_action(w, a); pack_fields(w, s); }
+DK_HD bool is_terminal(const Work& w) { return w.finish != 0; }
+DK_HD int env_current_player(const Work& w) { return current_player(w); }
+
+}  // namespace ttt
+}  // namespace dk

@@ -1,0 +1,536 @@
+// rs-full-doko rules as a register-resident bitboard state machine for gfx950.
+//
+// Reference behaviour (all under /root/reference/rs-full-doko/src):
+//   legal mask ............ action/allowed_actions.rs:68-169
+//   card order / winner ... card/card_in_trick_logic.rs:17-141, trick/trick_winning_player_logic.rs:15-44
+//   colours / masks ....... card/card_to_color.rs:11-259, card/card_color_masks.rs:7-249
+//   play_action ........... state/state.rs:184-358
+//   announcements ......... announcement/announcement.rs:83-215, announcement/calc_announcement.rs:21-229
+//   teams ................. team/team_logic.rs:37-122
+//   reservations .......... reservation/reservation_winning_logic.rs:16-73
+//   DKV scoring ........... stats/**
+//   rollout ............... state.rs:401-431 + rs-doko-mcts env_state_full_doko.rs:198-220
+//
+// Design (not a translation): the whole game state is ~90 bytes of scalars
+// (FdoWork) that live in VGPRs during a rollout — no trick history is kept;
+// scoring uses per-player accumulators (eyes, tricks, >=40-eye tricks, fox
+// events, Karlchen).  In the card phase of a rollout nobody announces, so each
+// announcement round collapses to "advance the RNG once per player whose
+// offer set is non-empty" (fdo_rollout, proven equal to the step-by-step path
+// by tests/native and the GPU parity tests).
+#pragma once
+#include "../../../include/doko_amd.h"
+#include "common.h"
+#include "rng.h"
+
+namespace dk {
+namespace fdo {
+
+enum : uint32_t { PH_RESERVATION = 0, PH_ANNOUNCEMENT = 1, PH_PLAYCARD = 2, PH_FINISHED = 3 };
+enum : uint32_t { GT_NORMAL = 0, GT_WEDDING, GT_DIAMONDS, GT_HEARTS, GT_SPADES, GT_CLUBS, GT_TRUMPLESS, GT_QUEENS, GT_JACKS };
+enum : uint32_t { C_TRUMP = 0, C_DIAMOND, C_HEART, C_SPADE, C_CLUB };
+enum : uint32_t { TK_INRES = 0, TK_WED_UNSOLVED, TK_WED_SOLVED, TK_NOWEDDING };
+enum : uint32_t { RR_NONE = 0, RR_SOLO = 1, RR_WEDDING = 2 };
+enum : uint32_t { R_HEALTHY = 0, R_WEDDING, R_DIAMONDS, R_HEARTS, R_SPADES, R_CLUBS, R_QUEENS, R_JACKS, R_TRUMPLESS };
+enum : uint32_t { AN_RE = 1, AN_90 = 2, AN_60 = 4, AN_30 = 8, AN_BLACK = 16, AN_COUNTER = 32 };
+enum : int { A_HEALTHY = 24, A_WEDDING = 25, A_RE = 33, A_NOANN = 38 };
+static constexpr uint64_t ANN_ACTIONS = 0x1FULL << 33;          // ReContra..Black
+static constexpr uint64_t SOLO_WEDDING_ACTIONS = 0xFFULL << 25; // Wedding + 7 solos
+static constexpr int CLUB_QUEEN = 15, CLUB_JACK = 14, DIAMOND_ACE = 5;
+
+// ---- card tables ------------------------------------------------------------
+// trump cards per game type (24-bit masks)
+DK_HD uint32_t trump_mask(uint32_t gt) {
+    const uint32_t JQ = 0x30C30Cu;      // all jacks and queens (kinds 2,3,8,9,14,15,20,21)
+    const uint32_t H10 = 1u << 7;
+    switch (gt) {
+        case GT_NORMAL: case GT_WEDDING: case GT_DIAMONDS: return 0x3Fu | H10 | JQ;
+        case GT_HEARTS: return (0x3Fu << 6) | JQ;
+        case GT_SPADES: return (0x3Fu << 18) | H10 | JQ;
+        case GT_CLUBS: return (0x3Fu << 12) | H10 | JQ;
+        case GT_TRUMPLESS: return 0u;
+        case GT_QUEENS: return 0x208208u;   // kinds 3, 9, 15, 21
+        default: return 0x104104u;          // GT_JACKS: kinds 2, 8, 14, 20
+    }
+}
+DK_HD uint32_t suit_color(int card) {
+    const int s = card / 6;  // 0 diamond, 1 heart, 2 club, 3 spade
+    return s == 0 ? C_DIAMOND : (s == 1 ? C_HEART : (s == 2 ? C_CLUB : C_SPADE));
+}
+DK_HD uint32_t card_color(int card, uint32_t gt) { return (trump_mask(gt) >> card & 1u) ? C_TRUMP : suit_color(card); }
+DK_HD uint32_t color_mask(uint32_t color, uint32_t gt) {
+    const uint32_t t = trump_mask(gt);
+    switch (color) {
+        case C_TRUMP: return t;
+        case C_DIAMOND: return 0x00003Fu & ~t;
+        case C_HEART: return 0x000FC0u & ~t;
+        case C_CLUB: return 0x03F000u & ~t;
+        default: return 0xFC0000u & ~t;
+    }
+}
+DK_HD uint32_t card_eyes(int card) { return (uint32_t)((0x0B040302'0A00ULL >> (8 * (card % 6))) & 0xFF); }
+// trump rank (card_in_trick_logic.rs:53-83), 4 bits per card kind
+DK_HD uint32_t trump_rank(int card) {
+    // kinds 0..15 in RANK_LO, 16..23 in RANK_HI
+    const uint64_t RANK_LO = 0xB720'2195'C031'8420ULL;  // see tests: D9 0,D10 2,DJ 4,DQ 8,DK 1,DA 3,H9 0,H10 12,HJ 5,HQ 9,HK 1,HA 2,C9 0,C10 2,CJ 7,CQ 11
+    const uint64_t RANK_HI = 0x0000'0000'31A6'2031ULL;  // CK 1,CA 3,S9 0,S10 2,SJ 6,SQ 10,SK 1,SA 3
+    return card < 16 ? (uint32_t)((RANK_LO >> (4 * card)) & 15) : (uint32_t)((RANK_HI >> (4 * (card - 16))) & 15);
+}
+// Strength of a card in a trick: trumps above everything, then the trick
+// colour by eyes (which order the colour cards), other colours never win.
+DK_HD int trick_key(int card, uint32_t trick_color, uint32_t gt) {
+    const uint32_t col = card_color(card, gt);
+    if (col == C_TRUMP) return 32 + (int)trump_rank(card);
+    return col == trick_color ? (int)card_eyes(card) : -1;
+}
+
+// ---- working state ----------------------------------------------------------
+struct Work {
+    uint64_t h[4];
+    uint32_t trick_cards;   // current trick, 8 bits per card in play order
+    uint32_t trick_winners; // 2 bits per completed trick
+    uint32_t eyes;          // 8 bits per player
+    uint32_t ntricks;       // 8 bits per player
+    uint32_t doko;          // tricks of >= 40 eyes won, per player
+    uint32_t res;           // reservation round entries, 8 bits each
+    uint8_t fox_n, fox0, fox1, karl;  // fox events (played_by<<2|winner); karl = 1+winner if last trick won by the club jack
+    uint8_t trick_len, trick_start, n_tricks, card_index;
+    uint8_t phase, cur, game_type, rr_kind;
+    uint8_t rr_player, rr_res, team_kind, wedding_player;
+    uint8_t solved_trick, re_players, re_lowest, contra_lowest;
+    uint8_t ann_turns, ann_start, ann_allowed, ann_count;
+    uint8_t ann_players, res_start, res_len, pad0;
+};
+
+DK_HD int hand_len(const Work& w, int p) { return popc64(sel4(w.h, p)); }
+
+// ---- announcements ----------------------------------------------------------
+DK_HD uint32_t all_higher_than(uint32_t lowest) {
+    switch (lowest) {
+        case AN_RE: return AN_RE;
+        case AN_90: return AN_RE | AN_90;
+        case AN_60: return AN_RE | AN_90 | AN_60;
+        case AN_30: return AN_RE | AN_90 | AN_60 | AN_30;
+        case AN_BLACK: return AN_RE | AN_90 | AN_60 | AN_30 | AN_BLACK;
+        case AN_COUNTER: return AN_COUNTER;
+        default: return 0;
+    }
+}
+// calc_announcement.rs:51-229
+DK_HD uint32_t allowed_announcements(const Work& w, int player, int n) {
+    if (w.team_kind == TK_WED_UNSOLVED || w.team_kind == TK_INRES) return 0;
+    const int ws = w.team_kind == TK_WED_SOLVED ? (int)w.solved_trick : 0;
+    const bool is_re = (w.re_players >> player) & 1;
+    const uint32_t prev = all_higher_than(is_re ? w.re_lowest : w.contra_lowest);
+    const uint32_t enemy = all_higher_than(is_re ? w.contra_lowest : w.re_lowest);
+    const bool p0 = n >= 11 - ws;
+    const bool p90 = p0 || (n >= 10 - ws && (prev & AN_RE));
+    const bool p60 = p90 || (n >= 9 - ws && (prev & AN_90));
+    const bool p30 = p60 || (n >= 8 - ws && (prev & AN_60));
+    const bool pb = p30 || (n >= 7 - ws && (prev & AN_30));
+    uint32_t rem = (p0 ? AN_RE : 0u) | (p90 ? AN_90 : 0u) | (p60 ? AN_60 : 0u) | (p30 ? AN_30 : 0u) | (pb ? AN_BLACK : 0u);
+    rem &= ~prev;
+    rem &= (0u - rem) | ~0x1Fu;  // keep only the lowest set bit among the five levels ("one below the current")
+    if (rem == 0) {
+        int ec = -1;
+        if (enemy & AN_BLACK) ec = 7 - ws;
+        else if (enemy & AN_30) ec = 8 - ws;
+        else if (enemy & AN_60) ec = 9 - ws;
+        else if (enemy & AN_90) ec = 10 - ws;
+        else if (enemy & AN_RE) ec = 11 - ws;
+        if (ec >= 0 && n >= ec - 1 && !(prev & (AN_COUNTER | AN_RE))) rem |= AN_COUNTER;
+    }
+    return rem;
+}
+
+// announcement.rs:182-215 (the announcing player's team decides which lowest moves)
+DK_HD void internal_play_announcement(Work& w, int player, uint32_t ann) {
+    if (ann == 0) { w.ann_turns += 1; return; }  // NoAnnouncement
+    w.ann_turns = 0;
+    if (w.ann_count < 12) { w.ann_count += 1; w.ann_players |= (uint8_t)(1u << player); }
+    if ((w.re_players >> player) & 1) w.re_lowest = (uint8_t)ann; else w.contra_lowest = (uint8_t)ann;
+}
+// announcement.rs:137-180. Returns true if the round is over.
+DK_HD bool internal_progress(Work& w, int player) {
+    int cp = player;
+    for (int guard = 0; guard < 8; ++guard) {
+        if (w.ann_turns == 4) { w.ann_allowed = 0; w.cur = w.ann_start; return true; }
+        const uint32_t a = allowed_announcements(w, cp, hand_len(w, cp));
+        if (a == 0) { internal_play_announcement(w, cp, 0); }
+        else { w.ann_allowed = (uint8_t)a; w.cur = (uint8_t)cp; return false; }
+        cp = (cp + 1) & 3;
+    }
+    w.ann_allowed = 0; w.cur = w.ann_start;
+    return true;
+}
+// state.rs:184-206
+DK_HD void progress_next_card_or_announcement(Work& w) {
+    w.ann_turns = 0;
+    w.ann_start = w.cur;
+    const bool over = internal_progress(w, w.cur);
+    w.phase = over ? PH_PLAYCARD : PH_ANNOUNCEMENT;
+}
+
+// ---- legal actions ------------------------------------------------------------
+DK_HD uint32_t current_trick_color(const Work& w) {
+    // state.rs:360-372: no colour while the trick is empty, and none during the 12th trick
+    if (w.trick_len == 0 || w.n_tricks >= 12 || w.n_tricks == 0) return 0xFF;
+    return card_color((int)(w.trick_cards & 0xFF), w.game_type);
+}
+DK_HD uint64_t legal_actions(const Work& w) {
+    switch (w.phase) {
+        case PH_RESERVATION: {
+            const uint64_t h = sel4(w.h, w.cur);
+            uint64_t a = (0x1FFULL << 24) & ~(1ULL << A_WEDDING);
+            if ((h >> CLUB_QUEEN & 1) && (h >> (CLUB_QUEEN + 24) & 1)) a |= 1ULL << A_WEDDING;
+            return a;
+        }
+        case PH_PLAYCARD: {
+            const uint64_t h = sel4(w.h, w.cur);
+            const uint64_t single = (h | (h >> 24)) & 0xFFFFFFULL;
+            const uint32_t tc = current_trick_color(w);
+            if (tc == 0xFF) return single;
+            const uint64_t follow = single & color_mask(tc, w.game_type);
+            return follow ? follow : single;
+        }
+        case PH_ANNOUNCEMENT: {
+            const uint32_t al = w.ann_allowed;
+            uint64_t a = 1ULL << A_NOANN;
+            if (al & (AN_COUNTER | AN_RE)) a |= 1ULL << 33;
+            if (al & AN_90) a |= 1ULL << 34;
+            if (al & AN_60) a |= 1ULL << 35;
+            if (al & AN_30) a |= 1ULL << 36;
+            if (al & AN_BLACK) a |= 1ULL << 37;
+            return a;
+        }
+        default: return 0;
+    }
+}
+// McFullDokoEnvState::allowed_actions (env_state_full_doko.rs:136-181)
+DK_HD uint64_t env_allowed(const Work& w, bool first_expansion) {
+    uint64_t a = legal_actions(w);
+    if (!first_expansion) {
+        bool any_solo = false;
+        for (int i = 0; i < 4; ++i)
+            if (i < w.res_len) { const uint32_t r = byte_get(w.res, i); any_solo |= r >= R_DIAMONDS; }
+        if (any_solo) a &= ~SOLO_WEDDING_ACTIONS;
+        a &= ~ANN_ACTIONS;
+    }
+    return a;
+}
+
+// ---- transitions ----------------------------------------------------------------
+// reservation_winning_logic.rs:37-73 + :16-33, team_logic.rs:37-122 (reservation end)
+DK_HD void finish_reservations(Work& w) {
+    int wedding = -1;
+    w.rr_kind = RR_NONE;
+    for (int i = 0; i < 4; ++i) {
+        const int p = (w.res_start + i) & 3;
+        const uint32_t r = byte_get(w.res, i);
+        if (w.rr_kind == RR_SOLO) continue;
+        if (r == R_WEDDING) wedding = p;
+        else if (r >= R_DIAMONDS) { w.rr_kind = RR_SOLO; w.rr_player = (uint8_t)p; w.rr_res = (uint8_t)r; }
+    }
+    if (w.rr_kind != RR_SOLO && wedding >= 0) { w.rr_kind = RR_WEDDING; w.rr_player = (uint8_t)wedding; }
+    if (w.rr_kind == RR_SOLO) {
+        // FdoReservation -> FdoGameType (nibble r of 0x687543200)
+        w.game_type = (uint8_t)((0x687543200ULL >> (4 * w.rr_res)) & 15);
+        w.team_kind = TK_NOWEDDING; w.re_players = (uint8_t)(1u << w.rr_player);
+    } else if (w.rr_kind == RR_WEDDING) {
+        w.game_type = GT_WEDDING;
+        w.team_kind = TK_WED_UNSOLVED; w.wedding_player = w.rr_player; w.re_players = 0;
+    } else {
+        w.game_type = GT_NORMAL;
+        uint8_t re = 0;
+        for (int p = 0; p < 4; ++p) {
+            const uint64_t h = sel4(w.h, p);
+            if ((h >> CLUB_QUEEN & 1) || (h >> (CLUB_QUEEN + 24) & 1)) re |= (uint8_t)(1u << p);
+        }
+        w.team_kind = TK_NOWEDDING; w.re_players = re;
+    }
+}
+
+// One completed trick: winner, eyes, scoring accumulators, wedding resolution.
+// Returns the winner.
+DK_HD int complete_trick(Work& w) {
+    const uint32_t tc = card_color((int)(w.trick_cards & 0xFF), w.game_type);
+    int best_key = -2, best_i = 0;
+    uint32_t e = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int c = (int)((w.trick_cards >> (8 * i)) & 0xFF);
+        const int k = trick_key(c, tc, w.game_type);
+        const bool better = k > best_key;
+        best_key = better ? k : best_key;
+        best_i = better ? i : best_i;
+        e += card_eyes(c);
+    }
+    const int winner = (w.trick_start + best_i) & 3;
+    const int win_card = (int)((w.trick_cards >> (8 * best_i)) & 0xFF);
+    const int t = w.n_tricks - 1;
+    w.trick_winners |= (uint32_t)winner << (2 * t);
+    w.eyes = byte_add(w.eyes, winner, e);
+    w.ntricks = byte_add(w.ntricks, winner, 1);
+    if (e >= 40) w.doko = byte_add(w.doko, winner, 1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        if ((int)((w.trick_cards >> (8 * i)) & 0xFF) == DIAMOND_ACE) {
+            const uint8_t ev = (uint8_t)((((w.trick_start + i) & 3) << 2) | winner);
+            if (w.fox_n == 0) w.fox0 = ev; else w.fox1 = ev;
+            w.fox_n += 1;
+        }
+    }
+    if (t == 11 && win_card == CLUB_JACK) w.karl = (uint8_t)(1 + winner);
+    if (w.team_kind == TK_WED_UNSOLVED && t < 3) {
+        if (winner != w.wedding_player) {
+            w.team_kind = TK_WED_SOLVED; w.solved_trick = (uint8_t)t;
+            w.re_players = (uint8_t)((1u << w.wedding_player) | (1u << winner));
+        } else if (t == 2) {
+            w.team_kind = TK_WED_SOLVED; w.solved_trick = 2; w.re_players = (uint8_t)(1u << w.wedding_player);
+        }
+    }
+    return winner;
+}
+
+// Remove one copy of `card` from player p's hand (second copy first, hand.rs:235-247).
+DK_HD void hand_remove(Work& w, int p, int card) {
+    const uint64_t h = sel4(w.h, p);
+    const uint64_t hi = 1ULL << (card + 24);
+    set4(w.h, p, (h & hi) ? (h & ~hi) : (h & ~(1ULL << card)));
+}
+
+// Plays a card for w.cur. Returns true when the game finished.
+DK_HD bool play_card_core(Work& w, int card) {
+    const int cp = w.cur;
+    hand_remove(w, cp, card);
+    w.trick_cards |= (uint32_t)card << (8 * w.trick_len);
+    w.trick_len += 1;
+    w.card_index += 1;
+    if (w.trick_len == 4) {
+        const int winner = complete_trick(w);
+        if (w.n_tricks == 12) { w.phase = PH_FINISHED; w.cur = 0xFF; return true; }
+        w.cur = (uint8_t)winner;
+        w.trick_cards = 0; w.trick_len = 0; w.trick_start = (uint8_t)winner; w.n_tricks += 1;
+        return false;
+    }
+    w.cur = (uint8_t)((cp + 1) & 3);
+    return false;
+}
+
+// FdoState::play_action (state.rs:208-358) for any phase.
+DK_HD void play_action(Work& w, int a) {
+    if (a <= 23) {
+        if (!play_card_core(w, a)) progress_next_card_or_announcement(w);
+    } else if (a <= 32) {
+        // FdoAction order -> FdoReservation discriminant (nibble a-24 of 0x768543210)
+        w.res = byte_set(w.res, w.res_len, (uint32_t)((0x768543210ULL >> (4 * (a - 24))) & 15));
+        w.res_len += 1;
+        w.cur = (uint8_t)((w.cur + 1) & 3);
+        if (w.res_len == 4) {
+            finish_reservations(w);
+            w.trick_cards = 0; w.trick_len = 0; w.trick_start = w.cur; w.n_tricks = 1;
+            progress_next_card_or_announcement(w);
+        }
+    } else {
+        const int cp = w.cur;
+        internal_play_announcement(w, cp, a < A_NOANN ? (1u << (a - 33)) : 0u);
+        const bool over = internal_progress(w, (cp + 1) & 3);
+        if (over) w.phase = PH_PLAYCARD;
+    }
+}
+
+// ---- DKV scoring (stats/stats.rs:46-243 and stats/**) -------------------------
+struct Flags { bool ann, u90, u60, u30, black, none, o_ann, o_90, o_60, o_30, o_black; };
+DK_HD Flags ann_flags(uint32_t prev) {
+    Flags f;
+    f.ann = (prev & (AN_RE | AN_COUNTER)) != 0; f.u90 = prev & AN_90; f.u60 = prev & AN_60; f.u30 = prev & AN_30;
+    f.black = prev & AN_BLACK; f.none = prev == 0;
+    f.o_ann = f.ann && !f.u90; f.o_90 = f.u90 && !f.u60; f.o_60 = f.u60 && !f.u30; f.o_30 = f.u30 && !f.black; f.o_black = f.black;
+    return f;
+}
+// player_points into pts[4]
+DK_HD void score(const Work& w, int pts[4]) {
+    const uint32_t re = w.re_players;
+    uint32_t re_eyes = 0, ko_eyes = 0, re_t = 0, ko_t = 0;
+    int doko_re = 0, doko_ko = 0;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        const bool r = (re >> p) & 1;
+        const uint32_t e = byte_get(w.eyes, p), t = byte_get(w.ntricks, p), d = byte_get(w.doko, p);
+        re_eyes += r ? e : 0; ko_eyes += r ? 0 : e; re_t += r ? t : 0; ko_t += r ? 0 : t;
+        doko_re += r ? (int)d : 0; doko_ko += r ? 0 : (int)d;
+    }
+    const bool re_all = re_t == 12, ko_all = ko_t == 12;
+    const uint32_t rp = all_higher_than(w.re_lowest), kp = all_higher_than(w.contra_lowest);
+    const Flags R = ann_flags(rp), K = ann_flags(kp);
+    const bool rw =
+        (re_eyes >= 121 && R.none && K.none) || (re_eyes >= 121 && R.o_ann && !K.ann) || (re_eyes >= 121 && R.o_ann && K.o_ann) ||
+        (re_eyes >= 120 && !R.ann && K.o_ann) || (re_eyes >= 151 && R.o_90) || (re_eyes >= 181 && R.o_60) ||
+        (re_eyes >= 211 && R.o_30) || (re_all && R.o_black) || (re_eyes >= 90 && K.o_90 && !R.u90) ||
+        (re_eyes >= 60 && K.o_60 && !R.u90) || (re_eyes >= 30 && K.o_30 && !R.u90) || (!ko_all && K.o_black && !R.u90);
+    const bool kw =
+        (ko_eyes >= 120 && R.none && K.none) || (ko_eyes >= 120 && R.o_ann && !K.ann) || (ko_eyes >= 120 && R.o_ann && K.o_ann) ||
+        (ko_eyes >= 121 && !R.ann && K.o_ann) || (ko_eyes >= 151 && K.o_90) || (ko_eyes >= 181 && K.o_60) ||
+        (ko_eyes >= 211 && K.o_30) || (ko_all && K.o_black) || (ko_eyes >= 90 && R.o_90 && !K.u90) ||
+        (ko_eyes >= 60 && R.o_60 && !K.u90) || (ko_eyes >= 30 && R.o_30 && !K.u90) || (!re_all && R.o_black && !K.u90);
+    const bool is_solo = popc32(re) == 1;
+    int ra = 0, ka = 0;
+    if (!is_solo) {
+        const int team_win = rw ? 0 : (kw ? 1 : -1);
+        if (team_win == 1) { ka += 1; ra -= 1; }
+        ra += doko_re - doko_ko; ka += doko_ko - doko_re;
+        int fre = 0, fko = 0;
+        for (int i = 0; i < 2; ++i) {
+            if (i >= w.fox_n) break;
+            const uint8_t ev = i == 0 ? w.fox0 : w.fox1;
+            const bool by_re = (re >> (ev >> 2)) & 1, win_re = (re >> (ev & 3)) & 1;
+            if (by_re != win_re) { if (win_re) fre++; else fko++; }
+        }
+        ra += fre - fko; ka += fko - fre;
+        if (w.karl) { if ((re >> (w.karl - 1)) & 1) { ra += 1; ka -= 1; } else { ra -= 1; ka += 1; } }
+    }
+    int re_pts, ko_pts;
+    if (!rw && !kw) {
+        int r = 0, k = 0;
+        if (re_eyes < 90) { k++; r--; }
+        if (ko_eyes < 90) { r++; k--; }
+        if (re_eyes < 60) { k++; r--; }
+        if (ko_eyes < 60) { r++; k--; }
+        if (re_eyes < 30) { k++; r--; }
+        if (ko_eyes < 30) { r++; k--; }
+        if (re_eyes >= 120 && K.u90) { r++; k--; }
+        if (re_eyes >= 90 && K.u60) { r++; k--; }
+        if (re_eyes >= 60 && K.u30) { r++; k--; }
+        if (re_eyes >= 30 && K.black) { r++; k--; }
+        if (ko_eyes >= 120 && R.u90) { k++; r--; }
+        if (ko_eyes >= 90 && R.u60) { k++; r--; }
+        if (ko_eyes >= 60 && R.u30) { k++; r--; }
+        if (ko_eyes >= 30 && R.black) { k++; r--; }
+        re_pts = r + ra; ko_pts = k + ka;
+    } else {
+        const uint32_t loser = rw ? ko_eyes : re_eyes;
+        const bool winner_all = rw ? re_all : ko_all;
+        int v = 1 + (loser < 90) + (loser < 60) + (loser < 30) + (winner_all ? 1 : 0);
+        v += (R.ann ? 2 : 0) + (K.ann ? 2 : 0);
+        v += (int)R.u90 + (int)R.u60 + (int)R.u30 + (int)R.black + (int)K.u90 + (int)K.u60 + (int)K.u30 + (int)K.black;
+        v += (re_eyes >= 120 && K.u90) + (re_eyes >= 90 && K.u60) + (re_eyes >= 60 && K.u30) + (re_eyes >= 30 && K.black);
+        v += (ko_eyes >= 120 && R.u90) + (ko_eyes >= 90 && R.u60) + (ko_eyes >= 60 && R.u30) + (ko_eyes >= 30 && R.black);
+        re_pts = (rw ? v : -v) + ra;
+        ko_pts = (kw ? v : -v) + ka;
+    }
+    if (is_solo) re_pts *= 3;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) pts[p] = ((re >> p) & 1) ? re_pts : ko_pts;
+}
+
+// ---- rollout (random_action_for_current_player_no_announcement until finished) -----
+// Number of players asked in an announcement round whose offer set is non-empty:
+// each of them consumes exactly one RNG draw (forced NoAnnouncement).
+DK_HD int round_draws(const Work& w) {
+    if (w.team_kind == TK_WED_UNSOLVED) return 0;
+    int d = 0;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) d += allowed_announcements(w, p, hand_len(w, p)) != 0 ? 1 : 0;
+    return d;
+}
+
+// Returns the rewards (player_points) and the number of plies played.
+DK_HD int rollout(Work w, Rng& rng, int pts[4]) {
+    int plies = 0;
+    // Generic steps until the card phase (reservation / pending announcement round).
+    while (w.phase != PH_PLAYCARD && w.phase != PH_FINISHED) {
+        const uint64_t a = legal_actions(w) & ~ANN_ACTIONS;
+        const int act = ctz64(random_single(a, rng));
+        play_action(w, act);
+        plies++;
+    }
+    // Card phase: nobody announces any more; collapse each announcement round.
+    while (w.phase != PH_FINISHED) {
+        const uint64_t a = legal_actions(w);
+        const int card = ctz64(random_single(a, rng));
+        plies++;
+        if (play_card_core(w, card)) break;
+        const int d = round_draws(w);
+        for (int i = 0; i < d; ++i) (void)rng.next_u64();
+        plies += d;
+    }
+    score(w, pts);
+    return plies;
+}
+
+// ---- wire format ----------------------------------------------------------------
+DK_HD void unpack(const dk_fdo_state& s, Work& w) {
+    for (int p = 0; p < 4; ++p) w.h[p] = s.hands[p];
+    w.eyes = (uint32_t)s.eyes[0] | (uint32_t)s.eyes[1] << 8 | (uint32_t)s.eyes[2] << 16 | (uint32_t)s.eyes[3] << 24;
+    w.ntricks = (uint32_t)s.ntricks[0] | (uint32_t)s.ntricks[1] << 8 | (uint32_t)s.ntricks[2] << 16 | (uint32_t)s.ntricks[3] << 24;
+    w.trick_winners = s.trick_winners;
+    w.res = (uint32_t)s.res[0] | (uint32_t)s.res[1] << 8 | (uint32_t)s.res[2] << 16 | (uint32_t)s.res[3] << 24;
+    w.res_start = s.res_start; w.res_len = s.res_len; w.card_index = s.card_index; w.phase = s.phase;
+    w.cur = s.current_player; w.game_type = s.game_type;
+    w.rr_kind = s.rr_kind == DK_NONE ? (uint8_t)RR_NONE : (s.rr_kind == 0 ? (uint8_t)RR_NONE : s.rr_kind);
+    w.rr_player = s.rr_player; w.rr_res = s.rr_reservation;
+    w.team_kind = s.team_kind; w.wedding_player = s.wedding_player; w.solved_trick = s.solved_trick; w.re_players = s.re_players;
+    w.re_lowest = s.re_lowest; w.contra_lowest = s.contra_lowest; w.ann_turns = s.ann_turns; w.ann_start = s.ann_start;
+    w.ann_allowed = s.ann_allowed; w.ann_count = s.ann_count; w.ann_players = s.ann_players; w.n_tricks = s.n_tricks;
+    w.pad0 = 0;
+    // current trick and scoring accumulators from the card history
+    w.doko = 0; w.fox_n = 0; w.fox0 = 0; w.fox1 = 0; w.karl = 0;
+    const int completed = s.card_index / 4;
+    for (int t = 0; t < completed && t < 12; ++t) {
+        const int winner = (int)((s.trick_winners >> (2 * t)) & 3);
+        const int start = t == 0 ? s.res_start : (int)((s.trick_winners >> (2 * (t - 1))) & 3);
+        uint32_t e = 0; int best_key = -2, best_i = 0;
+        const uint32_t tc = card_color(s.cards[4 * t], s.game_type);
+        for (int i = 0; i < 4; ++i) {
+            const int c = s.cards[4 * t + i];
+            e += card_eyes(c);
+            const int k = trick_key(c, tc, s.game_type);
+            if (k > best_key) { best_key = k; best_i = i; }
+            if (c == DIAMOND_ACE) {
+                const uint8_t ev = (uint8_t)((((start + i) & 3) << 2) | winner);
+                if (w.fox_n == 0) w.fox0 = ev; else w.fox1 = ev;
+                w.fox_n += 1;
+            }
+        }
+        if (e >= 40) w.doko = byte_add(w.doko, winner, 1);
+        if (t == 11 && s.cards[4 * t + best_i] == CLUB_JACK) w.karl = (uint8_t)(1 + winner);
+    }
+    w.trick_cards = 0; w.trick_len = 0;
+    w.trick_start = (uint8_t)(completed == 0 ? s.res_start : (int)((s.trick_winners >> (2 * (completed - 1))) & 3));
+    if (s.n_tricks > 0 && s.phase != PH_FINISHED) {
+        const int in_trick = s.card_index - 4 * (s.n_tricks - 1);
+        for (int i = 0; i < in_trick; ++i) w.trick_cards |= (uint32_t)s.cards[4 * (s.n_tricks - 1) + i] << (8 * i);
+        w.trick_len = (uint8_t)in_trick;
+    }
+}
+
+DK_HD void pack_fields(const Work& w, dk_fdo_state& s) {
+    for (int p = 0; p < 4; ++p) { s.hands[p] = w.h[p]; s.eyes[p] = (uint8_t)byte_get(w.eyes, p); s.ntricks[p] = (uint8_t)byte_get(w.ntricks, p); }
+    s.trick_winners = w.trick_winners;
+    for (int i = 0; i < 4; ++i) s.res[i] = i < w.res_len ? (uint8_t)byte_get(w.res, i) : (uint8_t)DK_NONE;
+    s.res_start = w.res_start; s.res_len = w.res_len; s.card_index = w.card_index; s.phase = w.phase;
+    s.current_player = w.phase == PH_FINISHED ? (uint8_t)DK_NONE : w.cur;
+    s.game_type = w.game_type;
+    s.rr_kind = w.res_len < 4 ? (uint8_t)DK_NONE : (w.rr_kind == RR_NONE ? (uint8_t)0 : w.rr_kind);
+    s.rr_player = w.rr_player; s.rr_reservation = w.rr_res;
+    s.team_kind = w.team_kind; s.wedding_player = w.wedding_player; s.solved_trick = w.solved_trick; s.re_players = w.re_players;
+    s.re_lowest = w.re_lowest; s.contra_lowest = w.contra_lowest; s.ann_turns = w.ann_turns; s.ann_start = w.ann_start;
+    s.ann_allowed = w.ann_allowed; s.ann_count = w.ann_count; s.ann_players = w.ann_players; s.n_tricks = w.n_tricks;
+    s.game = DK_GAME_FULL_DOKO;
+}
+
+// McEnvState::by_action on the wire format (keeps the card history).
+DK_HD void step_packed(dk_fdo_state& s, int a) {
+    Work w; unpack(s, w);
+    const uint8_t ci = w.card_index;
+    play_action(w, a);
+    if (a <= 23) s.cards[ci] = (uint8_t)a;
+    pack_fields(w, s);
+}
+
+// rewards_or_none / finished check on the working state
+DK_HD bool is_terminal(const Work& w) { return w.phase == PH_FINISHED; }
+DK_HD int env_current_player(const Work& w) { return w.phase == PH_FINISHED ? 0 : (int)w.cur; }
+
+}  // namespace fdo
+}  // namespace dk

@@ -1,0 +1,155 @@
+// SmallRng of rand 0.9.0 (= Xoshiro256++) for the GPU, keeping the draw order
+// of the reference: seed_from_u64 (SplitMix64), next_u32 = hi32(next_u64),
+// u32 random_range = Canon widening multiply (+1 draw in the biased zone),
+// shuffle = IncreasingUniform, IteratorRandom::choose = CoinFlipper path.
+// (Cargo.lock:1899-1946 pins rand 0.9.0 / rand_core 0.9.3.)
+#pragma once
+#include "common.h"
+
+namespace dk {
+
+struct Rng {
+    uint64_t s0, s1, s2, s3;
+
+    DK_HD static uint64_t rotl(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+
+    DK_HD static Rng seed_from_u64(uint64_t state) {
+        Rng r;
+        uint64_t out[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            state += 0x9e3779b97f4a7c15ULL;
+            uint64_t z = state;
+            z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+            z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+            out[i] = z ^ (z >> 31);
+        }
+        r.s0 = out[0]; r.s1 = out[1]; r.s2 = out[2]; r.s3 = out[3];
+        if ((r.s0 | r.s1 | r.s2 | r.s3) == 0) return seed_from_u64(0);
+        return r;
+    }
+
+    DK_HD uint64_t next_u64() {
+        const uint64_t res = rotl(s0 + s3, 23) + s0;
+        const uint64_t t = s1 << 17;
+        s2 ^= s0;
+        s3 ^= s1;
+        s1 ^= s2;
+        s0 ^= s3;
+        s2 ^= t;
+        s3 = rotl(s3, 45);
+        return res;
+    }
+    DK_HD uint32_t next_u32() { return (uint32_t)(next_u64() >> 32); }
+
+    // random_range(0..n) on u32 (n >= 1).
+    DK_HD uint32_t range_u32(uint32_t n) {
+        const uint64_t m = (uint64_t)next_u32() * (uint64_t)n;
+        uint32_t result = (uint32_t)(m >> 32);
+        const uint32_t lo = (uint32_t)m;
+        if (lo > (uint32_t)(0u - n)) {
+            const uint32_t hi2 = (uint32_t)(((uint64_t)next_u32() * (uint64_t)n) >> 32);
+            result += ((uint32_t)(lo + hi2) < lo) ? 1u : 0u;
+        }
+        return result;
+    }
+
+    // random_bool(p) (Bernoulli, one u64 draw; p < 1).
+    DK_HD bool random_bool(double p) {
+        const uint64_t p_int = (uint64_t)(p * 18446744073709551616.0);
+        return next_u64() < p_int;
+    }
+};
+
+// uniform pick of one set bit (Bitflag::random_single, bit_flag.rs:86-92)
+DK_HD uint64_t random_single(uint64_t mask, Rng& rng) {
+    const uint32_t r = rng.range_u32((uint32_t)popc64(mask));
+    return select_msb_rank(mask, r);
+}
+
+// SliceRandom::shuffle on a 48-entry array via IncreasingUniform.
+DK_HD void shuffle48(uint8_t* a, Rng& rng) {
+    uint32_t n = 0, chunk = 0;
+    uint32_t chunk_remaining = 1;  // IncreasingUniform::new(rng, 0)
+    for (int i = 0; i < 48; ++i) {
+        const uint32_t next_n = n + 1;
+        uint32_t ncr;
+        if (chunk_remaining == 0) {
+            uint32_t product = next_n, current = next_n + 1;
+            while ((uint64_t)product * current <= 0xFFFFFFFFULL) { product *= current; current += 1; }
+            chunk = rng.range_u32(product);
+            ncr = current - next_n - 1;
+        } else {
+            ncr = chunk_remaining - 1;
+        }
+        uint32_t idx;
+        if (ncr == 0) idx = chunk;
+        else { idx = chunk % next_n; chunk /= next_n; }
+        chunk_remaining = ncr;
+        n = next_n;
+        const uint8_t t = a[i]; a[i] = a[idx]; a[idx] = t;
+    }
+}
+
+// CoinFlipper of rand 0.9 seq/coin_flipper.rs (IteratorRandom::choose without a
+// size hint).  Parity with the reference is unpinned (no fixture exercises it).
+struct CoinFlipper {
+    uint32_t chunk = 0, remaining = 0;
+
+    DK_HD bool flip_c_heads(uint32_t c, Rng& rng) {
+        for (;;) {
+            const uint32_t zeros = (uint32_t)clz32(chunk);
+            if (zeros < c) {
+                const uint32_t sh = zeros + 1;
+                chunk = chunk << (sh & 31);
+                remaining = remaining > sh ? remaining - sh : 0;
+                return false;
+            }
+            if (remaining >= c) {
+                remaining -= c;
+                chunk = chunk << (c & 31);
+                return true;
+            }
+            c -= remaining;
+            chunk = rng.next_u32();
+            remaining = 32;
+        }
+    }
+    DK_HD bool random_ratio(uint64_t n, uint64_t d, Rng& rng) {
+        while (n < d) {
+            int cc = clz64(n) - (clz64(d) + 1);
+            if (cc < 1) cc = 1;
+            if (cc > 32) cc = 32;
+            const uint32_t c = (uint32_t)cc;
+            if (flip_c_heads(c, rng)) {
+                n = (c >= 64 || (n >> (64 - c)) != 0) ? ~0ULL : (n << c);
+            } else {
+                if (c == 1) {
+                    const uint64_t next_n = n + n - d;
+                    if (next_n == 0 || next_n > n) return false;
+                    n = next_n;
+                } else {
+                    return false;
+                }
+            }
+        }
+        return true;
+    }
+    DK_HD bool random_ratio_one_over(uint64_t d, Rng& rng) {
+        uint32_t c = 63u - (uint32_t)clz64(d);
+        if (c > 32) c = 32;
+        if (flip_c_heads(c, rng)) return random_ratio(1ULL << c, d, rng);
+        return false;
+    }
+};
+
+// Reservoir choice over `count` items in iteration order (CoinFlipper path).
+DK_HD int choose_unsized(int count, Rng& rng) {
+    CoinFlipper cf;
+    int result = -1;
+    for (int i = 0; i < count; ++i)
+        if (cf.random_ratio_one_over((uint64_t)(i + 1), rng)) result = i;
+    return result;
+}
+
+}  // namespace dk
