@@ -1,0 +1,305 @@
+"""Benchmark: determinized rollouts/sec (48-card full game, 1000 sims/root).
+
+One step = one determinized decision batch of BASELINE.json config 3 on every
+GPU, entirely on the device:
+    CAP determinization (card_matching_full)  -> 512 infostates x 64 samples = 32,768 roots
+    UCT search, 1000 simulations per root (select/expand/random rollout/backup)
+    policy fusion (MaxN) of the per-sample visit counts per infostate
+With N GPUs (config 4) the global batch holds 512*N infostates; the 64 samples
+of every infostate are split evenly over the ranks (32,768 roots per GPU, weak
+scaling) and the per-infostate fusion accumulators are summed with one RCCL
+all-reduce over xGMI before the fused action is selected.
+
+Rank 0 prints one JSON line.  `value` = simulations of all ranks / max-over-ranks
+wall time of the K timed steps.  Inputs (the infostates) are synthesised on the
+GPU before the timed region.
+"""
+import argparse
+import json
+import os
+import platform
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "determinized rollouts/sec (48-card full game, 1000 sims/root) at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--workload", choices=["c3", "c2"], default="c3")
+    p.add_argument("--iterations", type=int, default=1000)
+    p.add_argument("--infostates", type=int, default=512, help="infostates per GPU (c3)")
+    p.add_argument("--samples", type=int, default=64, help="CAP samples per infostate (c3)")
+    p.add_argument("--roots", type=int, default=32768, help="roots per GPU (c2)")
+    p.add_argument("--c", type=float, default=2.5)
+    p.add_argument("--fusion", choices=["maxn", "avg"], default="maxn")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-threads", type=int, default=0)
+    p.add_argument("--cpu-roots-per-thread", type=int, default=6)
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    import master_doko_reinforcement_learning_amd as dk
+    from master_doko_reinforcement_learning_amd import _native
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+    L = _native.lib()
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+
+    def ck(rc):
+        if rc != 0:
+            raise RuntimeError("doko_amd error %d: %s" % (rc, L.dk_status_string(rc).decode()))
+
+    def ptr(t):
+        return t.data_ptr()
+
+    iters = args.iterations
+    fuse_mode = dk.FUSE_MAXN if args.fusion == "maxn" else dk.FUSE_AVG
+
+    if args.workload == "c3":
+        if args.samples % world:
+            raise SystemExit("samples must be divisible by the number of GPUs")
+        I = args.infostates * world          # global infostates
+        S_r = args.samples // world          # samples of every infostate on this rank
+        n_roots = I * S_r
+    else:
+        I, S_r = 0, 0
+        n_roots = args.roots
+    eng = dk.Engine(device=local_rank, max_roots=n_roots, max_iterations=iters)
+
+    # ------------------------------------------------------------ inputs (untimed, on the GPU)
+    def healthy_round(states_t, n):
+        a = torch.full((n,), 1 << 24, dtype=torch.int64, device=dev)
+        for _ in range(4):
+            ck(L.dk_env_step_batch_async(eng.ctx, ptr(states_t), ptr(a), n, sp))
+
+    if args.workload == "c3":
+        info_seeds = torch.tensor(np.arange(I, dtype=np.uint64) + np.uint64(0xC3000000), device=dev)
+        info = torch.zeros((I, 128), dtype=torch.uint8, device=dev)
+        ck(L.dk_new_game_batch_async(eng.ctx, dk.GAME_FULL_DOKO, ptr(info_seeds), I, ptr(info), sp))
+        healthy_round(info, I)
+        plies = torch.tensor(np.array([[0, 8, 20, 32][j % 4] for j in range(I)], dtype=np.uint32).view(np.int32), device=dev)
+        ply_rng = torch.tensor(dk.splitmix_rng_states(np.arange(I, dtype=np.uint64) + np.uint64(0xC3100000)).view(np.int64), device=dev)
+        ck(L.dk_env_random_plies_batch_async(eng.ctx, ptr(info), ptr(ply_rng), ptr(plies), I, sp))
+        allowed = torch.zeros(I, dtype=torch.int64, device=dev)
+        ck(L.dk_legal_actions_async(eng.ctx, ptr(info), I, ptr(allowed), sp))
+        j = np.arange(I, dtype=np.uint64)[:, None]
+        s = np.arange(rank * S_r, (rank + 1) * S_r, dtype=np.uint64)[None, :]
+        samp_seeds = (np.uint64(0xC3200000) + j * np.uint64(args.samples) + s).reshape(-1)
+        srch_seeds = (np.uint64(0xC3300000) + j * np.uint64(args.samples) + s).reshape(-1)
+        d_samp = torch.tensor(samp_seeds.view(np.int64), device=dev)
+        d_srch = torch.tensor(srch_seeds.view(np.int64), device=dev)
+        roots = torch.zeros((n_roots, 128), dtype=torch.uint8, device=dev)
+        acc_u = torch.zeros((I, 39), dtype=torch.int32, device=dev)
+        acc_f = torch.zeros((I, 39), dtype=torch.float32, device=dev)
+        actions = torch.zeros(I, dtype=torch.uint8, device=dev)
+    else:
+        gidx = np.arange(rank * n_roots, (rank + 1) * n_roots, dtype=np.uint64)
+        d_rs = torch.tensor((gidx + np.uint64(0xD0C00000)).view(np.int64), device=dev)
+        roots = torch.zeros((n_roots, 128), dtype=torch.uint8, device=dev)
+        ck(L.dk_new_game_batch_async(eng.ctx, dk.GAME_DOKO, ptr(d_rs), n_roots, ptr(roots), sp))
+        healthy_round(roots, n_roots)
+        d_srch = torch.tensor((gidx * np.uint64(0x9E3779B97F4A7C15) + np.uint64(1)).view(np.int64), device=dev)
+    visits = torch.zeros((n_roots, 39), dtype=torch.int32, device=dev)
+    values = torch.zeros((n_roots, 39), dtype=torch.float64, device=dev)
+    best = torch.zeros(n_roots, dtype=torch.uint8, device=dev)
+    ck(L.dk_sync(eng.ctx, sp))
+
+    search_ms = []
+
+    def step():
+        if args.workload == "c3":
+            ck(L.dk_determinize_batch_async(eng.ctx, ptr(info), I, S_r, ptr(d_samp), ptr(roots), sp))
+            ck(L.dk_search_batch_async(eng.ctx, dk.GAME_FULL_DOKO, ptr(roots), ptr(d_srch), n_roots, iters, args.c,
+                                       ptr(visits), ptr(values), ptr(best), sp))
+            ck(L.dk_fuse_accumulate_async(eng.ctx, ptr(visits), I, S_r, ptr(allowed), fuse_mode, ptr(acc_u), ptr(acc_f), sp))
+            if world > 1:
+                dist.all_reduce(acc_u if fuse_mode == dk.FUSE_MAXN else acc_f)  # RCCL over xGMI
+            ck(L.dk_fuse_select_async(eng.ctx, I, fuse_mode, ptr(allowed), ptr(acc_u), ptr(acc_f), ptr(actions), sp))
+        else:
+            ck(L.dk_search_batch_async(eng.ctx, dk.GAME_DOKO, ptr(roots), ptr(d_srch), n_roots, iters, args.c,
+                                       ptr(visits), ptr(values), ptr(best), sp))
+
+    for _ in range(args.warmup):
+        step()
+    ck(L.dk_sync(eng.ctx, sp))
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        ms = eng.last_search_ms()  # waits for this step's search kernel (HIP events on its stream)
+        search_ms.append(ms)
+    torch.cuda.synchronize(dev)
+    ck(L.dk_sync(eng.ctx, sp))
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+
+    v = visits.cpu().numpy()
+    assert np.all(v.sum(axis=1) == iters), "every root must have exactly `iterations` simulations"
+    sims_total = n_roots * iters * args.steps * world
+    kernel_ms = float(np.mean(search_ms))
+
+    result = None
+    if rank == 0:
+        cpu = None
+        alg = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu, alg = cpu_baseline(args, dk)
+        if alg is None:
+            alg = {"b_sim": None}
+        b_sim = alg.get("b_sim")
+        if b_sim is None:
+            # measured oracle means on C3 roots (children scanned 42.7, path 22.5 nodes)
+            b_sim = 128 + 16 * 42.7 + 32 * 22.5 + 32
+        achieved = n_roots * iters * b_sim / (kernel_ms / 1e3) / 1e9
+        traffic = pmc_traffic(n_roots, iters)
+        result = {
+            "metric": METRIC,
+            "value": sims_total / elapsed,
+            "unit": "rollouts/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64+f64",
+            "data": "synthetic: seeded deals (SmallRng::seed_from_u64), 4x Healthy, k in {0,8,20,32} random plies; "
+                    "determinized on the GPU by CAP",
+            "config": {
+                "workload": ("C3 rs-full-doko determinized UCT: %d infostates x %d CAP samples/GPU-share, %d roots x %d sims per GPU"
+                             % (I, args.samples, n_roots, iters)) if args.workload == "c3" else
+                            ("C2 rs-doko random-rollout UCT: %d roots x %d sims per GPU" % (n_roots, iters)),
+                "roots_per_gpu": n_roots,
+                "iterations": iters,
+                "uct_c": args.c,
+                "fusion": args.fusion if args.workload == "c3" else None,
+                "parallelism": "dp%d (samples split over GPUs, RCCL all-reduce of fusion accumulators)" % world,
+            },
+            "search_kernel_ms": kernel_ms,
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "alg_bytes_per_sim": b_sim,
+                "note": "integer/branch-bound search; algorithmic bytes per simulation from the oracle's counters",
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(result))
+    if world > 1:
+        dist.destroy_process_group()
+    eng.close()
+    return result
+
+
+def cpu_baseline(args, dk):
+    """The ORACLE (C++ restatement of the reference hot path) timed on this box's
+    host cores on a bounded sample of the same workload."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import ctypes
+
+    import oracle_lib as ol
+    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    n = threads * args.cpu_roots_per_thread
+    iters = args.iterations
+    roots = []
+    seeds = []
+    if args.workload == "c3":
+        for k in range(n):
+            j, s = k % args.infostates, k // args.infostates
+            st = ol.FdoState.new_game(0xC3000000 + j)
+            for _ in range(4):
+                st.play(24)
+            rng = ol.arr(ctypes.c_uint64, 4, [int(x) for x in dk.splitmix_rng_states(np.array([0xC3100000 + j], dtype=np.uint64))[0]])
+            st.random_plies(rng, [0, 8, 20, 32][j % 4], True)
+            smp = st.card_matching(ol.rng_seed(0xC3200000 + j * args.samples + s))
+            roots.append(smp)
+            seeds.append(0xC3300000 + j * args.samples + s)
+        search_many = ol.lib().or_fdo_search_many
+        handles = (ctypes.c_void_p * n)(*[r.h for r in roots])
+        vis = (ctypes.c_uint32 * (39 * n))()
+        sd = ol.arr(ctypes.c_uint64, n, seeds)
+        secs = search_many(None, handles, sd, n, iters, args.c, vis, threads)
+        # algorithmic-byte model inputs: mean children scanned / path nodes per simulation
+        scanned = path = sims = 0
+        for r, s in zip(roots[:8], seeds[:8]):
+            _, _, _, ctr = r.search(ol.rng_seed(s), iters, args.c)
+            sims += ctr[0]
+            scanned += ctr[1]
+            path += ctr[2]
+        alg = {"children_scanned": scanned / sims, "path_nodes": path / sims}
+        alg["b_sim"] = 128 + 16 * alg["children_scanned"] + 32 * alg["path_nodes"] + 32
+    else:
+        for k in range(n):
+            st = ol.DoState.new_game(0xD0C00000 + k)
+            for _ in range(4):
+                st.play(24)
+            roots.append(st)
+            seeds.append((k * 0x9E3779B97F4A7C15 + 1) & 0xFFFFFFFFFFFFFFFF)
+        handles = (ctypes.c_void_p * n)(*[r.h for r in roots])
+        vis = (ctypes.c_uint32 * (39 * n))()
+        secs = ol.lib().or_do_search_many(handles, ol.arr(ctypes.c_uint64, n, seeds), n, iters, args.c, vis, threads)
+        alg = None
+    model = ""
+    try:
+        model = subprocess.run(["lscpu"], capture_output=True, text=True).stdout
+        model = [l.split(":", 1)[1].strip() for l in model.splitlines() if l.startswith("Model name")][0]
+    except Exception:
+        model = platform.processor()
+    cpu = {"value": n * iters / secs, "unit": "rollouts/s", "cores": threads, "kind": "port",
+           "sample": "%d roots x %d sims of the same workload (oracle C++ restatement, root-parallel like MCTSWorkers), "
+                     "%.1f s wall on %d threads of %s" % (n, iters, secs, threads, model)}
+    return cpu, alg
+
+
+def pmc_traffic(n_roots, iters):
+    """HBM bytes per search launch from the committed rocprofv3 PMC summary
+    (profiles/pmc_search.json), scaled to this launch size; None if absent."""
+    path = os.path.join(ROOT, "profiles", "pmc_search.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as fh:
+        d = json.load(fh)
+    try:
+        per_sim = d["hbm_bytes_per_launch"] / (d["roots"] * d["iterations"])
+        return per_sim * n_roots * iters
+    except Exception:
+        return None
+
+
+if __name__ == "__main__":
+    main()

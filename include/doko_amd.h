@@ -171,6 +171,11 @@ int dk_env_rollout_batch_async(dk_ctx* ctx, const dk_state* d_states, uint64_t* 
 /* random_action_for_current_player_no_announcement applied k[i] times
  * (rs-full-doko/src/state/state.rs:401-431; rs-doko uses random_action_for_current_player). */
 int dk_env_random_plies_batch(dk_ctx* ctx, dk_state* states, uint64_t* rng_states, const uint32_t* plies, uint32_t n);
+int dk_env_random_plies_batch_async(dk_ctx* ctx, dk_state* d_states, uint64_t* d_rng_states, const uint32_t* d_plies,
+                                    uint32_t n, void* stream);
+int dk_env_step_batch_async(dk_ctx* ctx, dk_state* d_states, const uint64_t* d_action_bits, uint32_t n, void* stream);
+/* observation.allowed_actions_current_player (legal set incl. announcements), state.rs:434-481 */
+int dk_legal_actions_async(dk_ctx* ctx, const dk_state* d_states, uint32_t n, uint64_t* d_masks, void* stream);
 
 /* ---- CachedMCTS::monte_carlo_tree_search (rs-doko-mcts/src/mcts/mcts.rs:284-315)
  * One independent UCT search per root (the reference's sequential per-root
@@ -180,9 +185,9 @@ int dk_env_random_plies_batch(dk_ctx* ctx, dk_state* states, uint64_t* rng_state
  * expansion order (last maximum wins), DK_NONE when the root has no children.
  * `c` is the UCT exploration constant as f64 (the evaluator passes (double)(float)c).
  */
-int dk_search_batch(dk_ctx* ctx, const dk_state* roots, const uint64_t* seeds, uint32_t n, uint32_t iterations,
-                    double c, uint32_t* visits, double* values, uint8_t* best);
-int dk_search_batch_async(dk_ctx* ctx, const dk_state* d_roots, const uint64_t* d_seeds, uint32_t n,
+int dk_search_batch(dk_ctx* ctx, int game, const dk_state* roots, const uint64_t* seeds, uint32_t n,
+                    uint32_t iterations, double c, uint32_t* visits, double* values, uint8_t* best);
+int dk_search_batch_async(dk_ctx* ctx, int game, const dk_state* d_roots, const uint64_t* d_seeds, uint32_t n,
                           uint32_t iterations, double c, uint32_t* d_visits, double* d_values, uint8_t* d_best,
                           void* stream);
 
@@ -196,8 +201,9 @@ int dk_determinize_batch_async(dk_ctx* ctx, const dk_state* d_infostates, uint32
                                const uint64_t* d_seeds, dk_state* d_out, void* stream);
 
 /* ---- PolicyFusionFn::fuse (policy_fusion.rs:23-123) --------------------------
- * mode DK_FUSE_MAXN: per infostate sum of per-sample visit ranks (u32, disallowed
- *   = UINT32_MAX) -> first minimum.   acc_u32 = [n_info][39] rank sums.
+ * mode DK_FUSE_MAXN: per infostate sum of per-sample visit ranks (u32) -> first
+ *   minimum, disallowed actions ranked UINT32_MAX.  acc_u32 = [n_info][39] rank
+ *   sums (0 for disallowed actions, so partial sums add across ranks).
  * mode DK_FUSE_AVG: per infostate sum over samples of visits/total (f32) -> last
  *   maximum.                           acc_f32 = [n_info][39] probability sums.
  * The _accumulate/_select split lets a multi-GPU caller all-reduce(sum) the
@@ -208,8 +214,8 @@ int dk_fuse(dk_ctx* ctx, const uint32_t* visits, uint32_t n_info, uint32_t sampl
             int mode, uint8_t* action);
 int dk_fuse_accumulate_async(dk_ctx* ctx, const uint32_t* d_visits, uint32_t n_info, uint32_t samples,
                              const uint64_t* d_allowed, int mode, uint32_t* d_acc_u32, float* d_acc_f32, void* stream);
-int dk_fuse_select_async(dk_ctx* ctx, uint32_t n_info, int mode, const uint32_t* d_acc_u32, const float* d_acc_f32,
-                         uint8_t* d_action, void* stream);
+int dk_fuse_select_async(dk_ctx* ctx, uint32_t n_info, int mode, const uint64_t* d_allowed, const uint32_t* d_acc_u32,
+                         const float* d_acc_f32, uint8_t* d_action, void* stream);
 
 /* ---- DefaultImpiPolicy::execute (compare_impi.rs:212-371), batched ----------
  * For each infostate: `samples` CAP determinizations -> one UCT search each ->
@@ -219,8 +225,16 @@ int dk_decide_batch(dk_ctx* ctx, const dk_state* infostates, uint32_t n_info, ui
                     const uint64_t* seeds, uint32_t iterations, double c, int fuse_mode, uint8_t* actions,
                     uint32_t* visits);
 
-/* ---- timing of the last *_async search launch (HIP events on its stream) ---- */
+/* ---- completion / errors / timing of *_async work -------------------------------
+ * dk_sync: waits for the stream and returns the first device-side error
+ * (DK_E_CAPACITY when a search ran out of child slots) since the last dk_sync.
+ * dk_last_search_ms: device time of the last search launch (HIP events recorded
+ * on the launch stream around the kernel).
+ */
+int dk_sync(dk_ctx* ctx, void* stream);
 int dk_last_search_ms(dk_ctx* ctx, float* ms);
+/* memory footprint of the node / state pools reserved by dk_create (bytes) */
+uint64_t dk_pool_bytes(const dk_ctx* ctx);
 
 #ifdef __cplusplus
 }

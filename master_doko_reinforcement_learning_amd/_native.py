@@ -1,0 +1,97 @@
+"""Loader and build recipe of libdoko_amd.so (HIP, gfx950).
+
+There is no CPU fallback: if the shared library is missing or no gfx950 device
+is usable, the product API raises.
+"""
+import ctypes
+import os
+import subprocess
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG_DIR)
+LIB_PATH = os.path.join(PKG_DIR, "libdoko_amd.so")
+SRC = os.path.join(PKG_DIR, "csrc", "doko_amd.hip")
+HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared"]
+
+
+def build(verbose=False):
+    """Compile csrc/doko_amd.hip for gfx950 into the package directory (in-tree)."""
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    cmd = [hipcc] + HIPCC_FLAGS + ["-o", LIB_PATH, SRC]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True, cwd=PKG_DIR)
+    return LIB_PATH
+
+
+class dk_config(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("max_roots", ctypes.c_uint32),
+                ("max_iterations", ctypes.c_uint32), ("slot_capacity", ctypes.c_uint32)]
+
+
+_lib = None
+vp = ctypes.c_void_p
+u32 = ctypes.c_uint32
+u64 = ctypes.c_uint64
+
+
+def lib():
+    """Load libdoko_amd.so (importing torch first when available so that the
+    process uses a single HIP runtime)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError("libdoko_amd.so not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
+                          "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+    try:
+        import torch  # noqa: F401  (shares libamdhip64 with the extension)
+    except Exception:
+        pass
+    L = ctypes.CDLL(LIB_PATH)
+    sigs = {
+        "dk_abi_version": (ctypes.c_int, []),
+        "dk_status_string": (ctypes.c_char_p, [ctypes.c_int]),
+        "dk_create": (vp, [ctypes.POINTER(dk_config)]),
+        "dk_destroy": (None, [vp]),
+        "dk_last_error": (ctypes.c_int, [vp]),
+        "dk_pool_bytes": (u64, [vp]),
+        "dk_sync": (ctypes.c_int, [vp, vp]),
+        "dk_last_search_ms": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_float)]),
+        "dk_new_game_batch": (ctypes.c_int, [vp, ctypes.c_int, vp, u32, vp]),
+        "dk_new_game_batch_async": (ctypes.c_int, [vp, ctypes.c_int, vp, u32, vp, vp]),
+        "dk_env_allowed_batch": (ctypes.c_int, [vp, vp, u32, ctypes.c_int, vp]),
+        "dk_env_step_batch": (ctypes.c_int, [vp, vp, vp, u32]),
+        "dk_env_rewards_batch": (ctypes.c_int, [vp, vp, u32, vp, vp]),
+        "dk_env_rollout_batch": (ctypes.c_int, [vp, vp, vp, u32, vp]),
+        "dk_env_rollout_batch_async": (ctypes.c_int, [vp, vp, vp, u32, vp, vp]),
+        "dk_env_random_plies_batch": (ctypes.c_int, [vp, vp, vp, vp, u32]),
+        "dk_search_batch": (ctypes.c_int, [vp, ctypes.c_int, vp, vp, u32, u32, ctypes.c_double, vp, vp, vp]),
+        "dk_search_batch_async": (ctypes.c_int, [vp, ctypes.c_int, vp, vp, u32, u32, ctypes.c_double, vp, vp, vp, vp]),
+        "dk_determinize_batch": (ctypes.c_int, [vp, vp, u32, u32, vp, vp]),
+        "dk_determinize_batch_async": (ctypes.c_int, [vp, vp, u32, u32, vp, vp, vp]),
+        "dk_fuse": (ctypes.c_int, [vp, vp, u32, u32, vp, ctypes.c_int, vp]),
+        "dk_fuse_accumulate_async": (ctypes.c_int, [vp, vp, u32, u32, vp, ctypes.c_int, vp, vp, vp]),
+        "dk_fuse_select_async": (ctypes.c_int, [vp, u32, ctypes.c_int, vp, vp, vp, vp, vp]),
+        "dk_legal_actions_async": (ctypes.c_int, [vp, vp, u32, vp, vp]),
+        "dk_env_step_batch_async": (ctypes.c_int, [vp, vp, vp, u32, vp]),
+        "dk_env_random_plies_batch_async": (ctypes.c_int, [vp, vp, vp, vp, u32, vp]),
+        "dk_decide_batch": (ctypes.c_int, [vp, vp, u32, u32, vp, u32, ctypes.c_double, ctypes.c_int, vp, vp]),
+    }
+    for name, (res, args) in sigs.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+# every symbol include/doko_amd.h declares (checked by the CPU test suite)
+EXPORTED = [
+    "dk_create", "dk_destroy", "dk_last_error", "dk_status_string", "dk_abi_version", "dk_new_game_batch",
+    "dk_new_game_batch_async", "dk_env_allowed_batch", "dk_env_step_batch", "dk_env_rewards_batch",
+    "dk_env_rollout_batch", "dk_env_rollout_batch_async", "dk_env_random_plies_batch", "dk_search_batch",
+    "dk_search_batch_async", "dk_determinize_batch", "dk_determinize_batch_async", "dk_fuse",
+    "dk_fuse_accumulate_async", "dk_fuse_select_async", "dk_decide_batch", "dk_sync", "dk_last_search_ms",
+    "dk_pool_bytes", "dk_legal_actions_async", "dk_env_step_batch_async", "dk_env_random_plies_batch_async",
+]

@@ -1,0 +1,224 @@
+"""Host-side mirror of the reference's operator interfaces for the hot path.
+
+Names follow the Rust types they replace:
+
+* ``Engine``                      — a dk_ctx (device, node/state pools)
+* ``McEnv``                       — McEnvState (rs-doko-mcts/src/env/env_state.rs:7-28), batched
+* ``CachedMCTS``                  — CachedMCTS::monte_carlo_tree_search (mcts.rs:284-315), batched over roots
+* ``card_matching_full``          — CAP determinization (rs-full-doko/src/matching/card_matching.rs:469-497)
+* ``PolicyFusionMaxN`` / ``PolicyFusionAverageStrategy`` — policy_fusion.rs:18-123
+* ``DefaultImpiPolicy``           — sample -> search -> fuse (compare_impi.rs:212-371)
+
+States are ``numpy.uint8`` arrays of shape (n, 128) in the dk_state wire format
+of include/doko_amd.h.  Every call runs on the GPU; errors raise DokoError
+(the Rust path panics in the same situations).
+"""
+import ctypes
+
+import numpy as np
+
+from . import _native
+
+GAME_FULL_DOKO = 0
+GAME_DOKO = 1
+GAME_TTT = 2
+FUSE_MAXN = 0
+FUSE_AVG = 1
+NUM_ACTIONS = 39
+STATE_BYTES = 128
+
+
+class DokoError(RuntimeError):
+    pass
+
+
+def _check(rc):
+    if rc != 0:
+        raise DokoError("doko_amd: %s (%d)" % (_native.lib().dk_status_string(rc).decode(), rc))
+
+
+def _ptr(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def _states(a):
+    a = np.ascontiguousarray(a, dtype=np.uint8)
+    if a.ndim != 2 or a.shape[1] != STATE_BYTES:
+        raise ValueError("states must have shape (n, 128)")
+    return a
+
+
+def splitmix_rng_states(seeds):
+    """SmallRng::seed_from_u64(seed) states (Xoshiro256++ words) for a seed array."""
+    seeds = np.asarray(seeds, dtype=np.uint64)
+    out = np.empty((seeds.shape[0], 4), dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        st = seeds.copy()
+        for i in range(4):
+            st = st + np.uint64(0x9E3779B97F4A7C15)
+            z = st.copy()
+            z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+            z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+            out[:, i] = z ^ (z >> np.uint64(31))
+    return out
+
+
+class Engine:
+    """A device context: node pools for `max_roots` searches of up to
+    `max_iterations` iterations (the reference's CachedMCTS arenas, one per root)."""
+
+    def __init__(self, device=0, max_roots=4096, max_iterations=1000, slot_capacity=0):
+        L = _native.lib()
+        cfg = _native.dk_config(device, max_roots, max_iterations, slot_capacity)
+        self._ctx = L.dk_create(ctypes.byref(cfg))
+        if not self._ctx:
+            raise DokoError("dk_create failed: no usable gfx950 device %d (or out of device memory)" % device)
+        self.max_roots = max_roots
+        self.max_iterations = max_iterations
+
+    @property
+    def ctx(self):
+        return self._ctx
+
+    def close(self):
+        if getattr(self, "_ctx", None):
+            _native.lib().dk_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def pool_bytes(self):
+        return int(_native.lib().dk_pool_bytes(self._ctx))
+
+    def last_search_ms(self):
+        ms = ctypes.c_float()
+        _check(_native.lib().dk_last_search_ms(self._ctx, ctypes.byref(ms)))
+        return float(ms.value)
+
+    # ---- game construction (FdoState::new_game / DoState::new_game)
+    def new_games(self, game, seeds):
+        seeds = np.ascontiguousarray(seeds, dtype=np.uint64)
+        out = np.zeros((seeds.shape[0], STATE_BYTES), dtype=np.uint8)
+        _check(_native.lib().dk_new_game_batch(self._ctx, game, _ptr(seeds), seeds.shape[0], _ptr(out)))
+        return out
+
+
+class McEnv:
+    """Batched McEnvState (rs-doko-mcts/src/env/env_state.rs:7-28) on the GPU."""
+
+    def __init__(self, engine):
+        self.engine = engine
+
+    def allowed_actions(self, states, first_expansion):
+        s = _states(states)
+        m = np.zeros(s.shape[0], dtype=np.uint64)
+        _check(_native.lib().dk_env_allowed_batch(self.engine.ctx, _ptr(s), s.shape[0], 1 if first_expansion else 0, _ptr(m)))
+        return m
+
+    def by_action(self, states, action_bits):
+        s = _states(states).copy()
+        a = np.ascontiguousarray(action_bits, dtype=np.uint64)
+        _check(_native.lib().dk_env_step_batch(self.engine.ctx, _ptr(s), _ptr(a), s.shape[0]))
+        return s
+
+    def rewards_or_none(self, states):
+        s = _states(states)
+        has = np.zeros(s.shape[0], dtype=np.int32)
+        r = np.zeros((s.shape[0], 4), dtype=np.float64)
+        _check(_native.lib().dk_env_rewards_batch(self.engine.ctx, _ptr(s), s.shape[0], _ptr(has), _ptr(r)))
+        return has.astype(bool), r
+
+    def random_rollout(self, states, rng_states):
+        """Returns (rewards[n,4], advanced rng states[n,4])."""
+        s = _states(states)
+        g = np.ascontiguousarray(rng_states, dtype=np.uint64).copy()
+        r = np.zeros((s.shape[0], 4), dtype=np.float64)
+        _check(_native.lib().dk_env_rollout_batch(self.engine.ctx, _ptr(s), _ptr(g), s.shape[0], _ptr(r)))
+        return r, g
+
+    def random_plies(self, states, rng_states, plies):
+        s = _states(states).copy()
+        g = np.ascontiguousarray(rng_states, dtype=np.uint64).copy()
+        k = np.ascontiguousarray(plies, dtype=np.uint32)
+        _check(_native.lib().dk_env_random_plies_batch(self.engine.ctx, _ptr(s), _ptr(g), _ptr(k), s.shape[0]))
+        return s, g
+
+
+class CachedMCTS:
+    """CachedMCTS::monte_carlo_tree_search for a batch of roots (one independent
+    search per root, SmallRng::seed_from_u64(seed) each)."""
+
+    def __init__(self, engine, game=GAME_FULL_DOKO):
+        self.engine = engine
+        self.game = game
+
+    def monte_carlo_tree_search(self, roots, uct_exploration_constant, iterations, seeds):
+        s = _states(roots)
+        n = s.shape[0]
+        seeds = np.ascontiguousarray(seeds, dtype=np.uint64)
+        visits = np.zeros((n, NUM_ACTIONS), dtype=np.uint32)
+        values = np.zeros((n, NUM_ACTIONS), dtype=np.float64)
+        best = np.zeros(n, dtype=np.uint8)
+        _check(_native.lib().dk_search_batch(self.engine.ctx, self.game, _ptr(s), _ptr(seeds), n, iterations,
+                                             float(uct_exploration_constant), _ptr(visits), _ptr(values), _ptr(best)))
+        return visits, values, best
+
+
+def card_matching_full(engine, infostates, samples, seeds):
+    """CAPSampling::sample for each infostate, `samples` times: returns
+    (n_info*samples, 128) determinized states."""
+    s = _states(infostates)
+    seeds = np.ascontiguousarray(seeds, dtype=np.uint64)
+    out = np.zeros((s.shape[0] * samples, STATE_BYTES), dtype=np.uint8)
+    _check(_native.lib().dk_determinize_batch(engine.ctx, _ptr(s), s.shape[0], samples, _ptr(seeds), _ptr(out)))
+    return out
+
+
+class _Fusion:
+    mode = None
+
+    def fuse(self, engine, visits, allowed):
+        """visits: (n_info, samples, 39); allowed: (n_info,) FdoAllowedActions bits."""
+        v = np.ascontiguousarray(visits, dtype=np.uint32)
+        n_info, samples = v.shape[0], v.shape[1]
+        a = np.ascontiguousarray(allowed, dtype=np.uint64)
+        out = np.zeros(n_info, dtype=np.uint8)
+        _check(_native.lib().dk_fuse(engine.ctx, _ptr(v), n_info, samples, _ptr(a), self.mode, _ptr(out)))
+        return out
+
+
+class PolicyFusionMaxN(_Fusion):
+    mode = FUSE_MAXN
+
+
+class PolicyFusionAverageStrategy(_Fusion):
+    mode = FUSE_AVG
+
+
+class DefaultImpiPolicy:
+    """Determinized decision: `num_samples` CAP samples -> UCT each -> fusion."""
+
+    def __init__(self, engine, uct_exploration_constant=2.5, iterations=1000, num_samples=64, fusion=FUSE_MAXN):
+        self.engine = engine
+        self.c = float(uct_exploration_constant)
+        self.iterations = iterations
+        self.num_samples = num_samples
+        self.fusion = fusion
+
+    def execute(self, infostates, seeds, return_visits=False):
+        """seeds: 2*n_info*num_samples u64 (sampling seeds, then search seeds)."""
+        s = _states(infostates)
+        n_info = s.shape[0]
+        seeds = np.ascontiguousarray(seeds, dtype=np.uint64)
+        if seeds.shape[0] != 2 * n_info * self.num_samples:
+            raise ValueError("need 2*n_info*num_samples seeds")
+        actions = np.zeros(n_info, dtype=np.uint8)
+        visits = np.zeros((n_info * self.num_samples, NUM_ACTIONS), dtype=np.uint32) if return_visits else None
+        _check(_native.lib().dk_decide_batch(self.engine.ctx, _ptr(s), n_info, self.num_samples, _ptr(seeds),
+                                             self.iterations, self.c, self.fusion, _ptr(actions),
+                                             _ptr(visits) if return_visits else None))
+        return (actions, visits) if return_visits else actions

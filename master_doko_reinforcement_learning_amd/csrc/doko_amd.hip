@@ -1,0 +1,750 @@
+// libdoko_amd.so — HIP kernels for gfx950 and the C-ABI of include/doko_amd.h.
+//
+// One lane = one determinized root (or one env state).  The UCT search keeps
+// the reference's sequential per-root semantics; all parallelism is across
+// roots.  Node pools are interleaved across roots ([slot][root]) so that the
+// lanes of a wave — which hold roots of the same infostate in the determinized
+// workload — touch the same slot indices (root children) with coalesced loads.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "../../include/doko_amd.h"
+#include "engine/adapters.h"
+#include "engine/cap_engine.h"
+#include "engine/search_core.h"
+
+namespace {
+
+constexpr int WAVE = 64;
+constexpr int MAX_PATH = 128;  // LDS path entries per lane (deeper paths fall back to parent links)
+
+#define DK_HIP(call)                                              \
+    do {                                                          \
+        hipError_t e_ = (call);                                   \
+        if (e_ != hipSuccess) {                                   \
+            fprintf(stderr, "doko_amd: %s failed: %s (%s:%d)\n", #call, hipGetErrorString(e_), __FILE__, __LINE__); \
+            return DK_E_LAUNCH;                                   \
+        }                                                         \
+    } while (0)
+
+// ---------------------------------------------------------------- node pool access
+template <class W>
+struct GpuMem {
+    uint64_t* stats;
+    dk::NodeMeta* meta;
+    W* states;
+    uint32_t* path;  // LDS, this lane's column (stride WAVE)
+    size_t R, root;
+    uint32_t cap_slots, cap_states, max_path;
+
+    __device__ size_t at(uint32_t s) const { return (size_t)s * R + root; }
+    __device__ uint64_t load_stats(uint32_t s) const {
+        return __hip_atomic_load(stats + at(s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __device__ void store_stats(uint32_t s, uint64_t v) const {
+        __hip_atomic_store(stats + at(s), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __device__ void add_stats(uint32_t s, uint64_t d) const {
+        (void)__hip_atomic_fetch_add(stats + at(s), d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __device__ dk::NodeMeta load_meta(uint32_t s) const { return meta[at(s)]; }
+    __device__ void store_meta(uint32_t s, const dk::NodeMeta& m) const { meta[at(s)] = m; }
+    __device__ void store_meta_expand(uint32_t s, uint64_t unexp, uint32_t base, uint8_t n) const {
+        dk::NodeMeta* p = meta + at(s);
+        p->unexpanded = unexp;
+        p->child_base = base;
+        p->nchild = n;
+    }
+    __device__ W load_state(uint32_t i) const { return states[(size_t)i * R + root]; }
+    __device__ void store_state(uint32_t i, const W& w) const { states[(size_t)i * R + root] = w; }
+    __device__ uint32_t path_get(int k) const { return path[k * WAVE]; }
+    __device__ void path_set(int k, uint32_t v) const { path[k * WAVE] = v; }
+};
+
+// ---------------------------------------------------------------- kernels
+template <class E>
+__global__ void __launch_bounds__(WAVE) search_kernel(const dk_state* __restrict__ roots,
+                                                      const uint64_t* __restrict__ seeds, uint32_t n,
+                                                      uint32_t iters, double c, const double* __restrict__ ln_table,
+                                                      uint64_t* stats, dk::NodeMeta* meta, typename E::Work* states,
+                                                      uint32_t cap_slots, uint32_t* visits, double* values,
+                                                      uint8_t* best, int* err) {
+    __shared__ uint32_t lds_path[MAX_PATH * WAVE];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t root = blockIdx.x * WAVE + lane;
+    if (root >= n) return;
+    typename E::Work w;
+    E::load(roots[root], w);
+    dk::Rng rng = dk::Rng::seed_from_u64(seeds[root]);
+    GpuMem<typename E::Work> mem{stats, meta, states, lds_path + lane, (size_t)n, (size_t)root,
+                                 cap_slots, iters + 1, MAX_PATH};
+    uint8_t b;
+    const int st = dk::search_root<E>(w, rng, iters, c, ln_table, mem, visits + (size_t)root * 39,
+                                      values + (size_t)root * 39, &b, nullptr);
+    if (st != dk::SR_OK) atomicOr(err, 1);
+    best[root] = b;
+}
+
+__device__ void new_game_packed(int game, uint64_t seed, dk_state& out) {
+    dk::Rng rng = dk::Rng::seed_from_u64(seed);
+    const uint32_t start = rng.range_u32(4);  // FdoPlayer::from_rng / gen_range(0..4)
+    uint8_t deck[48];
+    for (int i = 0; i < 24; ++i) { deck[2 * i] = (uint8_t)i; deck[2 * i + 1] = (uint8_t)i; }
+    dk::shuffle48(deck, rng);
+    for (int i = 0; i < DK_STATE_BYTES; ++i) out.raw[i] = 0;
+    uint64_t hands[4] = {0, 0, 0, 0};
+    for (int p = 0; p < 4; ++p)
+        for (int j = 0; j < 12; ++j) hands[p] = dk::cap::h_add(hands[p], deck[p * 12 + j]);
+    if (game == DK_GAME_FULL_DOKO) {
+        dk_fdo_state& s = out.fdo;
+        for (int p = 0; p < 4; ++p) s.hands[p] = hands[p];
+        for (int i = 0; i < 48; ++i) s.cards[i] = DK_NONE;
+        for (int i = 0; i < 4; ++i) s.res[i] = DK_NONE;
+        s.res_start = (uint8_t)start; s.current_player = (uint8_t)start;
+        s.game_type = DK_NONE; s.rr_kind = DK_NONE; s.game = DK_GAME_FULL_DOKO;
+    } else {
+        dk_do_state& s = out.dk;
+        for (int p = 0; p < 4; ++p) s.hands[p] = hands[p];
+        for (int i = 0; i < 48; ++i) s.cards[i] = DK_NONE;
+        for (int i = 0; i < 4; ++i) s.res[i] = DK_NONE;
+        s.res_start = (uint8_t)start; s.current_player = (uint8_t)start;
+        s.rr_kind = DK_NONE; s.game = DK_GAME_DOKO;
+    }
+}
+
+__global__ void new_game_kernel(int game, const uint64_t* seeds, uint32_t n, dk_state* out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    dk_state s;
+    new_game_packed(game, seeds[i], s);
+    out[i] = s;
+}
+
+__device__ uint64_t legal_of(const dk_state& s) {
+    switch (s.raw[127]) {
+        case DK_GAME_FULL_DOKO: { dk::fdo::Work w; dk::fdo::unpack(s.fdo, w); return dk::fdo::legal_actions(w); }
+        case DK_GAME_DOKO: { dk::dko::Work w; dk::dko::unpack(s.dk, w); return dk::dko::legal_actions(w); }
+        case DK_GAME_TTT: { dk::ttt::Work w; dk::ttt::unpack(s.ttt, w); return dk::ttt::env_allowed(w, true); }
+    }
+    return 0;
+}
+
+__global__ void env_allowed_kernel(const dk_state* states, uint32_t n, int first, uint64_t* masks, int* err) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const dk_state s = states[i];
+    uint64_t m = 0;
+    switch (s.raw[127]) {
+        case DK_GAME_FULL_DOKO: { dk::fdo::Work w; dk::fdo::unpack(s.fdo, w); m = dk::fdo::env_allowed(w, first != 0); break; }
+        case DK_GAME_DOKO: { dk::dko::Work w; dk::dko::unpack(s.dk, w); m = dk::dko::env_allowed(w, first != 0); break; }
+        case DK_GAME_TTT: { dk::ttt::Work w; dk::ttt::unpack(s.ttt, w); m = dk::ttt::env_allowed(w, first != 0); break; }
+        default: atomicOr(err, 2);
+    }
+    masks[i] = m;
+}
+
+__global__ void legal_kernel(const dk_state* states, uint32_t n, uint64_t* masks) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    masks[i] = legal_of(states[i]);
+}
+
+__global__ void env_step_kernel(dk_state* states, const uint64_t* actions, uint32_t n, int* err) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    dk_state s = states[i];
+    const uint64_t a = actions[i];
+    if (__builtin_popcountll(a) != 1 || !(legal_of(s) & a)) { atomicOr(err, 2); return; }
+    const int ai = __builtin_ctzll(a);
+    switch (s.raw[127]) {
+        case DK_GAME_FULL_DOKO: dk::FdoE::step_packed(s, ai); break;
+        case DK_GAME_DOKO: dk::DoE::step_packed(s, ai); break;
+        case DK_GAME_TTT: dk::TttE::step_packed(s, ai); break;
+    }
+    states[i] = s;
+}
+
+__global__ void env_rewards_kernel(const dk_state* states, uint32_t n, int32_t* has, double* rewards) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const dk_state s = states[i];
+    int r[4] = {0, 0, 0, 0};
+    bool fin = false;
+    switch (s.raw[127]) {
+        case DK_GAME_FULL_DOKO: { dk::fdo::Work w; dk::fdo::unpack(s.fdo, w); fin = dk::fdo::is_terminal(w); if (fin) dk::fdo::score(w, r); break; }
+        case DK_GAME_DOKO: { dk::dko::Work w; dk::dko::unpack(s.dk, w); fin = dk::dko::is_terminal(w); if (fin) dk::dko::score(w, r); break; }
+        case DK_GAME_TTT: { dk::ttt::Work w; dk::ttt::unpack(s.ttt, w); fin = dk::ttt::is_terminal(w); if (fin) dk::ttt::score(w, r); break; }
+    }
+    has[i] = fin ? 1 : 0;
+    for (int p = 0; p < 4; ++p) rewards[4 * (size_t)i + p] = fin ? (double)r[p] : 0.0;
+}
+
+template <class E>
+__device__ void rollout_one(const dk_state& s, dk::Rng& rng, double* out) {
+    typename E::Work w;
+    E::load(s, w);
+    int r[4];
+    E::rollout(w, rng, r);
+    for (int p = 0; p < 4; ++p) out[p] = (double)r[p];
+}
+
+__global__ void __launch_bounds__(WAVE) env_rollout_kernel(const dk_state* states, uint64_t* rng_states, uint32_t n,
+                                                           double* rewards) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const dk_state s = states[i];
+    dk::Rng rng{rng_states[4 * (size_t)i], rng_states[4 * (size_t)i + 1], rng_states[4 * (size_t)i + 2], rng_states[4 * (size_t)i + 3]};
+    double out[4] = {0, 0, 0, 0};
+    switch (s.raw[127]) {
+        case DK_GAME_FULL_DOKO: rollout_one<dk::FdoE>(s, rng, out); break;
+        case DK_GAME_DOKO: rollout_one<dk::DoE>(s, rng, out); break;
+        case DK_GAME_TTT: rollout_one<dk::TttE>(s, rng, out); break;
+    }
+    for (int p = 0; p < 4; ++p) rewards[4 * (size_t)i + p] = out[p];
+    rng_states[4 * (size_t)i] = rng.s0; rng_states[4 * (size_t)i + 1] = rng.s1;
+    rng_states[4 * (size_t)i + 2] = rng.s2; rng_states[4 * (size_t)i + 3] = rng.s3;
+}
+
+// random_action_for_current_player_no_announcement (full doko) /
+// random_action_for_current_player (rs-doko, tic-tac-toe), k times, on the wire format.
+__global__ void random_plies_kernel(dk_state* states, uint64_t* rng_states, const uint32_t* plies, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    dk_state s = states[i];
+    dk::Rng rng{rng_states[4 * (size_t)i], rng_states[4 * (size_t)i + 1], rng_states[4 * (size_t)i + 2], rng_states[4 * (size_t)i + 3]};
+    for (uint32_t k = 0; k < plies[i]; ++k) {
+        uint64_t a = legal_of(s);
+        if (s.raw[127] == DK_GAME_FULL_DOKO) {
+            if (s.fdo.phase == dk::fdo::PH_FINISHED) break;
+            a &= ~dk::fdo::ANN_ACTIONS;
+        } else if (s.raw[127] == DK_GAME_DOKO) {
+            if (s.dk.phase == dk::dko::PH_FINISHED) break;
+        }
+        if (a == 0) break;
+        const int ai = dk::ctz64(dk::random_single(a, rng));
+        switch (s.raw[127]) {
+            case DK_GAME_FULL_DOKO: dk::FdoE::step_packed(s, ai); break;
+            case DK_GAME_DOKO: dk::DoE::step_packed(s, ai); break;
+            default: dk::TttE::step_packed(s, ai); break;
+        }
+    }
+    states[i] = s;
+    rng_states[4 * (size_t)i] = rng.s0; rng_states[4 * (size_t)i + 1] = rng.s1;
+    rng_states[4 * (size_t)i + 2] = rng.s2; rng_states[4 * (size_t)i + 3] = rng.s3;
+}
+
+__global__ void __launch_bounds__(WAVE) determinize_kernel(const dk_state* info, uint32_t n_info, uint32_t samples,
+                                                           const uint64_t* seeds, dk_state* out, int* err) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_info * samples) return;
+    const dk_state s = info[i / samples];
+    dk_state o;
+    if (s.raw[127] != DK_GAME_FULL_DOKO || s.fdo.current_player == DK_NONE) {
+        atomicOr(err, 2);
+        o = s;
+    } else {
+        dk::Rng rng = dk::Rng::seed_from_u64(seeds[i]);
+        dk::cap::card_matching_full(s.fdo, rng, o.fdo);
+    }
+    out[i] = o;
+}
+
+// PolicyFusionMaxN / PolicyFusionAverageStrategy accumulators (policy_fusion.rs:23-123).
+// One thread per (infostate, action).
+__global__ void fuse_accumulate_kernel(const uint32_t* visits, uint32_t n_info, uint32_t samples,
+                                       const uint64_t* allowed, int mode, uint32_t* acc_u32, float* acc_f32) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n_info * 39) return;
+    const uint32_t info = t / 39, a = t % 39;
+    const uint64_t al = allowed[info];
+    if (mode == DK_FUSE_MAXN) {
+        if (!((al >> a) & 1)) { acc_u32[t] = 0u; return; }   // masked to UINT32_MAX in select (summable across ranks)
+        uint32_t cum = 0;
+        for (uint32_t s = 0; s < samples; ++s) {
+            const uint32_t* row = visits + ((size_t)info * samples + s) * 39;
+            const uint32_t va = row[a];
+            uint32_t rank = 1;
+            for (uint32_t b = 0; b < 39; ++b) {
+                if (!((al >> b) & 1)) continue;
+                const uint32_t vb = row[b];
+                rank += (vb > va || (vb == va && b < a)) ? 1u : 0u;   // stable sort by Reverse(visits)
+            }
+            cum += rank;
+        }
+        acc_u32[t] = cum;
+    } else {
+        float sum = 0.0f;
+        for (uint32_t s = 0; s < samples; ++s) {
+            const uint32_t* row = visits + ((size_t)info * samples + s) * 39;
+            uint64_t total = 0;
+            for (uint32_t b = 0; b < 39; ++b) total += row[b];
+            sum += (float)row[a] / (float)total;
+        }
+        acc_f32[t] = sum;
+    }
+}
+
+__global__ void fuse_select_kernel(uint32_t n_info, int mode, const uint64_t* allowed, const uint32_t* acc_u32,
+                                   const float* acc_f32, uint8_t* action) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_info) return;
+    int best = 0;
+    if (mode == DK_FUSE_MAXN) {
+        const uint32_t* r = acc_u32 + (size_t)i * 39;
+        const uint64_t al = allowed[i];
+        uint32_t bk = (al & 1) ? r[0] : 0xFFFFFFFFu;   // disallowed actions rank u32::MAX (policy_fusion.rs:33-39)
+        for (int a = 1; a < 39; ++a) {
+            const uint32_t k = ((al >> a) & 1) ? r[a] : 0xFFFFFFFFu;
+            if (k < bk) { bk = k; best = a; }                          // min_by_key: first minimum
+        }
+    } else {
+        const float* p = acc_f32 + (size_t)i * 39;
+        for (int a = 1; a < 39; ++a) if (!(p[best] > p[a])) best = a;     // max_by: last maximum
+    }
+    action[i] = (uint8_t)best;
+}
+
+}  // namespace
+
+// ==================================================================== host side
+struct dk_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    uint32_t max_roots = 0, max_iters = 0, cap_slots = 0;
+    uint64_t* stats = nullptr;
+    dk::NodeMeta* meta = nullptr;
+    void* states = nullptr;
+    double* ln_table = nullptr;
+    int* err = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool timed = false;
+    int last_error = DK_OK;
+    uint64_t pool_bytes = 0;
+    std::vector<void*> scratch;
+    std::vector<size_t> scratch_size;
+    std::mutex mu;
+};
+
+namespace {
+
+constexpr size_t STATE_SLOT_BYTES =
+    sizeof(dk::fdo::Work) > sizeof(dk::dko::Work) ? sizeof(dk::fdo::Work) : sizeof(dk::dko::Work);
+
+unsigned grid_for(size_t n, unsigned block) { return (unsigned)((n + block - 1) / block); }
+
+hipStream_t pick(dk_ctx* ctx, void* s) { return s ? (hipStream_t)s : ctx->stream; }
+
+// scratch buffer k of at least `bytes` (host-pointer convenience API only)
+void* scratch(dk_ctx* ctx, int k, size_t bytes) {
+    if ((int)ctx->scratch.size() <= k) { ctx->scratch.resize(k + 1, nullptr); ctx->scratch_size.resize(k + 1, 0); }
+    if (ctx->scratch_size[k] < bytes) {
+        if (ctx->scratch[k]) (void)hipFree(ctx->scratch[k]);
+        ctx->scratch[k] = nullptr;
+        if (hipMalloc(&ctx->scratch[k], bytes) != hipSuccess) { ctx->scratch_size[k] = 0; return nullptr; }
+        ctx->scratch_size[k] = bytes;
+    }
+    return ctx->scratch[k];
+}
+
+int finish(dk_ctx* ctx, hipStream_t st) {
+    if (hipStreamSynchronize(st) != hipSuccess) return ctx->last_error = DK_E_LAUNCH;
+    int flag = 0;
+    if (hipMemcpy(&flag, ctx->err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return ctx->last_error = DK_E_LAUNCH;
+    (void)hipMemset(ctx->err, 0, sizeof(int));
+    if (flag & 1) return ctx->last_error = DK_E_CAPACITY;
+    if (flag & 2) return ctx->last_error = DK_E_STATE;
+    return ctx->last_error = DK_OK;
+}
+
+template <class E>
+hipError_t launch_search(dk_ctx* ctx, const dk_state* roots, const uint64_t* seeds, uint32_t n, uint32_t iters,
+                         double c, uint32_t* visits, double* values, uint8_t* best, hipStream_t st) {
+    hipLaunchKernelGGL(search_kernel<E>, dim3(grid_for(n, WAVE)), dim3(WAVE), 0, st, roots, seeds, n, iters, c,
+                       ctx->ln_table, ctx->stats, ctx->meta, (typename E::Work*)ctx->states, ctx->cap_slots, visits,
+                       values, best, ctx->err);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" {
+
+int dk_abi_version(void) { return DK_ABI_VERSION; }
+
+const char* dk_status_string(int s) {
+    switch (s) {
+        case DK_OK: return "ok";
+        case DK_E_INVALID: return "invalid argument";
+        case DK_E_CAPACITY: return "capacity exceeded";
+        case DK_E_STATE: return "illegal action or malformed state";
+        case DK_E_NO_DEVICE: return "no usable gfx950 device";
+        case DK_E_LAUNCH: return "kernel launch failure";
+    }
+    return "unknown";
+}
+
+dk_ctx* dk_create(const dk_config* cfg) {
+    if (!cfg || cfg->max_roots == 0 || cfg->max_iterations == 0) return nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || cfg->device < 0 || cfg->device >= count) return nullptr;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, cfg->device) != hipSuccess) return nullptr;
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        fprintf(stderr, "doko_amd: device %d is %s, this library is built for gfx950 only\n", cfg->device, prop.gcnArchName);
+        return nullptr;
+    }
+    if (hipSetDevice(cfg->device) != hipSuccess) return nullptr;
+    dk_ctx* ctx = new dk_ctx();
+    ctx->device = cfg->device;
+    ctx->max_roots = cfg->max_roots;
+    ctx->max_iters = cfg->max_iterations;
+    // Proven bound: the root block (<= 39) plus one block of <= 12 children per
+    // iteration (non-root nodes offer at most 12 cards / 9 reservations / 1 pass).
+    ctx->cap_slots = cfg->slot_capacity ? cfg->slot_capacity : 40u + 12u * cfg->max_iterations;
+    const size_t R = cfg->max_roots, S = ctx->cap_slots, T = (size_t)cfg->max_iterations + 1;
+    bool ok = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) == hipSuccess;
+    ok = ok && hipMalloc(&ctx->stats, R * S * sizeof(uint64_t)) == hipSuccess;
+    ok = ok && hipMalloc(&ctx->meta, R * S * sizeof(dk::NodeMeta)) == hipSuccess;
+    ok = ok && hipMalloc(&ctx->states, R * T * STATE_SLOT_BYTES) == hipSuccess;
+    ok = ok && hipMalloc(&ctx->ln_table, (T + 1) * sizeof(double)) == hipSuccess;
+    ok = ok && hipMalloc(&ctx->err, sizeof(int)) == hipSuccess;
+    ok = ok && hipEventCreate(&ctx->ev0) == hipSuccess && hipEventCreate(&ctx->ev1) == hipSuccess;
+    if (ok) {
+        // ln(N) exactly as glibc `log` computes it — what Rust's f64::ln calls (node.rs:253).
+        std::vector<double> ln(T + 1);
+        for (size_t i = 0; i < ln.size(); ++i) ln[i] = std::log((double)i);
+        ok = hipMemcpy(ctx->ln_table, ln.data(), ln.size() * sizeof(double), hipMemcpyHostToDevice) == hipSuccess;
+        ok = ok && hipMemset(ctx->err, 0, sizeof(int)) == hipSuccess;
+    }
+    ctx->pool_bytes = R * S * (sizeof(uint64_t) + sizeof(dk::NodeMeta)) + R * T * STATE_SLOT_BYTES;
+    if (!ok) { dk_destroy(ctx); return nullptr; }
+    return ctx;
+}
+
+void dk_destroy(dk_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    for (void* p : ctx->scratch) if (p) (void)hipFree(p);
+    if (ctx->stats) (void)hipFree(ctx->stats);
+    if (ctx->meta) (void)hipFree(ctx->meta);
+    if (ctx->states) (void)hipFree(ctx->states);
+    if (ctx->ln_table) (void)hipFree(ctx->ln_table);
+    if (ctx->err) (void)hipFree(ctx->err);
+    if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
+    if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+int dk_last_error(const dk_ctx* ctx) { return ctx ? ctx->last_error : DK_E_INVALID; }
+uint64_t dk_pool_bytes(const dk_ctx* ctx) { return ctx ? ctx->pool_bytes : 0; }
+
+int dk_sync(dk_ctx* ctx, void* stream) {
+    if (!ctx) return DK_E_INVALID;
+    return finish(ctx, pick(ctx, stream));
+}
+
+int dk_last_search_ms(dk_ctx* ctx, float* ms) {
+    if (!ctx || !ms || !ctx->timed) return DK_E_INVALID;
+    DK_HIP(hipEventSynchronize(ctx->ev1));
+    DK_HIP(hipEventElapsedTime(ms, ctx->ev0, ctx->ev1));
+    return DK_OK;
+}
+
+// ---------------------------------------------------------------- new games
+int dk_new_game_batch_async(dk_ctx* ctx, int game, const uint64_t* d_seeds, uint32_t n, dk_state* d_out, void* stream) {
+    if (!ctx || (game != DK_GAME_FULL_DOKO && game != DK_GAME_DOKO)) return DK_E_INVALID;
+    if (n == 0) return DK_OK;
+    hipLaunchKernelGGL(new_game_kernel, dim3(grid_for(n, 64)), dim3(64), 0, pick(ctx, stream), game, d_seeds, n, d_out);
+    DK_HIP(hipGetLastError());
+    return DK_OK;
+}
+
+int dk_new_game_batch(dk_ctx* ctx, int game, const uint64_t* seeds, uint32_t n, dk_state* out) {
+    if (!ctx || !seeds || !out) return DK_E_INVALID;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    if (n == 0) return DK_OK;
+    uint64_t* d_seeds = (uint64_t*)scratch(ctx, 0, n * sizeof(uint64_t));
+    dk_state* d_out = (dk_state*)scratch(ctx, 1, n * sizeof(dk_state));
+    if (!d_seeds || !d_out) return DK_E_CAPACITY;
+    DK_HIP(hipMemcpyAsync(d_seeds, seeds, n * sizeof(uint64_t), hipMemcpyHostToDevice, ctx->stream));
+    int rc = dk_new_game_batch_async(ctx, game, d_seeds, n, d_out, ctx->stream);
+    if (rc) return rc;
+    DK_HIP(hipMemcpyAsync(out, d_out, n * sizeof(dk_state), hipMemcpyDeviceToHost, ctx->stream));
+    return finish(ctx, ctx->stream);
+}
+
+// ---------------------------------------------------------------- env
+int dk_env_allowed_batch(dk_ctx* ctx, const dk_state* states, uint32_t n, int first_expansion, uint64_t* masks) {
+    if (!ctx || !states || !masks) return DK_E_INVALID;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    if (n == 0) return DK_OK;
+    dk_state* d_s = (dk_state*)scratch(ctx, 0, n * sizeof(dk_state));
+    uint64_t* d_m = (uint64_t*)scratch(ctx, 1, n * sizeof(uint64_t));
+    if (!d_s || !d_m) return DK_E_CAPACITY;
+    DK_HIP(hipMemcpyAsync(d_s, states, n * sizeof(dk_state), hipMemcpyHostToDevice, ctx->stream));
+    hipLaunchKernelGGL(env_allowed_kernel, dim3(grid_for(n, 64)), dim3(64), 0, ctx->stream, d_s, n, first_expansion, d_m, ctx->err);
+    DK_HIP(hipGetLastError());
+    DK_HIP(hipMemcpyAsync(masks, d_m, n * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream));
+    return finish(ctx, ctx->stream);
+}
+
+int dk_env_step_batch(dk_ctx* ctx, dk_state* states, const uint64_t* action_bits, uint32_t n) {
+    if (!ctx || !states || !action_bits) return DK_E_INVALID;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    if (n == 0) return DK_OK;
+    dk_state* d_s = (dk_state*)scratch(ctx, 0, n * sizeof(dk_state));
+    uint64_t* d_a = (uint64_t*)scratch(ctx, 1, n * sizeof(uint64_t));
+    if (!d_s || !d_a) return DK_E_CAPACITY;
+    DK_HIP(hipMemcpyAsync(d_s, states, n * sizeof(dk_state), hipMemcpyHostToDevice, ctx->stream));
+    DK_HIP(hipMemcpyAsync(d_a, action_bits, n * sizeof(uint64_t), hipMemcpyHostToDevice, ctx->stream));
+    hipLaunchKernelGGL(env_step_kernel, dim3(grid_for(n, 64)), dim3(64), 0, ctx->stream, d_s, d_a, n, ctx->err);
+    DK_HIP(hipGetLastError());
+    DK_HIP(hipMemcpyAsync(states, d_s, n * sizeof(dk_state), hipMemcpyDeviceToHost, ctx->stream));
+    return finish(ctx, ctx->stream);
+}
+
+int dk_env_rewards_batch(dk_ctx* ctx, const dk_state* states, uint32_t n, int32_t* has_rewards, double* rewards) {
+    if (!ctx || !states || !has_rewards || !rewards) return DK_E_INVALID;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    if (n == 0) return DK_OK;
+    dk_state* d_s = (dk_state*)scratch(ctx, 0, n * sizeof(dk_state));
+    int32_t* d_h = (int32_t*)scratch(ctx, 1, n * sizeof(int32_t));
+    double* d_r = (double*)scratch(ctx, 2, 4 * n * sizeof(double));
+    if (!d_s || !d_h || !d_r) return DK_E_CAPACITY;
+    DK_HIP(hipMemcpyAsync(d_s, states, n * sizeof(dk_state), hipMemcpyHostToDevice, ctx->stream));
+    hipLaunchKernelGGL(env_rewards_kernel, dim3(grid_for(n, 64)), dim3(64), 0, ctx->stream, d_s, n, d_h, d_r);
+    DK_HIP(hipGetLastError());
+    DK_HIP(hipMemcpyAsync(has_rewards, d_h, n * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+    DK_HIP(hipMemcpyAsync(rewards, d_r, 4 * n * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    return finish(ctx, ctx->stream);
+}
+
+int dk_env_rollout_batch_async(dk_ctx* ctx, const dk_state* d_states, uint64_t* d_rng, uint32_t n, double* d_rewards, void* stream) {
+    if (!ctx) return DK_E_INVALID;
+    if (n == 0) return DK_OK;
+    hipLaunchKernelGGL(env_rollout_kernel, dim3(grid_for(n, WAVE)), dim3(WAVE), 0, pick(ctx, stream), d_states, d_rng, n, d_rewards);
+    DK_HIP(hipGetLastError());
+    return DK_OK;
+}
+
+int dk_env_rollout_batch(dk_ctx* ctx, const dk_state* states, uint64_t* rng_states, uint32_t n, double* rewards) {
+    if (!ctx || !states || !rng_states || !rewards) return DK_E_INVALID;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    if (n == 0) return DK_OK;
+    dk_state* d_s = (dk_state*)scratch(ctx, 0, n * sizeof(dk_state));
+    uint64_t* d_g = (uint64_t*)scratch(ctx, 1, 4 * n * sizeof(uint64_t));
+    double* d_r = (double*)scratch(ctx, 2, 4 * n * sizeof(double));
+    if (!d_s || !d_g || !d_r) return DK_E_CAPACITY;
+    DK_HIP(hipMemcpyAsync(d_s, states, n * sizeof(dk_state), hipMemcpyHostToDevice, ctx->stream));
+    DK_HIP(hipMemcpyAsync(d_g, rng_states, 4 * n * sizeof(uint64_t), hipMemcpyHostToDevice, ctx->stream));
+    int rc = dk_env_rollout_batch_async(ctx, d_s, d_g, n, d_r, ctx->stream);
+    if (rc) return rc;
+    DK_HIP(hipMemcpyAsync(rewards, d_r, 4 * n * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    DK_HIP(hipMemcpyAsync(rng_states, d_g, 4 * n * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream));
+    return finish(ctx, ctx->stream);
+}
+
+int dk_env_random_plies_batch(dk_ctx* ctx, dk_state* states, uint64_t* rng_states, const uint32_t* plies, uint32_t n) {
+    if (!ctx || !states || !rng_states || !plies) return DK_E_INVALID;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    if (n == 0) return DK_OK;
+    dk_state* d_s = (dk_state*)scratch(ctx, 0, n * sizeof(dk_state));
+    uint64_t* d_g = (uint64_t*)scratch(ctx, 1, 4 * n * sizeof(uint64_t));
+    uint32_t* d_p = (uint32_t*)scratch(ctx, 2, n * sizeof(uint32_t));
+    if (!d_s || !d_g || !d_p) return DK_E_CAPACITY;
+    DK_HIP(hipMemcpyAsync(d_s, states, n * sizeof(dk_state), hipMemcpyHostToDevice, ctx->stream));
+    DK_HIP(hipMemcpyAsync(d_g, rng_states, 4 * n * sizeof(uint64_t), hipMemcpyHostToDevice, ctx->stream));
+    DK_HIP(hipMemcpyAsync(d_p, plies, n * sizeof(uint32_t), hipMemcpyHostToDevice, ctx->stream));
+    hipLaunchKernelGGL(random_plies_kernel, dim3(grid_for(n, 64)), dim3(64), 0, ctx->stream, d_s, d_g, d_p, n);
+    DK_HIP(hipGetLastError());
+    DK_HIP(hipMemcpyAsync(states, d_s, n * sizeof(dk_state), hipMemcpyDeviceToHost, ctx->stream));
+    DK_HIP(hipMemcpyAsync(rng_states, d_g, 4 * n * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream));
+    return finish(ctx, ctx->stream);
+}
+
+// ---------------------------------------------------------------- search
+int dk_search_batch_async(dk_ctx* ctx, int game, const dk_state* d_roots, const uint64_t* d_seeds, uint32_t n,
+                          uint32_t iterations, double c, uint32_t* d_visits, double* d_values, uint8_t* d_best,
+                          void* stream) {
+    if (!ctx) return DK_E_INVALID;
+    if (n > ctx->max_roots || iterations > ctx->max_iters) return ctx->last_error = DK_E_CAPACITY;
+    if (n == 0 || iterations == 0) return DK_E_INVALID;
+    hipStream_t st = pick(ctx, stream);
+    DK_HIP(hipEventRecord(ctx->ev0, st));
+    hipError_t e;
+    switch (game) {
+        case DK_GAME_FULL_DOKO: e = launch_search<dk::FdoE>(ctx, d_roots, d_seeds, n, iterations, c, d_visits, d_values, d_best, st); break;
+        case DK_GAME_DOKO: e = launch_search<dk::DoE>(ctx, d_roots, d_seeds, n, iterations, c, d_visits, d_values, d_best, st); break;
+        case DK_GAME_TTT: e = launch_search<dk::TttE>(ctx, d_roots, d_seeds, n, iterations, c, d_visits, d_values, d_best, st); break;
+        default: return DK_E_INVALID;
+    }
+    if (e != hipSuccess) { fprintf(stderr, "doko_amd: search launch: %s\n", hipGetErrorString(e)); return DK_E_LAUNCH; }
+    DK_HIP(hipEventRecord(ctx->ev1, st));
+    ctx->timed = true;
+    return DK_OK;
+}
+
+int dk_search_batch(dk_ctx* ctx, int game, const dk_state* roots, const uint64_t* seeds, uint32_t n, uint32_t iterations,
+                    double c, uint32_t* visits, double* values, uint8_t* best) {
+    if (!ctx || !roots || !seeds || !visits || !values || !best) return DK_E_INVALID;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    if (n > ctx->max_roots || iterations > ctx->max_iters) return ctx->last_error = DK_E_CAPACITY;
+    dk_state* d_r = (dk_state*)scratch(ctx, 0, n * sizeof(dk_state));
+    uint64_t* d_s = (uint64_t*)scratch(ctx, 1, n * sizeof(uint64_t));
+    uint32_t* d_v = (uint32_t*)scratch(ctx, 2, (size_t)n * 39 * sizeof(uint32_t));
+    double* d_val = (double*)scratch(ctx, 3, (size_t)n * 39 * sizeof(double));
+    uint8_t* d_b = (uint8_t*)scratch(ctx, 4, n);
+    if (!d_r || !d_s || !d_v || !d_val || !d_b) return DK_E_CAPACITY;
+    DK_HIP(hipMemcpyAsync(d_r, roots, n * sizeof(dk_state), hipMemcpyHostToDevice, ctx->stream));
+    DK_HIP(hipMemcpyAsync(d_s, seeds, n * sizeof(uint64_t), hipMemcpyHostToDevice, ctx->stream));
+    int rc = dk_search_batch_async(ctx, game, d_r, d_s, n, iterations, c, d_v, d_val, d_b, ctx->stream);
+    if (rc) return rc;
+    DK_HIP(hipMemcpyAsync(visits, d_v, (size_t)n * 39 * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+    DK_HIP(hipMemcpyAsync(values, d_val, (size_t)n * 39 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    DK_HIP(hipMemcpyAsync(best, d_b, n, hipMemcpyDeviceToHost, ctx->stream));
+    return finish(ctx, ctx->stream);
+}
+
+// ---------------------------------------------------------------- determinization
+int dk_determinize_batch_async(dk_ctx* ctx, const dk_state* d_info, uint32_t n_info, uint32_t samples,
+                               const uint64_t* d_seeds, dk_state* d_out, void* stream) {
+    if (!ctx) return DK_E_INVALID;
+    const size_t n = (size_t)n_info * samples;
+    if (n == 0) return DK_OK;
+    hipLaunchKernelGGL(determinize_kernel, dim3(grid_for(n, WAVE)), dim3(WAVE), 0, pick(ctx, stream), d_info, n_info,
+                       samples, d_seeds, d_out, ctx->err);
+    DK_HIP(hipGetLastError());
+    return DK_OK;
+}
+
+int dk_determinize_batch(dk_ctx* ctx, const dk_state* infostates, uint32_t n_info, uint32_t samples,
+                         const uint64_t* seeds, dk_state* out) {
+    if (!ctx || !infostates || !seeds || !out) return DK_E_INVALID;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    const size_t n = (size_t)n_info * samples;
+    if (n == 0) return DK_OK;
+    dk_state* d_i = (dk_state*)scratch(ctx, 0, n_info * sizeof(dk_state));
+    uint64_t* d_s = (uint64_t*)scratch(ctx, 1, n * sizeof(uint64_t));
+    dk_state* d_o = (dk_state*)scratch(ctx, 2, n * sizeof(dk_state));
+    if (!d_i || !d_s || !d_o) return DK_E_CAPACITY;
+    DK_HIP(hipMemcpyAsync(d_i, infostates, n_info * sizeof(dk_state), hipMemcpyHostToDevice, ctx->stream));
+    DK_HIP(hipMemcpyAsync(d_s, seeds, n * sizeof(uint64_t), hipMemcpyHostToDevice, ctx->stream));
+    int rc = dk_determinize_batch_async(ctx, d_i, n_info, samples, d_s, d_o, ctx->stream);
+    if (rc) return rc;
+    DK_HIP(hipMemcpyAsync(out, d_o, n * sizeof(dk_state), hipMemcpyDeviceToHost, ctx->stream));
+    return finish(ctx, ctx->stream);
+}
+
+// ---------------------------------------------------------------- fusion
+int dk_fuse_accumulate_async(dk_ctx* ctx, const uint32_t* d_visits, uint32_t n_info, uint32_t samples,
+                             const uint64_t* d_allowed, int mode, uint32_t* d_acc_u32, float* d_acc_f32, void* stream) {
+    if (!ctx || (mode != DK_FUSE_MAXN && mode != DK_FUSE_AVG)) return DK_E_INVALID;
+    if (n_info == 0) return DK_OK;
+    hipLaunchKernelGGL(fuse_accumulate_kernel, dim3(grid_for((size_t)n_info * 39, 64)), dim3(64), 0, pick(ctx, stream),
+                       d_visits, n_info, samples, d_allowed, mode, d_acc_u32, d_acc_f32);
+    DK_HIP(hipGetLastError());
+    return DK_OK;
+}
+
+int dk_fuse_select_async(dk_ctx* ctx, uint32_t n_info, int mode, const uint64_t* d_allowed, const uint32_t* d_acc_u32,
+                         const float* d_acc_f32, uint8_t* d_action, void* stream) {
+    if (!ctx || (mode != DK_FUSE_MAXN && mode != DK_FUSE_AVG)) return DK_E_INVALID;
+    if (n_info == 0) return DK_OK;
+    hipLaunchKernelGGL(fuse_select_kernel, dim3(grid_for(n_info, 64)), dim3(64), 0, pick(ctx, stream), n_info, mode,
+                       d_allowed, d_acc_u32, d_acc_f32, d_action);
+    DK_HIP(hipGetLastError());
+    return DK_OK;
+}
+
+int dk_fuse(dk_ctx* ctx, const uint32_t* visits, uint32_t n_info, uint32_t samples, const uint64_t* allowed, int mode,
+            uint8_t* action) {
+    if (!ctx || !visits || !allowed || !action) return DK_E_INVALID;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    if (n_info == 0) return DK_OK;
+    const size_t nv = (size_t)n_info * samples * 39;
+    uint32_t* d_v = (uint32_t*)scratch(ctx, 0, nv * sizeof(uint32_t));
+    uint64_t* d_a = (uint64_t*)scratch(ctx, 1, n_info * sizeof(uint64_t));
+    uint32_t* d_u = (uint32_t*)scratch(ctx, 2, (size_t)n_info * 39 * sizeof(uint32_t));
+    float* d_f = (float*)scratch(ctx, 3, (size_t)n_info * 39 * sizeof(float));
+    uint8_t* d_out = (uint8_t*)scratch(ctx, 4, n_info);
+    if (!d_v || !d_a || !d_u || !d_f || !d_out) return DK_E_CAPACITY;
+    DK_HIP(hipMemcpyAsync(d_v, visits, nv * sizeof(uint32_t), hipMemcpyHostToDevice, ctx->stream));
+    DK_HIP(hipMemcpyAsync(d_a, allowed, n_info * sizeof(uint64_t), hipMemcpyHostToDevice, ctx->stream));
+    int rc = dk_fuse_accumulate_async(ctx, d_v, n_info, samples, d_a, mode, d_u, d_f, ctx->stream);
+    if (rc) return rc;
+    rc = dk_fuse_select_async(ctx, n_info, mode, d_a, d_u, d_f, d_out, ctx->stream);
+    if (rc) return rc;
+    DK_HIP(hipMemcpyAsync(action, d_out, n_info, hipMemcpyDeviceToHost, ctx->stream));
+    return finish(ctx, ctx->stream);
+}
+
+int dk_legal_actions_async(dk_ctx* ctx, const dk_state* d_states, uint32_t n, uint64_t* d_masks, void* stream) {
+    if (!ctx) return DK_E_INVALID;
+    if (n == 0) return DK_OK;
+    hipLaunchKernelGGL(legal_kernel, dim3(grid_for(n, 64)), dim3(64), 0, pick(ctx, stream), d_states, n, d_masks);
+    DK_HIP(hipGetLastError());
+    return DK_OK;
+}
+
+int dk_env_step_batch_async(dk_ctx* ctx, dk_state* d_states, const uint64_t* d_actions, uint32_t n, void* stream) {
+    if (!ctx) return DK_E_INVALID;
+    if (n == 0) return DK_OK;
+    hipLaunchKernelGGL(env_step_kernel, dim3(grid_for(n, 64)), dim3(64), 0, pick(ctx, stream), d_states, d_actions, n, ctx->err);
+    DK_HIP(hipGetLastError());
+    return DK_OK;
+}
+
+int dk_env_random_plies_batch_async(dk_ctx* ctx, dk_state* d_states, uint64_t* d_rng, const uint32_t* d_plies, uint32_t n,
+                                    void* stream) {
+    if (!ctx) return DK_E_INVALID;
+    if (n == 0) return DK_OK;
+    hipLaunchKernelGGL(random_plies_kernel, dim3(grid_for(n, 64)), dim3(64), 0, pick(ctx, stream), d_states, d_rng, d_plies, n);
+    DK_HIP(hipGetLastError());
+    return DK_OK;
+}
+
+// ---------------------------------------------------------------- end-to-end decision
+int dk_decide_batch(dk_ctx* ctx, const dk_state* infostates, uint32_t n_info, uint32_t samples, const uint64_t* seeds,
+                    uint32_t iterations, double c, int fuse_mode, uint8_t* actions, uint32_t* visits) {
+    if (!ctx || !infostates || !seeds || !actions) return DK_E_INVALID;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    const size_t n = (size_t)n_info * samples;
+    if (n == 0) return DK_OK;
+    if (n > ctx->max_roots || iterations > ctx->max_iters) return ctx->last_error = DK_E_CAPACITY;
+    dk_state* d_i = (dk_state*)scratch(ctx, 0, n_info * sizeof(dk_state));
+    uint64_t* d_seeds = (uint64_t*)scratch(ctx, 1, 2 * n * sizeof(uint64_t));
+    dk_state* d_roots = (dk_state*)scratch(ctx, 2, n * sizeof(dk_state));
+    uint32_t* d_v = (uint32_t*)scratch(ctx, 3, n * 39 * sizeof(uint32_t));
+    double* d_val = (double*)scratch(ctx, 4, n * 39 * sizeof(double));
+    uint8_t* d_b = (uint8_t*)scratch(ctx, 5, n + n_info);
+    uint64_t* d_allowed = (uint64_t*)scratch(ctx, 6, n_info * sizeof(uint64_t));
+    uint32_t* d_u = (uint32_t*)scratch(ctx, 7, (size_t)n_info * 39 * sizeof(uint32_t));
+    float* d_f = (float*)scratch(ctx, 8, (size_t)n_info * 39 * sizeof(float));
+    if (!d_i || !d_seeds || !d_roots || !d_v || !d_val || !d_b || !d_allowed || !d_u || !d_f) return DK_E_CAPACITY;
+    // seeds: [n] sampling seeds followed by [n] search seeds
+    DK_HIP(hipMemcpyAsync(d_i, infostates, n_info * sizeof(dk_state), hipMemcpyHostToDevice, ctx->stream));
+    DK_HIP(hipMemcpyAsync(d_seeds, seeds, 2 * n * sizeof(uint64_t), hipMemcpyHostToDevice, ctx->stream));
+    int rc = dk_determinize_batch_async(ctx, d_i, n_info, samples, d_seeds, d_roots, ctx->stream);
+    if (rc) return rc;
+    rc = dk_search_batch_async(ctx, DK_GAME_FULL_DOKO, d_roots, d_seeds + n, (uint32_t)n, iterations, c, d_v, d_val, d_b, ctx->stream);
+    if (rc) return rc;
+    hipLaunchKernelGGL(legal_kernel, dim3(grid_for(n_info, 64)), dim3(64), 0, ctx->stream, d_i, n_info, d_allowed);
+    DK_HIP(hipGetLastError());
+    rc = dk_fuse_accumulate_async(ctx, d_v, n_info, samples, d_allowed, fuse_mode, d_u, d_f, ctx->stream);
+    if (rc) return rc;
+    rc = dk_fuse_select_async(ctx, n_info, fuse_mode, d_allowed, d_u, d_f, d_b + n, ctx->stream);
+    if (rc) return rc;
+    DK_HIP(hipMemcpyAsync(actions, d_b + n, n_info, hipMemcpyDeviceToHost, ctx->stream));
+    if (visits) DK_HIP(hipMemcpyAsync(visits, d_v, n * 39 * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+    return finish(ctx, ctx->stream);
+}
+
+}  // extern "C"

@@ -199,8 +199,32 @@ def fusion_kats():
     path = os.path.join(REF, "rs-doko-py-bridge/src/compare_impi/policy_fusion.rs")
     with open(path, encoding="utf-8") as fh:
         text = fh.read()
-    return {"source": "rs-doko-py-bridge/src/compare_impi/policy_fusion.rs:130-311",
-            "raw_test_count": text.count("#[tokio::test]")}
+    tests = text[text.find("#[cfg(test)]"):]
+    names = {"idx_ten": 1, "idx_nine": 0, "idx_jack": 2, "idx_queen": 3,
+             "a1_idx": 1, "a2_idx": 0, "a3_idx": 2, "a4_idx": 3}
+
+    def action(tok):
+        tok = tok.strip()
+        m = re.match(r"FdoAction::from_index\((\d+)\)", tok)
+        if m:
+            return int(m.group(1))
+        return ACTION_NAMES.index(tok.split("::")[1])
+
+    cases = []
+    for name, body in re.findall(r"async fn (test_\w+)\(\) \{(.*?)\n    \}\n", tests, re.S):
+        mode = "maxn" if "PolicyFusionMaxN" in body else "avg"
+        rows = []
+        for blk in re.findall(r"\{\s*let mut s = dummy;(.*?)\bs\s*\}", body, re.S):
+            row = [0] * 39
+            for k, v in re.findall(r"s\[(\w+)\]\s*=\s*(\d+)", blk):
+                row[int(k) if k.isdigit() else names[k]] = int(v)
+            rows.append(row)
+        allowed_blk = body[body.find("from_vec("):]
+        allowed = [action(t) for t in re.findall(r"FdoAction::(?:from_index\(\d+\)|\w+)", allowed_blk.split("))")[0])]
+        exp = re.search(r"assert_eq!\(\s*result,\s*(FdoAction::(?:from_index\(\d+\)|\w+))", body).group(1)
+        cases.append({"name": name, "mode": mode, "visits": rows, "allowed": sorted(set(allowed)),
+                      "expect": action(exp)})
+    return {"source": "rs-doko-py-bridge/src/compare_impi/policy_fusion.rs:130-311", "cases": cases}
 
 
 def main():
@@ -214,6 +238,8 @@ def main():
         json.dump(select_rank(), fh, indent=1)
     with open(os.path.join(OUT, "ttt_kats.json"), "w") as fh:
         json.dump(ttt_kats(), fh, indent=1)
+    with open(os.path.join(OUT, "fusion_kats.json"), "w") as fh:
+        json.dump(fusion_kats(), fh, indent=1)
     print("wrote fixtures to", OUT)
 
 

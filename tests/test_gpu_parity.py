@@ -1,0 +1,301 @@
+"""GPU parity: the HIP path (through the C-ABI) against the ORACLE on identical inputs.
+
+Integer / byte / index results are compared bit-exactly; the UCT values
+(f64 win_score/visits) are compared bitwise too, because the kernel uses the
+same IEEE f64 operations in the same order and glibc `log` values for ln(N).
+"""
+import numpy as np
+import pytest
+
+import oracle_lib as ol
+
+pytestmark = pytest.mark.gpu
+
+CMP = 117  # dk_fdo_state bytes with semantics (the rest is reserved/padding + tag at 127)
+
+
+@pytest.fixture(scope="module")
+def eng():
+    import master_doko_reinforcement_learning_amd as dk
+    e = dk.Engine(device=0, max_roots=4096, max_iterations=1000)
+    yield e
+    e.close()
+
+
+def fdo_states(n_games, seed, with_announcements=True):
+    """Random full-doko positions from oracle trajectories (all phases)."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for g in range(n_games):
+        s = ol.FdoState.new_game(int(seed * 1000 + g))
+        mode = g % 4
+        while True:
+            out.append(s.clone())
+            info = s.info()
+            if info["phase"] == 3:
+                break
+            legal = s.allowed()
+            acts = [a for a in range(39) if legal >> a & 1]
+            if info["phase"] == 0:
+                a = 24
+                if mode == 1 and (legal >> 25) & 1:
+                    a = 25
+                elif mode == 2 and rng.integers(3) == 0:
+                    a = int(rng.choice([a for a in acts if a >= 26]))
+            elif info["phase"] == 1:
+                anns = [a for a in acts if 33 <= a <= 37]
+                a = int(rng.choice(anns)) if (with_announcements and anns and rng.integers(3) == 0) else 38
+            else:
+                a = int(rng.choice(acts))
+            s.play(a)
+    return out
+
+
+def pack_all(states):
+    return np.frombuffer(b"".join(s.pack() for s in states), dtype=np.uint8).reshape(-1, 128).copy()
+
+
+def test_new_game_fdo_and_doko(eng):
+    seeds = np.arange(200, dtype=np.uint64) * 7919 + 3
+    got = eng.new_games(0, seeds)
+    exp = pack_all([ol.FdoState.new_game(int(x)) for x in seeds])
+    assert np.array_equal(got[:, :CMP], exp[:, :CMP]) and np.all(got[:, 127] == 0)
+    got = eng.new_games(1, seeds)
+    exp = pack_all([ol.DoState.new_game(int(x)) for x in seeds])
+    assert np.array_equal(got[:, :108], exp[:, :108]) and np.all(got[:, 127] == 1)
+
+
+def test_env_allowed_and_step_fdo(eng):
+    import master_doko_reinforcement_learning_amd as dk
+    env = dk.McEnv(eng)
+    states = fdo_states(24, 1)
+    live = [s for s in states if s.info()["phase"] != 3]
+    packed = pack_all(live)
+    for first in (True, False):
+        got = env.allowed_actions(packed, first)
+        exp = np.array([s.env_allowed(first) for s in live], dtype=np.uint64)
+        assert np.array_equal(got, exp)
+    # step every state with a legal action and compare the resulting wire state
+    rng = np.random.default_rng(5)
+    acts = []
+    nxt = []
+    for s in live:
+        legal = s.allowed()
+        a = int(rng.choice([x for x in range(39) if legal >> x & 1]))
+        acts.append(np.uint64(1) << np.uint64(a))
+        t = s.clone()
+        t.play(a)
+        nxt.append(t)
+    got = env.by_action(packed, np.array(acts, dtype=np.uint64))
+    exp = pack_all(nxt)
+    assert np.array_equal(got[:, :CMP], exp[:, :CMP])
+    # illegal action -> DK_E_STATE
+    bad = np.array([np.uint64(1) << np.uint64(38)], dtype=np.uint64)
+    card_phase = [i for i, s in enumerate(live) if s.info()["phase"] == 2][0]
+    with pytest.raises(dk.DokoError):
+        env.by_action(packed[card_phase:card_phase + 1], bad)
+
+
+def test_rewards_fdo(eng):
+    import master_doko_reinforcement_learning_amd as dk
+    env = dk.McEnv(eng)
+    states = fdo_states(16, 2)
+    packed = pack_all(states)
+    has, r = env.rewards_or_none(packed)
+    for i, s in enumerate(states):
+        info = s.info()
+        assert has[i] == bool(info["has_stats"])
+        if has[i]:
+            assert list(r[i]) == [float(x) for x in info["player_points"]]
+
+
+def test_rollout_parity_fdo(eng):
+    import master_doko_reinforcement_learning_amd as dk
+    env = dk.McEnv(eng)
+    states = fdo_states(40, 3)
+    packed = pack_all(states)
+    seeds = np.arange(len(states), dtype=np.uint64) * 31 + 11
+    rs = dk.splitmix_rng_states(seeds)
+    got_r, got_g = env.random_rollout(packed, rs)
+    for i, s in enumerate(states):
+        g = ol.arr(ol.ctypes.c_uint64, 4, [int(x) for x in rs[i]])
+        exp = s.rollout(g)
+        assert list(got_r[i]) == exp, i
+        assert [int(x) for x in got_g[i]] == list(g), i
+
+
+def test_rollout_parity_doko(eng):
+    import master_doko_reinforcement_learning_amd as dk
+    env = dk.McEnv(eng)
+    states = []
+    for g in range(300):
+        s = ol.DoState.new_game(9000 + g)
+        rng = ol.rng_seed(77 + g)
+        s.random_plies(rng, g % 53)
+        states.append(s)
+    packed = pack_all(states)
+    rs = dk.splitmix_rng_states(np.arange(len(states), dtype=np.uint64) + 5)
+    got_r, got_g = env.random_rollout(packed, rs)
+    for i, s in enumerate(states):
+        g = ol.arr(ol.ctypes.c_uint64, 4, [int(x) for x in rs[i]])
+        assert list(got_r[i]) == s.rollout(g)
+        assert [int(x) for x in got_g[i]] == list(g)
+
+
+def test_random_plies_match_oracle(eng):
+    """C3 infostate generation: seeded deal, 4x Healthy, k plies of
+    random_action_for_current_player_no_announcement."""
+    import master_doko_reinforcement_learning_amd as dk
+    env = dk.McEnv(eng)
+    seeds = np.arange(64, dtype=np.uint64) + 100
+    base = eng.new_games(0, seeds)
+    base = env.by_action(base, np.full(64, np.uint64(1) << np.uint64(24)))
+    for _ in range(3):
+        base = env.by_action(base, np.full(64, np.uint64(1) << np.uint64(24)))
+    plies = np.array([[0, 8, 20, 32][i % 4] for i in range(64)], dtype=np.uint32)
+    rs = dk.splitmix_rng_states(seeds + np.uint64(5000))
+    got, got_g = env.random_plies(base, rs, plies)
+    for i in range(64):
+        s = ol.FdoState.new_game(int(seeds[i]))
+        for _ in range(4):
+            s.play(24)
+        g = ol.arr(ol.ctypes.c_uint64, 4, [int(x) for x in rs[i]])
+        s.random_plies(g, int(plies[i]), True)
+        assert got[i, :CMP].tobytes() == s.pack()[:CMP]
+        assert [int(x) for x in got_g[i]] == list(g)
+
+
+def _oracle_search(states, seeds, iters, c, kind):
+    out = []
+    for s, sd in zip(states, seeds):
+        rng = ol.rng_seed(int(sd))
+        if kind == "ttt":
+            best, v, val = ol.ttt_search(s, rng, iters, c)
+        else:
+            best, v, val, _ = s.search(rng, iters, c)
+        out.append((best, v, val))
+    return out
+
+
+@pytest.mark.parametrize("iters", [200, 1000])
+def test_search_parity_fdo(eng, iters):
+    import master_doko_reinforcement_learning_amd as dk
+    pool = [s for s in fdo_states(30, 11) if s.info()["phase"] != 3]
+    rng = np.random.default_rng(iters)
+    pick = [pool[i] for i in rng.choice(len(pool), size=48 if iters == 200 else 16, replace=False)]
+    seeds = rng.integers(0, 2**63, size=len(pick), dtype=np.uint64)
+    visits, values, best = dk.CachedMCTS(eng, dk.GAME_FULL_DOKO).monte_carlo_tree_search(pack_all(pick), 2.5, iters, seeds)
+    for i, (b, v, val) in enumerate(_oracle_search(pick, seeds, iters, 2.5, "fdo")):
+        assert list(visits[i]) == v, i
+        assert values[i].tobytes() == np.array(val, dtype=np.float64).tobytes(), i
+        assert int(best[i]) == (b if b >= 0 else 255), i
+
+
+def test_search_parity_doko(eng):
+    import master_doko_reinforcement_learning_amd as dk
+    states = []
+    for g in range(32):
+        s = ol.DoState.new_game(0xD0C00000 + g)
+        for _ in range(4):
+            s.play(24)
+        s.random_plies(ol.rng_seed(g), g % 30)
+        states.append(s)
+    seeds = np.arange(32, dtype=np.uint64) * 13 + 1
+    visits, values, best = dk.CachedMCTS(eng, dk.GAME_DOKO).monte_carlo_tree_search(pack_all(states), 2.5, 500, seeds)
+    for i, (b, v, val) in enumerate(_oracle_search(states, seeds, 500, 2.5, "do")):
+        assert list(visits[i]) == v
+        assert values[i].tobytes() == np.array(val, dtype=np.float64).tobytes()
+        assert int(best[i]) == b
+
+
+def test_search_parity_ttt(eng):
+    """Config 1 plumbing: tic-tac-toe from the empty board, c = 2.0, seed 999."""
+    import master_doko_reinforcement_learning_amd as dk
+    boards = [[0] * 9, [1, 0, 0, 2, 1, 0, 0, 0, 0], [1, 2, 1, 0, 2, 0, 0, 0, 0]]
+    packed = np.frombuffer(b"".join(ol.ttt_pack(b) for b in boards), dtype=np.uint8).reshape(-1, 128).copy()
+    seeds = np.array([999, 1, 2], dtype=np.uint64)
+    visits, values, best = dk.CachedMCTS(eng, dk.GAME_TTT).monte_carlo_tree_search(packed, 2.0, 1000, seeds)
+    for i, (b, v, val) in enumerate(_oracle_search(boards, seeds, 1000, 2.0, "ttt")):
+        assert list(visits[i]) == v
+        assert values[i].tobytes() == np.array(val, dtype=np.float64).tobytes()
+        assert int(best[i]) == b
+
+
+def test_determinize_parity(eng):
+    import master_doko_reinforcement_learning_amd as dk
+    pool = [s for s in fdo_states(20, 21) if s.info()["phase"] != 3]
+    info = pool[::3]
+    samples = 8
+    seeds = np.arange(len(info) * samples, dtype=np.uint64) * 101 + 7
+    got = dk.card_matching_full(eng, pack_all(info), samples, seeds)
+    for i, s in enumerate(info):
+        for k in range(samples):
+            smp = s.card_matching(ol.rng_seed(int(seeds[i * samples + k])))
+            row = got[i * samples + k]
+            assert row[:32].tobytes() == smp.pack()[:32]          # hands
+            assert row[92:98].tobytes() == smp.pack()[92:98]      # reservations round
+            assert s.consistent_sample(smp)
+
+
+def test_fusion_parity(eng):
+    import master_doko_reinforcement_learning_amd as dk
+    rng = np.random.default_rng(3)
+    n_info, S = 40, 16
+    visits = rng.integers(0, 50, size=(n_info, S, 39)).astype(np.uint32)
+    visits[:, :, 30:] = 0
+    visits[5] = 7  # all ties
+    allowed = rng.integers(1, 2**39, size=n_info, dtype=np.uint64)
+    got_m = dk.PolicyFusionMaxN().fuse(eng, visits, allowed)
+    got_a = dk.PolicyFusionAverageStrategy().fuse(eng, visits, allowed)
+    for i in range(n_info):
+        em, _ = ol.fuse_maxn([list(r) for r in visits[i]], int(allowed[i]))
+        ea, _ = ol.fuse_avg([list(r) for r in visits[i]])
+        assert int(got_m[i]) == em
+        assert int(got_a[i]) == ea
+
+
+def test_decide_end_to_end(eng):
+    """DefaultImpiPolicy: CAP samples -> UCT -> MaxN fusion, against the oracle pipeline."""
+    import master_doko_reinforcement_learning_amd as dk
+    info = []
+    for j in range(6):
+        s = ol.FdoState.new_game(500 + j)
+        for _ in range(4):
+            s.play(24)
+        s.random_plies(ol.rng_seed(900 + j), [0, 8, 20, 32][j % 4], True)
+        info.append(s)
+    S, iters = 8, 200
+    seeds = np.arange(2 * len(info) * S, dtype=np.uint64) * 17 + 3
+    pol = dk.DefaultImpiPolicy(eng, 2.5, iters, S, dk.FUSE_MAXN)
+    actions, visits = pol.execute(pack_all(info), seeds, return_visits=True)
+    n = len(info) * S
+    for j, s in enumerate(info):
+        rows = []
+        for k in range(S):
+            smp = s.card_matching(ol.rng_seed(int(seeds[j * S + k])))
+            _, v, _, _ = smp.search(ol.rng_seed(int(seeds[n + j * S + k])), iters, 2.5)
+            rows.append(v)
+            assert list(visits[j * S + k]) == v
+        exp, _ = ol.fuse_maxn(rows, s.allowed())
+        assert int(actions[j]) == exp
+
+
+def test_full_size_properties(eng):
+    """Bench-sized batch shape (4096 roots x 1000 iterations here): every root's
+    visits sum to the iteration count, only root-legal actions are visited, and
+    a repeat run is bit-identical."""
+    import master_doko_reinforcement_learning_amd as dk
+    n = 4096
+    seeds = np.arange(n, dtype=np.uint64) + 1234
+    roots = eng.new_games(0, seeds)
+    env = dk.McEnv(eng)
+    for _ in range(4):
+        roots = env.by_action(roots, np.full(n, np.uint64(1) << np.uint64(24)))
+    mcts = dk.CachedMCTS(eng, dk.GAME_FULL_DOKO)
+    v1, val1, b1 = mcts.monte_carlo_tree_search(roots, 2.5, 1000, seeds)
+    assert np.all(v1.sum(axis=1) == 1000)
+    allowed = env.allowed_actions(roots, True)
+    bits = (allowed[:, None] >> np.arange(39, dtype=np.uint64)[None, :]) & np.uint64(1)
+    assert np.all((v1 > 0) <= (bits == 1))
+    v2, val2, b2 = mcts.monte_carlo_tree_search(roots, 2.5, 1000, seeds)
+    assert np.array_equal(v1, v2) and np.array_equal(val1.view(np.uint64), val2.view(np.uint64)) and np.array_equal(b1, b2)
