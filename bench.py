@@ -45,29 +45,14 @@ def parse():
     p.add_argument("--fusion", choices=["maxn", "avg"], default="maxn")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=0)
-    p.add_argument("--cpu-roots-per-thread", type=int, default=6)
+    p.add_argument("--cpu-roots-per-thread", type=int, default=64)
     return p.parse_args()
 
 
-def main():
-    args = parse()
+def make_workload(args, dk, L, dev, sp, rank, world, local_rank, dist=None):
+    """Build the synthetic inputs on the GPU (untimed) and return (engine, step,
+    n_roots, buffers).  `step()` runs one pass of the hot path on stream `sp`."""
     import torch
-    import torch.distributed as dist
-
-    import master_doko_reinforcement_learning_amd as dk
-    from master_doko_reinforcement_learning_amd import _native
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    dev = torch.device("cuda", local_rank)
-    L = _native.lib()
-    stream = torch.cuda.current_stream(dev)
-    sp = stream.cuda_stream
-
     def ck(rc):
         if rc != 0:
             raise RuntimeError("doko_amd error %d: %s" % (rc, L.dk_status_string(rc).decode()))
@@ -127,8 +112,6 @@ def main():
     best = torch.zeros(n_roots, dtype=torch.uint8, device=dev)
     ck(L.dk_sync(eng.ctx, sp))
 
-    search_ms = []
-
     def step():
         if args.workload == "c3":
             ck(L.dk_determinize_batch_async(eng.ctx, ptr(info), I, S_r, ptr(d_samp), ptr(roots), sp))
@@ -141,6 +124,41 @@ def main():
         else:
             ck(L.dk_search_batch_async(eng.ctx, dk.GAME_DOKO, ptr(roots), ptr(d_srch), n_roots, iters, args.c,
                                        ptr(visits), ptr(values), ptr(best), sp))
+
+    return eng, step, n_roots, {"visits": visits, "values": values, "best": best, "roots": roots}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    import master_doko_reinforcement_learning_amd as dk
+    from master_doko_reinforcement_learning_amd import _native
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+    L = _native.lib()
+    # one explicit stream for torch's allocations/copies AND the library's launches
+    # (handle 0 would mean the library's own non-blocking stream: no ordering with torch)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    sp = stream.cuda_stream
+    assert sp != 0
+
+    def ck(rc):
+        if rc != 0:
+            raise RuntimeError("doko_amd error %d: %s" % (rc, L.dk_status_string(rc).decode()))
+
+    eng, step, n_roots, bufs = make_workload(args, dk, L, dev, sp, rank, world, local_rank, dist)
+    search_ms = []
+    iters = args.iterations
+    visits = bufs["visits"]
 
     for _ in range(args.warmup):
         step()

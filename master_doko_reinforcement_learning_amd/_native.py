@@ -10,18 +10,22 @@ import subprocess
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG_DIR)
 LIB_PATH = os.path.join(PKG_DIR, "libdoko_amd.so")
+# profiling builds (-DDK_PHASE_PROF) are loaded by setting DK_LIB to their path
+PROF_LIB_PATH = os.path.join(PKG_DIR, "libdoko_amd_prof.so")
 SRC = os.path.join(PKG_DIR, "csrc", "doko_amd.hip")
 HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared"]
 
 
-def build(verbose=False):
-    """Compile csrc/doko_amd.hip for gfx950 into the package directory (in-tree)."""
+def build(verbose=False, profiling=False):
+    """Compile csrc/doko_amd.hip for gfx950 into the package directory (in-tree).
+    profiling=True builds the phase-timer variant libdoko_amd_prof.so."""
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    cmd = [hipcc] + HIPCC_FLAGS + ["-o", LIB_PATH, SRC]
+    out = PROF_LIB_PATH if profiling else LIB_PATH
+    cmd = [hipcc] + HIPCC_FLAGS + (["-DDK_PHASE_PROF"] if profiling else []) + ["-o", out, SRC]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True, cwd=PKG_DIR)
-    return LIB_PATH
+    return out
 
 
 class dk_config(ctypes.Structure):
@@ -41,14 +45,15 @@ def lib():
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
+    path = os.environ.get("DK_LIB", LIB_PATH)
+    if not os.path.exists(path):
         raise ImportError("libdoko_amd.so not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
                           "(hipcc --offload-arch=gfx950); there is no CPU fallback")
     try:
         import torch  # noqa: F401  (shares libamdhip64 with the extension)
     except Exception:
         pass
-    L = ctypes.CDLL(LIB_PATH)
+    L = ctypes.CDLL(path)
     sigs = {
         "dk_abi_version": (ctypes.c_int, []),
         "dk_status_string": (ctypes.c_char_p, [ctypes.c_int]),

@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -22,7 +23,7 @@
 namespace {
 
 constexpr int WAVE = 64;
-constexpr int MAX_PATH = 128;  // LDS path entries per lane (deeper paths fall back to parent links)
+constexpr int MAX_PATH = 64;   // LDS path entries per lane (deeper paths spill to a global overflow)
 
 #define DK_HIP(call)                                              \
     do {                                                          \
@@ -34,56 +35,97 @@ constexpr int MAX_PATH = 128;  // LDS path entries per lane (deeper paths fall b
     } while (0)
 
 // ---------------------------------------------------------------- node pool access
+// Node pool of one root, root-major: [root][slot] so that a node's child block
+// is one contiguous run of 16-byte hot records (one or a few cache lines).
+// Only the owning lane ever touches a root's tree, so plain loads and stores
+// (L1-cacheable, program-ordered within the lane) are sufficient.
 template <class W>
 struct GpuMem {
-    uint64_t* stats;
-    dk::NodeMeta* meta;
+    dk::NodeHot* hot;
+    dk::NodeCold* cold;
     W* states;
-    uint32_t* path;  // LDS, this lane's column (stride WAVE)
-    size_t R, root;
-    uint32_t cap_slots, cap_states, max_path;
+    uint32_t* path;       // LDS, this lane's column (stride path_stride)
+    uint64_t* path_st;    // LDS, stats read on the way down
+    uint32_t* ovf;        // global overflow of the path (entries >= MAX_PATH)
+    uint64_t* ovf_st;
+    uint32_t path_stride;
+    int lds_n;            // path entries held in LDS
+    uint32_t cap_slots, cap_states;
+#ifdef DK_PHASE_PROF
+    uint64_t* prof;
+#endif
 
-    __device__ size_t at(uint32_t s) const { return (size_t)s * R + root; }
-    __device__ uint64_t load_stats(uint32_t s) const {
-        return __hip_atomic_load(stats + at(s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __device__ dk::NodeHot load_hot(uint32_t s) const { return hot[s]; }
+    __device__ void store_hot(uint32_t s, const dk::NodeHot& h) const { hot[s] = h; }
+    __device__ void store_stats(uint32_t s, uint64_t v) const { hot[s].stats = v; }
+    __device__ void store_child_base(uint32_t s, uint32_t child_base) const { hot[s].child_base = child_base; }
+    __device__ void store_node_tail(uint32_t s, uint32_t child_base, uint32_t info) const {
+        hot[s].child_base = child_base;
+        hot[s].info = info;
     }
-    __device__ void store_stats(uint32_t s, uint64_t v) const {
-        __hip_atomic_store(stats + at(s), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __device__ dk::NodeCold load_cold(uint32_t s) const { return cold[s]; }
+    __device__ void store_cold(uint32_t s, const dk::NodeCold& c) const { cold[s] = c; }
+    __device__ void store_unexpanded(uint32_t s, uint64_t u) const { cold[s].unexpanded = u; }
+    __device__ W load_state(uint32_t i) const { return states[i]; }
+    __device__ void store_state(uint32_t i, const W& w) const { states[i] = w; }
+    __device__ uint32_t path_get(int k, uint64_t* st) const {
+        if (k < lds_n) {
+            *st = path_st[k * path_stride];
+            return path[k * path_stride];
+        }
+        *st = ovf_st[k - lds_n];
+        return ovf[k - lds_n];
     }
-    __device__ void add_stats(uint32_t s, uint64_t d) const {
-        (void)__hip_atomic_fetch_add(stats + at(s), d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __device__ void path_set(int k, uint32_t v, uint64_t st) const {
+        if (k < lds_n) {
+            path[k * path_stride] = v;
+            path_st[k * path_stride] = st;
+        } else {
+            ovf[k - lds_n] = v;
+            ovf_st[k - lds_n] = st;
+        }
     }
-    __device__ dk::NodeMeta load_meta(uint32_t s) const { return meta[at(s)]; }
-    __device__ void store_meta(uint32_t s, const dk::NodeMeta& m) const { meta[at(s)] = m; }
-    __device__ void store_meta_expand(uint32_t s, uint64_t unexp, uint32_t base, uint8_t n) const {
-        dk::NodeMeta* p = meta + at(s);
-        p->unexpanded = unexp;
-        p->child_base = base;
-        p->nchild = n;
-    }
-    __device__ W load_state(uint32_t i) const { return states[(size_t)i * R + root]; }
-    __device__ void store_state(uint32_t i, const W& w) const { states[(size_t)i * R + root] = w; }
-    __device__ uint32_t path_get(int k) const { return path[k * WAVE]; }
-    __device__ void path_set(int k, uint32_t v) const { path[k * WAVE] = v; }
+#ifdef DK_PHASE_PROF
+    __device__ void prof_add(int k, uint64_t v) const { prof[k] += v; }
+#endif
 };
 
 // ---------------------------------------------------------------- kernels
+// One lane per root, `rpw` roots per 64-lane wave (lanes >= rpw idle).  The
+// LDS holds each lane's selection path: MAX_PATH x (u32 slot|player, u64 stats).
 template <class E>
 __global__ void __launch_bounds__(WAVE) search_kernel(const dk_state* __restrict__ roots,
                                                       const uint64_t* __restrict__ seeds, uint32_t n,
                                                       uint32_t iters, double c, const double* __restrict__ ln_table,
-                                                      uint64_t* stats, dk::NodeMeta* meta, typename E::Work* states,
-                                                      uint32_t cap_slots, uint32_t* visits, double* values,
-                                                      uint8_t* best, int* err) {
-    __shared__ uint32_t lds_path[MAX_PATH * WAVE];
+                                                      dk::NodeHot* hot, dk::NodeCold* cold, typename E::Work* states,
+                                                      uint32_t* ovf, uint64_t* ovf_st,
+                                                      uint32_t cap_slots, uint32_t rpw, int lds_n,
+                                                      uint32_t* visits, double* values,
+                                                      uint8_t* best, int* err, uint64_t* prof) {
+    extern __shared__ uint64_t lds_raw[];   // lds_n * rpw u64 stats, then lds_n * rpw u32 slots
     const uint32_t lane = threadIdx.x;
-    const uint32_t root = blockIdx.x * WAVE + lane;
-    if (root >= n) return;
+    const uint32_t root = blockIdx.x * rpw + lane;
+    if (lane >= rpw || root >= n) return;
     typename E::Work w;
     E::load(roots[root], w);
     dk::Rng rng = dk::Rng::seed_from_u64(seeds[root]);
-    GpuMem<typename E::Work> mem{stats, meta, states, lds_path + lane, (size_t)n, (size_t)root,
-                                 cap_slots, iters + 1, MAX_PATH};
+    const uint32_t T = iters + 1;
+    GpuMem<typename E::Work> mem;
+    mem.hot = hot + (size_t)root * cap_slots;
+    mem.cold = cold + (size_t)root * cap_slots;
+    mem.states = states + (size_t)root * T;
+    mem.path_st = lds_raw + lane;
+    mem.path = reinterpret_cast<uint32_t*>(lds_raw + lds_n * rpw) + lane;
+    mem.lds_n = lds_n;
+    mem.path_stride = rpw;
+    mem.ovf = ovf + (size_t)root * dk::MAX_DEPTH;
+    mem.ovf_st = ovf_st + (size_t)root * dk::MAX_DEPTH;
+    mem.cap_slots = cap_slots; mem.cap_states = T;
+#ifdef DK_PHASE_PROF
+    mem.prof = prof + (size_t)root * 8;
+#else
+    (void)prof;
+#endif
     uint8_t b;
     const int st = dk::search_root<E>(w, rng, iters, c, ln_table, mem, visits + (size_t)root * 39,
                                       values + (size_t)root * 39, &b, nullptr);
@@ -317,8 +359,10 @@ struct dk_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     uint32_t max_roots = 0, max_iters = 0, cap_slots = 0;
-    uint64_t* stats = nullptr;
-    dk::NodeMeta* meta = nullptr;
+    dk::NodeHot* hot = nullptr;
+    dk::NodeCold* cold = nullptr;
+    uint32_t* ovf = nullptr;
+    uint64_t* ovf_st = nullptr;
     void* states = nullptr;
     double* ln_table = nullptr;
     int* err = nullptr;
@@ -326,6 +370,9 @@ struct dk_ctx {
     bool timed = false;
     int last_error = DK_OK;
     uint64_t pool_bytes = 0;
+    uint32_t roots_per_wave = 64;   // DK_ROOTS_PER_WAVE
+    int lds_path = MAX_PATH;        // DK_LDS_PATH (path entries kept in LDS; tests shrink it)
+    uint64_t* prof = nullptr;       // phase timers (DK_PHASE_PROF builds only)
     std::vector<void*> scratch;
     std::vector<size_t> scratch_size;
     std::mutex mu;
@@ -365,9 +412,12 @@ int finish(dk_ctx* ctx, hipStream_t st) {
 template <class E>
 hipError_t launch_search(dk_ctx* ctx, const dk_state* roots, const uint64_t* seeds, uint32_t n, uint32_t iters,
                          double c, uint32_t* visits, double* values, uint8_t* best, hipStream_t st) {
-    hipLaunchKernelGGL(search_kernel<E>, dim3(grid_for(n, WAVE)), dim3(WAVE), 0, st, roots, seeds, n, iters, c,
-                       ctx->ln_table, ctx->stats, ctx->meta, (typename E::Work*)ctx->states, ctx->cap_slots, visits,
-                       values, best, ctx->err);
+    const uint32_t rpw = ctx->roots_per_wave;
+    const int lds_n = ctx->lds_path;
+    hipLaunchKernelGGL(search_kernel<E>, dim3(grid_for(n, rpw)), dim3(WAVE), (size_t)lds_n * rpw * 12, st,
+                       roots, seeds, n, iters, c, ctx->ln_table, ctx->hot, ctx->cold,
+                       (typename E::Work*)ctx->states, ctx->ovf, ctx->ovf_st, ctx->cap_slots, rpw, lds_n, visits, values, best,
+                       ctx->err, ctx->prof);
     return hipGetLastError();
 }
 
@@ -391,6 +441,7 @@ const char* dk_status_string(int s) {
 
 dk_ctx* dk_create(const dk_config* cfg) {
     if (!cfg || cfg->max_roots == 0 || cfg->max_iterations == 0) return nullptr;
+    if (cfg->max_iterations >= dk::NI_MAX_STATES) return nullptr;  // node state index is 22 bits
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || cfg->device < 0 || cfg->device >= count) return nullptr;
     hipDeviceProp_t prop;
@@ -409,12 +460,26 @@ dk_ctx* dk_create(const dk_config* cfg) {
     ctx->cap_slots = cfg->slot_capacity ? cfg->slot_capacity : 40u + 12u * cfg->max_iterations;
     const size_t R = cfg->max_roots, S = ctx->cap_slots, T = (size_t)cfg->max_iterations + 1;
     bool ok = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) == hipSuccess;
-    ok = ok && hipMalloc(&ctx->stats, R * S * sizeof(uint64_t)) == hipSuccess;
-    ok = ok && hipMalloc(&ctx->meta, R * S * sizeof(dk::NodeMeta)) == hipSuccess;
+    ok = ok && hipMalloc(&ctx->hot, R * S * sizeof(dk::NodeHot)) == hipSuccess;
+    ok = ok && hipMalloc(&ctx->cold, R * S * sizeof(dk::NodeCold)) == hipSuccess;
+    ok = ok && hipMalloc(&ctx->ovf, R * dk::MAX_DEPTH * sizeof(uint32_t)) == hipSuccess;
+    ok = ok && hipMalloc(&ctx->ovf_st, R * dk::MAX_DEPTH * sizeof(uint64_t)) == hipSuccess;
     ok = ok && hipMalloc(&ctx->states, R * T * STATE_SLOT_BYTES) == hipSuccess;
     ok = ok && hipMalloc(&ctx->ln_table, (T + 1) * sizeof(double)) == hipSuccess;
     ok = ok && hipMalloc(&ctx->err, sizeof(int)) == hipSuccess;
     ok = ok && hipEventCreate(&ctx->ev0) == hipSuccess && hipEventCreate(&ctx->ev1) == hipSuccess;
+    if (const char* e = getenv("DK_ROOTS_PER_WAVE")) {
+        const int v = atoi(e);
+        if (v >= 1 && v <= WAVE) ctx->roots_per_wave = (uint32_t)v;
+    }
+    if (const char* e = getenv("DK_LDS_PATH")) {
+        const int v = atoi(e);
+        if (v >= 1 && v <= MAX_PATH) ctx->lds_path = v;
+    }
+#ifdef DK_PHASE_PROF
+    ok = ok && hipMalloc(&ctx->prof, R * 8 * sizeof(uint64_t)) == hipSuccess;
+    ok = ok && hipMemset(ctx->prof, 0, R * 8 * sizeof(uint64_t)) == hipSuccess;
+#endif
     if (ok) {
         // ln(N) exactly as glibc `log` computes it — what Rust's f64::ln calls (node.rs:253).
         std::vector<double> ln(T + 1);
@@ -422,7 +487,7 @@ dk_ctx* dk_create(const dk_config* cfg) {
         ok = hipMemcpy(ctx->ln_table, ln.data(), ln.size() * sizeof(double), hipMemcpyHostToDevice) == hipSuccess;
         ok = ok && hipMemset(ctx->err, 0, sizeof(int)) == hipSuccess;
     }
-    ctx->pool_bytes = R * S * (sizeof(uint64_t) + sizeof(dk::NodeMeta)) + R * T * STATE_SLOT_BYTES;
+    ctx->pool_bytes = R * S * (sizeof(dk::NodeHot) + sizeof(dk::NodeCold)) + R * T * STATE_SLOT_BYTES;
     if (!ok) { dk_destroy(ctx); return nullptr; }
     return ctx;
 }
@@ -432,11 +497,14 @@ void dk_destroy(dk_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     for (void* p : ctx->scratch) if (p) (void)hipFree(p);
-    if (ctx->stats) (void)hipFree(ctx->stats);
-    if (ctx->meta) (void)hipFree(ctx->meta);
+    if (ctx->hot) (void)hipFree(ctx->hot);
+    if (ctx->cold) (void)hipFree(ctx->cold);
+    if (ctx->ovf) (void)hipFree(ctx->ovf);
+    if (ctx->ovf_st) (void)hipFree(ctx->ovf_st);
     if (ctx->states) (void)hipFree(ctx->states);
     if (ctx->ln_table) (void)hipFree(ctx->ln_table);
     if (ctx->err) (void)hipFree(ctx->err);
+    if (ctx->prof) (void)hipFree(ctx->prof);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -444,6 +512,17 @@ void dk_destroy(dk_ctx* ctx) {
 }
 
 int dk_last_error(const dk_ctx* ctx) { return ctx ? ctx->last_error : DK_E_INVALID; }
+
+#ifdef DK_PHASE_PROF
+// profiling builds only (not part of the ABI): per-root phase cycle totals
+int dk_phase_profile(dk_ctx* ctx, uint64_t* out, uint32_t n) {
+    if (!ctx || !ctx->prof || n > ctx->max_roots) return DK_E_INVALID;
+    DK_HIP(hipDeviceSynchronize());
+    DK_HIP(hipMemcpy(out, ctx->prof, (size_t)n * 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    DK_HIP(hipMemset(ctx->prof, 0, (size_t)ctx->max_roots * 8 * sizeof(uint64_t)));
+    return DK_OK;
+}
+#endif
 uint64_t dk_pool_bytes(const dk_ctx* ctx) { return ctx ? ctx->pool_bytes : 0; }
 
 int dk_sync(dk_ctx* ctx, void* stream) {

@@ -434,6 +434,167 @@ DK_HD int round_draws(const Work& w) {
     return d;
 }
 
+// ---- card-phase rollout fast path ------------------------------------------------
+// The card phase of a rollout rewritten for a 64-wide SIMD: 32-bit words only,
+// selects instead of branches, and the per-card announcement round reduced to
+// arithmetic.  With nobody announcing, player p is offered an announcement
+// after a card iff its hand size n_p >= theta_p (allowed_announcements is
+// monotone in n; the thresholds change only when a wedding is resolved), so
+// the forced NoAnnouncement draws of a round are popc over 4 byte compares.
+//
+//   theta (own levels)  = 11 - ws - |prev & {Re,90,60,30}|      unless Black is in prev
+//   theta (counter)     = 11 - ws - |enemy levels|               if enemy announced and
+//                                                                prev has neither Re nor Counter
+// (calc_announcement.rs:51-229; derivation in DESIGN.md).  Equality with the
+// step-by-step path is checked by tests/native/fdo_engine_check and the GPU tests.
+DK_HD uint32_t ann_theta(uint32_t prev, uint32_t enemy, int ws) {
+    uint32_t t = 99u;
+    if (!(prev & AN_BLACK)) t = (uint32_t)(11 - ws - popc32(prev & 0xFu));
+    if ((enemy & 0x1Fu) && !(prev & (AN_COUNTER | AN_RE))) {
+        const uint32_t tc = (uint32_t)(11 - ws - popc32(enemy & 0x1Fu));
+        t = tc < t ? tc : t;
+    }
+    return t;
+}
+// theta_p packed one byte per player (99 = never offered)
+DK_HD uint32_t ann_thetas(uint32_t team_kind, uint32_t solved_trick, uint32_t re_players, uint32_t re_lowest,
+                          uint32_t contra_lowest) {
+    if (team_kind == TK_WED_UNSOLVED || team_kind == TK_INRES) return 0x63636363u;
+    const int ws = team_kind == TK_WED_SOLVED ? (int)solved_trick : 0;
+    const uint32_t pr = all_higher_than(re_lowest), pk = all_higher_than(contra_lowest);
+    const uint32_t tre = ann_theta(pr, pk, ws), tko = ann_theta(pk, pr, ws);
+    uint32_t out = 0;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) out |= (((re_players >> p) & 1u) ? tre : tko) << (8 * p);
+    return out;
+}
+DK_HD uint32_t sel4u(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, uint32_t p) {
+    const uint32_t lo = (p & 1u) ? a1 : a0, hi = (p & 1u) ? a3 : a2;
+    return (p & 2u) ? hi : lo;
+}
+// trump rank nibbles (same table as trump_rank), 8 cards per word
+DK_HD uint32_t rank_fast(uint32_t c) {
+    const uint32_t wv = c < 8u ? 0xC0318420u : (c < 16u ? 0xB7202195u : 0x31A62031u);
+    return (wv >> (4u * (c & 7u))) & 15u;
+}
+DK_HD uint32_t suit_of(uint32_t c) { return (c * 43u) >> 8; }   // c / 6 for c < 24
+DK_HD uint32_t eyes_fast(uint32_t c) { return (0xB432A0u >> (4u * (c - 6u * suit_of(c)))) & 15u; }
+// colour class mask of card c (trumps, or its suit minus trumps)
+DK_HD uint32_t class_mask(uint32_t c, uint32_t tm) {
+    return ((tm >> c) & 1u) ? tm : ((0x3Fu << (6u * suit_of(c))) & ~tm);
+}
+// key of card c in a trick led with colour class `lead` (trick_key)
+DK_HD int key_fast(uint32_t c, uint32_t tm, uint32_t lead) {
+    const int k_t = 32 + (int)rank_fast(c), k_c = (int)eyes_fast(c);
+    return ((tm >> c) & 1u) ? k_t : (((lead >> c) & 1u) ? k_c : -1);
+}
+
+// Card phase to the end (w.phase == PH_PLAYCARD).  Returns plies played.
+DK_HD int rollout_cards(const Work& w0, Rng& rng, int pts[4]) {
+    // hands as "kinds held" / "kinds held twice" (removal takes the second copy first)
+    uint32_t any0, any1, any2, any3, two0, two1, two2, two3;
+    {
+        const uint64_t h0 = w0.h[0], h1 = w0.h[1], h2 = w0.h[2], h3 = w0.h[3];
+        const uint32_t M = 0xFFFFFFu;
+        any0 = ((uint32_t)h0 | (uint32_t)(h0 >> 24)) & M; two0 = ((uint32_t)h0 & (uint32_t)(h0 >> 24)) & M;
+        any1 = ((uint32_t)h1 | (uint32_t)(h1 >> 24)) & M; two1 = ((uint32_t)h1 & (uint32_t)(h1 >> 24)) & M;
+        any2 = ((uint32_t)h2 | (uint32_t)(h2 >> 24)) & M; two2 = ((uint32_t)h2 & (uint32_t)(h2 >> 24)) & M;
+        any3 = ((uint32_t)h3 | (uint32_t)(h3 >> 24)) & M; two3 = ((uint32_t)h3 & (uint32_t)(h3 >> 24)) & M;
+    }
+    uint32_t nb = (uint32_t)(popc32(any0) + popc32(two0)) | (uint32_t)(popc32(any1) + popc32(two1)) << 8 |
+                  (uint32_t)(popc32(any2) + popc32(two2)) << 16 | (uint32_t)(popc32(any3) + popc32(two3)) << 24;
+    const uint32_t tm = trump_mask(w0.game_type);
+    uint32_t team_kind = w0.team_kind, re_players = w0.re_players, solved = w0.solved_trick;
+    const uint32_t wedding_player = w0.wedding_player;
+    uint32_t theta = ann_thetas(team_kind, solved, re_players, w0.re_lowest, w0.contra_lowest);
+    uint32_t cur = w0.cur, trick_start = w0.trick_start, trick_len = w0.trick_len, n_tricks = w0.n_tricks;
+    uint32_t trick_cards = w0.trick_cards;
+    uint32_t eyes = w0.eyes, ntr = w0.ntricks, doko = w0.doko;
+    uint32_t fox_n = w0.fox_n, fox0 = w0.fox0, fox1 = w0.fox1, karl = w0.karl;
+    uint32_t lead = trick_len ? class_mask(trick_cards & 0xFFu, tm) : 0xFFFFFFu;
+    int plies = 0;
+    for (;;) {
+        // ---- one card for `cur`
+        const uint32_t a = sel4u(any0, any1, any2, any3, cur);
+        const uint32_t t2 = sel4u(two0, two1, two2, two3, cur);
+        const uint32_t follow_mask = (trick_len == 0u || n_tricks >= 12u) ? 0xFFFFFFu : lead;
+        const uint32_t f = a & follow_mask;
+        const uint32_t legal = f ? f : a;
+        const uint32_t r = rng.range_u32((uint32_t)popc32(legal));
+        // bit of rank r from the MSB = bit of rank popc-1-r from the LSB
+        uint32_t k = (uint32_t)popc32(legal) - 1u - r, pos = 0;
+#pragma unroll
+        for (int wdt = 16; wdt >= 1; wdt >>= 1) {
+            const uint32_t cnt = (uint32_t)popc32((legal >> pos) & ((1u << wdt) - 1u));
+            const bool hi = k >= cnt;
+            k = hi ? k - cnt : k;
+            pos = hi ? pos + (uint32_t)wdt : pos;
+        }
+        const uint32_t card = pos, bit = 1u << card;
+        const bool dup = (t2 & bit) != 0u;
+        const uint32_t na = dup ? a : (a ^ bit), nt = dup ? (t2 ^ bit) : t2;
+        any0 = cur == 0u ? na : any0; any1 = cur == 1u ? na : any1; any2 = cur == 2u ? na : any2; any3 = cur == 3u ? na : any3;
+        two0 = cur == 0u ? nt : two0; two1 = cur == 1u ? nt : two1; two2 = cur == 2u ? nt : two2; two3 = cur == 3u ? nt : two3;
+        nb -= 1u << (8u * cur);
+        lead = trick_len == 0u ? class_mask(card, tm) : lead;
+        trick_cards |= card << (8u * trick_len);
+        trick_len += 1u;
+        cur = (cur + 1u) & 3u;
+        plies += 1;
+        if (trick_len == 4u) {
+            // ---- trick complete (complete_trick)
+            const uint32_t c0 = trick_cards & 0xFFu, c1 = (trick_cards >> 8) & 0xFFu;
+            const uint32_t c2 = (trick_cards >> 16) & 0xFFu, c3 = trick_cards >> 24;
+            int bk = key_fast(c0, tm, lead);
+            uint32_t bi = 0, wc = c0;
+            const int k1 = key_fast(c1, tm, lead), k2 = key_fast(c2, tm, lead), k3 = key_fast(c3, tm, lead);
+            if (k1 > bk) { bk = k1; bi = 1; wc = c1; }
+            if (k2 > bk) { bk = k2; bi = 2; wc = c2; }
+            if (k3 > bk) { bk = k3; bi = 3; wc = c3; }
+            const uint32_t winner = (trick_start + bi) & 3u;
+            const uint32_t e = eyes_fast(c0) + eyes_fast(c1) + eyes_fast(c2) + eyes_fast(c3);
+            const uint32_t sh = 8u * winner;
+            eyes += e << sh;
+            ntr += 1u << sh;
+            doko += (e >= 40u ? 1u : 0u) << sh;
+            // foxes in play order
+#pragma unroll
+            for (uint32_t i = 0; i < 4; ++i) {
+                const uint32_t ci = (trick_cards >> (8u * i)) & 0xFFu;
+                if (ci == (uint32_t)DIAMOND_ACE) {
+                    const uint32_t ev = (((trick_start + i) & 3u) << 2) | winner;
+                    fox0 = fox_n == 0u ? ev : fox0;
+                    fox1 = fox_n == 0u ? fox1 : ev;
+                    fox_n += 1u;
+                }
+            }
+            const uint32_t t = n_tricks - 1u;
+            if (t == 11u && wc == (uint32_t)CLUB_JACK) karl = 1u + winner;
+            if (team_kind == TK_WED_UNSOLVED && t < 3u) {
+                if (winner != wedding_player) {
+                    team_kind = TK_WED_SOLVED; solved = t; re_players = (1u << wedding_player) | (1u << winner);
+                    theta = ann_thetas(team_kind, solved, re_players, w0.re_lowest, w0.contra_lowest);
+                } else if (t == 2u) {
+                    team_kind = TK_WED_SOLVED; solved = 2; re_players = 1u << wedding_player;
+                    theta = ann_thetas(team_kind, solved, re_players, w0.re_lowest, w0.contra_lowest);
+                }
+            }
+            if (n_tricks == 12u) break;
+            cur = winner; trick_start = winner; trick_cards = 0; trick_len = 0; n_tricks += 1u;
+        }
+        // ---- collapsed announcement round: one forced NoAnnouncement draw per offered player
+        const uint32_t d = (uint32_t)popc32(((nb | 0x80808080u) - theta) & 0x80808080u);
+        for (uint32_t i = 0; i < d; ++i) rng.advance();
+        plies += (int)d;
+    }
+    Work fin = w0;
+    fin.eyes = eyes; fin.ntricks = ntr; fin.doko = doko;
+    fin.fox_n = (uint8_t)fox_n; fin.fox0 = (uint8_t)fox0; fin.fox1 = (uint8_t)fox1; fin.karl = (uint8_t)karl;
+    fin.re_players = (uint8_t)re_players;
+    score(fin, pts);
+    return plies;
+}
+
 // Returns the rewards (player_points) and the number of plies played.
 DK_HD int rollout(Work w, Rng& rng, int pts[4]) {
     int plies = 0;
@@ -444,7 +605,20 @@ DK_HD int rollout(Work w, Rng& rng, int pts[4]) {
         play_action(w, act);
         plies++;
     }
-    // Card phase: nobody announces any more; collapse each announcement round.
+    if (w.phase == PH_FINISHED) { score(w, pts); return plies; }
+    return plies + rollout_cards(w, rng, pts);
+}
+
+// Reference restatement of the card phase on the full Work state, step by step
+// (kept as the host-side cross-check of rollout_cards).
+DK_HD int rollout_stepwise(Work w, Rng& rng, int pts[4]) {
+    int plies = 0;
+    while (w.phase != PH_PLAYCARD && w.phase != PH_FINISHED) {
+        const uint64_t a = legal_actions(w) & ~ANN_ACTIONS;
+        const int act = ctz64(random_single(a, rng));
+        play_action(w, act);
+        plies++;
+    }
     while (w.phase != PH_FINISHED) {
         const uint64_t a = legal_actions(w);
         const int card = ctz64(random_single(a, rng));

@@ -14,18 +14,23 @@ struct Rng {
     DK_HD static uint64_t rotl(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
 
     DK_HD static Rng seed_from_u64(uint64_t state) {
+        // rand_core 0.9 SeedableRng::seed_from_u64 (SplitMix64); Xoshiro256++ maps an
+        // all-zero seed to seed_from_u64(0), whose output is non-zero (no recursion needed)
         Rng r;
         uint64_t out[4];
+        for (int pass = 0; pass < 2; ++pass) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            state += 0x9e3779b97f4a7c15ULL;
-            uint64_t z = state;
-            z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
-            z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
-            out[i] = z ^ (z >> 31);
+            for (int i = 0; i < 4; ++i) {
+                state += 0x9e3779b97f4a7c15ULL;
+                uint64_t z = state;
+                z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+                z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+                out[i] = z ^ (z >> 31);
+            }
+            if ((out[0] | out[1] | out[2] | out[3]) != 0) break;
+            state = 0;
         }
         r.s0 = out[0]; r.s1 = out[1]; r.s2 = out[2]; r.s3 = out[3];
-        if ((r.s0 | r.s1 | r.s2 | r.s3) == 0) return seed_from_u64(0);
         return r;
     }
 
@@ -41,6 +46,16 @@ struct Rng {
         return res;
     }
     DK_HD uint32_t next_u32() { return (uint32_t)(next_u64() >> 32); }
+    // state transition only (a draw whose value is discarded)
+    DK_HD void advance() {
+        const uint64_t t = s1 << 17;
+        s2 ^= s0;
+        s3 ^= s1;
+        s1 ^= s2;
+        s0 ^= s3;
+        s2 ^= t;
+        s3 = rotl(s3, 45);
+    }
 
     // random_range(0..n) on u32 (n >= 1).
     DK_HD uint32_t range_u32(uint32_t n) {

@@ -8,16 +8,28 @@
 //   backup  : visits += 1 on every path node; win_score += r[parent.player]
 //   end     : one random_bool(1/1000) draw (mcts.rs:231)
 //
-// MI355X layout (not the reference's pointer tree): every node owns a
+// MI355X layout (not the reference's pointer tree).  Every node owns a
 // contiguous child block reserved at its first expansion (size = number of
-// actions it allows), so a level's children are scanned with independent
-// 8-byte loads; visits and the integer-exact win_score share one u64
-// (visits low, win_score high) updated by a single fire-and-forget atomic add;
-// node states live in a per-root pool (the reference's state arena).  The
-// select path (slot + parent player) is kept in LDS.  Sibling min/max is
-// computed once per level (identical values to the reference's per-child
-// recomputation).  ln(N) comes from a host-built table of glibc `log`
-// values, which is what Rust's f64::ln calls, so UCT values are bit-exact.
+// actions it allows).  A node is split into
+//   hot  (16 B): stats (visits low 32 | integer win_score high 32), child_base, info
+//   cold (16 B): unexpanded actions, parent, action   -- touched at expansion only
+// so one tree level of the selection is ONE round trip: the child block's hot
+// records (contiguous) are loaded together, the UCT pick is computed in
+// registers and the picked record is already the next level's node.  The
+// stats read on the way down are kept in the LDS path, so the backup is
+// store-only (no loads, no atomics): only this lane ever touches this tree.
+// Forced chains (nodes with a single allowed action, e.g. the NoAnnouncement
+// passes after every card) are walked in ONE step: the chain head (a child of
+// a branching node or of the root) keeps in child_base a pointer to the chain
+// end, updated whenever the chain grows.  The reference reads a node's
+// win_score only when its parent has >= 2 children (UCT) or it is a root child,
+// and a node's visits only as ln(N) of a branching node or as a root child, so
+// the interior of a chain needs no bookkeeping; which nodes exist, and every
+// value that is read, stay identical to the reference's.
+// Sibling min/max is computed once per level (identical values to the
+// reference's per-child recomputation).  ln(N) comes from a host-built table
+// of glibc `log` values, which is what Rust's f64::ln calls, so UCT values are
+// bit-exact.
 #pragma once
 #include <math.h>
 #include "common.h"
@@ -25,154 +37,302 @@
 
 namespace dk {
 
-struct NodeMeta {
-    uint64_t unexpanded;   // actions not yet expanded
-    uint32_t child_base;   // first slot of the child block (0 = none yet)
-    uint32_t state_idx;    // index into the state pool
-    uint32_t parent;       // parent slot (0xFFFFFFFF for the root)
-    uint8_t nchild;        // children expanded so far (block prefix)
-    uint8_t action;        // action that led here
-    uint8_t player;        // current_player of this node's state
-    uint8_t flags;         // bit0 terminal
-    uint64_t pad;
+// Phase timers (profiling builds only): wave-uniform shader-clock stamps taken at
+// the reconvergence points between select / expand / rollout / backup.
+#if defined(DK_PHASE_PROF) && defined(__HIP_DEVICE_COMPILE__)
+#define DK_STAMP(t) const uint64_t t = __builtin_amdgcn_s_memtime()
+#define DK_PROF(mem, k, v) prof_acc[k] += (v)
+#define DK_PROF_DECL uint64_t prof_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}
+#define DK_PROF_FLUSH(mem) for (int k_ = 0; k_ < 8; ++k_) mem.prof_add(k_, prof_acc[k_])
+#define DK_PROF_WAVEMAX(k, v) do { int m_ = (v); for (int o_ = 32; o_ >= 1; o_ >>= 1) { const int t_ = __shfl_xor(m_, o_); m_ = t_ > m_ ? t_ : m_; } prof_acc[k] += (uint64_t)m_; } while (0)
+#else
+#define DK_STAMP(t) [[maybe_unused]] const uint64_t t = 0
+#define DK_PROF(mem, k, v) ((void)0)
+#define DK_PROF_DECL
+#define DK_PROF_FLUSH(mem) ((void)0)
+#define DK_PROF_WAVEMAX(k, v) ((void)0)
+#endif
+
+struct alignas(16) NodeHot {
+    uint64_t stats;       // visits (low 32) | win_score (high 32, two's complement)
+    uint32_t child_base;  // first slot of the child block (valid when nchild > 0)
+    uint32_t info;        // nchild:6 | player:2 | has_unexpanded:1 | chain_head:1 | state_idx:22
 };
+struct alignas(16) NodeCold {
+    uint64_t unexpanded;  // actions not yet expanded
+    uint32_t parent;      // parent slot (0xFFFFFFFF for the root)
+    uint32_t action;      // action that led here
+};
+
+DK_HD uint32_t ni_nchild(uint32_t info) { return info & 63u; }
+DK_HD uint32_t ni_player(uint32_t info) { return (info >> 6) & 3u; }
+DK_HD bool ni_open(uint32_t info) { return (info >> 8) & 1u; }
+DK_HD bool ni_head(uint32_t info) { return (info >> 9) & 1u; }
+DK_HD uint32_t ni_state(uint32_t info) { return info >> 10; }
+DK_HD uint32_t ni_make(uint32_t nchild, uint32_t player, bool open, bool head, uint32_t state) {
+    return nchild | (player << 6) | (open ? 1u << 8 : 0u) | (head ? 1u << 9 : 0u) | (state << 10);
+}
+static constexpr uint32_t NI_MAX_STATES = 1u << 22;
+static constexpr int MAX_DEPTH = 512;   // selection path bound (LDS part + global overflow)
 
 DK_HD int sel4i(const int r[4], int p) { return p == 0 ? r[0] : (p == 1 ? r[1] : (p == 2 ? r[2] : r[3])); }
 
 static constexpr double DK_F64_EPSILON = 2.220446049250313e-16;
+static constexpr int SCAN_REG = 12;  // child blocks up to this size are scanned from registers
 
 // Outcome codes of search_root
 enum { SR_OK = 0, SR_CAPACITY = 1 };
+
+DK_HD double mean_of(uint64_t st) {
+    const uint32_t v = (uint32_t)st;
+    return v > 0 ? (double)(int32_t)(st >> 32) / (double)v : 0.0;
+}
+
+// Exact UCT value of one child (node.rs:238-277), the reference's f64 ops in order.
+DK_HD double uct_exact(uint64_t st, bool flat, double min_q, double max_q, double lnN, double c) {
+    const uint32_t v = (uint32_t)st;
+    if (v == 0) return INFINITY;
+    const double nq = flat ? 1.0 : 2.0 * (mean_of(st) - min_q) / (max_q - min_q) - 1.0;
+    return nq + c * sqrt(lnN / (double)v);
+}
+
+#if defined(__HIP_DEVICE_COMPILE__)
+DK_HD float rcp_approx(float x) { return __builtin_amdgcn_rcpf(x); }
+DK_HD float sqrt_approx(float x) { return __builtin_amdgcn_sqrtf(x); }
+#elif defined(DK_APPROX_HOOKS)   // host tests: adversarially perturbed approximations
+float rcp_approx(float x);
+float sqrt_approx(float x);
+#else
+DK_HD float rcp_approx(float x) { return 1.0f / x; }
+DK_HD float sqrt_approx(float x) { return sqrtf(x); }
+#endif
+
+// UCT pick over a child block of n <= SCAN_REG records held in registers;
+// returns the index, *pick_rec receives the picked record.  Bit-exact with
+// the reference's first-strict-maximum over f64 UCT values, computed as:
+//  1. sibling min / max of the means by exact integer cross-multiplication
+//     (rounding s/v to f64 is monotone, so the exact extreme is the f64 extreme);
+//  2. every child's UCT value estimated in f32 from exact integer numerators,
+//     error < B (|u_f32 - u_f64| <= ~5e-6 for |mean| <= 100);
+//  3. exact f64 UCT only for children whose estimate is within 2B of the best
+//     estimate (all others are strictly below the maximum), first strict max.
+// Blocks whose mean spread is tiny but non-zero (< 1e-7, only reachable past
+// ~3000 visits) take the exact path for every child.
+DK_HD uint32_t pick_child_reg(const NodeHot* rec, uint32_t n, double lnN, double c, NodeHot* pick_rec) {
+    // 1. exact argmin / argmax of s/v (v = 0 counts as 0/1)
+    int64_t smin = 0, smax = 0, vmin = 1, vmax = 1;
+#pragma unroll
+    for (int j = 0; j < SCAN_REG; ++j) {
+        if ((uint32_t)j < n) {
+            const uint32_t v = (uint32_t)rec[j].stats;
+            const int64_t sj = v ? (int64_t)(int32_t)(rec[j].stats >> 32) : 0, vj = v ? (int64_t)v : 1;
+            if (j == 0) { smin = smax = sj; vmin = vmax = vj; }
+            else {
+                if (sj * vmin < smin * vj) { smin = sj; vmin = vj; }
+                if (sj * vmax > smax * vj) { smax = sj; vmax = vj; }
+            }
+        }
+    }
+    const double min_q = (double)smin / (double)vmin, max_q = (double)smax / (double)vmax;
+    const bool flat = fabs(max_q - min_q) < DK_F64_EPSILON;
+    const bool exact_all = !flat && (max_q - min_q) < 1e-7;
+    // 2. f32 estimates: nq = 2 * (s_j v_m - s_m v_j) v_M / (v_j (s_M v_m - s_m v_M)) - 1
+    const float num_r = (float)(smax * vmin - smin * vmax);
+    const float inv_r = flat ? 0.0f : rcp_approx(num_r);
+    const float lnf = (float)lnN, cf = (float)c;
+    float ue[SCAN_REG];
+    float umax = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < SCAN_REG; ++j) {
+        ue[j] = -INFINITY;
+        if ((uint32_t)j < n) {
+            const uint32_t v = (uint32_t)rec[j].stats;
+            const int64_t sj = (int64_t)(int32_t)(rec[j].stats >> 32);
+            const float vf = (float)v;
+            const float ivf = rcp_approx(vf);
+            const float nq = flat ? 1.0f
+                                  : 2.0f * ((float)(sj * vmin - smin * (int64_t)v) * (float)vmax * ivf * inv_r) - 1.0f;
+            const float u = nq + cf * sqrt_approx(lnf * ivf);
+            ue[j] = v == 0 ? INFINITY : u;
+            umax = ue[j] > umax ? ue[j] : umax;
+        }
+    }
+    const float cut = umax - 1e-4f * (1.0f + fabsf(cf));   // 2B
+    // 3. exact f64 UCT over the candidates, first strict maximum
+    double best = -INFINITY;
+    uint32_t pick = 0;
+    NodeHot pr = rec[0];
+#pragma unroll
+    for (int j = 0; j < SCAN_REG; ++j) {
+        if ((uint32_t)j < n && (exact_all || ue[j] >= cut)) {
+            const double u = uct_exact(rec[j].stats, flat, min_q, max_q, lnN, c);
+            if (u > best) { best = u; pick = (uint32_t)j; pr = rec[j]; }
+        }
+    }
+    *pick_rec = pr;
+    return pick;
+}
 
 template <class E, class Mem>
 DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, double c, const double* ln_table,
                       Mem& mem, uint32_t* visits39, double* values39, uint8_t* best_out, uint64_t* ctr_scanned) {
     using Work = typename E::Work;
-    NodeMeta rm;
-    rm.unexpanded = E::allowed(root, true);
-    rm.child_base = 0; rm.state_idx = 0; rm.parent = 0xFFFFFFFFu; rm.nchild = 0; rm.action = 0xFF;
-    rm.player = (uint8_t)E::current_player(root); rm.flags = E::terminal(root) ? 1 : 0; rm.pad = 0;
-    mem.store_meta(0, rm);
-    mem.store_stats(0, 0ULL);
-    mem.store_state(0, root);
+    {
+        const uint64_t ra = E::allowed(root, true);
+        NodeHot h;
+        h.stats = 0; h.child_base = 0; h.info = ni_make(0, (uint32_t)E::current_player(root), ra != 0, false, 0);
+        NodeCold cd;
+        cd.unexpanded = ra; cd.parent = 0xFFFFFFFFu; cd.action = 0xFFu;
+        mem.store_hot(0, h);
+        mem.store_cold(0, cd);
+        mem.store_state(0, root);
+    }
     uint32_t next_slot = 1, next_state = 1;
     int status = SR_OK;
     uint64_t scanned = 0;
+    DK_PROF_DECL;
 
     for (uint32_t it = 0; it < iters; ++it) {
+        DK_STAMP(t0);
         // ---------------- selection
         uint32_t slot = 0;
-        NodeMeta x = mem.load_meta(0);
+        NodeHot x = mem.load_hot(0);
         uint32_t x_visits = it;   // root visits == completed iterations
         int depth = 0;
-        mem.path_set(0, 0u);
-        while (x.nchild > 0 && x.unexpanded == 0) {
-            uint32_t pick = 0;
-            uint32_t pick_visits;
-            if (x.nchild == 1) {
-                pick_visits = (uint32_t)mem.load_stats(x.child_base);
-                scanned += 1;
+        uint32_t chain_head = 0xFFFFFFFFu;   // head whose skip pointer led to x
+        mem.path_set(0, 0u, x.stats);
+        while (ni_nchild(x.info) > 0 && !ni_open(x.info)) {
+            const uint32_t n = ni_nchild(x.info);
+            uint32_t pick;
+            NodeHot y;
+            if (n == 1) {
+                // single child: a chain head jumps straight to its chain end
+                pick = 0;
+                chain_head = ni_head(x.info) ? slot : 0xFFFFFFFFu;
+                y = mem.load_hot(x.child_base);
+            } else if (n <= (uint32_t)SCAN_REG) {
+                NodeHot rec[SCAN_REG];
+#pragma unroll
+                for (int j = 0; j < SCAN_REG; ++j) {
+                    if ((uint32_t)j < n) rec[j] = mem.load_hot(x.child_base + (uint32_t)j);
+                    else { rec[j].stats = 0; rec[j].child_base = 0; rec[j].info = 0; }
+                }
+                pick = pick_child_reg(rec, n, ln_table[x_visits], c, &y);
             } else {
+                // generic block (never produced by the doko engines, whose nodes offer <= 12 actions)
                 const double lnN = ln_table[x_visits];
                 double min_q = INFINITY, max_q = -INFINITY;
-                // pass 1: sibling min/max of the mean value (node.rs:202-235)
-                for (int j = 0; j < x.nchild; ++j) {
-                    const uint64_t st = mem.load_stats(x.child_base + j);
-                    const uint32_t v = (uint32_t)st;
-                    const double q = v > 0 ? (double)(int32_t)(st >> 32) / (double)v : 0.0;
+                for (uint32_t j = 0; j < n; ++j) {
+                    const double q = mean_of(mem.load_hot(x.child_base + j).stats);
                     min_q = q < min_q ? q : min_q;
                     max_q = q > max_q ? q : max_q;
                 }
                 const bool flat = fabs(max_q - min_q) < DK_F64_EPSILON;
-                // pass 2: UCT, first strict maximum (node.rs:238-277)
                 double best = -INFINITY;
-                pick_visits = 0;
-                for (int j = 0; j < x.nchild; ++j) {
-                    const uint64_t st = mem.load_stats(x.child_base + j);
-                    const uint32_t v = (uint32_t)st;
+                pick = 0;
+                y = mem.load_hot(x.child_base);
+                for (uint32_t j = 0; j < n; ++j) {
+                    const NodeHot r = mem.load_hot(x.child_base + j);
+                    const uint32_t v = (uint32_t)r.stats;
                     double u;
-                    if (v == 0) {
-                        u = INFINITY;
-                    } else {
-                        const double q = (double)(int32_t)(st >> 32) / (double)v;
-                        const double nq = flat ? 1.0 : 2.0 * (q - min_q) / (max_q - min_q) - 1.0;
+                    if (v == 0) u = INFINITY;
+                    else {
+                        const double nq = flat ? 1.0 : 2.0 * (mean_of(r.stats) - min_q) / (max_q - min_q) - 1.0;
                         u = nq + c * sqrt(lnN / (double)v);
                     }
-                    if (u > best) { best = u; pick = (uint32_t)j; pick_visits = v; }
+                    if (u > best) { best = u; pick = j; y = r; }
                 }
-                scanned += x.nchild;
             }
+            if (n > 1) chain_head = 0xFFFFFFFFu;
+            scanned += n;
+            DK_PROF(mem, n == 1 ? 5 : 6, 1);
             const uint32_t child = x.child_base + pick;
             depth += 1;
-            if (depth < (int)mem.max_path) mem.path_set(depth, child | ((uint32_t)x.player << 30));
+            if (depth >= MAX_DEPTH - 1) { status = SR_CAPACITY; break; }
+            mem.path_set(depth, child | (ni_player(x.info) << 30), y.stats);
             slot = child;
-            x = mem.load_meta(child);
-            x_visits = pick_visits;
+            x_visits = (uint32_t)y.stats;
+            x = y;
         }
+        if (status != SR_OK) break;
+        DK_STAMP(t1);
+        DK_PROF(mem, 0, t1 - t0);
+        DK_PROF(mem, 4, (uint64_t)depth);
+        DK_PROF_WAVEMAX(7, depth);
         // ---------------- expansion
         Work w;
-        if (x.unexpanded != 0) {
-            const uint64_t bit = random_single(x.unexpanded, rng);
+        if (ni_open(x.info)) {
+            NodeCold cd = mem.load_cold(slot);
+            const uint64_t bit = random_single(cd.unexpanded, rng);
             const int a = ctz64(bit);
-            if (x.nchild == 0) {
-                const uint32_t block = (uint32_t)popc64(x.unexpanded);
-                if (next_slot + block > mem.cap_slots || next_state >= mem.cap_states) { status = SR_CAPACITY; break; }
+            uint32_t nch = ni_nchild(x.info);
+            const uint32_t block = nch + (uint32_t)popc64(cd.unexpanded);
+            if (nch == 0) {
+                if (next_slot + block > mem.cap_slots || next_state >= mem.cap_states || next_state >= NI_MAX_STATES) {
+                    status = SR_CAPACITY;
+                    break;
+                }
                 x.child_base = next_slot;
                 next_slot += block;
             }
-            x.unexpanded &= ~bit;
-            const uint32_t child = x.child_base + x.nchild;
-            x.nchild += 1;
-            mem.store_meta_expand(slot, x.unexpanded, x.child_base, x.nchild);
-            w = mem.load_state(x.state_idx);
+            cd.unexpanded &= ~bit;
+            const uint32_t child = x.child_base + nch;
+            nch += 1;
+            mem.store_node_tail(slot, x.child_base,
+                                ni_make(nch, ni_player(x.info), cd.unexpanded != 0, ni_head(x.info), ni_state(x.info)));
+            mem.store_unexpanded(slot, cd.unexpanded);
+            // a forced chain grew: its head now points at the new end
+            if (block == 1 && chain_head != 0xFFFFFFFFu) mem.store_child_base(chain_head, child);
+            w = mem.load_state(ni_state(x.info));
             E::step(w, a);
-            NodeMeta cm;
-            cm.unexpanded = E::allowed(w, false);
-            cm.child_base = 0; cm.state_idx = next_state; cm.parent = slot; cm.nchild = 0; cm.action = (uint8_t)a;
-            cm.player = (uint8_t)E::current_player(w); cm.flags = E::terminal(w) ? 1 : 0; cm.pad = 0;
-            mem.store_meta(child, cm);
-            mem.store_stats(child, 0ULL);
+            const uint64_t ca = E::allowed(w, false);
+            NodeHot ch;
+            ch.stats = 0; ch.child_base = 0;
+            ch.info = ni_make(0, (uint32_t)E::current_player(w), ca != 0, slot == 0 || block >= 2, next_state);
+            NodeCold cc;
+            cc.unexpanded = ca; cc.parent = slot; cc.action = (uint32_t)a;
+            mem.store_hot(child, ch);
+            mem.store_cold(child, cc);
             mem.store_state(next_state, w);
             next_state += 1;
             depth += 1;
-            if (depth < (int)mem.max_path) mem.path_set(depth, child | ((uint32_t)x.player << 30));
+            mem.path_set(depth, child | (ni_player(x.info) << 30), 0ULL);
             slot = child;
         } else {
-            w = mem.load_state(x.state_idx);
+            w = mem.load_state(ni_state(x.info));
         }
+        DK_STAMP(t2);
+        DK_PROF(mem, 1, t2 - t1);
         // ---------------- rollout
         int r[4];
         E::rollout(w, rng, r);
-        // ---------------- backup (leaf -> root); deep tails beyond the LDS path use parent links
-        int k = depth;
-        uint32_t s = slot;
-        while (k >= (int)mem.max_path) {
-            const NodeMeta nm = mem.load_meta(s);
-            const NodeMeta pm = mem.load_meta(nm.parent);
-            mem.add_stats(s, ((uint64_t)(uint32_t)sel4i(r, pm.player) << 32) | 1ULL);
-            s = nm.parent;
-            k -= 1;
+        DK_STAMP(t3);
+        DK_PROF(mem, 2, t3 - t2);
+        // ---------------- backup (leaf -> root): stores of the stats read on the way down
+        for (int k = depth; k >= 1; --k) {
+            uint64_t st;
+            const uint32_t e = mem.path_get(k, &st);
+            mem.store_stats(e & 0x3FFFFFFFu, st + (((uint64_t)(uint32_t)sel4i(r, (int)(e >> 30)) << 32) | 1ULL));
         }
-        for (; k >= 1; --k) {
-            const uint32_t e = mem.path_get(k);
-            mem.add_stats(e & 0x3FFFFFFFu, ((uint64_t)(uint32_t)sel4i(r, (int)(e >> 30)) << 32) | 1ULL);
-        }
-        mem.add_stats(0, 1ULL);
+        mem.store_stats(0, (uint64_t)(it + 1));
         if (it + 1 == iters) (void)rng.next_u64();  // random_bool((1f32/1000f32) as f64)
+        DK_STAMP(t4);
+        DK_PROF(mem, 3, t4 - t3);
     }
     if (ctr_scanned) *ctr_scanned = scanned;
+    DK_PROF_FLUSH(mem);
 
     // ---------------- result: root children in expansion order
     for (int a = 0; a < 39; ++a) { visits39[a] = 0; values39[a] = 0.0; }
-    const NodeMeta r0 = mem.load_meta(0);
+    const NodeHot r0 = mem.load_hot(0);
     int best = -1; uint32_t bv = 0;
-    for (int j = 0; j < r0.nchild; ++j) {
-        const uint64_t st = mem.load_stats(r0.child_base + j);
-        const NodeMeta cm = mem.load_meta(r0.child_base + j);
+    for (uint32_t j = 0; j < ni_nchild(r0.info); ++j) {
+        const uint64_t st = mem.load_hot(r0.child_base + j).stats;
+        const uint32_t act = mem.load_cold(r0.child_base + j).action;
         const uint32_t v = (uint32_t)st;
-        visits39[cm.action] = v;
-        values39[cm.action] = (double)(int32_t)(st >> 32) / (double)v;
-        if (best < 0 || v >= bv) { best = cm.action; bv = v; }   // max_by_key: last maximum
+        visits39[act] = v;
+        values39[act] = (double)(int32_t)(st >> 32) / (double)v;
+        if (best < 0 || v >= bv) { best = (int)act; bv = v; }   // max_by_key: last maximum
     }
     *best_out = best < 0 ? (uint8_t)0xFF : (uint8_t)best;
     return status;

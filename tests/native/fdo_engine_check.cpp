@@ -53,6 +53,12 @@ static void check_state(const fdo::State& s, int game, int step, uint64_t seed) 
                     if (dk::fdo::allowed_announcements(w, p, n) !=
                         fdo::calc_allowed_announcements(p, n, s.team_state, s.announcements.re_lowest, s.announcements.contra_lowest))
                         fail("allowed_announcements", game, step);
+            // the rollout fast path's hand-size thresholds (rollout_cards)
+            const uint32_t th = dk::fdo::ann_thetas(w.team_kind, w.solved_trick, w.re_players, w.re_lowest, w.contra_lowest);
+            for (int p = 0; p < 4; ++p)
+                for (int n = 0; n <= 12; ++n)
+                    if ((n >= (int)((th >> (8 * p)) & 0xFF)) != (dk::fdo::allowed_announcements(w, p, n) != 0))
+                        fail("announcement thresholds", game, step);
         }
     }
     // rollout parity (rewards + RNG stream position)

@@ -9,6 +9,7 @@
 
 #include "../../master_doko_reinforcement_learning_amd/csrc/engine/adapters.h"
 #include "../../master_doko_reinforcement_learning_amd/csrc/engine/search_core.h"
+#include "host_mem.h"
 #include "../../oracle/doko.hpp"
 #include "../../oracle/full_doko.hpp"
 #include "../../oracle/mcts.hpp"
@@ -18,26 +19,6 @@ using namespace oracle;
 extern "C" void or_fdo_pack(void* sp, uint8_t* out);
 extern "C" void or_do_pack(void* sp, uint8_t* out);
 
-template <class W>
-struct HostMem {
-    uint32_t cap_slots, cap_states, max_path;
-    std::vector<uint64_t> stats;
-    std::vector<dk::NodeMeta> meta;
-    std::vector<W> states;
-    std::vector<uint32_t> path;
-    HostMem(uint32_t slots, uint32_t nstates, uint32_t mp) : cap_slots(slots), cap_states(nstates), max_path(mp),
-        stats(slots), meta(slots), states(nstates), path(mp) {}
-    uint64_t load_stats(uint32_t s) { return stats[s]; }
-    void store_stats(uint32_t s, uint64_t v) { stats[s] = v; }
-    void add_stats(uint32_t s, uint64_t d) { stats[s] += d; }
-    dk::NodeMeta load_meta(uint32_t s) { return meta[s]; }
-    void store_meta(uint32_t s, const dk::NodeMeta& m) { meta[s] = m; }
-    void store_meta_expand(uint32_t s, uint64_t unexp, uint32_t base, uint8_t n) { meta[s].unexpanded = unexp; meta[s].child_base = base; meta[s].nchild = n; }
-    W load_state(uint32_t i) { return states[i]; }
-    void store_state(uint32_t i, const W& w) { states[i] = w; }
-    uint32_t path_get(int k) { return path[k]; }
-    void path_set(int k, uint32_t v) { path[k] = v; }
-};
 
 static void fail(const char* w, int i) { printf("MISMATCH %s root %d\n", w, i); exit(1); }
 

@@ -1,0 +1,78 @@
+// TEST INFRASTRUCTURE: pick_child_reg (filtered exact UCT) against the plain
+// two-pass f64 UCT of the reference (node.rs:202-277) on random and near-tied
+// child blocks, with the f32 reciprocal / sqrt perturbed by up to 4 ulp (the
+// GPU's v_rcp_f32 / v_sqrt_f32 are within 1 ulp).  Prints "OK <n>".
+#define DK_APPROX_HOOKS
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+
+#include "../../master_doko_reinforcement_learning_amd/csrc/engine/search_core.h"
+
+static std::mt19937_64 g_pert(7);
+static float perturb(float y) {
+    const int k = (int)(g_pert() % 9) - 4;
+    for (int i = 0; i < k; ++i) y = nextafterf(y, INFINITY);
+    for (int i = 0; i > k; --i) y = nextafterf(y, -INFINITY);
+    return y;
+}
+float dk::rcp_approx(float x) { return perturb(1.0f / x); }
+float dk::sqrt_approx(float x) { return perturb(sqrtf(x)); }
+
+static uint32_t naive(const dk::NodeHot* rec, uint32_t n, double lnN, double c) {
+    double min_q = INFINITY, max_q = -INFINITY;
+    for (uint32_t j = 0; j < n; ++j) {
+        const double q = dk::mean_of(rec[j].stats);
+        min_q = q < min_q ? q : min_q;
+        max_q = q > max_q ? q : max_q;
+    }
+    const bool flat = fabs(max_q - min_q) < dk::DK_F64_EPSILON;
+    double best = -INFINITY;
+    uint32_t pick = 0;
+    for (uint32_t j = 0; j < n; ++j) {
+        const double u = dk::uct_exact(rec[j].stats, flat, min_q, max_q, lnN, c);
+        if (u > best) { best = u; pick = j; }
+    }
+    return pick;
+}
+
+int main(int argc, char** argv) {
+    const long cases = argc > 1 ? atol(argv[1]) : 1000000;
+    std::mt19937_64 r(argc > 2 ? strtoull(argv[2], 0, 10) : 1);
+    long ties = 0;
+    for (long t = 0; t < cases; ++t) {
+        dk::NodeHot rec[dk::SCAN_REG];
+        memset(rec, 0, sizeof(rec));
+        const uint32_t n = 2 + (uint32_t)(r() % 11);
+        const int mode = (int)(r() % 6);
+        const uint32_t vmax = mode == 5 ? 100000u : 1000u;
+        uint32_t total = 0;
+        for (uint32_t j = 0; j < n; ++j) {
+            uint32_t v = 1 + (uint32_t)(r() % vmax);
+            int32_t s;
+            if (mode == 0) s = (int32_t)(r() % (2 * 60 * v + 1)) - (int32_t)(60 * v);     // any mean in [-60, 60]
+            else if (mode == 1) { const int32_t q = (int32_t)(r() % 7) - 3; s = q * (int32_t)v; }   // equal means
+            else if (mode == 2) { s = (int32_t)(r() % 5) - 2; }                             // means near 0
+            else if (mode == 3) { v = 1 + (uint32_t)(r() % 3); s = (int32_t)(r() % 9) - 4; } // tiny visits
+            else if (mode == 4 && j > 0) { v = (uint32_t)rec[0].stats + (uint32_t)(r() % 3); s = (int32_t)(rec[0].stats >> 32) + (int32_t)(r() % 3) - 1; }
+            else s = (int32_t)(r() % (2 * 20 * v + 1)) - (int32_t)(20 * v);
+            rec[j].stats = (uint64_t)v | ((uint64_t)(uint32_t)s << 32);
+            total += v;
+        }
+        if (r() % 50 == 0) rec[r() % n].stats = 0;   // an unvisited child
+        const double lnN = std::log((double)(total + (uint32_t)(r() % 5)));
+        const double c = (r() % 4 == 0) ? 0.7 + (double)(r() % 100) / 10.0 : 2.5;
+        dk::NodeHot got;
+        const uint32_t a = dk::pick_child_reg(rec, n, lnN, c, &got);
+        const uint32_t b = naive(rec, n, lnN, c);
+        if (a != b || got.stats != rec[b].stats) {
+            printf("MISMATCH case %ld n %u mode %d: got %u want %u\n", t, n, mode, a, b);
+            return 1;
+        }
+        ties += mode == 1 || mode == 4;
+    }
+    printf("OK %ld\n", cases);
+    return 0;
+}

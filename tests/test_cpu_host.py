@@ -40,7 +40,13 @@ def test_engine_rules_vs_oracle(native_bins):
 def test_engine_search_vs_oracle(native_bins):
     """search_core.h (host build) = oracle UCT: visits, f64 values bitwise, best, RNG stream."""
     assert _run("search_check", 6, 400, 5) > 10
-    assert _run("search_check", 3, 200, 6, 3) > 5   # tiny LDS path: exercises the parent-link fallback
+    assert _run("search_check", 20, 300, 17) > 30
+
+
+def test_uct_pick_filter_exact(native_bins):
+    """Filtered UCT pick (f32 estimate + exact f64 on candidates) == plain f64 UCT,
+    with the f32 reciprocal / sqrt adversarially perturbed by up to 4 ulp."""
+    assert _run("uct_pick_check", 1000000, 3) == 1000000
 
 
 def test_engine_cap_vs_oracle(native_bins):

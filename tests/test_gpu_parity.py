@@ -191,6 +191,27 @@ def test_search_parity_fdo(eng, iters):
         assert int(best[i]) == (b if b >= 0 else 255), i
 
 
+@pytest.mark.parametrize("env", [{"DK_LDS_PATH": "2"}, {"DK_ROOTS_PER_WAVE": "7"}, {"DK_ROOTS_PER_WAVE": "16"}])
+def test_search_parity_fdo_launch_variants(env, monkeypatch):
+    """Path overflow into global memory (2 LDS entries) and partial / narrow waves."""
+    import master_doko_reinforcement_learning_amd as dk
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    e = dk.Engine(device=0, max_roots=64, max_iterations=400)
+    try:
+        pool = [s for s in fdo_states(12, 23) if s.info()["phase"] != 3]
+        rng = np.random.default_rng(5)
+        pick = [pool[i] for i in rng.choice(len(pool), size=24, replace=False)]
+        seeds = rng.integers(0, 2**63, size=len(pick), dtype=np.uint64)
+        visits, values, best = dk.CachedMCTS(e, dk.GAME_FULL_DOKO).monte_carlo_tree_search(pack_all(pick), 2.5, 400, seeds)
+        for i, (b, v, val) in enumerate(_oracle_search(pick, seeds, 400, 2.5, "fdo")):
+            assert list(visits[i]) == v, i
+            assert values[i].tobytes() == np.array(val, dtype=np.float64).tobytes(), i
+            assert int(best[i]) == (b if b >= 0 else 255), i
+    finally:
+        e.close()
+
+
 def test_search_parity_doko(eng):
     import master_doko_reinforcement_learning_amd as dk
     states = []

@@ -1,0 +1,58 @@
+"""Phase breakdown of the search kernel (profiling build, -DDK_PHASE_PROF).
+
+Runs the bench workload once with libdoko_amd_prof.so and prints, per phase,
+the mean wave-clock cycles per simulation (select / expand / rollout / backup)
+plus the mean select depth.  Usage (GPU box):
+    DK_LIB=master_doko_reinforcement_learning_amd/libdoko_amd_prof.so python tools/phase_prof.py [bench args]
+"""
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import torch
+
+    import bench
+    import master_doko_reinforcement_learning_amd as dk
+    from master_doko_reinforcement_learning_amd import _native
+    sys.argv = [sys.argv[0]] + sys.argv[1:]
+    args = bench.parse()
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(0)
+    L = _native.lib()
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    eng, step, n_roots, bufs = bench.make_workload(args, dk, L, dev, stream.cuda_stream, 0, 1, 0)
+    prof = getattr(L, "dk_phase_profile", None)
+    if prof is not None:
+        prof.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]
+        out = np.zeros((n_roots, 8), dtype=np.uint64)
+        prof(eng.ctx, out.ctypes.data, n_roots)  # clear
+    step()
+    torch.cuda.synchronize(dev)
+    ms = eng.last_search_ms()
+    res = {"roots": n_roots, "iterations": args.iterations, "search_ms": ms,
+           "rpw": os.environ.get("DK_ROOTS_PER_WAVE", "64"), "layout": os.environ.get("DK_LAYOUT", "0")}
+    if prof is not None:
+        prof(eng.ctx, out.ctypes.data, n_roots)
+        sims = n_roots * args.iterations
+        tot = out[:, :4].astype(np.float64).sum(axis=0) / sims
+        res.update({"cyc_per_sim": {"select": tot[0], "expand": tot[1], "rollout": tot[2], "backup": tot[3]},
+                    "mean_depth": float(out[:, 4].astype(np.float64).sum() / sims),
+                    "forced_levels": float(out[:, 5].astype(np.float64).sum() / sims),
+                    "branch_levels": float(out[:, 6].astype(np.float64).sum() / sims),
+                    "wave_max_depth": float(out[:, 7].astype(np.float64).sum() / sims)})
+    print(json.dumps(res))
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()
