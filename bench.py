@@ -125,7 +125,7 @@ def make_workload(args, dk, L, dev, sp, rank, world, local_rank, dist=None):
             ck(L.dk_search_batch_async(eng.ctx, dk.GAME_DOKO, ptr(roots), ptr(d_srch), n_roots, iters, args.c,
                                        ptr(visits), ptr(values), ptr(best), sp))
 
-    return eng, step, n_roots, {"visits": visits, "values": values, "best": best, "roots": roots}
+    return eng, step, n_roots, {"visits": visits, "values": values, "best": best, "roots": roots, "I": I, "S_r": S_r}
 
 
 def main():
@@ -159,6 +159,7 @@ def main():
     search_ms = []
     iters = args.iterations
     visits = bufs["visits"]
+    I = bufs["I"]
 
     for _ in range(args.warmup):
         step()

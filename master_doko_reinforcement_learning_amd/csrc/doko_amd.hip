@@ -34,6 +34,10 @@ constexpr int MAX_PATH = 64;   // LDS path entries per lane (deeper paths spill 
         }                                                         \
     } while (0)
 
+// Dynamic LDS of the search kernel: [ln table (optional)][path stats][path slots]
+extern __shared__ uint64_t dk_lds[];
+constexpr uint32_t LN_LDS_MAX = 2048;   // ln(N) entries staged in LDS (16 KB)
+
 // ---------------------------------------------------------------- node pool access
 // Node pool of one root, root-major: [root][slot] so that a node's child block
 // is one contiguous run of 16-byte hot records (one or a few cache lines).
@@ -50,14 +54,24 @@ struct GpuMem {
     uint64_t* ovf_st;
     uint32_t path_stride;
     int lds_n;            // path entries held in LDS
+    const double* ln_glob;
+    bool ln_in_lds;
     uint32_t cap_slots, cap_states;
 #ifdef DK_PHASE_PROF
     uint64_t* prof;
 #endif
 
+    __device__ double ln(uint32_t v) const {
+        return ln_in_lds ? __longlong_as_double((long long)dk_lds[v]) : ln_glob[v];
+    }
     __device__ dk::NodeHot load_hot(uint32_t s) const { return hot[s]; }
     __device__ void store_hot(uint32_t s, const dk::NodeHot& h) const { hot[s] = h; }
     __device__ void store_stats(uint32_t s, uint64_t v) const { hot[s].stats = v; }
+    __device__ void store_backup(uint32_t s, uint64_t v, double q, float isv) const {
+        hot[s].stats = v;
+        hot[s].q = q;
+        hot[s].isv = isv;
+    }
     __device__ void store_child_base(uint32_t s, uint32_t child_base) const { hot[s].child_base = child_base; }
     __device__ void store_node_tail(uint32_t s, uint32_t child_base, uint32_t info) const {
         hot[s].child_base = child_base;
@@ -102,32 +116,37 @@ __global__ void __launch_bounds__(WAVE) search_kernel(const dk_state* __restrict
                                                       uint32_t cap_slots, uint32_t rpw, int lds_n,
                                                       uint32_t* visits, double* values,
                                                       uint8_t* best, int* err, uint64_t* prof) {
-    extern __shared__ uint64_t lds_raw[];   // lds_n * rpw u64 stats, then lds_n * rpw u32 slots
     const uint32_t lane = threadIdx.x;
+    const uint32_t T = iters + 1;
+    const uint32_t n_ln = T <= LN_LDS_MAX ? T : 0u;
+    for (uint32_t i = lane; i < n_ln; i += WAVE) dk_lds[i] = (uint64_t)__double_as_longlong(ln_table[i]);
+    __syncthreads();
     const uint32_t root = blockIdx.x * rpw + lane;
     if (lane >= rpw || root >= n) return;
+    uint64_t* lds_path_st = dk_lds + n_ln;
     typename E::Work w;
     E::load(roots[root], w);
     dk::Rng rng = dk::Rng::seed_from_u64(seeds[root]);
-    const uint32_t T = iters + 1;
     GpuMem<typename E::Work> mem;
     mem.hot = hot + (size_t)root * cap_slots;
     mem.cold = cold + (size_t)root * cap_slots;
     mem.states = states + (size_t)root * T;
-    mem.path_st = lds_raw + lane;
-    mem.path = reinterpret_cast<uint32_t*>(lds_raw + lds_n * rpw) + lane;
+    mem.path_st = lds_path_st + lane;
+    mem.path = reinterpret_cast<uint32_t*>(lds_path_st + lds_n * rpw) + lane;
+    mem.ln_glob = ln_table;
+    mem.ln_in_lds = n_ln != 0;
     mem.lds_n = lds_n;
     mem.path_stride = rpw;
     mem.ovf = ovf + (size_t)root * dk::MAX_DEPTH;
     mem.ovf_st = ovf_st + (size_t)root * dk::MAX_DEPTH;
     mem.cap_slots = cap_slots; mem.cap_states = T;
 #ifdef DK_PHASE_PROF
-    mem.prof = prof + (size_t)root * 8;
+    mem.prof = prof + (size_t)root * 12;
 #else
     (void)prof;
 #endif
     uint8_t b;
-    const int st = dk::search_root<E>(w, rng, iters, c, ln_table, mem, visits + (size_t)root * 39,
+    const int st = dk::search_root<E>(w, rng, iters, c, mem, visits + (size_t)root * 39,
                                       values + (size_t)root * 39, &b, nullptr);
     if (st != dk::SR_OK) atomicOr(err, 1);
     best[root] = b;
@@ -370,7 +389,7 @@ struct dk_ctx {
     bool timed = false;
     int last_error = DK_OK;
     uint64_t pool_bytes = 0;
-    uint32_t roots_per_wave = 64;   // DK_ROOTS_PER_WAVE
+    uint32_t roots_per_wave = 32;   // DK_ROOTS_PER_WAVE (32: one wave per SIMD for 32K roots, less divergence than 64)
     int lds_path = MAX_PATH;        // DK_LDS_PATH (path entries kept in LDS; tests shrink it)
     uint64_t* prof = nullptr;       // phase timers (DK_PHASE_PROF builds only)
     std::vector<void*> scratch;
@@ -414,7 +433,8 @@ hipError_t launch_search(dk_ctx* ctx, const dk_state* roots, const uint64_t* see
                          double c, uint32_t* visits, double* values, uint8_t* best, hipStream_t st) {
     const uint32_t rpw = ctx->roots_per_wave;
     const int lds_n = ctx->lds_path;
-    hipLaunchKernelGGL(search_kernel<E>, dim3(grid_for(n, rpw)), dim3(WAVE), (size_t)lds_n * rpw * 12, st,
+    const size_t lds_bytes = (iters + 1 <= LN_LDS_MAX ? (size_t)(iters + 1) * 8 : 0) + (size_t)lds_n * rpw * 12;
+    hipLaunchKernelGGL(search_kernel<E>, dim3(grid_for(n, rpw)), dim3(WAVE), lds_bytes, st,
                        roots, seeds, n, iters, c, ctx->ln_table, ctx->hot, ctx->cold,
                        (typename E::Work*)ctx->states, ctx->ovf, ctx->ovf_st, ctx->cap_slots, rpw, lds_n, visits, values, best,
                        ctx->err, ctx->prof);
@@ -477,8 +497,8 @@ dk_ctx* dk_create(const dk_config* cfg) {
         if (v >= 1 && v <= MAX_PATH) ctx->lds_path = v;
     }
 #ifdef DK_PHASE_PROF
-    ok = ok && hipMalloc(&ctx->prof, R * 8 * sizeof(uint64_t)) == hipSuccess;
-    ok = ok && hipMemset(ctx->prof, 0, R * 8 * sizeof(uint64_t)) == hipSuccess;
+    ok = ok && hipMalloc(&ctx->prof, R * 12 * sizeof(uint64_t)) == hipSuccess;
+    ok = ok && hipMemset(ctx->prof, 0, R * 12 * sizeof(uint64_t)) == hipSuccess;
 #endif
     if (ok) {
         // ln(N) exactly as glibc `log` computes it — what Rust's f64::ln calls (node.rs:253).
@@ -518,8 +538,8 @@ int dk_last_error(const dk_ctx* ctx) { return ctx ? ctx->last_error : DK_E_INVAL
 int dk_phase_profile(dk_ctx* ctx, uint64_t* out, uint32_t n) {
     if (!ctx || !ctx->prof || n > ctx->max_roots) return DK_E_INVALID;
     DK_HIP(hipDeviceSynchronize());
-    DK_HIP(hipMemcpy(out, ctx->prof, (size_t)n * 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
-    DK_HIP(hipMemset(ctx->prof, 0, (size_t)ctx->max_roots * 8 * sizeof(uint64_t)));
+    DK_HIP(hipMemcpy(out, ctx->prof, (size_t)n * 12 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    DK_HIP(hipMemset(ctx->prof, 0, (size_t)ctx->max_roots * 12 * sizeof(uint64_t)));
     return DK_OK;
 }
 #endif

@@ -11,7 +11,8 @@
 // MI355X layout (not the reference's pointer tree).  Every node owns a
 // contiguous child block reserved at its first expansion (size = number of
 // actions it allows).  A node is split into
-//   hot  (16 B): stats (visits low 32 | integer win_score high 32), child_base, info
+//   hot  (32 B): stats (visits low 32 | integer win_score high 32), child_base, info,
+//                the exact f64 mean and an f32 1/sqrt(visits), both refreshed at backup
 //   cold (16 B): unexpanded actions, parent, action   -- touched at expansion only
 // so one tree level of the selection is ONE round trip: the child block's hot
 // records (contiguous) are loaded together, the UCT pick is computed in
@@ -42,8 +43,9 @@ namespace dk {
 #if defined(DK_PHASE_PROF) && defined(__HIP_DEVICE_COMPILE__)
 #define DK_STAMP(t) const uint64_t t = __builtin_amdgcn_s_memtime()
 #define DK_PROF(mem, k, v) prof_acc[k] += (v)
-#define DK_PROF_DECL uint64_t prof_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}
-#define DK_PROF_FLUSH(mem) for (int k_ = 0; k_ < 8; ++k_) mem.prof_add(k_, prof_acc[k_])
+#define DK_PROF_DECL uint64_t prof_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}
+#define DK_PROF_FLUSH(mem) for (int k_ = 0; k_ < 12; ++k_) mem.prof_add(k_, prof_acc[k_])
+#define DK_STAMP_DRAINED(t) __builtin_amdgcn_s_waitcnt(0); const uint64_t t = __builtin_amdgcn_s_memtime()
 #define DK_PROF_WAVEMAX(k, v) do { int m_ = (v); for (int o_ = 32; o_ >= 1; o_ >>= 1) { const int t_ = __shfl_xor(m_, o_); m_ = t_ > m_ ? t_ : m_; } prof_acc[k] += (uint64_t)m_; } while (0)
 #else
 #define DK_STAMP(t) [[maybe_unused]] const uint64_t t = 0
@@ -51,12 +53,16 @@ namespace dk {
 #define DK_PROF_DECL
 #define DK_PROF_FLUSH(mem) ((void)0)
 #define DK_PROF_WAVEMAX(k, v) ((void)0)
+#define DK_STAMP_DRAINED(t) [[maybe_unused]] const uint64_t t = 0
 #endif
 
-struct alignas(16) NodeHot {
+struct alignas(32) NodeHot {
     uint64_t stats;       // visits (low 32) | win_score (high 32, two's complement)
     uint32_t child_base;  // first slot of the child block (valid when nchild > 0)
     uint32_t info;        // nchild:6 | player:2 | has_unexpanded:1 | chain_head:1 | state_idx:22
+    double q;             // win_score / visits exactly as the reference computes it (0 if unvisited)
+    float isv;            // ~1/sqrt(visits) (f32 estimate for the UCT filter)
+    uint32_t pad;
 };
 struct alignas(16) NodeCold {
     uint64_t unexpanded;  // actions not yet expanded
@@ -89,98 +95,120 @@ DK_HD double mean_of(uint64_t st) {
 }
 
 // Exact UCT value of one child (node.rs:238-277), the reference's f64 ops in order.
-DK_HD double uct_exact(uint64_t st, bool flat, double min_q, double max_q, double lnN, double c) {
+// (q = the child's mean as computed by mean_of)
+DK_HD double uct_exact(uint64_t st, double q, bool flat, double min_q, double max_q, double lnN, double c) {
     const uint32_t v = (uint32_t)st;
     if (v == 0) return INFINITY;
-    const double nq = flat ? 1.0 : 2.0 * (mean_of(st) - min_q) / (max_q - min_q) - 1.0;
+    const double nq = flat ? 1.0 : 2.0 * (q - min_q) / (max_q - min_q) - 1.0;
     return nq + c * sqrt(lnN / (double)v);
 }
 
 #if defined(__HIP_DEVICE_COMPILE__)
 DK_HD float rcp_approx(float x) { return __builtin_amdgcn_rcpf(x); }
 DK_HD float sqrt_approx(float x) { return __builtin_amdgcn_sqrtf(x); }
+DK_HD float rsqrt_approx(float x) { return __builtin_amdgcn_rsqf(x); }
 #elif defined(DK_APPROX_HOOKS)   // host tests: adversarially perturbed approximations
 float rcp_approx(float x);
 float sqrt_approx(float x);
+float rsqrt_approx(float x);
 #else
 DK_HD float rcp_approx(float x) { return 1.0f / x; }
 DK_HD float sqrt_approx(float x) { return sqrtf(x); }
+DK_HD float rsqrt_approx(float x) { return 1.0f / sqrtf(x); }
 #endif
 
-// UCT pick over a child block of n <= SCAN_REG records held in registers;
-// returns the index, *pick_rec receives the picked record.  Bit-exact with
-// the reference's first-strict-maximum over f64 UCT values, computed as:
-//  1. sibling min / max of the means by exact integer cross-multiplication
-//     (rounding s/v to f64 is monotone, so the exact extreme is the f64 extreme);
-//  2. every child's UCT value estimated in f32 from exact integer numerators,
-//     error < B (|u_f32 - u_f64| <= ~5e-6 for |mean| <= 100);
-//  3. exact f64 UCT only for children whose estimate is within 2B of the best
-//     estimate (all others are strictly below the maximum), first strict max.
-// Blocks whose mean spread is tiny but non-zero (< 1e-7, only reachable past
-// ~3000 visits) take the exact path for every child.
-DK_HD uint32_t pick_child_reg(const NodeHot* rec, uint32_t n, double lnN, double c, NodeHot* pick_rec) {
-    // 1. exact argmin / argmax of s/v (v = 0 counts as 0/1)
-    int64_t smin = 0, smax = 0, vmin = 1, vmax = 1;
+// Child block of n <= SCAN_REG records held in registers, structure of arrays
+// (constant indices only, so everything stays in VGPRs).
+struct Block {
+    uint64_t st[SCAN_REG];
+    uint32_t cb[SCAN_REG], inf[SCAN_REG];
+    double q[SCAN_REG];
+    float isv[SCAN_REG];
+};
+
+// UCT pick over a register block; returns the index and the picked node's
+// stats / child_base / info.  Bit-exact with the reference's first-strict-
+// maximum over f64 UCT values:
+//  1. sibling min / max over the stored exact means (the reference's values);
+//  2. every child's UCT value estimated in f32 from the same f64 differences
+//     and the stored 1/sqrt(v): |u_f32 - u_f64| <= B with
+//     B ~ 4e-7 * (2 + c*sqrt(ln N)) + 5e-7 (derivation in DESIGN.md);
+//  3. exact f64 UCT only for children whose estimate is within 2B (taken
+//     with a x3.7 safety factor) of the best estimate -- all others are
+//     strictly below the maximum -- first strict maximum among them.  The
+//     first two candidates are gathered with selects; more is rare and takes
+//     a full exact pass.
+DK_HD uint32_t pick_child_reg(const Block& b, uint32_t n, double lnN, double c, uint64_t* p_st, uint32_t* p_cb,
+                              uint32_t* p_inf) {
+    double min_q = INFINITY, max_q = -INFINITY;
 #pragma unroll
     for (int j = 0; j < SCAN_REG; ++j) {
         if ((uint32_t)j < n) {
-            const uint32_t v = (uint32_t)rec[j].stats;
-            const int64_t sj = v ? (int64_t)(int32_t)(rec[j].stats >> 32) : 0, vj = v ? (int64_t)v : 1;
-            if (j == 0) { smin = smax = sj; vmin = vmax = vj; }
-            else {
-                if (sj * vmin < smin * vj) { smin = sj; vmin = vj; }
-                if (sj * vmax > smax * vj) { smax = sj; vmax = vj; }
-            }
+            min_q = b.q[j] < min_q ? b.q[j] : min_q;
+            max_q = b.q[j] > max_q ? b.q[j] : max_q;
         }
     }
-    const double min_q = (double)smin / (double)vmin, max_q = (double)smax / (double)vmax;
-    const bool flat = fabs(max_q - min_q) < DK_F64_EPSILON;
-    const bool exact_all = !flat && (max_q - min_q) < 1e-7;
-    // 2. f32 estimates: nq = 2 * (s_j v_m - s_m v_j) v_M / (v_j (s_M v_m - s_m v_M)) - 1
-    const float num_r = (float)(smax * vmin - smin * vmax);
-    const float inv_r = flat ? 0.0f : rcp_approx(num_r);
-    const float lnf = (float)lnN, cf = (float)c;
+    const double range = max_q - min_q;
+    const bool flat = fabs(range) < DK_F64_EPSILON;
+    const float inv_r = flat ? 0.0f : 2.0f * rcp_approx((float)range);
+    const float ex = (float)c * sqrt_approx((float)lnN);
     float ue[SCAN_REG];
     float umax = -INFINITY;
 #pragma unroll
     for (int j = 0; j < SCAN_REG; ++j) {
-        ue[j] = -INFINITY;
-        if ((uint32_t)j < n) {
-            const uint32_t v = (uint32_t)rec[j].stats;
-            const int64_t sj = (int64_t)(int32_t)(rec[j].stats >> 32);
-            const float vf = (float)v;
-            const float ivf = rcp_approx(vf);
-            const float nq = flat ? 1.0f
-                                  : 2.0f * ((float)(sj * vmin - smin * (int64_t)v) * (float)vmax * ivf * inv_r) - 1.0f;
-            const float u = nq + cf * sqrt_approx(lnf * ivf);
-            ue[j] = v == 0 ? INFINITY : u;
-            umax = ue[j] > umax ? ue[j] : umax;
-        }
+        const float nq = flat ? 1.0f : (float)(b.q[j] - min_q) * inv_r - 1.0f;
+        const float u = (uint32_t)b.st[j] == 0 ? INFINITY : nq + ex * b.isv[j];
+        ue[j] = (uint32_t)j < n ? u : -INFINITY;
+        umax = ue[j] > umax ? ue[j] : umax;
     }
-    const float cut = umax - 1e-4f * (1.0f + fabsf(cf));   // 2B
-    // 3. exact f64 UCT over the candidates, first strict maximum
-    double best = -INFINITY;
-    uint32_t pick = 0;
-    NodeHot pr = rec[0];
+    const float cut = umax - 3e-6f * (3.0f + fabsf(ex));
+    uint64_t s1 = b.st[0], s2 = b.st[0];
+    double q1 = b.q[0], q2 = b.q[0];
+    uint32_t j1 = 0, j2 = 0, nc = 0;
 #pragma unroll
     for (int j = 0; j < SCAN_REG; ++j) {
-        if ((uint32_t)j < n && (exact_all || ue[j] >= cut)) {
-            const double u = uct_exact(rec[j].stats, flat, min_q, max_q, lnN, c);
-            if (u > best) { best = u; pick = (uint32_t)j; pr = rec[j]; }
+        const bool cj = ue[j] >= cut;   // implies j < n
+        const bool first = cj && nc == 0, second = cj && nc == 1;
+        s1 = first ? b.st[j] : s1; q1 = first ? b.q[j] : q1; j1 = first ? (uint32_t)j : j1;
+        s2 = second ? b.st[j] : s2; q2 = second ? b.q[j] : q2; j2 = second ? (uint32_t)j : j2;
+        nc += cj ? 1u : 0u;
+    }
+    double best = uct_exact(s1, q1, flat, min_q, max_q, lnN, c);
+    uint32_t pick = j1;
+    if (nc == 2) {
+        const double u2 = uct_exact(s2, q2, flat, min_q, max_q, lnN, c);
+        if (u2 > best) { best = u2; pick = j2; }
+    } else if (nc > 2) {
+        best = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < SCAN_REG; ++j) {
+            if (ue[j] >= cut) {
+                const double u = uct_exact(b.st[j], b.q[j], flat, min_q, max_q, lnN, c);
+                if (u > best) { best = u; pick = (uint32_t)j; }
+            }
         }
     }
-    *pick_rec = pr;
+    uint64_t ps = b.st[0];
+    uint32_t pc = b.cb[0], pi = b.inf[0];
+#pragma unroll
+    for (int j = 1; j < SCAN_REG; ++j) {
+        ps = (uint32_t)j == pick ? b.st[j] : ps;
+        pc = (uint32_t)j == pick ? b.cb[j] : pc;
+        pi = (uint32_t)j == pick ? b.inf[j] : pi;
+    }
+    *p_st = ps; *p_cb = pc; *p_inf = pi;
     return pick;
 }
 
 template <class E, class Mem>
-DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, double c, const double* ln_table,
+DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, double c,
                       Mem& mem, uint32_t* visits39, double* values39, uint8_t* best_out, uint64_t* ctr_scanned) {
     using Work = typename E::Work;
     {
         const uint64_t ra = E::allowed(root, true);
         NodeHot h;
         h.stats = 0; h.child_base = 0; h.info = ni_make(0, (uint32_t)E::current_player(root), ra != 0, false, 0);
+        h.q = 0.0; h.isv = 0.0f; h.pad = 0;
         NodeCold cd;
         cd.unexpanded = ra; cd.parent = 0xFFFFFFFFu; cd.action = 0xFFu;
         mem.store_hot(0, h);
@@ -205,22 +233,35 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
             const uint32_t n = ni_nchild(x.info);
             uint32_t pick;
             NodeHot y;
-            if (n == 1) {
-                // single child: a chain head jumps straight to its chain end
-                pick = 0;
-                chain_head = ni_head(x.info) ? slot : 0xFFFFFFFFu;
-                y = mem.load_hot(x.child_base);
-            } else if (n <= (uint32_t)SCAN_REG) {
-                NodeHot rec[SCAN_REG];
+            if (n <= (uint32_t)SCAN_REG) {
+                // one round trip for every lane of the wave: forced (n == 1) and
+                // branching blocks load together
+                DK_STAMP_DRAINED(tl0);
+                const double lnN = mem.ln(x_visits);
+                Block blk;
 #pragma unroll
                 for (int j = 0; j < SCAN_REG; ++j) {
-                    if ((uint32_t)j < n) rec[j] = mem.load_hot(x.child_base + (uint32_t)j);
-                    else { rec[j].stats = 0; rec[j].child_base = 0; rec[j].info = 0; }
+                    if ((uint32_t)j < n) {
+                        const NodeHot h = mem.load_hot(x.child_base + (uint32_t)j);
+                        blk.st[j] = h.stats; blk.cb[j] = h.child_base; blk.inf[j] = h.info; blk.q[j] = h.q; blk.isv[j] = h.isv;
+                    } else {
+                        blk.st[j] = 0; blk.cb[j] = 0; blk.inf[j] = 0; blk.q[j] = 0.0; blk.isv[j] = 0.0f;
+                    }
                 }
-                pick = pick_child_reg(rec, n, ln_table[x_visits], c, &y);
+                DK_STAMP_DRAINED(tl1);
+                DK_PROF(mem, 8, tl1 - tl0);
+                if (n == 1) {
+                    // single child: a chain head's child_base is its chain end
+                    pick = 0;
+                    y.stats = blk.st[0]; y.child_base = blk.cb[0]; y.info = blk.inf[0];
+                } else {
+                    pick = pick_child_reg(blk, n, lnN, c, &y.stats, &y.child_base, &y.info);
+                }
+                DK_STAMP_DRAINED(tl2);
+                DK_PROF(mem, 9, tl2 - tl1);
             } else {
                 // generic block (never produced by the doko engines, whose nodes offer <= 12 actions)
-                const double lnN = ln_table[x_visits];
+                const double lnN = mem.ln(x_visits);
                 double min_q = INFINITY, max_q = -INFINITY;
                 for (uint32_t j = 0; j < n; ++j) {
                     const double q = mean_of(mem.load_hot(x.child_base + j).stats);
@@ -233,17 +274,11 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
                 y = mem.load_hot(x.child_base);
                 for (uint32_t j = 0; j < n; ++j) {
                     const NodeHot r = mem.load_hot(x.child_base + j);
-                    const uint32_t v = (uint32_t)r.stats;
-                    double u;
-                    if (v == 0) u = INFINITY;
-                    else {
-                        const double nq = flat ? 1.0 : 2.0 * (mean_of(r.stats) - min_q) / (max_q - min_q) - 1.0;
-                        u = nq + c * sqrt(lnN / (double)v);
-                    }
+                    const double u = uct_exact(r.stats, mean_of(r.stats), flat, min_q, max_q, lnN, c);
                     if (u > best) { best = u; pick = j; y = r; }
                 }
             }
-            if (n > 1) chain_head = 0xFFFFFFFFu;
+            chain_head = (n == 1 && ni_head(x.info)) ? slot : 0xFFFFFFFFu;
             scanned += n;
             DK_PROF(mem, n == 1 ? 5 : 6, 1);
             const uint32_t child = x.child_base + pick;
@@ -287,7 +322,7 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
             E::step(w, a);
             const uint64_t ca = E::allowed(w, false);
             NodeHot ch;
-            ch.stats = 0; ch.child_base = 0;
+            ch.stats = 0; ch.child_base = 0; ch.q = 0.0; ch.isv = 0.0f; ch.pad = 0;
             ch.info = ni_make(0, (uint32_t)E::current_player(w), ca != 0, slot == 0 || block >= 2, next_state);
             NodeCold cc;
             cc.unexpanded = ca; cc.parent = slot; cc.action = (uint32_t)a;
@@ -312,7 +347,8 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
         for (int k = depth; k >= 1; --k) {
             uint64_t st;
             const uint32_t e = mem.path_get(k, &st);
-            mem.store_stats(e & 0x3FFFFFFFu, st + (((uint64_t)(uint32_t)sel4i(r, (int)(e >> 30)) << 32) | 1ULL));
+            const uint64_t ns = st + (((uint64_t)(uint32_t)sel4i(r, (int)(e >> 30)) << 32) | 1ULL);
+            mem.store_backup(e & 0x3FFFFFFFu, ns, mean_of(ns), rsqrt_approx((float)(uint32_t)ns));
         }
         mem.store_stats(0, (uint64_t)(it + 1));
         if (it + 1 == iters) (void)rng.next_u64();  // random_bool((1f32/1000f32) as f64)

@@ -48,9 +48,10 @@ int main(int argc, char** argv) {
     uint64_t scanned = 0;
     for (int j = 0; j < nroots; ++j) {
         HostMem<dk::fdo::Work> mem(40 + 12 * iters, iters + 1, 128);
+        mem.ln_table = ln.data();
         dk::Rng r2 = dk::Rng::seed_from_u64(0xC3300000ULL + j);
         uint32_t v[39]; double val[39]; uint8_t b; uint64_t sc = 0;
-        dk::search_root<dk::FdoE>(roots[j], r2, iters, 2.5, ln.data(), mem, v, val, &b, &sc);
+        dk::search_root<dk::FdoE>(roots[j], r2, iters, 2.5, mem, v, val, &b, &sc);
         scanned += sc; sink += v[0];
     }
     double ss = std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();

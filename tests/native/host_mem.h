@@ -13,6 +13,8 @@ struct HostMem {
     std::vector<W> states;
     std::vector<uint32_t> path;
     std::vector<uint64_t> path_st;
+    const double* ln_table = nullptr;
+    double ln(uint32_t v) const { return ln_table[v]; }
     // `mp` = entries of the fast (LDS) part of the path on the GPU; the host keeps
     // the overflow in the same vector, so `mp` only matters to the GPU layout.
     HostMem(uint32_t slots, uint32_t nstates, uint32_t mp)
@@ -21,6 +23,7 @@ struct HostMem {
     dk::NodeHot load_hot(uint32_t s) { return hot[s]; }
     void store_hot(uint32_t s, const dk::NodeHot& h) { hot[s] = h; }
     void store_stats(uint32_t s, uint64_t v) { hot[s].stats = v; }
+    void store_backup(uint32_t s, uint64_t v, double q, float isv) { hot[s].stats = v; hot[s].q = q; hot[s].isv = isv; }
     void store_child_base(uint32_t s, uint32_t cb) { hot[s].child_base = cb; }
     void store_node_tail(uint32_t s, uint32_t cb, uint32_t info) { hot[s].child_base = cb; hot[s].info = info; }
     dk::NodeCold load_cold(uint32_t s) { return cold[s]; }

@@ -27,9 +27,10 @@ static void compare(const dk_state& packed, const OEnv& oenv, uint64_t seed, uin
                     const double* ln, uint32_t max_path, int idx, const char* name) {
     typename E::Work w; E::load(packed, w);
     HostMem<typename E::Work> mem(40 + 12 * iters, iters + 1, max_path);
+    mem.ln_table = ln;
     dk::Rng rng = dk::Rng::seed_from_u64(seed);
     uint32_t v[39]; double val[39]; uint8_t best;
-    int st = dk::search_root<E>(w, rng, iters, c, ln, mem, v, val, &best, nullptr);
+    int st = dk::search_root<E>(w, rng, iters, c, mem, v, val, &best, nullptr);
     if (st != 0) fail("capacity", idx);
     SmallRng r = SmallRng::seed_from_u64(seed);
     Mcts<OEnv> m;

@@ -20,6 +20,7 @@ static float perturb(float y) {
 }
 float dk::rcp_approx(float x) { return perturb(1.0f / x); }
 float dk::sqrt_approx(float x) { return perturb(sqrtf(x)); }
+float dk::rsqrt_approx(float x) { return perturb(1.0f / sqrtf(x)); }
 
 static uint32_t naive(const dk::NodeHot* rec, uint32_t n, double lnN, double c) {
     double min_q = INFINITY, max_q = -INFINITY;
@@ -32,7 +33,7 @@ static uint32_t naive(const dk::NodeHot* rec, uint32_t n, double lnN, double c) 
     double best = -INFINITY;
     uint32_t pick = 0;
     for (uint32_t j = 0; j < n; ++j) {
-        const double u = dk::uct_exact(rec[j].stats, flat, min_q, max_q, lnN, c);
+        const double u = dk::uct_exact(rec[j].stats, dk::mean_of(rec[j].stats), flat, min_q, max_q, lnN, c);
         if (u > best) { best = u; pick = j; }
     }
     return pick;
@@ -62,12 +63,21 @@ int main(int argc, char** argv) {
             total += v;
         }
         if (r() % 50 == 0) rec[r() % n].stats = 0;   // an unvisited child
+        for (uint32_t j = 0; j < n; ++j) {                // what the backup stores next to the stats
+            rec[j].q = dk::mean_of(rec[j].stats);
+            rec[j].isv = (uint32_t)rec[j].stats ? dk::rsqrt_approx((float)(uint32_t)rec[j].stats) : 0.0f;
+        }
         const double lnN = std::log((double)(total + (uint32_t)(r() % 5)));
         const double c = (r() % 4 == 0) ? 0.7 + (double)(r() % 100) / 10.0 : 2.5;
-        dk::NodeHot got;
-        const uint32_t a = dk::pick_child_reg(rec, n, lnN, c, &got);
+        dk::Block blk;
+        for (int j = 0; j < dk::SCAN_REG; ++j) {
+            blk.st[j] = rec[j].stats; blk.cb[j] = (uint32_t)j * 7; blk.inf[j] = (uint32_t)j * 13;
+            blk.q[j] = rec[j].q; blk.isv[j] = rec[j].isv;
+        }
+        uint64_t gs; uint32_t gc, gi;
+        const uint32_t a = dk::pick_child_reg(blk, n, lnN, c, &gs, &gc, &gi);
         const uint32_t b = naive(rec, n, lnN, c);
-        if (a != b || got.stats != rec[b].stats) {
+        if (a != b || gs != rec[b].stats || gc != b * 7 || gi != b * 13) {
             printf("MISMATCH case %ld n %u mode %d: got %u want %u\n", t, n, mode, a, b);
             return 1;
         }

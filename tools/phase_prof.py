@@ -34,7 +34,7 @@ def main():
     prof = getattr(L, "dk_phase_profile", None)
     if prof is not None:
         prof.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]
-        out = np.zeros((n_roots, 8), dtype=np.uint64)
+        out = np.zeros((n_roots, 12), dtype=np.uint64)
         prof(eng.ctx, out.ctypes.data, n_roots)  # clear
     step()
     torch.cuda.synchronize(dev)
@@ -49,7 +49,9 @@ def main():
                     "mean_depth": float(out[:, 4].astype(np.float64).sum() / sims),
                     "forced_levels": float(out[:, 5].astype(np.float64).sum() / sims),
                     "branch_levels": float(out[:, 6].astype(np.float64).sum() / sims),
-                    "wave_max_depth": float(out[:, 7].astype(np.float64).sum() / sims)})
+                    "wave_max_depth": float(out[:, 7].astype(np.float64).sum() / sims),
+                    "select_load_cyc": float(out[:, 8].astype(np.float64).sum() / sims),
+                    "select_pick_cyc": float(out[:, 9].astype(np.float64).sum() / sims)})
     print(json.dumps(res))
     eng.close()
 
