@@ -45,7 +45,7 @@ def lib():
     global _lib
     if _lib is not None:
         return _lib
-    path = os.environ.get("DK_LIB", LIB_PATH)
+    path = os.environ.get("DK_LIB") or LIB_PATH
     if not os.path.exists(path):
         raise ImportError("libdoko_amd.so not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
                           "(hipcc --offload-arch=gfx950); there is no CPU fallback")

@@ -490,6 +490,10 @@ DK_HD int key_fast(uint32_t c, uint32_t tm, uint32_t lead) {
 }
 
 // Card phase to the end (w.phase == PH_PLAYCARD).  Returns plies played.
+// The trick is evaluated incrementally as its cards are played (running best
+// key = first strict maximum, eyes, Diamond-Ace players), so completing a trick
+// is a handful of register updates: with the lanes of a wave at different trick
+// positions, the wave no longer pays a full trick evaluation on most plies.
 DK_HD int rollout_cards(const Work& w0, Rng& rng, int pts[4]) {
     // hands as "kinds held" / "kinds held twice" (removal takes the second copy first)
     uint32_t any0, any1, any2, any3, two0, two1, two2, two3;
@@ -508,10 +512,19 @@ DK_HD int rollout_cards(const Work& w0, Rng& rng, int pts[4]) {
     const uint32_t wedding_player = w0.wedding_player;
     uint32_t theta = ann_thetas(team_kind, solved, re_players, w0.re_lowest, w0.contra_lowest);
     uint32_t cur = w0.cur, trick_start = w0.trick_start, trick_len = w0.trick_len, n_tricks = w0.n_tricks;
-    uint32_t trick_cards = w0.trick_cards;
     uint32_t eyes = w0.eyes, ntr = w0.ntricks, doko = w0.doko;
     uint32_t fox_n = w0.fox_n, fox0 = w0.fox0, fox1 = w0.fox1, karl = w0.karl;
-    uint32_t lead = trick_len ? class_mask(trick_cards & 0xFFu, tm) : 0xFFFFFFu;
+    // running evaluation of the current trick (cards already on the table replayed)
+    uint32_t lead = 0xFFFFFFu, best_pos = 0, win_card = 0, t_eyes = 0, da_n = 0, da0 = 0, da1 = 0;
+    int best_key = -2;
+    for (uint32_t i = 0; i < trick_len; ++i) {
+        const uint32_t c = (w0.trick_cards >> (8u * i)) & 0xFFu;
+        if (i == 0) lead = class_mask(c, tm);
+        const int k = key_fast(c, tm, lead);
+        if (k > best_key) { best_key = k; best_pos = i; win_card = c; }
+        t_eyes += eyes_fast(c);
+        if (c == (uint32_t)DIAMOND_ACE) { const uint32_t pl = (trick_start + i) & 3u; if (da_n == 0) da0 = pl; else da1 = pl; da_n += 1; }
+    }
     int plies = 0;
     for (;;) {
         // ---- one card for `cur`
@@ -536,51 +549,47 @@ DK_HD int rollout_cards(const Work& w0, Rng& rng, int pts[4]) {
         any0 = cur == 0u ? na : any0; any1 = cur == 1u ? na : any1; any2 = cur == 2u ? na : any2; any3 = cur == 3u ? na : any3;
         two0 = cur == 0u ? nt : two0; two1 = cur == 1u ? nt : two1; two2 = cur == 2u ? nt : two2; two3 = cur == 3u ? nt : two3;
         nb -= 1u << (8u * cur);
-        lead = trick_len == 0u ? class_mask(card, tm) : lead;
-        trick_cards |= card << (8u * trick_len);
+        // ---- running trick evaluation (complete_trick, spread over the four cards)
+        const bool first = trick_len == 0u;
+        lead = first ? class_mask(card, tm) : lead;
+        const int key = key_fast(card, tm, lead);
+        const bool better = first || key > best_key;
+        best_key = better ? key : best_key;
+        best_pos = better ? trick_len : best_pos;
+        win_card = better ? card : win_card;
+        t_eyes = (first ? 0u : t_eyes) + eyes_fast(card);
+        da_n = first ? 0u : da_n;
+        const bool is_da = card == (uint32_t)DIAMOND_ACE;
+        da0 = (is_da && da_n == 0u) ? cur : da0;
+        da1 = (is_da && da_n == 1u) ? cur : da1;
+        da_n += is_da ? 1u : 0u;
         trick_len += 1u;
         cur = (cur + 1u) & 3u;
         plies += 1;
         if (trick_len == 4u) {
-            // ---- trick complete (complete_trick)
-            const uint32_t c0 = trick_cards & 0xFFu, c1 = (trick_cards >> 8) & 0xFFu;
-            const uint32_t c2 = (trick_cards >> 16) & 0xFFu, c3 = trick_cards >> 24;
-            int bk = key_fast(c0, tm, lead);
-            uint32_t bi = 0, wc = c0;
-            const int k1 = key_fast(c1, tm, lead), k2 = key_fast(c2, tm, lead), k3 = key_fast(c3, tm, lead);
-            if (k1 > bk) { bk = k1; bi = 1; wc = c1; }
-            if (k2 > bk) { bk = k2; bi = 2; wc = c2; }
-            if (k3 > bk) { bk = k3; bi = 3; wc = c3; }
-            const uint32_t winner = (trick_start + bi) & 3u;
-            const uint32_t e = eyes_fast(c0) + eyes_fast(c1) + eyes_fast(c2) + eyes_fast(c3);
+            const uint32_t winner = (trick_start + best_pos) & 3u;
             const uint32_t sh = 8u * winner;
-            eyes += e << sh;
+            eyes += t_eyes << sh;
             ntr += 1u << sh;
-            doko += (e >= 40u ? 1u : 0u) << sh;
-            // foxes in play order
-#pragma unroll
-            for (uint32_t i = 0; i < 4; ++i) {
-                const uint32_t ci = (trick_cards >> (8u * i)) & 0xFFu;
-                if (ci == (uint32_t)DIAMOND_ACE) {
-                    const uint32_t ev = (((trick_start + i) & 3u) << 2) | winner;
-                    fox0 = fox_n == 0u ? ev : fox0;
-                    fox1 = fox_n == 0u ? fox1 : ev;
-                    fox_n += 1u;
-                }
+            doko += (t_eyes >= 40u ? 1u : 0u) << sh;
+            // Diamond-Ace events in play order (fox0 / fox1)
+            if (da_n != 0u) {
+                const uint32_t e0 = (da0 << 2) | winner, e1 = (da1 << 2) | winner;
+                fox0 = fox_n == 0u ? e0 : fox0;
+                fox1 = fox_n == 1u ? e0 : fox1;
+                fox_n += 1u;
+                if (da_n == 2u) { fox1 = fox_n == 1u ? e1 : fox1; fox_n += 1u; }
             }
             const uint32_t t = n_tricks - 1u;
-            if (t == 11u && wc == (uint32_t)CLUB_JACK) karl = 1u + winner;
-            if (team_kind == TK_WED_UNSOLVED && t < 3u) {
-                if (winner != wedding_player) {
-                    team_kind = TK_WED_SOLVED; solved = t; re_players = (1u << wedding_player) | (1u << winner);
-                    theta = ann_thetas(team_kind, solved, re_players, w0.re_lowest, w0.contra_lowest);
-                } else if (t == 2u) {
-                    team_kind = TK_WED_SOLVED; solved = 2; re_players = 1u << wedding_player;
-                    theta = ann_thetas(team_kind, solved, re_players, w0.re_lowest, w0.contra_lowest);
-                }
+            karl = (t == 11u && win_card == (uint32_t)CLUB_JACK) ? 1u + winner : karl;
+            if (team_kind == TK_WED_UNSOLVED && t < 3u && (winner != wedding_player || t == 2u)) {
+                team_kind = TK_WED_SOLVED;
+                solved = winner != wedding_player ? t : 2u;
+                re_players = (1u << wedding_player) | (winner != wedding_player ? 1u << winner : 0u);
+                theta = ann_thetas(team_kind, solved, re_players, w0.re_lowest, w0.contra_lowest);
             }
             if (n_tricks == 12u) break;
-            cur = winner; trick_start = winner; trick_cards = 0; trick_len = 0; n_tricks += 1u;
+            cur = winner; trick_start = winner; trick_len = 0; n_tricks += 1u;
         }
         // ---- collapsed announcement round: one forced NoAnnouncement draw per offered player
         const uint32_t d = (uint32_t)popc32(((nb | 0x80808080u) - theta) & 0x80808080u);
@@ -595,16 +604,36 @@ DK_HD int rollout_cards(const Work& w0, Rng& rng, int pts[4]) {
     return plies;
 }
 
+// The rest of a pending announcement round when nobody announces: the asked
+// player and each later player of the round (4 - ann_turns asks in all) with a
+// non-empty offer take one forced NoAnnouncement draw; then the card phase
+// resumes with the player who started the round (announcement.rs:137-180).
+DK_HD int collapse_announcement_round(Work& w, Rng& rng) {
+    const uint32_t theta = ann_thetas(w.team_kind, w.solved_trick, w.re_players, w.re_lowest, w.contra_lowest);
+    const uint32_t asks = 4u - (uint32_t)w.ann_turns;
+    int draws = 1;   // the asked player (its offer is non-empty)
+#pragma unroll
+    for (uint32_t i = 1; i < 4; ++i) {
+        const uint32_t p = ((uint32_t)w.cur + i) & 3u;
+        const bool offered = (uint32_t)hand_len(w, (int)p) >= ((theta >> (8u * p)) & 0xFFu);
+        draws += (i < asks && offered) ? 1 : 0;
+    }
+    for (int i = 0; i < draws; ++i) rng.advance();
+    w.ann_turns = 4; w.ann_allowed = 0; w.cur = w.ann_start; w.phase = PH_PLAYCARD;
+    return draws;
+}
+
 // Returns the rewards (player_points) and the number of plies played.
 DK_HD int rollout(Work w, Rng& rng, int pts[4]) {
     int plies = 0;
-    // Generic steps until the card phase (reservation / pending announcement round).
-    while (w.phase != PH_PLAYCARD && w.phase != PH_FINISHED) {
+    // Generic steps through the reservation round.
+    while (w.phase == PH_RESERVATION) {
         const uint64_t a = legal_actions(w) & ~ANN_ACTIONS;
         const int act = ctz64(random_single(a, rng));
         play_action(w, act);
         plies++;
     }
+    if (w.phase == PH_ANNOUNCEMENT) plies += collapse_announcement_round(w, rng);
     if (w.phase == PH_FINISHED) { score(w, pts); return plies; }
     return plies + rollout_cards(w, rng, pts);
 }

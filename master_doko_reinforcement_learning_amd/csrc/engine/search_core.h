@@ -204,11 +204,15 @@ template <class E, class Mem>
 DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, double c,
                       Mem& mem, uint32_t* visits39, double* values39, uint8_t* best_out, uint64_t* ctr_scanned) {
     using Work = typename E::Work;
+    // the root's structure (child_base, info) lives in registers: it changes only
+    // when the root itself is expanded, and its visits are the iteration count
+    uint32_t root_cb = 0, root_info;
     {
         const uint64_t ra = E::allowed(root, true);
         NodeHot h;
         h.stats = 0; h.child_base = 0; h.info = ni_make(0, (uint32_t)E::current_player(root), ra != 0, false, 0);
         h.q = 0.0; h.isv = 0.0f; h.pad = 0;
+        root_info = h.info;
         NodeCold cd;
         cd.unexpanded = ra; cd.parent = 0xFFFFFFFFu; cd.action = 0xFFu;
         mem.store_hot(0, h);
@@ -224,7 +228,8 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
         DK_STAMP(t0);
         // ---------------- selection
         uint32_t slot = 0;
-        NodeHot x = mem.load_hot(0);
+        NodeHot x;
+        x.stats = (uint64_t)it; x.child_base = root_cb; x.info = root_info;
         uint32_t x_visits = it;   // root visits == completed iterations
         int depth = 0;
         uint32_t chain_head = 0xFFFFFFFFu;   // head whose skip pointer led to x
@@ -297,7 +302,9 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
         // ---------------- expansion
         Work w;
         if (ni_open(x.info)) {
+            // both loads in flight together (the state index is already known)
             NodeCold cd = mem.load_cold(slot);
+            w = mem.load_state(ni_state(x.info));
             const uint64_t bit = random_single(cd.unexpanded, rng);
             const int a = ctz64(bit);
             uint32_t nch = ni_nchild(x.info);
@@ -313,12 +320,12 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
             cd.unexpanded &= ~bit;
             const uint32_t child = x.child_base + nch;
             nch += 1;
-            mem.store_node_tail(slot, x.child_base,
-                                ni_make(nch, ni_player(x.info), cd.unexpanded != 0, ni_head(x.info), ni_state(x.info)));
+            const uint32_t new_info = ni_make(nch, ni_player(x.info), cd.unexpanded != 0, ni_head(x.info), ni_state(x.info));
+            mem.store_node_tail(slot, x.child_base, new_info);
+            if (slot == 0) { root_cb = x.child_base; root_info = new_info; }
             mem.store_unexpanded(slot, cd.unexpanded);
             // a forced chain grew: its head now points at the new end
             if (block == 1 && chain_head != 0xFFFFFFFFu) mem.store_child_base(chain_head, child);
-            w = mem.load_state(ni_state(x.info));
             E::step(w, a);
             const uint64_t ca = E::allowed(w, false);
             NodeHot ch;
