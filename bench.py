@@ -45,7 +45,7 @@ def parse():
     p.add_argument("--fusion", choices=["maxn", "avg"], default="maxn")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=0)
-    p.add_argument("--cpu-roots-per-thread", type=int, default=64)
+    p.add_argument("--cpu-roots-per-thread", type=int, default=96)
     return p.parse_args()
 
 
@@ -190,17 +190,12 @@ def main():
     result = None
     if rank == 0:
         cpu = None
-        alg = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu, alg = cpu_baseline(args, dk)
-        if alg is None:
-            alg = {"b_sim": None}
-        b_sim = alg.get("b_sim")
-        if b_sim is None:
-            # measured oracle means on C3 roots (children scanned 42.7, path 22.5 nodes)
-            b_sim = 128 + 16 * 42.7 + 32 * 22.5 + 32
-        achieved = n_roots * iters * b_sim / (kernel_ms / 1e3) / 1e9
-        traffic = pmc_traffic(n_roots, iters)
+            cpu = cpu_baseline(args, dk)
+        b_sim = alg_bytes_per_sim(args.workload)
+        achieved = n_roots * iters * b_sim / (kernel_ms / 1e3) / 1e9 if b_sim else None
+        traffic = pmc_traffic(n_roots, iters) if args.workload == "c3" else None
+        stream_peak = stream_copy_gbs(torch, dev)
         result = {
             "metric": METRIC,
             "value": sims_total / elapsed,
@@ -225,16 +220,20 @@ def main():
                 "fusion": args.fusion if args.workload == "c3" else None,
                 "parallelism": "dp%d (samples split over GPUs, RCCL all-reduce of fusion accumulators)" % world,
             },
+            "kernel_only_rollouts_per_s": n_roots * iters * world / (kernel_ms / 1e3),
             "search_kernel_ms": kernel_ms,
             "roofline": {
                 "bound": "hbm",
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS,
+                "frac": achieved / HBM_PEAK_GBS if achieved else None,
                 "traffic": traffic,
                 "alg_bytes_per_sim": b_sim,
-                "note": "integer/branch-bound search; algorithmic bytes per simulation from the oracle's counters",
+                "stream_copy_peak_measured_gbs": stream_peak,
+                "note": "the search is VALU/SALU-issue bound (one 32-root wave per SIMD, PMC: ~65% of wave cycles "
+                        "issuing); HBM bytes are the SURVEY 8(d) algorithmic model from the oracle's counters, "
+                        "traffic = 2*FETCH_SIZE+WRITE_SIZE from profiles/pmc_search.json scaled per launch",
             },
             "cpu_baseline": cpu,
         }
@@ -268,20 +267,12 @@ def cpu_baseline(args, dk):
             smp = st.card_matching(ol.rng_seed(0xC3200000 + j * args.samples + s))
             roots.append(smp)
             seeds.append(0xC3300000 + j * args.samples + s)
-        search_many = ol.lib().or_fdo_search_many
         handles = (ctypes.c_void_p * n)(*[r.h for r in roots])
         vis = (ctypes.c_uint32 * (39 * n))()
         sd = ol.arr(ctypes.c_uint64, n, seeds)
-        secs = search_many(None, handles, sd, n, iters, args.c, vis, threads)
-        # algorithmic-byte model inputs: mean children scanned / path nodes per simulation
-        scanned = path = sims = 0
-        for r, s in zip(roots[:8], seeds[:8]):
-            _, _, _, ctr = r.search(ol.rng_seed(s), iters, args.c)
-            sims += ctr[0]
-            scanned += ctr[1]
-            path += ctr[2]
-        alg = {"children_scanned": scanned / sims, "path_nodes": path / sims}
-        alg["b_sim"] = 128 + 16 * alg["children_scanned"] + 32 * alg["path_nodes"] + 32
+        secs = ol.lib().or_fdo_search_many(None, handles, sd, n, iters, args.c, vis, threads)
+        n1 = min(n, 64)
+        secs1 = ol.lib().or_fdo_search_many(None, handles, sd, n1, iters, args.c, vis, 1)
     else:
         for k in range(n):
             st = ol.DoState.new_game(0xD0C00000 + k)
@@ -291,8 +282,10 @@ def cpu_baseline(args, dk):
             seeds.append((k * 0x9E3779B97F4A7C15 + 1) & 0xFFFFFFFFFFFFFFFF)
         handles = (ctypes.c_void_p * n)(*[r.h for r in roots])
         vis = (ctypes.c_uint32 * (39 * n))()
-        secs = ol.lib().or_do_search_many(handles, ol.arr(ctypes.c_uint64, n, seeds), n, iters, args.c, vis, threads)
-        alg = None
+        sd = ol.arr(ctypes.c_uint64, n, seeds)
+        secs = ol.lib().or_do_search_many(handles, sd, n, iters, args.c, vis, threads)
+        n1 = min(n, 64)
+        secs1 = ol.lib().or_do_search_many(handles, sd, n1, iters, args.c, vis, 1)
     model = ""
     try:
         model = subprocess.run(["lscpu"], capture_output=True, text=True).stdout
@@ -301,8 +294,37 @@ def cpu_baseline(args, dk):
         model = platform.processor()
     cpu = {"value": n * iters / secs, "unit": "rollouts/s", "cores": threads, "kind": "port",
            "sample": "%d roots x %d sims of the same workload (oracle C++ restatement, root-parallel like MCTSWorkers), "
-                     "%.1f s wall on %d threads of %s" % (n, iters, secs, threads, model)}
-    return cpu, alg
+                     "%.1f s wall on %d threads of %s; 1-thread figure on the first %d roots"
+                     % (n, iters, secs, threads, model, n1),
+           "value_1_thread": n1 * iters / secs1}
+    return cpu
+
+
+def alg_bytes_per_sim(workload):
+    """SURVEY.md 8(d) byte model per simulation, measured by tools/alg_bytes.py
+    on the oracle (committed as profiles/alg_bytes_c3.json)."""
+    path = os.path.join(ROOT, "profiles", "alg_bytes_%s.json" % workload)
+    if not os.path.exists(path):
+        return None
+    with open(path) as fh:
+        return json.load(fh)["b_sim"]
+
+
+def stream_copy_gbs(torch, dev, nbytes=1 << 31, reps=10):
+    """Measured device-to-device copy rate (read + write bytes / time) on this box."""
+    a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    gbs = 2.0 * nbytes * reps / (e0.elapsed_time(e1) / 1e3) / 1e9
+    del a, b
+    return gbs
 
 
 def pmc_traffic(n_roots, iters):
