@@ -10,8 +10,10 @@
  *
  * Two flavours of every batched call:
  *   dk_xxx(...)        host pointers; the call copies in/out and synchronises.
- *   dk_xxx_async(...)  device pointers + an opaque stream handle (hipStream_t,
- *                      NULL = the context's stream); nothing is synchronised.
+ *   dk_xxx_async(...)  device pointers + an opaque stream handle (hipStream_t);
+ *                      nothing is synchronised.  NULL selects the context's own
+ *                      non-blocking stream, which is NOT ordered after work queued
+ *                      on the legacy default stream: pass the caller's stream.
  *
  * Reference interfaces (file:line under /root/reference):
  *   McEnvState trait ......... rs-doko-mcts/src/env/env_state.rs:7-28

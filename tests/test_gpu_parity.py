@@ -275,6 +275,54 @@ def test_fusion_parity(eng):
         assert int(got_a[i]) == ea
 
 
+def test_fusion_sharded_accumulators(eng):
+    """The multi-GPU split of bench.py on one device: each 'rank' accumulates its
+    half of every infostate's samples, the accumulators are summed (what the RCCL
+    all-reduce does), and the select equals the oracle's fusion over all samples."""
+    import torch
+
+    from master_doko_reinforcement_learning_amd import _native
+    import master_doko_reinforcement_learning_amd as dk
+    L = _native.lib()
+    rng = np.random.default_rng(11)
+    n_info, S, world = 24, 16, 2
+    visits = rng.integers(0, 40, size=(n_info, S, 39)).astype(np.uint32)
+    visits[:, :, 28:] = 0
+    allowed = rng.integers(1, 2**39, size=n_info, dtype=np.uint64)
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.Stream(dev)
+    with torch.cuda.stream(stream):
+        sp = stream.cuda_stream
+        d_allowed = torch.tensor(allowed.view(np.int64), device=dev)
+        for mode in (dk.FUSE_MAXN, dk.FUSE_AVG):
+            tot_u = torch.zeros((n_info, 39), dtype=torch.int32, device=dev)
+            tot_f = torch.zeros((n_info, 39), dtype=torch.float32, device=dev)
+            for r in range(world):
+                part = np.ascontiguousarray(visits[:, r * S // world:(r + 1) * S // world])
+                d_v = torch.tensor(part.view(np.int32), device=dev)
+                acc_u = torch.zeros((n_info, 39), dtype=torch.int32, device=dev)
+                acc_f = torch.zeros((n_info, 39), dtype=torch.float32, device=dev)
+                assert L.dk_fuse_accumulate_async(eng.ctx, d_v.data_ptr(), n_info, S // world, d_allowed.data_ptr(),
+                                                  mode, acc_u.data_ptr(), acc_f.data_ptr(), sp) == 0
+                tot_u += acc_u
+                tot_f += acc_f
+            act = torch.zeros(n_info, dtype=torch.uint8, device=dev)
+            assert L.dk_fuse_select_async(eng.ctx, n_info, mode, d_allowed.data_ptr(), tot_u.data_ptr(),
+                                          tot_f.data_ptr(), act.data_ptr(), sp) == 0
+            assert L.dk_sync(eng.ctx, sp) == 0
+            got = act.cpu().numpy()
+            for i in range(n_info):
+                rows = [list(map(int, r)) for r in visits[i]]
+                if mode == dk.FUSE_MAXN:
+                    want, _ = ol.fuse_maxn(rows, int(allowed[i]))
+                    assert int(got[i]) == want, i
+                else:
+                    want, probs = ol.fuse_avg(rows)
+                    top = sorted(probs)[-2:]
+                    if top[1] - top[0] > 1e-4:
+                        assert int(got[i]) == want, i
+
+
 def test_decide_end_to_end(eng):
     """DefaultImpiPolicy: CAP samples -> UCT -> MaxN fusion, against the oracle pipeline."""
     import master_doko_reinforcement_learning_amd as dk
