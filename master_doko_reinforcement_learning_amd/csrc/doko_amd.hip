@@ -43,26 +43,30 @@ constexpr uint32_t LN_LDS_MAX = 2048;   // ln(N) entries staged in LDS (16 KB)
 // is one contiguous run of 16-byte hot records (one or a few cache lines).
 // Only the owning lane ever touches a root's tree, so plain loads and stores
 // (L1-cacheable, program-ordered within the lane) are sufficient.
-template <class W>
+template <class W, bool LN_LDS>
 struct GpuMem {
     dk::NodeHot* hot;
     dk::NodeCold* cold;
     W* states;
-    uint32_t* path;       // LDS, this lane's column (stride path_stride)
-    uint64_t* path_st;    // LDS, stats read on the way down
-    uint32_t* ovf;        // global overflow of the path (entries >= MAX_PATH)
+    // LDS regions are addressed as offsets into dk_lds (u64 words) so that the
+    // compiler keeps the LDS address space (ds_* instructions, not flat_*)
+    uint32_t path_st_off; // path stats: dk_lds[path_st_off + k*stride]
+    uint32_t path_off;    // path slots: ((uint32_t*)dk_lds)[path_off + k*stride]
+    uint32_t* ovf;        // global overflow of the path (entries >= lds_n)
     uint64_t* ovf_st;
     uint32_t path_stride;
     int lds_n;            // path entries held in LDS
     const double* ln_glob;
-    bool ln_in_lds;
     uint32_t cap_slots, cap_states;
 #ifdef DK_PHASE_PROF
     uint64_t* prof;
 #endif
 
     __device__ double ln(uint32_t v) const {
-        return ln_in_lds ? __longlong_as_double((long long)dk_lds[v]) : ln_glob[v];
+        // one address space per instantiation: a runtime choice would make the compiler
+        // select between pointers and emit flat loads
+        if constexpr (LN_LDS) return __longlong_as_double((long long)dk_lds[v]);
+        else return ln_glob[v];
     }
     __device__ dk::NodeHot load_hot(uint32_t s) const { return hot[s]; }
     __device__ void store_hot(uint32_t s, const dk::NodeHot& h) const { hot[s] = h; }
@@ -82,18 +86,19 @@ struct GpuMem {
     __device__ void store_unexpanded(uint32_t s, uint64_t u) const { cold[s].unexpanded = u; }
     __device__ W load_state(uint32_t i) const { return states[i]; }
     __device__ void store_state(uint32_t i, const W& w) const { states[i] = w; }
-    __device__ uint32_t path_get(int k, uint64_t* st) const {
-        if (k < lds_n) {
-            *st = path_st[k * path_stride];
-            return path[k * path_stride];
-        }
+    __device__ int lds_entries() const { return lds_n; }
+    __device__ uint32_t path_get_lds(int k, uint64_t* st) const {
+        *st = dk_lds[path_st_off + k * path_stride];
+        return reinterpret_cast<const uint32_t*>(dk_lds)[path_off + k * path_stride];
+    }
+    __device__ uint32_t path_get_ovf(int k, uint64_t* st) const {
         *st = ovf_st[k - lds_n];
         return ovf[k - lds_n];
     }
     __device__ void path_set(int k, uint32_t v, uint64_t st) const {
         if (k < lds_n) {
-            path[k * path_stride] = v;
-            path_st[k * path_stride] = st;
+            reinterpret_cast<uint32_t*>(dk_lds)[path_off + k * path_stride] = v;
+            dk_lds[path_st_off + k * path_stride] = st;
         } else {
             ovf[k - lds_n] = v;
             ovf_st[k - lds_n] = st;
@@ -107,7 +112,7 @@ struct GpuMem {
 // ---------------------------------------------------------------- kernels
 // One lane per root, `rpw` roots per 64-lane wave (lanes >= rpw idle).  The
 // LDS holds each lane's selection path: MAX_PATH x (u32 slot|player, u64 stats).
-template <class E>
+template <class E, bool LN_LDS>
 __global__ void __launch_bounds__(WAVE) search_kernel(const dk_state* __restrict__ roots,
                                                       const uint64_t* __restrict__ seeds, uint32_t n,
                                                       uint32_t iters, double c, const double* __restrict__ ln_table,
@@ -118,23 +123,24 @@ __global__ void __launch_bounds__(WAVE) search_kernel(const dk_state* __restrict
                                                       uint8_t* best, int* err, uint64_t* prof) {
     const uint32_t lane = threadIdx.x;
     const uint32_t T = iters + 1;
-    const uint32_t n_ln = T <= LN_LDS_MAX ? T : 0u;
+    const uint32_t n_ln = LN_LDS ? T : 0u;
     for (uint32_t i = lane; i < n_ln; i += WAVE) dk_lds[i] = (uint64_t)__double_as_longlong(ln_table[i]);
     __syncthreads();
     const uint32_t root = blockIdx.x * rpw + lane;
     if (lane >= rpw || root >= n) return;
-    uint64_t* lds_path_st = dk_lds + n_ln;
+    const uint32_t n_ln16 = (n_ln + 1u) & ~1u;                           // keep the next region 16-B aligned
+    const uint32_t path_st_base = n_ln16;
+    const uint32_t path_base32 = 2u * (path_st_base + (uint32_t)lds_n * rpw);   // in u32 units
     typename E::Work w;
     E::load(roots[root], w);
     dk::Rng rng = dk::Rng::seed_from_u64(seeds[root]);
-    GpuMem<typename E::Work> mem;
+    GpuMem<typename E::Work, LN_LDS> mem;
     mem.hot = hot + (size_t)root * cap_slots;
     mem.cold = cold + (size_t)root * cap_slots;
     mem.states = states + (size_t)root * T;
-    mem.path_st = lds_path_st + lane;
-    mem.path = reinterpret_cast<uint32_t*>(lds_path_st + lds_n * rpw) + lane;
+    mem.path_st_off = path_st_base + lane;
+    mem.path_off = path_base32 + lane;
     mem.ln_glob = ln_table;
-    mem.ln_in_lds = n_ln != 0;
     mem.lds_n = lds_n;
     mem.path_stride = rpw;
     mem.ovf = ovf + (size_t)root * dk::MAX_DEPTH;
@@ -433,11 +439,17 @@ hipError_t launch_search(dk_ctx* ctx, const dk_state* roots, const uint64_t* see
                          double c, uint32_t* visits, double* values, uint8_t* best, hipStream_t st) {
     const uint32_t rpw = ctx->roots_per_wave;
     const int lds_n = ctx->lds_path;
-    const size_t lds_bytes = (iters + 1 <= LN_LDS_MAX ? (size_t)(iters + 1) * 8 : 0) + (size_t)lds_n * rpw * 12;
-    hipLaunchKernelGGL(search_kernel<E>, dim3(grid_for(n, rpw)), dim3(WAVE), lds_bytes, st,
-                       roots, seeds, n, iters, c, ctx->ln_table, ctx->hot, ctx->cold,
-                       (typename E::Work*)ctx->states, ctx->ovf, ctx->ovf_st, ctx->cap_slots, rpw, lds_n, visits, values, best,
-                       ctx->err, ctx->prof);
+    const size_t lds_bytes = (iters + 1 <= LN_LDS_MAX ? (size_t)((iters + 2) & ~1u) * 8 : 0) + (size_t)lds_n * rpw * 12;
+    if (iters + 1 <= LN_LDS_MAX)
+        hipLaunchKernelGGL((search_kernel<E, true>), dim3(grid_for(n, rpw)), dim3(WAVE), lds_bytes, st,
+                           roots, seeds, n, iters, c, ctx->ln_table, ctx->hot, ctx->cold,
+                           (typename E::Work*)ctx->states, ctx->ovf, ctx->ovf_st, ctx->cap_slots, rpw, lds_n, visits,
+                           values, best, ctx->err, ctx->prof);
+    else
+        hipLaunchKernelGGL((search_kernel<E, false>), dim3(grid_for(n, rpw)), dim3(WAVE), lds_bytes, st,
+                           roots, seeds, n, iters, c, ctx->ln_table, ctx->hot, ctx->cold,
+                           (typename E::Work*)ctx->states, ctx->ovf, ctx->ovf_st, ctx->cap_slots, rpw, lds_n, visits,
+                           values, best, ctx->err, ctx->prof);
     return hipGetLastError();
 }
 

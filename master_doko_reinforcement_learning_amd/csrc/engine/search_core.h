@@ -347,13 +347,23 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
         DK_PROF(mem, 1, t2 - t1);
         // ---------------- rollout
         int r[4];
-        E::rollout(w, rng, r);
+        [[maybe_unused]] const int rplies = E::rollout(w, rng, r);
+        DK_PROF(mem, 10, (uint64_t)rplies);
+        DK_PROF_WAVEMAX(11, rplies);
         DK_STAMP(t3);
         DK_PROF(mem, 2, t3 - t2);
         // ---------------- backup (leaf -> root): stores of the stats read on the way down
-        for (int k = depth; k >= 1; --k) {
+        // (two loops: the global overflow part and the LDS part keep distinct address spaces)
+        const int k_lds = depth < mem.lds_entries() - 1 ? depth : mem.lds_entries() - 1;
+        for (int k = depth; k > k_lds; --k) {
             uint64_t st;
-            const uint32_t e = mem.path_get(k, &st);
+            const uint32_t e = mem.path_get_ovf(k, &st);
+            const uint64_t ns = st + (((uint64_t)(uint32_t)sel4i(r, (int)(e >> 30)) << 32) | 1ULL);
+            mem.store_backup(e & 0x3FFFFFFFu, ns, mean_of(ns), rsqrt_approx((float)(uint32_t)ns));
+        }
+        for (int k = k_lds; k >= 1; --k) {
+            uint64_t st;
+            const uint32_t e = mem.path_get_lds(k, &st);
             const uint64_t ns = st + (((uint64_t)(uint32_t)sel4i(r, (int)(e >> 30)) << 32) | 1ULL);
             mem.store_backup(e & 0x3FFFFFFFu, ns, mean_of(ns), rsqrt_approx((float)(uint32_t)ns));
         }

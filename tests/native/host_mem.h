@@ -31,6 +31,8 @@ struct HostMem {
     void store_unexpanded(uint32_t s, uint64_t u) { cold[s].unexpanded = u; }
     W load_state(uint32_t i) { return states[i]; }
     void store_state(uint32_t i, const W& w) { states[i] = w; }
-    uint32_t path_get(int k, uint64_t* st) { *st = path_st[k]; return path[k]; }
+    int lds_entries() const { return (int)max_path; }
+    uint32_t path_get_lds(int k, uint64_t* st) { *st = path_st[k]; return path[k]; }
+    uint32_t path_get_ovf(int k, uint64_t* st) { *st = path_st[k]; return path[k]; }
     void path_set(int k, uint32_t v, uint64_t st) { path[k] = v; path_st[k] = st; }
 };

@@ -51,7 +51,9 @@ def main():
                     "branch_levels": float(out[:, 6].astype(np.float64).sum() / sims),
                     "wave_max_depth": float(out[:, 7].astype(np.float64).sum() / sims),
                     "select_load_cyc": float(out[:, 8].astype(np.float64).sum() / sims),
-                    "select_pick_cyc": float(out[:, 9].astype(np.float64).sum() / sims)})
+                    "select_pick_cyc": float(out[:, 9].astype(np.float64).sum() / sims),
+                    "rollout_plies": float(out[:, 10].astype(np.float64).sum() / sims),
+                    "rollout_plies_wave_max": float(out[:, 11].astype(np.float64).sum() / sims)})
     print(json.dumps(res))
     eng.close()
 
