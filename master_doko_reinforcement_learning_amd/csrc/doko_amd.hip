@@ -147,7 +147,7 @@ __global__ void __launch_bounds__(WAVE) search_kernel(const dk_state* __restrict
     mem.ovf_st = ovf_st + (size_t)root * dk::MAX_DEPTH;
     mem.cap_slots = cap_slots; mem.cap_states = T;
 #ifdef DK_PHASE_PROF
-    mem.prof = prof + (size_t)root * 12;
+    mem.prof = prof + (size_t)root * 16;
 #else
     (void)prof;
 #endif
@@ -509,8 +509,8 @@ dk_ctx* dk_create(const dk_config* cfg) {
         if (v >= 1 && v <= MAX_PATH) ctx->lds_path = v;
     }
 #ifdef DK_PHASE_PROF
-    ok = ok && hipMalloc(&ctx->prof, R * 12 * sizeof(uint64_t)) == hipSuccess;
-    ok = ok && hipMemset(ctx->prof, 0, R * 12 * sizeof(uint64_t)) == hipSuccess;
+    ok = ok && hipMalloc(&ctx->prof, R * 16 * sizeof(uint64_t)) == hipSuccess;
+    ok = ok && hipMemset(ctx->prof, 0, R * 16 * sizeof(uint64_t)) == hipSuccess;
 #endif
     if (ok) {
         // ln(N) exactly as glibc `log` computes it — what Rust's f64::ln calls (node.rs:253).
@@ -550,8 +550,8 @@ int dk_last_error(const dk_ctx* ctx) { return ctx ? ctx->last_error : DK_E_INVAL
 int dk_phase_profile(dk_ctx* ctx, uint64_t* out, uint32_t n) {
     if (!ctx || !ctx->prof || n > ctx->max_roots) return DK_E_INVALID;
     DK_HIP(hipDeviceSynchronize());
-    DK_HIP(hipMemcpy(out, ctx->prof, (size_t)n * 12 * sizeof(uint64_t), hipMemcpyDeviceToHost));
-    DK_HIP(hipMemset(ctx->prof, 0, (size_t)ctx->max_roots * 12 * sizeof(uint64_t)));
+    DK_HIP(hipMemcpy(out, ctx->prof, (size_t)n * 16 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    DK_HIP(hipMemset(ctx->prof, 0, (size_t)ctx->max_roots * 16 * sizeof(uint64_t)));
     return DK_OK;
 }
 #endif

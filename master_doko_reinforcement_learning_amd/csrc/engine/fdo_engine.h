@@ -143,6 +143,61 @@ DK_HD uint32_t allowed_announcements(const Work& w, int player, int n) {
     return rem;
 }
 
+// ---- card-phase rollout fast path ------------------------------------------------
+// The card phase of a rollout rewritten for a 64-wide SIMD: 32-bit words only,
+// selects instead of branches, and the per-card announcement round reduced to
+// arithmetic.  With nobody announcing, player p is offered an announcement
+// after a card iff its hand size n_p >= theta_p (allowed_announcements is
+// monotone in n; the thresholds change only when a wedding is resolved), so
+// the forced NoAnnouncement draws of a round are popc over 4 byte compares.
+//
+//   theta (own levels)  = 11 - ws - |prev & {Re,90,60,30}|      unless Black is in prev
+//   theta (counter)     = 11 - ws - |enemy levels|               if enemy announced and
+//                                                                prev has neither Re nor Counter
+// (calc_announcement.rs:51-229; derivation in DESIGN.md).  Equality with the
+// step-by-step path is checked by tests/native/fdo_engine_check and the GPU tests.
+DK_HD uint32_t ann_theta(uint32_t prev, uint32_t enemy, int ws) {
+    uint32_t t = 99u;
+    if (!(prev & AN_BLACK)) t = (uint32_t)(11 - ws - popc32(prev & 0xFu));
+    if ((enemy & 0x1Fu) && !(prev & (AN_COUNTER | AN_RE))) {
+        const uint32_t tc = (uint32_t)(11 - ws - popc32(enemy & 0x1Fu));
+        t = tc < t ? tc : t;
+    }
+    return t;
+}
+// theta_p packed one byte per player (99 = never offered)
+DK_HD uint32_t ann_thetas(uint32_t team_kind, uint32_t solved_trick, uint32_t re_players, uint32_t re_lowest,
+                          uint32_t contra_lowest) {
+    if (team_kind == TK_WED_UNSOLVED || team_kind == TK_INRES) return 0x63636363u;
+    const int ws = team_kind == TK_WED_SOLVED ? (int)solved_trick : 0;
+    const uint32_t pr = all_higher_than(re_lowest), pk = all_higher_than(contra_lowest);
+    const uint32_t tre = ann_theta(pr, pk, ws), tko = ann_theta(pk, pr, ws);
+    uint32_t out = 0;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) out |= (((re_players >> p) & 1u) ? tre : tko) << (8 * p);
+    return out;
+}
+DK_HD uint32_t sel4u(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, uint32_t p) {
+    const uint32_t lo = (p & 1u) ? a1 : a0, hi = (p & 1u) ? a3 : a2;
+    return (p & 2u) ? hi : lo;
+}
+// trump rank nibbles (same table as trump_rank), 8 cards per word
+DK_HD uint32_t rank_fast(uint32_t c) {
+    const uint32_t wv = c < 8u ? 0xC0318420u : (c < 16u ? 0xB7202195u : 0x31A62031u);
+    return (wv >> (4u * (c & 7u))) & 15u;
+}
+DK_HD uint32_t suit_of(uint32_t c) { return (c * 43u) >> 8; }   // c / 6 for c < 24
+DK_HD uint32_t eyes_fast(uint32_t c) { return (0xB432A0u >> (4u * (c - 6u * suit_of(c)))) & 15u; }
+// colour class mask of card c (trumps, or its suit minus trumps)
+DK_HD uint32_t class_mask(uint32_t c, uint32_t tm) {
+    return ((tm >> c) & 1u) ? tm : ((0x3Fu << (6u * suit_of(c))) & ~tm);
+}
+// key of card c in a trick led with colour class `lead` (trick_key)
+DK_HD int key_fast(uint32_t c, uint32_t tm, uint32_t lead) {
+    const int k_t = 32 + (int)rank_fast(c), k_c = (int)eyes_fast(c);
+    return ((tm >> c) & 1u) ? k_t : (((lead >> c) & 1u) ? k_c : -1);
+}
+
 // announcement.rs:182-215 (the announcing player's team decides which lowest moves)
 DK_HD void internal_play_announcement(Work& w, int player, uint32_t ann) {
     if (ann == 0) { w.ann_turns += 1; return; }  // NoAnnouncement
@@ -150,18 +205,31 @@ DK_HD void internal_play_announcement(Work& w, int player, uint32_t ann) {
     if (w.ann_count < 12) { w.ann_count += 1; w.ann_players |= (uint8_t)(1u << player); }
     if ((w.re_players >> player) & 1) w.re_lowest = (uint8_t)ann; else w.contra_lowest = (uint8_t)ann;
 }
-// announcement.rs:137-180. Returns true if the round is over.
+// announcement.rs:137-180. Returns true if the round is over.  The players are
+// asked in order from `player`; one without an offer passes automatically
+// (number_of_turns_without_announcement += 1) and the round ends after four
+// consecutive passes.  Offers are non-empty iff hand size >= theta (see
+// ann_theta), so the first player to ask is found from the thresholds and only
+// that player's offer set is computed.
 DK_HD bool internal_progress(Work& w, int player) {
-    int cp = player;
-    for (int guard = 0; guard < 8; ++guard) {
-        if (w.ann_turns == 4) { w.ann_allowed = 0; w.cur = w.ann_start; return true; }
-        const uint32_t a = allowed_announcements(w, cp, hand_len(w, cp));
-        if (a == 0) { internal_play_announcement(w, cp, 0); }
-        else { w.ann_allowed = (uint8_t)a; w.cur = (uint8_t)cp; return false; }
-        cp = (cp + 1) & 3;
+    const uint32_t theta = ann_thetas(w.team_kind, w.solved_trick, w.re_players, w.re_lowest, w.contra_lowest);
+    const uint32_t t = w.ann_turns;
+    uint32_t found = 4;   // index (from `player`) of the first offered player within the round
+#pragma unroll
+    for (uint32_t i = 0; i < 4; ++i) {
+        const uint32_t p = ((uint32_t)player + i) & 3u;
+        const bool offered = (uint32_t)hand_len(w, (int)p) >= ((theta >> (8u * p)) & 0xFFu);
+        found = (found == 4u && i + t < 4u && offered) ? i : found;
     }
-    w.ann_allowed = 0; w.cur = w.ann_start;
-    return true;
+    if (found == 4u) {
+        w.ann_turns = 4; w.ann_allowed = 0; w.cur = w.ann_start;
+        return true;
+    }
+    const int p = (player + (int)found) & 3;
+    w.ann_turns = (uint8_t)(t + found);
+    w.ann_allowed = (uint8_t)allowed_announcements(w, p, hand_len(w, p));
+    w.cur = (uint8_t)p;
+    return false;
 }
 // state.rs:184-206
 DK_HD void progress_next_card_or_announcement(Work& w) {
@@ -253,17 +321,18 @@ DK_HD void finish_reservations(Work& w) {
 // One completed trick: winner, eyes, scoring accumulators, wedding resolution.
 // Returns the winner.
 DK_HD int complete_trick(Work& w) {
-    const uint32_t tc = card_color((int)(w.trick_cards & 0xFF), w.game_type);
+    const uint32_t tm = trump_mask(w.game_type);
+    const uint32_t lead = class_mask(w.trick_cards & 0xFFu, tm);
     int best_key = -2, best_i = 0;
     uint32_t e = 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const int c = (int)((w.trick_cards >> (8 * i)) & 0xFF);
-        const int k = trick_key(c, tc, w.game_type);
+        const uint32_t c = (w.trick_cards >> (8 * i)) & 0xFFu;
+        const int k = key_fast(c, tm, lead);
         const bool better = k > best_key;
         best_key = better ? k : best_key;
         best_i = better ? i : best_i;
-        e += card_eyes(c);
+        e += eyes_fast(c);
     }
     const int winner = (w.trick_start + best_i) & 3;
     const int win_card = (int)((w.trick_cards >> (8 * best_i)) & 0xFF);
@@ -317,10 +386,17 @@ DK_HD bool play_card_core(Work& w, int card) {
     return false;
 }
 
-// FdoState::play_action (state.rs:208-358) for any phase.
+// FdoState::play_action (state.rs:208-358) for any phase.  The three action
+// kinds share ONE announcement-round progression (internal_progress), so a wave
+// whose lanes play different kinds of actions runs it once.
 DK_HD void play_action(Work& w, int a) {
+    int start = -1;   // player the announcement round continues from (-1: no round step)
     if (a <= 23) {
-        if (!play_card_core(w, a)) progress_next_card_or_announcement(w);
+        if (!play_card_core(w, a)) {   // progress_next_card_or_announcement (state.rs:184-206)
+            w.ann_turns = 0;
+            w.ann_start = w.cur;
+            start = w.cur;
+        }
     } else if (a <= 32) {
         // FdoAction order -> FdoReservation discriminant (nibble a-24 of 0x768543210)
         w.res = byte_set(w.res, w.res_len, (uint32_t)((0x768543210ULL >> (4 * (a - 24))) & 15));
@@ -329,14 +405,16 @@ DK_HD void play_action(Work& w, int a) {
         if (w.res_len == 4) {
             finish_reservations(w);
             w.trick_cards = 0; w.trick_len = 0; w.trick_start = w.cur; w.n_tricks = 1;
-            progress_next_card_or_announcement(w);
+            w.ann_turns = 0;
+            w.ann_start = w.cur;
+            start = w.cur;
         }
     } else {
         const int cp = w.cur;
         internal_play_announcement(w, cp, a < A_NOANN ? (1u << (a - 33)) : 0u);
-        const bool over = internal_progress(w, (cp + 1) & 3);
-        if (over) w.phase = PH_PLAYCARD;
+        start = (cp + 1) & 3;
     }
+    if (start >= 0) w.phase = internal_progress(w, start) ? PH_PLAYCARD : PH_ANNOUNCEMENT;
 }
 
 // ---- DKV scoring (stats/stats.rs:46-243 and stats/**) -------------------------
@@ -432,61 +510,6 @@ DK_HD int round_draws(const Work& w) {
 #pragma unroll
     for (int p = 0; p < 4; ++p) d += allowed_announcements(w, p, hand_len(w, p)) != 0 ? 1 : 0;
     return d;
-}
-
-// ---- card-phase rollout fast path ------------------------------------------------
-// The card phase of a rollout rewritten for a 64-wide SIMD: 32-bit words only,
-// selects instead of branches, and the per-card announcement round reduced to
-// arithmetic.  With nobody announcing, player p is offered an announcement
-// after a card iff its hand size n_p >= theta_p (allowed_announcements is
-// monotone in n; the thresholds change only when a wedding is resolved), so
-// the forced NoAnnouncement draws of a round are popc over 4 byte compares.
-//
-//   theta (own levels)  = 11 - ws - |prev & {Re,90,60,30}|      unless Black is in prev
-//   theta (counter)     = 11 - ws - |enemy levels|               if enemy announced and
-//                                                                prev has neither Re nor Counter
-// (calc_announcement.rs:51-229; derivation in DESIGN.md).  Equality with the
-// step-by-step path is checked by tests/native/fdo_engine_check and the GPU tests.
-DK_HD uint32_t ann_theta(uint32_t prev, uint32_t enemy, int ws) {
-    uint32_t t = 99u;
-    if (!(prev & AN_BLACK)) t = (uint32_t)(11 - ws - popc32(prev & 0xFu));
-    if ((enemy & 0x1Fu) && !(prev & (AN_COUNTER | AN_RE))) {
-        const uint32_t tc = (uint32_t)(11 - ws - popc32(enemy & 0x1Fu));
-        t = tc < t ? tc : t;
-    }
-    return t;
-}
-// theta_p packed one byte per player (99 = never offered)
-DK_HD uint32_t ann_thetas(uint32_t team_kind, uint32_t solved_trick, uint32_t re_players, uint32_t re_lowest,
-                          uint32_t contra_lowest) {
-    if (team_kind == TK_WED_UNSOLVED || team_kind == TK_INRES) return 0x63636363u;
-    const int ws = team_kind == TK_WED_SOLVED ? (int)solved_trick : 0;
-    const uint32_t pr = all_higher_than(re_lowest), pk = all_higher_than(contra_lowest);
-    const uint32_t tre = ann_theta(pr, pk, ws), tko = ann_theta(pk, pr, ws);
-    uint32_t out = 0;
-#pragma unroll
-    for (int p = 0; p < 4; ++p) out |= (((re_players >> p) & 1u) ? tre : tko) << (8 * p);
-    return out;
-}
-DK_HD uint32_t sel4u(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, uint32_t p) {
-    const uint32_t lo = (p & 1u) ? a1 : a0, hi = (p & 1u) ? a3 : a2;
-    return (p & 2u) ? hi : lo;
-}
-// trump rank nibbles (same table as trump_rank), 8 cards per word
-DK_HD uint32_t rank_fast(uint32_t c) {
-    const uint32_t wv = c < 8u ? 0xC0318420u : (c < 16u ? 0xB7202195u : 0x31A62031u);
-    return (wv >> (4u * (c & 7u))) & 15u;
-}
-DK_HD uint32_t suit_of(uint32_t c) { return (c * 43u) >> 8; }   // c / 6 for c < 24
-DK_HD uint32_t eyes_fast(uint32_t c) { return (0xB432A0u >> (4u * (c - 6u * suit_of(c)))) & 15u; }
-// colour class mask of card c (trumps, or its suit minus trumps)
-DK_HD uint32_t class_mask(uint32_t c, uint32_t tm) {
-    return ((tm >> c) & 1u) ? tm : ((0x3Fu << (6u * suit_of(c))) & ~tm);
-}
-// key of card c in a trick led with colour class `lead` (trick_key)
-DK_HD int key_fast(uint32_t c, uint32_t tm, uint32_t lead) {
-    const int k_t = 32 + (int)rank_fast(c), k_c = (int)eyes_fast(c);
-    return ((tm >> c) & 1u) ? k_t : (((lead >> c) & 1u) ? k_c : -1);
 }
 
 // Card phase to the end (w.phase == PH_PLAYCARD).  Returns plies played.

@@ -43,8 +43,8 @@ namespace dk {
 #if defined(DK_PHASE_PROF) && defined(__HIP_DEVICE_COMPILE__)
 #define DK_STAMP(t) const uint64_t t = __builtin_amdgcn_s_memtime()
 #define DK_PROF(mem, k, v) prof_acc[k] += (v)
-#define DK_PROF_DECL uint64_t prof_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}
-#define DK_PROF_FLUSH(mem) for (int k_ = 0; k_ < 12; ++k_) mem.prof_add(k_, prof_acc[k_])
+#define DK_PROF_DECL uint64_t prof_acc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}
+#define DK_PROF_FLUSH(mem) for (int k_ = 0; k_ < 16; ++k_) mem.prof_add(k_, prof_acc[k_])
 #define DK_STAMP_DRAINED(t) __builtin_amdgcn_s_waitcnt(0); const uint64_t t = __builtin_amdgcn_s_memtime()
 #define DK_PROF_WAVEMAX(k, v) do { int m_ = (v); for (int o_ = 32; o_ >= 1; o_ >>= 1) { const int t_ = __shfl_xor(m_, o_); m_ = t_ > m_ ? t_ : m_; } prof_acc[k] += (uint64_t)m_; } while (0)
 #else
@@ -326,7 +326,10 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
             mem.store_unexpanded(slot, cd.unexpanded);
             // a forced chain grew: its head now points at the new end
             if (block == 1 && chain_head != 0xFFFFFFFFu) mem.store_child_base(chain_head, child);
+            DK_STAMP_DRAINED(te0);
             E::step(w, a);
+            DK_STAMP_DRAINED(te1);
+            DK_PROF(mem, 12, te1 - te0);
             const uint64_t ca = E::allowed(w, false);
             NodeHot ch;
             ch.stats = 0; ch.child_base = 0; ch.q = 0.0; ch.isv = 0.0f; ch.pad = 0;
@@ -335,6 +338,8 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
             cc.unexpanded = ca; cc.parent = slot; cc.action = (uint32_t)a;
             mem.store_hot(child, ch);
             mem.store_cold(child, cc);
+            DK_STAMP_DRAINED(te2);
+            DK_PROF(mem, 13, te2 - te1);
             mem.store_state(next_state, w);
             next_state += 1;
             depth += 1;

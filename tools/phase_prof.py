@@ -34,7 +34,7 @@ def main():
     prof = getattr(L, "dk_phase_profile", None)
     if prof is not None:
         prof.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]
-        out = np.zeros((n_roots, 12), dtype=np.uint64)
+        out = np.zeros((n_roots, 16), dtype=np.uint64)
         prof(eng.ctx, out.ctypes.data, n_roots)  # clear
     step()
     torch.cuda.synchronize(dev)
@@ -53,7 +53,9 @@ def main():
                     "select_load_cyc": float(out[:, 8].astype(np.float64).sum() / sims),
                     "select_pick_cyc": float(out[:, 9].astype(np.float64).sum() / sims),
                     "rollout_plies": float(out[:, 10].astype(np.float64).sum() / sims),
-                    "rollout_plies_wave_max": float(out[:, 11].astype(np.float64).sum() / sims)})
+                    "rollout_plies_wave_max": float(out[:, 11].astype(np.float64).sum() / sims),
+                    "expand_step_cyc": float(out[:, 12].astype(np.float64).sum() / sims),
+                    "expand_allowed_cyc": float(out[:, 13].astype(np.float64).sum() / sims)})
     print(json.dumps(res))
     eng.close()
 
