@@ -46,6 +46,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=0)
     p.add_argument("--cpu-roots-per-thread", type=int, default=96)
+    p.add_argument("--dump-actions", default="", help="rank 0 writes the fused actions (.npy) of the last step")
     return p.parse_args()
 
 
@@ -125,7 +126,8 @@ def make_workload(args, dk, L, dev, sp, rank, world, local_rank, dist=None):
             ck(L.dk_search_batch_async(eng.ctx, dk.GAME_DOKO, ptr(roots), ptr(d_srch), n_roots, iters, args.c,
                                        ptr(visits), ptr(values), ptr(best), sp))
 
-    return eng, step, n_roots, {"visits": visits, "values": values, "best": best, "roots": roots, "I": I, "S_r": S_r}
+    return eng, step, n_roots, {"visits": visits, "values": values, "best": best, "roots": roots, "I": I, "S_r": S_r,
+                                "actions": actions if args.workload == "c3" else None}
 
 
 def main():
@@ -139,10 +141,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
+    # one GPU per rank; DK_DIST_BACKEND=gloo + more ranks than GPUs is the
+    # rehearsal mode for the multi-GPU path on a one-GPU box (ranks share a device)
+    backend = os.environ.get("DK_DIST_BACKEND", "nccl")
+    device = local_rank % max(1, torch.cuda.device_count()) if backend != "nccl" else local_rank
+    torch.cuda.set_device(device)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    dev = torch.device("cuda", local_rank)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))   # RCCL over xGMI
+        else:
+            dist.init_process_group(backend)
+    dev = torch.device("cuda", device)
+    local_rank = device
     L = _native.lib()
     # one explicit stream for torch's allocations/copies AND the library's launches
     # (handle 0 would mean the library's own non-blocking stream: no ordering with torch)
@@ -182,6 +192,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
 
+    if rank == 0 and args.dump_actions and bufs["actions"] is not None:
+        np.save(args.dump_actions, bufs["actions"].cpu().numpy())
     v = visits.cpu().numpy()
     assert np.all(v.sum(axis=1) == iters), "every root must have exactly `iterations` simulations"
     sims_total = n_roots * iters * args.steps * world
