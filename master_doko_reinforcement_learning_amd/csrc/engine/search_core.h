@@ -234,13 +234,28 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
         int depth = 0;
         uint32_t chain_head = 0xFFFFFFFFu;   // head whose skip pointer led to x
         mem.path_set(0, 0u, x.stats);
-        while (ni_nchild(x.info) > 0 && !ni_open(x.info)) {
+        // One trip per BRANCHING level: a lane first hops through single-child nodes
+        // (a chain head jumps to its chain end), then picks among its children.  A wave
+        // whose lanes sit at forced and branching levels at the same time thus pays one
+        // pick per trip, not one trip per tree level.
+        for (;;) {
+            while (ni_nchild(x.info) == 1 && !ni_open(x.info)) {
+                chain_head = ni_head(x.info) ? slot : 0xFFFFFFFFu;
+                const NodeHot y = mem.load_hot(x.child_base);
+                scanned += 1;
+                DK_PROF(mem, 5, 1);
+                depth += 1;
+                if (depth >= MAX_DEPTH - 1) { status = SR_CAPACITY; break; }
+                mem.path_set(depth, x.child_base | (ni_player(x.info) << 30), y.stats);
+                slot = x.child_base;
+                x_visits = (uint32_t)y.stats;
+                x = y;
+            }
+            if (status != SR_OK || ni_nchild(x.info) == 0 || ni_open(x.info)) break;
             const uint32_t n = ni_nchild(x.info);
             uint32_t pick;
             NodeHot y;
             if (n <= (uint32_t)SCAN_REG) {
-                // one round trip for every lane of the wave: forced (n == 1) and
-                // branching blocks load together
                 DK_STAMP_DRAINED(tl0);
                 const double lnN = mem.ln(x_visits);
                 Block blk;
@@ -255,13 +270,7 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
                 }
                 DK_STAMP_DRAINED(tl1);
                 DK_PROF(mem, 8, tl1 - tl0);
-                if (n == 1) {
-                    // single child: a chain head's child_base is its chain end
-                    pick = 0;
-                    y.stats = blk.st[0]; y.child_base = blk.cb[0]; y.info = blk.inf[0];
-                } else {
-                    pick = pick_child_reg(blk, n, lnN, c, &y.stats, &y.child_base, &y.info);
-                }
+                pick = pick_child_reg(blk, n, lnN, c, &y.stats, &y.child_base, &y.info);
                 DK_STAMP_DRAINED(tl2);
                 DK_PROF(mem, 9, tl2 - tl1);
             } else {
@@ -283,9 +292,9 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
                     if (u > best) { best = u; pick = j; y = r; }
                 }
             }
-            chain_head = (n == 1 && ni_head(x.info)) ? slot : 0xFFFFFFFFu;
+            chain_head = 0xFFFFFFFFu;
             scanned += n;
-            DK_PROF(mem, n == 1 ? 5 : 6, 1);
+            DK_PROF(mem, 6, 1);
             const uint32_t child = x.child_base + pick;
             depth += 1;
             if (depth >= MAX_DEPTH - 1) { status = SR_CAPACITY; break; }
