@@ -138,8 +138,14 @@ struct Block {
 //     strictly below the maximum -- first strict maximum among them.  The
 //     first two candidates are gathered with selects; more is rare and takes
 //     a full exact pass.
-DK_HD uint32_t pick_child_reg(const Block& b, uint32_t n, double lnN, double c, uint64_t* p_st, uint32_t* p_cb,
-                              uint32_t* p_inf) {
+//
+// Chain-end prefetch: once the (usually one or two) candidates are known, the
+// chain ends of candidates that are expanded single-action nodes (forced chain
+// heads) are loaded while the exact evaluation runs; *end_ok tells whether
+// *end holds the picked child's chain end.
+template <class Mem>
+DK_HD uint32_t pick_child_reg(const Block& b, uint32_t n, double lnN, double c, Mem& mem, uint64_t* p_st, uint32_t* p_cb,
+                              uint32_t* p_inf, NodeHot* end, bool* end_ok) {
     double min_q = INFINITY, max_q = -INFINITY;
 #pragma unroll
     for (int j = 0; j < SCAN_REG; ++j) {
@@ -164,15 +170,23 @@ DK_HD uint32_t pick_child_reg(const Block& b, uint32_t n, double lnN, double c, 
     const float cut = umax - 3e-6f * (3.0f + fabsf(ex));
     uint64_t s1 = b.st[0], s2 = b.st[0];
     double q1 = b.q[0], q2 = b.q[0];
-    uint32_t j1 = 0, j2 = 0, nc = 0;
+    uint32_t j1 = 0, j2 = 0, nc = 0, cb1 = b.cb[0], cb2 = b.cb[0], in1 = b.inf[0], in2 = b.inf[0];
 #pragma unroll
     for (int j = 0; j < SCAN_REG; ++j) {
         const bool cj = ue[j] >= cut;   // implies j < n
         const bool first = cj && nc == 0, second = cj && nc == 1;
         s1 = first ? b.st[j] : s1; q1 = first ? b.q[j] : q1; j1 = first ? (uint32_t)j : j1;
+        cb1 = first ? b.cb[j] : cb1; in1 = first ? b.inf[j] : in1;
         s2 = second ? b.st[j] : s2; q2 = second ? b.q[j] : q2; j2 = second ? (uint32_t)j : j2;
+        cb2 = second ? b.cb[j] : cb2; in2 = second ? b.inf[j] : in2;
         nc += cj ? 1u : 0u;
     }
+    // prefetch the chain ends of forced candidates (their child_base is the chain end)
+    const bool f1 = ni_nchild(in1) == 1 && !ni_open(in1);
+    const bool f2 = nc >= 2 && ni_nchild(in2) == 1 && !ni_open(in2);
+    NodeHot e1, e2;
+    if (f1) e1 = mem.load_hot(cb1);
+    if (f2) e2 = mem.load_hot(cb2);
     double best = uct_exact(s1, q1, flat, min_q, max_q, lnN, c);
     uint32_t pick = j1;
     if (nc == 2) {
@@ -197,6 +211,9 @@ DK_HD uint32_t pick_child_reg(const Block& b, uint32_t n, double lnN, double c, 
         pi = (uint32_t)j == pick ? b.inf[j] : pi;
     }
     *p_st = ps; *p_cb = pc; *p_inf = pi;
+    *end_ok = (pick == j1 && f1) || (nc >= 2 && pick == j2 && f2);
+    if (pick == j1 && f1) *end = e1;
+    else if (nc >= 2 && pick == j2 && f2) *end = e2;
     return pick;
 }
 
@@ -254,7 +271,8 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
             if (status != SR_OK || ni_nchild(x.info) == 0 || ni_open(x.info)) break;
             const uint32_t n = ni_nchild(x.info);
             uint32_t pick;
-            NodeHot y;
+            NodeHot y, end;
+            bool end_ok = false;
             if (n <= (uint32_t)SCAN_REG) {
                 DK_STAMP_DRAINED(tl0);
                 const double lnN = mem.ln(x_visits);
@@ -270,7 +288,7 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
                 }
                 DK_STAMP_DRAINED(tl1);
                 DK_PROF(mem, 8, tl1 - tl0);
-                pick = pick_child_reg(blk, n, lnN, c, &y.stats, &y.child_base, &y.info);
+                pick = pick_child_reg(blk, n, lnN, c, mem, &y.stats, &y.child_base, &y.info, &end, &end_ok);
                 DK_STAMP_DRAINED(tl2);
                 DK_PROF(mem, 9, tl2 - tl1);
             } else {
@@ -302,6 +320,18 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
             slot = child;
             x_visits = (uint32_t)y.stats;
             x = y;
+            if (end_ok) {
+                // the picked child is a forced chain head: its prefetched chain end
+                chain_head = ni_head(x.info) ? slot : 0xFFFFFFFFu;
+                scanned += 1;
+                DK_PROF(mem, 5, 1);
+                depth += 1;
+                if (depth >= MAX_DEPTH - 1) { status = SR_CAPACITY; break; }
+                mem.path_set(depth, x.child_base | (ni_player(x.info) << 30), end.stats);
+                slot = x.child_base;
+                x_visits = (uint32_t)end.stats;
+                x = end;
+            }
         }
         if (status != SR_OK) break;
         DK_STAMP(t1);

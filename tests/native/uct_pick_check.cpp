@@ -22,6 +22,10 @@ float dk::rcp_approx(float x) { return perturb(1.0f / x); }
 float dk::sqrt_approx(float x) { return perturb(sqrtf(x)); }
 float dk::rsqrt_approx(float x) { return perturb(1.0f / sqrtf(x)); }
 
+struct NullMem {   // chain-end prefetch target (never a forced node here: info = j*13 has nchild 13*j & 63)
+    dk::NodeHot load_hot(uint32_t) const { dk::NodeHot h; memset(&h, 0, sizeof(h)); return h; }
+};
+
 static uint32_t naive(const dk::NodeHot* rec, uint32_t n, double lnN, double c) {
     double min_q = INFINITY, max_q = -INFINITY;
     for (uint32_t j = 0; j < n; ++j) {
@@ -75,7 +79,9 @@ int main(int argc, char** argv) {
             blk.q[j] = rec[j].q; blk.isv[j] = rec[j].isv;
         }
         uint64_t gs; uint32_t gc, gi;
-        const uint32_t a = dk::pick_child_reg(blk, n, lnN, c, &gs, &gc, &gi);
+        dk::NodeHot end; bool end_ok;
+        NullMem nm;
+        const uint32_t a = dk::pick_child_reg(blk, n, lnN, c, nm, &gs, &gc, &gi, &end, &end_ok);
         const uint32_t b = naive(rec, n, lnN, c);
         if (a != b || gs != rec[b].stats || gc != b * 7 || gi != b * 13) {
             printf("MISMATCH case %ld n %u mode %d: got %u want %u\n", t, n, mode, a, b);
