@@ -187,13 +187,14 @@ DK_HD uint32_t pick_child_reg(const Block& b, uint32_t n, double lnN, double c, 
     NodeHot e1, e2;
     if (f1) e1 = mem.load_hot(cb1);
     if (f2) e2 = mem.load_hot(cb2);
-    double best = uct_exact(s1, q1, flat, min_q, max_q, lnN, c);
+    // a single candidate is the unique maximum: no exact evaluation needed
     uint32_t pick = j1;
     if (nc == 2) {
+        const double u1 = uct_exact(s1, q1, flat, min_q, max_q, lnN, c);
         const double u2 = uct_exact(s2, q2, flat, min_q, max_q, lnN, c);
-        if (u2 > best) { best = u2; pick = j2; }
+        if (u2 > u1) pick = j2;
     } else if (nc > 2) {
-        best = -INFINITY;
+        double best = -INFINITY;
 #pragma unroll
         for (int j = 0; j < SCAN_REG; ++j) {
             if (ue[j] >= cut) {
