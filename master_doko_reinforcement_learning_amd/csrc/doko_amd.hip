@@ -125,6 +125,7 @@ __global__ void __launch_bounds__(WAVE) search_kernel(const dk_state* __restrict
     const uint32_t T = iters + 1;
     const uint32_t n_ln = LN_LDS ? T : 0u;
     for (uint32_t i = lane; i < n_ln; i += WAVE) dk_lds[i] = (uint64_t)__double_as_longlong(ln_table[i]);
+    if (E::GAME == DK_GAME_FULL_DOKO) dk::fdo::card_table_init();   // ends with a barrier
     __syncthreads();
     const uint32_t root = blockIdx.x * rpw + lane;
     if (lane >= rpw || root >= n) return;
@@ -263,6 +264,7 @@ __device__ void rollout_one(const dk_state& s, dk::Rng& rng, double* out) {
 
 __global__ void __launch_bounds__(WAVE) env_rollout_kernel(const dk_state* states, uint64_t* rng_states, uint32_t n,
                                                            double* rewards) {
+    dk::fdo::card_table_init();
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const dk_state s = states[i];

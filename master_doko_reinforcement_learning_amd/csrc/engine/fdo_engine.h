@@ -198,6 +198,41 @@ DK_HD int key_fast(uint32_t c, uint32_t tm, uint32_t lead) {
     return ((tm >> c) & 1u) ? k_t : (((lead >> c) & 1u) ? k_c : -1);
 }
 
+// Per-(game type, card) facts for the rollout, one 8-byte entry:
+//   x = colour-class mask of the card (24 bits) | eyes << 24 | trump << 28
+//   y = trick key when it can win: 32 + trump rank for trumps, eyes otherwise
+// On the GPU the 9 x 24 table lives in LDS (built by card_table_init at kernel
+// start); on the host it is computed on the fly.
+struct CardInfo { uint32_t x, y; };
+DK_HD CardInfo card_info_calc(uint32_t gt, uint32_t c) {
+    const uint32_t tm = trump_mask(gt);
+    const bool tr = (tm >> c) & 1u;
+    CardInfo ci;
+    ci.x = class_mask(c, tm) | (eyes_fast(c) << 24) | (tr ? 1u << 28 : 0u);
+    ci.y = tr ? 32u + rank_fast(c) : eyes_fast(c);
+    return ci;
+}
+#if defined(__HIP_DEVICE_COMPILE__)
+__shared__ uint2 dk_card_tab[9 * 24];
+__device__ inline void card_table_init() {
+    for (uint32_t i = threadIdx.x; i < 9u * 24u; i += blockDim.x) {
+        const CardInfo ci = card_info_calc(i / 24u, i % 24u);
+        dk_card_tab[i] = make_uint2(ci.x, ci.y);
+    }
+    __syncthreads();
+}
+__device__ inline CardInfo card_info(uint32_t gt, uint32_t c) {
+    const uint2 v = dk_card_tab[gt * 24u + c];
+    CardInfo ci;
+    ci.x = v.x; ci.y = v.y;
+    return ci;
+}
+#else
+inline void card_table_init() {}
+inline CardInfo card_info(uint32_t gt, uint32_t c) { return card_info_calc(gt, c); }
+#endif
+
+
 // announcement.rs:182-215 (the announcing player's team decides which lowest moves)
 DK_HD void internal_play_announcement(Work& w, int player, uint32_t ann) {
     if (ann == 0) { w.ann_turns += 1; return; }  // NoAnnouncement
@@ -531,6 +566,7 @@ DK_HD int rollout_cards(const Work& w0, Rng& rng, int pts[4]) {
     uint32_t nb = (uint32_t)(popc32(any0) + popc32(two0)) | (uint32_t)(popc32(any1) + popc32(two1)) << 8 |
                   (uint32_t)(popc32(any2) + popc32(two2)) << 16 | (uint32_t)(popc32(any3) + popc32(two3)) << 24;
     const uint32_t tm = trump_mask(w0.game_type);
+    const uint32_t gt = w0.game_type;
     uint32_t team_kind = w0.team_kind, re_players = w0.re_players, solved = w0.solved_trick;
     const uint32_t wedding_player = w0.wedding_player;
     uint32_t theta = ann_thetas(team_kind, solved, re_players, w0.re_lowest, w0.contra_lowest);
@@ -573,14 +609,15 @@ DK_HD int rollout_cards(const Work& w0, Rng& rng, int pts[4]) {
         two0 = cur == 0u ? nt : two0; two1 = cur == 1u ? nt : two1; two2 = cur == 2u ? nt : two2; two3 = cur == 3u ? nt : two3;
         nb -= 1u << (8u * cur);
         // ---- running trick evaluation (complete_trick, spread over the four cards)
+        const CardInfo ci = card_info(gt, card);
         const bool first = trick_len == 0u;
-        lead = first ? class_mask(card, tm) : lead;
-        const int key = key_fast(card, tm, lead);
+        lead = first ? (ci.x & 0xFFFFFFu) : lead;
+        const int key = (((ci.x >> 28) & 1u) || ((lead >> card) & 1u)) ? (int)ci.y : -1;
         const bool better = first || key > best_key;
         best_key = better ? key : best_key;
         best_pos = better ? trick_len : best_pos;
         win_card = better ? card : win_card;
-        t_eyes = (first ? 0u : t_eyes) + eyes_fast(card);
+        t_eyes = (first ? 0u : t_eyes) + ((ci.x >> 24) & 15u);
         da_n = first ? 0u : da_n;
         const bool is_da = card == (uint32_t)DIAMOND_ACE;
         da0 = (is_da && da_n == 0u) ? cur : da0;
