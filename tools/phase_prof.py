@@ -56,6 +56,12 @@ def main():
                     "rollout_plies_wave_max": float(out[:, 11].astype(np.float64).sum() / sims),
                     "expand_step_cyc": float(out[:, 12].astype(np.float64).sum() / sims),
                     "expand_allowed_cyc": float(out[:, 13].astype(np.float64).sum() / sims)})
+        tot = out[:, :4].astype(np.float64).sum(axis=1)   # per-root wave-clock cycles over the whole search
+        if args.workload == "c3":
+            k = np.array([[0, 8, 20, 32][(r // args.samples) % 4] for r in range(n_roots)])
+            res["wave_cycles_by_k"] = {int(kk): [float(tot[k == kk].min()), float(tot[k == kk].mean()), float(tot[k == kk].max())]
+                                       for kk in (0, 8, 20, 32)}
+        res["wave_cycles_min_mean_max"] = [float(tot.min()), float(tot.mean()), float(tot.max())]
     print(json.dumps(res))
     eng.close()
 
