@@ -23,6 +23,13 @@
 namespace {
 
 constexpr int WAVE = 64;
+// register budget of the search kernel: default = compiler's choice (one wave per SIMD
+// worth of VGPRs); -DDK_SEARCH_MIN_WAVES=n budgets for n waves per SIMD
+#ifdef DK_SEARCH_MIN_WAVES
+#define DK_SEARCH_BOUNDS __launch_bounds__(WAVE, DK_SEARCH_MIN_WAVES)
+#else
+#define DK_SEARCH_BOUNDS __launch_bounds__(WAVE)
+#endif
 constexpr int MAX_PATH = 64;   // LDS path entries per lane (deeper paths spill to a global overflow)
 
 #define DK_HIP(call)                                              \
@@ -113,7 +120,7 @@ struct GpuMem {
 // One lane per root, `rpw` roots per 64-lane wave (lanes >= rpw idle).  The
 // LDS holds each lane's selection path: MAX_PATH x (u32 slot|player, u64 stats).
 template <class E, bool LN_LDS>
-__global__ void __launch_bounds__(WAVE) search_kernel(const dk_state* __restrict__ roots,
+__global__ void DK_SEARCH_BOUNDS search_kernel(const dk_state* __restrict__ roots,
                                                       const uint64_t* __restrict__ seeds, uint32_t n,
                                                       uint32_t iters, double c, const double* __restrict__ ln_table,
                                                       dk::NodeHot* hot, dk::NodeCold* cold, typename E::Work* states,
@@ -398,7 +405,9 @@ struct dk_ctx {
     int last_error = DK_OK;
     uint64_t pool_bytes = 0;
     uint32_t roots_per_wave = 32;   // DK_ROOTS_PER_WAVE (32: one wave per SIMD for 32K roots, less divergence than 64)
-    int lds_path = MAX_PATH;        // DK_LDS_PATH (path entries kept in LDS; tests shrink it)
+    int lds_path = 24;              // DK_LDS_PATH (path entries kept in LDS, <= MAX_PATH; deeper ones
+                                    // spill to global).  24 keeps a workgroup at ~17 KB of LDS so that
+                                    // 8 single-wave workgroups (2 per SIMD) fit a CU's 160 KB.
     uint64_t* prof = nullptr;       // phase timers (DK_PHASE_PROF builds only)
     std::vector<void*> scratch;
     std::vector<size_t> scratch_size;
