@@ -45,8 +45,12 @@ DK_HD uint32_t byte_add(uint32_t w, int i, uint32_t v) { return w + (v << (8 * i
 DK_HD uint32_t byte_set(uint32_t w, int i, uint32_t v) { return (w & ~(0xFFu << (8 * i))) | ((v & 0xFFu) << (8 * i)); }
 
 // 4-element selects without dynamic register indexing (keeps arrays in VGPRs).
+// Written as mask arithmetic: a select chain on the index is recognised by the
+// optimiser as h[p] and turned back into a (scratch-memory) array access.
 DK_HD uint64_t sel4(const uint64_t h[4], int p) {
-    return p == 0 ? h[0] : (p == 1 ? h[1] : (p == 2 ? h[2] : h[3]));
+    const uint64_t m0 = 0ULL - (uint64_t)(p == 0), m1 = 0ULL - (uint64_t)(p == 1);
+    const uint64_t m2 = 0ULL - (uint64_t)(p == 2), m3 = 0ULL - (uint64_t)(p == 3);
+    return (h[0] & m0) | (h[1] & m1) | (h[2] & m2) | (h[3] & m3);
 }
 DK_HD void set4(uint64_t h[4], int p, uint64_t v) {
     h[0] = p == 0 ? v : h[0];

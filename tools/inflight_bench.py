@@ -13,13 +13,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def main(m=2, steps=6):
+def main(m=2, steps=6, infostates=1024):
     import torch
 
     import bench
     import master_doko_reinforcement_learning_amd as dk
     from master_doko_reinforcement_learning_amd import _native
-    sys.argv = [sys.argv[0]]
+    sys.argv = [sys.argv[0], "--infostates", str(infostates)]
     args = bench.parse()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(0)
@@ -51,4 +51,4 @@ def main(m=2, steps=6):
 
 
 if __name__ == "__main__":
-    main(*(int(a) for a in sys.argv[1:3]))
+    main(*(int(a) for a in sys.argv[1:4]))
