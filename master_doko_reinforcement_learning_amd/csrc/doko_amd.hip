@@ -23,9 +23,15 @@
 namespace {
 
 constexpr int WAVE = 64;
-// register budget of the search kernel: default = compiler's choice (one wave per SIMD
-// worth of VGPRs); -DDK_SEARCH_MIN_WAVES=n budgets for n waves per SIMD
-#ifdef DK_SEARCH_MIN_WAVES
+// register budget of the search kernel: 3 waves per SIMD (<= 168 VGPRs).  The kernel is
+// latency bound (a lane waits on one dependent node load per tree level), so a third
+// resident wave per SIMD hides more of it than the ~40 spilled VGPRs cost (+10% over
+// the unconstrained 217-VGPR build at 2 waves/SIMD).  -DDK_SEARCH_MIN_WAVES=0 restores
+// the compiler's choice.
+#ifndef DK_SEARCH_MIN_WAVES
+#define DK_SEARCH_MIN_WAVES 3
+#endif
+#if DK_SEARCH_MIN_WAVES > 0
 #define DK_SEARCH_BOUNDS __launch_bounds__(WAVE, DK_SEARCH_MIN_WAVES)
 #else
 #define DK_SEARCH_BOUNDS __launch_bounds__(WAVE)
@@ -405,9 +411,11 @@ struct dk_ctx {
     int last_error = DK_OK;
     uint64_t pool_bytes = 0;
     uint32_t roots_per_wave = 32;   // DK_ROOTS_PER_WAVE (32: one wave per SIMD for 32K roots, less divergence than 64)
-    int lds_path = 24;              // DK_LDS_PATH (path entries kept in LDS, <= MAX_PATH; deeper ones
-                                    // spill to global).  24 keeps a workgroup at ~17 KB of LDS so that
-                                    // 8 single-wave workgroups (2 per SIMD) fit a CU's 160 KB.
+    bool ln_in_lds = false;         // DK_LN_LDS=1: ln(N) table copied into every workgroup's LDS (8 KB at
+                                    // 1000 iterations); by default it is read through the L1/L2 caches
+    int lds_path = 16;              // DK_LDS_PATH (path entries kept in LDS, <= MAX_PATH; deeper ones
+                                    // spill to global).  16 keeps a workgroup at 6 KB of LDS so that
+                                    // 12 single-wave workgroups (3 per SIMD) fit a CU's 160 KB.
     uint64_t* prof = nullptr;       // phase timers (DK_PHASE_PROF builds only)
     std::vector<void*> scratch;
     std::vector<size_t> scratch_size;
@@ -450,8 +458,9 @@ hipError_t launch_search(dk_ctx* ctx, const dk_state* roots, const uint64_t* see
                          double c, uint32_t* visits, double* values, uint8_t* best, hipStream_t st) {
     const uint32_t rpw = ctx->roots_per_wave;
     const int lds_n = ctx->lds_path;
-    const size_t lds_bytes = (iters + 1 <= LN_LDS_MAX ? (size_t)((iters + 2) & ~1u) * 8 : 0) + (size_t)lds_n * rpw * 12;
-    if (iters + 1 <= LN_LDS_MAX)
+    const size_t lds_bytes = (iters + 1 <= LN_LDS_MAX && ctx->ln_in_lds ? (size_t)((iters + 2) & ~1u) * 8 : 0) +
+                             (size_t)lds_n * rpw * 12;
+    if (iters + 1 <= LN_LDS_MAX && ctx->ln_in_lds)
         hipLaunchKernelGGL((search_kernel<E, true>), dim3(grid_for(n, rpw)), dim3(WAVE), lds_bytes, st,
                            roots, seeds, n, iters, c, ctx->ln_table, ctx->hot, ctx->cold,
                            (typename E::Work*)ctx->states, ctx->ovf, ctx->ovf_st, ctx->cap_slots, rpw, lds_n, visits,
@@ -515,6 +524,7 @@ dk_ctx* dk_create(const dk_config* cfg) {
         const int v = atoi(e);
         if (v >= 1 && v <= WAVE) ctx->roots_per_wave = (uint32_t)v;
     }
+    if (const char* e = getenv("DK_LN_LDS")) ctx->ln_in_lds = atoi(e) != 0;
     if (const char* e = getenv("DK_LDS_PATH")) {
         const int v = atoi(e);
         if (v >= 1 && v <= MAX_PATH) ctx->lds_path = v;
