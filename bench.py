@@ -2,11 +2,11 @@
 
 One step = one determinized decision batch of BASELINE.json config 3 on every
 GPU, entirely on the device:
-    CAP determinization (card_matching_full)  -> 1536 infostates x 64 samples = 98,304 roots
+    CAP determinization (card_matching_full)  -> 4096 infostates x 64 samples = 262,144 roots
     UCT search, 1000 simulations per root (select/expand/random rollout/backup)
     policy fusion (MaxN) of the per-sample visit counts per infostate
-With N GPUs (config 4) the global batch holds 1536*N infostates; the 64 samples
-of every infostate are split evenly over the ranks (98,304 roots per GPU, weak
+With N GPUs (config 4) the global batch holds 4096*N infostates; the 64 samples
+of every infostate are split evenly over the ranks (262,144 roots per GPU, weak
 scaling) and the per-infostate fusion accumulators are summed with one RCCL
 all-reduce over xGMI before the fused action is selected.
 
@@ -38,8 +38,8 @@ def parse():
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--workload", choices=["c3", "c2"], default="c3")
     p.add_argument("--iterations", type=int, default=1000)
-    p.add_argument("--infostates", type=int, default=1536,
-                   help="infostates per GPU (c3): 1536 x 64 samples = 98,304 roots = three 32-root waves per SIMD")
+    p.add_argument("--infostates", type=int, default=4096,
+                   help="infostates per GPU (c3): 4096 x 64 samples = 262,144 roots, streamed through the resident waves' node pools (131,072 roots)")
     p.add_argument("--samples", type=int, default=64, help="CAP samples per infostate (c3)")
     p.add_argument("--roots", type=int, default=32768, help="roots per GPU (c2)")
     p.add_argument("--c", type=float, default=2.5)

@@ -145,6 +145,10 @@ typedef struct dk_config {
 
 typedef struct dk_ctx dk_ctx;
 
+/* The node / state pools hold min(max_roots, resident roots) trees at once (resident
+ * roots = CUs x 8 waves x 64 lanes; env DK_POOL_ROOTS overrides).  The search grid is
+ * persistent: a batch larger than the pools streams through them, one wave-sized group of
+ * roots at a time, so max_roots bounds the batch, not the memory. */
 dk_ctx* dk_create(const dk_config* cfg);
 void dk_destroy(dk_ctx* ctx);
 int dk_last_error(const dk_ctx* ctx);

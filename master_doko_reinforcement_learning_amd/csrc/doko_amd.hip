@@ -23,13 +23,12 @@
 namespace {
 
 constexpr int WAVE = 64;
-// register budget of the search kernel: 3 waves per SIMD (<= 168 VGPRs).  The kernel is
-// latency bound (a lane waits on one dependent node load per tree level), so a third
-// resident wave per SIMD hides more of it than the ~40 spilled VGPRs cost (+10% over
-// the unconstrained 217-VGPR build at 2 waves/SIMD).  -DDK_SEARCH_MIN_WAVES=0 restores
-// the compiler's choice.
+// register budget of the search kernel: by default the compiler's choice (~217 VGPRs, two
+// waves per SIMD, no spills).  With 64 roots per wave two full waves per SIMD beat three
+// half-filled ones at a 168-VGPR budget (which spills ~40 VGPRs); -DDK_SEARCH_MIN_WAVES=n
+// forces an n-wave budget for experiments.
 #ifndef DK_SEARCH_MIN_WAVES
-#define DK_SEARCH_MIN_WAVES 3
+#define DK_SEARCH_MIN_WAVES 0
 #endif
 #if DK_SEARCH_MIN_WAVES > 0
 #define DK_SEARCH_BOUNDS __launch_bounds__(WAVE, DK_SEARCH_MIN_WAVES)
@@ -86,8 +85,12 @@ struct GpuMem {
     __device__ void store_stats(uint32_t s, uint64_t v) const { hot[s].stats = v; }
     __device__ void store_backup(uint32_t s, uint64_t v, double q, float isv) const {
         hot[s].stats = v;
+#if DK_HOT16
+        (void)q; (void)isv;
+#else
         hot[s].q = q;
         hot[s].isv = isv;
+#endif
     }
     __device__ void store_child_base(uint32_t s, uint32_t child_base) const { hot[s].child_base = child_base; }
     __device__ void store_node_tail(uint32_t s, uint32_t child_base, uint32_t info) const {
@@ -123,8 +126,13 @@ struct GpuMem {
 };
 
 // ---------------------------------------------------------------- kernels
-// One lane per root, `rpw` roots per 64-lane wave (lanes >= rpw idle).  The
-// LDS holds each lane's selection path: MAX_PATH x (u32 slot|player, u64 stats).
+// One lane per root, `rpw` roots per 64-lane wave (lanes >= rpw idle).  The grid is
+// persistent: each single-wave workgroup owns one pool region of `rpw` roots (node
+// records, states, path overflow) and pulls root groups g = [g*rpw, (g+1)*rpw) from a
+// queue counter until the batch is drained, so a wave that finishes early takes the
+// next group instead of idling until the slowest wave of the launch ends, and the pools
+// are sized for the resident waves, not for the batch.  The LDS holds each lane's
+// selection path: lds_n x (u32 slot|player, u64 stats).
 template <class E, bool LN_LDS>
 __global__ void DK_SEARCH_BOUNDS search_kernel(const dk_state* __restrict__ roots,
                                                       const uint64_t* __restrict__ seeds, uint32_t n,
@@ -133,43 +141,51 @@ __global__ void DK_SEARCH_BOUNDS search_kernel(const dk_state* __restrict__ root
                                                       uint32_t* ovf, uint64_t* ovf_st,
                                                       uint32_t cap_slots, uint32_t rpw, int lds_n,
                                                       uint32_t* visits, double* values,
-                                                      uint8_t* best, int* err, uint64_t* prof) {
+                                                      uint8_t* best, int* err, uint32_t* queue, uint64_t* prof) {
     const uint32_t lane = threadIdx.x;
     const uint32_t T = iters + 1;
     const uint32_t n_ln = LN_LDS ? T : 0u;
     for (uint32_t i = lane; i < n_ln; i += WAVE) dk_lds[i] = (uint64_t)__double_as_longlong(ln_table[i]);
     if (E::GAME == DK_GAME_FULL_DOKO) dk::fdo::card_table_init();   // ends with a barrier
     __syncthreads();
-    const uint32_t root = blockIdx.x * rpw + lane;
-    if (lane >= rpw || root >= n) return;
     const uint32_t n_ln16 = (n_ln + 1u) & ~1u;                           // keep the next region 16-B aligned
     const uint32_t path_st_base = n_ln16;
     const uint32_t path_base32 = 2u * (path_st_base + (uint32_t)lds_n * rpw);   // in u32 units
-    typename E::Work w;
-    E::load(roots[root], w);
-    dk::Rng rng = dk::Rng::seed_from_u64(seeds[root]);
-    GpuMem<typename E::Work, LN_LDS> mem;
-    mem.hot = hot + (size_t)root * cap_slots;
-    mem.cold = cold + (size_t)root * cap_slots;
-    mem.states = states + (size_t)root * T;
-    mem.path_st_off = path_st_base + lane;
-    mem.path_off = path_base32 + lane;
-    mem.ln_glob = ln_table;
-    mem.lds_n = lds_n;
-    mem.path_stride = rpw;
-    mem.ovf = ovf + (size_t)root * dk::MAX_DEPTH;
-    mem.ovf_st = ovf_st + (size_t)root * dk::MAX_DEPTH;
-    mem.cap_slots = cap_slots; mem.cap_states = T;
+    const uint32_t groups = (n + rpw - 1) / rpw;
+    const size_t pr = (size_t)blockIdx.x * rpw + lane;                  // this lane's pool region
+    for (;;) {
+        uint32_t g = 0;
+        if (lane == 0) g = atomicAdd(queue, 1u);
+        g = __shfl(g, 0);
+        if (g >= groups) break;                                         // every wave reaches this
+        const uint32_t root = g * rpw + lane;
+        if (lane >= rpw || root >= n) continue;
+        typename E::Work w;
+        E::load(roots[root], w);
+        dk::Rng rng = dk::Rng::seed_from_u64(seeds[root]);
+        GpuMem<typename E::Work, LN_LDS> mem;
+        mem.hot = hot + pr * cap_slots;
+        mem.cold = cold + pr * cap_slots;
+        mem.states = states + pr * T;
+        mem.path_st_off = path_st_base + lane;
+        mem.path_off = path_base32 + lane;
+        mem.ln_glob = ln_table;
+        mem.lds_n = lds_n;
+        mem.path_stride = rpw;
+        mem.ovf = ovf + pr * dk::MAX_DEPTH;
+        mem.ovf_st = ovf_st + pr * dk::MAX_DEPTH;
+        mem.cap_slots = cap_slots; mem.cap_states = T;
 #ifdef DK_PHASE_PROF
-    mem.prof = prof + (size_t)root * 16;
+        mem.prof = prof + (size_t)root * 16;
 #else
-    (void)prof;
+        (void)prof;
 #endif
-    uint8_t b;
-    const int st = dk::search_root<E>(w, rng, iters, c, mem, visits + (size_t)root * 39,
-                                      values + (size_t)root * 39, &b, nullptr);
-    if (st != dk::SR_OK) atomicOr(err, 1);
-    best[root] = b;
+        uint8_t b;
+        const int st = dk::search_root<E>(w, rng, iters, c, mem, visits + (size_t)root * 39,
+                                          values + (size_t)root * 39, &b, nullptr);
+        if (st != dk::SR_OK) atomicOr(err, 1);
+        best[root] = b;
+    }
 }
 
 __device__ void new_game_packed(int game, uint64_t seed, dk_state& out) {
@@ -399,6 +415,10 @@ struct dk_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     uint32_t max_roots = 0, max_iters = 0, cap_slots = 0;
+    uint32_t pool_roots = 0;        // roots the node pools hold at once (min(max_roots, DK_POOL_ROOTS or
+                                    // the resident capacity: CUs x 8 single-wave workgroups x 64 lanes))
+    int cu_count = 0;
+    uint32_t* queue = nullptr;      // root-group counter of the persistent search grid
     dk::NodeHot* hot = nullptr;
     dk::NodeCold* cold = nullptr;
     uint32_t* ovf = nullptr;
@@ -410,12 +430,12 @@ struct dk_ctx {
     bool timed = false;
     int last_error = DK_OK;
     uint64_t pool_bytes = 0;
-    uint32_t roots_per_wave = 32;   // DK_ROOTS_PER_WAVE (32: one wave per SIMD for 32K roots, less divergence than 64)
+    uint32_t roots_per_wave = 64;   // DK_ROOTS_PER_WAVE
     bool ln_in_lds = false;         // DK_LN_LDS=1: ln(N) table copied into every workgroup's LDS (8 KB at
                                     // 1000 iterations); by default it is read through the L1/L2 caches
     int lds_path = 16;              // DK_LDS_PATH (path entries kept in LDS, <= MAX_PATH; deeper ones
-                                    // spill to global).  16 keeps a workgroup at 6 KB of LDS so that
-                                    // 12 single-wave workgroups (3 per SIMD) fit a CU's 160 KB.
+                                    // spill to global).  16 keeps a workgroup at 12 KB of LDS so that
+                                    // 8 single-wave workgroups (2 per SIMD) fit a CU's 160 KB.
     uint64_t* prof = nullptr;       // phase timers (DK_PHASE_PROF builds only)
     std::vector<void*> scratch;
     std::vector<size_t> scratch_size;
@@ -453,24 +473,36 @@ int finish(dk_ctx* ctx, hipStream_t st) {
     return ctx->last_error = DK_OK;
 }
 
+template <class E, bool LN>
+hipError_t launch_search_t(dk_ctx* ctx, const dk_state* roots, const uint64_t* seeds, uint32_t n, uint32_t iters,
+                           double c, uint32_t* visits, double* values, uint8_t* best, hipStream_t st,
+                           size_t lds_bytes) {
+    const uint32_t rpw = ctx->roots_per_wave;
+    const auto kern = search_kernel<E, LN>;
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, WAVE, lds_bytes) != hipSuccess || per_cu < 1)
+        per_cu = 1;
+    const uint32_t groups = grid_for(n, rpw);
+    const uint32_t resident = (uint32_t)per_cu * (uint32_t)ctx->cu_count;
+    const uint32_t regions = ctx->pool_roots / rpw;
+    uint32_t grid = groups < resident ? groups : resident;
+    grid = grid < regions ? grid : regions;
+    if (grid == 0) return hipErrorInvalidValue;
+    hipError_t e = hipMemsetAsync(ctx->queue, 0, sizeof(uint32_t), st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(WAVE), lds_bytes, st, roots, seeds, n, iters, c, ctx->ln_table,
+                       ctx->hot, ctx->cold, (typename E::Work*)ctx->states, ctx->ovf, ctx->ovf_st, ctx->cap_slots,
+                       rpw, ctx->lds_path, visits, values, best, ctx->err, ctx->queue, ctx->prof);
+    return hipGetLastError();
+}
+
 template <class E>
 hipError_t launch_search(dk_ctx* ctx, const dk_state* roots, const uint64_t* seeds, uint32_t n, uint32_t iters,
                          double c, uint32_t* visits, double* values, uint8_t* best, hipStream_t st) {
-    const uint32_t rpw = ctx->roots_per_wave;
-    const int lds_n = ctx->lds_path;
-    const size_t lds_bytes = (iters + 1 <= LN_LDS_MAX && ctx->ln_in_lds ? (size_t)((iters + 2) & ~1u) * 8 : 0) +
-                             (size_t)lds_n * rpw * 12;
-    if (iters + 1 <= LN_LDS_MAX && ctx->ln_in_lds)
-        hipLaunchKernelGGL((search_kernel<E, true>), dim3(grid_for(n, rpw)), dim3(WAVE), lds_bytes, st,
-                           roots, seeds, n, iters, c, ctx->ln_table, ctx->hot, ctx->cold,
-                           (typename E::Work*)ctx->states, ctx->ovf, ctx->ovf_st, ctx->cap_slots, rpw, lds_n, visits,
-                           values, best, ctx->err, ctx->prof);
-    else
-        hipLaunchKernelGGL((search_kernel<E, false>), dim3(grid_for(n, rpw)), dim3(WAVE), lds_bytes, st,
-                           roots, seeds, n, iters, c, ctx->ln_table, ctx->hot, ctx->cold,
-                           (typename E::Work*)ctx->states, ctx->ovf, ctx->ovf_st, ctx->cap_slots, rpw, lds_n, visits,
-                           values, best, ctx->err, ctx->prof);
-    return hipGetLastError();
+    const bool ln = iters + 1 <= LN_LDS_MAX && ctx->ln_in_lds;
+    const size_t lds_bytes = (ln ? (size_t)((iters + 2) & ~1u) * 8 : 0) + (size_t)ctx->lds_path * ctx->roots_per_wave * 12;
+    return ln ? launch_search_t<E, true>(ctx, roots, seeds, n, iters, c, visits, values, best, st, lds_bytes)
+              : launch_search_t<E, false>(ctx, roots, seeds, n, iters, c, visits, values, best, st, lds_bytes);
 }
 
 }  // namespace
@@ -510,16 +542,7 @@ dk_ctx* dk_create(const dk_config* cfg) {
     // Proven bound: the root block (<= 39) plus one block of <= 12 children per
     // iteration (non-root nodes offer at most 12 cards / 9 reservations / 1 pass).
     ctx->cap_slots = cfg->slot_capacity ? cfg->slot_capacity : 40u + 12u * cfg->max_iterations;
-    const size_t R = cfg->max_roots, S = ctx->cap_slots, T = (size_t)cfg->max_iterations + 1;
-    bool ok = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) == hipSuccess;
-    ok = ok && hipMalloc(&ctx->hot, R * S * sizeof(dk::NodeHot)) == hipSuccess;
-    ok = ok && hipMalloc(&ctx->cold, R * S * sizeof(dk::NodeCold)) == hipSuccess;
-    ok = ok && hipMalloc(&ctx->ovf, R * dk::MAX_DEPTH * sizeof(uint32_t)) == hipSuccess;
-    ok = ok && hipMalloc(&ctx->ovf_st, R * dk::MAX_DEPTH * sizeof(uint64_t)) == hipSuccess;
-    ok = ok && hipMalloc(&ctx->states, R * T * STATE_SLOT_BYTES) == hipSuccess;
-    ok = ok && hipMalloc(&ctx->ln_table, (T + 1) * sizeof(double)) == hipSuccess;
-    ok = ok && hipMalloc(&ctx->err, sizeof(int)) == hipSuccess;
-    ok = ok && hipEventCreate(&ctx->ev0) == hipSuccess && hipEventCreate(&ctx->ev1) == hipSuccess;
+    ctx->cu_count = prop.multiProcessorCount;
     if (const char* e = getenv("DK_ROOTS_PER_WAVE")) {
         const int v = atoi(e);
         if (v >= 1 && v <= WAVE) ctx->roots_per_wave = (uint32_t)v;
@@ -529,9 +552,30 @@ dk_ctx* dk_create(const dk_config* cfg) {
         const int v = atoi(e);
         if (v >= 1 && v <= MAX_PATH) ctx->lds_path = v;
     }
+    // The search grid is persistent (search_kernel): the pools hold the resident waves'
+    // roots, and a larger batch streams through them.
+    uint64_t pool = (uint64_t)prop.multiProcessorCount * 8u * WAVE;
+    if (const char* e = getenv("DK_POOL_ROOTS")) {
+        const long long v = atoll(e);
+        if (v >= 1) pool = (uint64_t)v;
+    }
+    if (pool > cfg->max_roots) pool = cfg->max_roots;
+    const uint32_t rpw = ctx->roots_per_wave;
+    ctx->pool_roots = (uint32_t)((pool + rpw - 1) / rpw * rpw);   // whole regions of rpw roots
+    const size_t R = ctx->pool_roots, S = ctx->cap_slots, T = (size_t)cfg->max_iterations + 1;
+    bool ok = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) == hipSuccess;
+    ok = ok && hipMalloc(&ctx->hot, R * S * sizeof(dk::NodeHot)) == hipSuccess;
+    ok = ok && hipMalloc(&ctx->cold, R * S * sizeof(dk::NodeCold)) == hipSuccess;
+    ok = ok && hipMalloc(&ctx->ovf, R * dk::MAX_DEPTH * sizeof(uint32_t)) == hipSuccess;
+    ok = ok && hipMalloc(&ctx->ovf_st, R * dk::MAX_DEPTH * sizeof(uint64_t)) == hipSuccess;
+    ok = ok && hipMalloc(&ctx->states, R * T * STATE_SLOT_BYTES) == hipSuccess;
+    ok = ok && hipMalloc(&ctx->ln_table, (T + 1) * sizeof(double)) == hipSuccess;
+    ok = ok && hipMalloc(&ctx->err, sizeof(int)) == hipSuccess;
+    ok = ok && hipMalloc(&ctx->queue, sizeof(uint32_t)) == hipSuccess;
+    ok = ok && hipEventCreate(&ctx->ev0) == hipSuccess && hipEventCreate(&ctx->ev1) == hipSuccess;
 #ifdef DK_PHASE_PROF
-    ok = ok && hipMalloc(&ctx->prof, R * 16 * sizeof(uint64_t)) == hipSuccess;
-    ok = ok && hipMemset(ctx->prof, 0, R * 16 * sizeof(uint64_t)) == hipSuccess;
+    ok = ok && hipMalloc(&ctx->prof, (size_t)cfg->max_roots * 16 * sizeof(uint64_t)) == hipSuccess;
+    ok = ok && hipMemset(ctx->prof, 0, (size_t)cfg->max_roots * 16 * sizeof(uint64_t)) == hipSuccess;
 #endif
     if (ok) {
         // ln(N) exactly as glibc `log` computes it — what Rust's f64::ln calls (node.rs:253).
@@ -557,6 +601,7 @@ void dk_destroy(dk_ctx* ctx) {
     if (ctx->states) (void)hipFree(ctx->states);
     if (ctx->ln_table) (void)hipFree(ctx->ln_table);
     if (ctx->err) (void)hipFree(ctx->err);
+    if (ctx->queue) (void)hipFree(ctx->queue);
     if (ctx->prof) (void)hipFree(ctx->prof);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);

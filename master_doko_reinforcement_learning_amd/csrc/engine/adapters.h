@@ -14,7 +14,11 @@ struct FdoE {
     DK_HD static uint64_t allowed(const Work& w, bool first) { return fdo::env_allowed(w, first); }
     DK_HD static int current_player(const Work& w) { return fdo::env_current_player(w); }
     DK_HD static bool terminal(const Work& w) { return fdo::is_terminal(w); }
-    DK_HD static void step(Work& w, int a) { fdo::play_action(w, a); }
+    DK_HD static void step(Work& w, int a) {
+        fdo::play_action(w, a);
+        w.pad0 = 0;   // padding is don't-care: constant stores instead of carrying the loaded bytes
+        w.pad1 = 0;
+    }
     DK_HD static int rollout(const Work& w, Rng& rng, int r[4]) { return fdo::rollout(w, rng, r); }
     DK_HD static void rewards(const Work& w, int r[4]) { fdo::score(w, r); }
     DK_HD static void step_packed(dk_state& s, int a) { fdo::step_packed(s.fdo, a); }

@@ -100,6 +100,7 @@ struct Work {
     uint8_t solved_trick, re_players, re_lowest, contra_lowest;
     uint8_t ann_turns, ann_start, ann_allowed, ann_count;
     uint8_t ann_players, res_start, res_len, pad0;
+    uint32_t pad1;          // explicit tail padding (88 B): stored as 0, never carried through registers
 };
 
 DK_HD int hand_len(const Work& w, int p) { return popc64(sel4(w.h, p)); }

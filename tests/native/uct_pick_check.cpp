@@ -67,16 +67,13 @@ int main(int argc, char** argv) {
             total += v;
         }
         if (r() % 50 == 0) rec[r() % n].stats = 0;   // an unvisited child
-        for (uint32_t j = 0; j < n; ++j) {                // what the backup stores next to the stats
-            rec[j].q = dk::mean_of(rec[j].stats);
-            rec[j].isv = (uint32_t)rec[j].stats ? dk::rsqrt_approx((float)(uint32_t)rec[j].stats) : 0.0f;
-        }
+        for (uint32_t j = 0; j < n; ++j) rec[j] = dk::make_hot(rec[j].stats, 0, 0);   // as the backup leaves it
         const double lnN = std::log((double)(total + (uint32_t)(r() % 5)));
         const double c = (r() % 4 == 0) ? 0.7 + (double)(r() % 100) / 10.0 : 2.5;
         dk::Block blk;
         for (int j = 0; j < dk::SCAN_REG; ++j) {
             blk.st[j] = rec[j].stats; blk.cb[j] = (uint32_t)j * 7; blk.inf[j] = (uint32_t)j * 13;
-            blk.q[j] = rec[j].q; blk.isv[j] = rec[j].isv;
+            blk.q[j] = dk::hot_q(rec[j]); blk.isv[j] = dk::hot_isv(rec[j]);
         }
         uint64_t gs; uint32_t gc, gi;
         dk::NodeHot end; bool end_ok;

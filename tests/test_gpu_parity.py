@@ -191,9 +191,15 @@ def test_search_parity_fdo(eng, iters):
         assert int(best[i]) == (b if b >= 0 else 255), i
 
 
-@pytest.mark.parametrize("env", [{"DK_LDS_PATH": "2"}, {"DK_ROOTS_PER_WAVE": "7"}, {"DK_ROOTS_PER_WAVE": "16"}])
+@pytest.mark.parametrize("env", [{"DK_LDS_PATH": "2"}, {"DK_ROOTS_PER_WAVE": "7"}, {"DK_ROOTS_PER_WAVE": "16"},
+                                 {"DK_ROOTS_PER_WAVE": "32", "DK_LN_LDS": "1"},
+                                 {"DK_POOL_ROOTS": "1", "DK_ROOTS_PER_WAVE": "4"},
+                                 {"DK_POOL_ROOTS": "16", "DK_ROOTS_PER_WAVE": "5"}])
 def test_search_parity_fdo_launch_variants(env, monkeypatch):
-    """Path overflow into global memory (2 LDS entries) and partial / narrow waves."""
+    """Path overflow into global memory (2 LDS entries), partial / narrow waves, the LDS
+    ln table, and batches larger than the node pools: with DK_POOL_ROOTS=1 one wave
+    streams all six 4-root groups through a single pool region (stale trees of the
+    previous group stay in it), with 16 four waves share five groups."""
     import master_doko_reinforcement_learning_amd as dk
     for k, v in env.items():
         monkeypatch.setenv(k, v)

@@ -13,7 +13,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def main(m=2, steps=6, infostates=1536):
+def main(m=2, steps=6, infostates=2048):
     import torch
 
     import bench

@@ -1,7 +1,8 @@
 """Summarise a tools/collect_profiles.sh run (gpurun_out/prof_<tag>) into profiles/<tag>/.
 
 Writes kernel_stats.csv (rocprofv3 --stats, unchanged), kernel_trace_search.csv
-(search-kernel rows of the trace) and pmc_search.json (PMC values of the search
+(search-kernel rows of the trace), bench_under_trace.json (the traced bench's own
+JSON line) and pmc_search.json (PMC values of the search
 kernel per launch, HBM bytes with the MI355X_MICROARCH.md gfx950 correction),
 and refreshes profiles/pmc_search.json, which bench.py reads for roofline.traffic.
 """
@@ -15,7 +16,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def main(tag="r01", roots=98304, iterations=1000):
+def main(tag="r01", roots=262144, iterations=1000):
     src = os.path.join(ROOT, "gpurun_out", "prof_" + tag)
     dst = os.path.join(ROOT, "profiles", tag)
     os.makedirs(dst, exist_ok=True)
@@ -32,6 +33,16 @@ def main(tag="r01", roots=98304, iterations=1000):
             d["Duration_ns"] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
             w.writerow(d)
     durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows]
+    # the bench line printed by the traced run itself: its HIP-event search time is the
+    # one the trace durations must agree with (box-to-box clocks differ by several %)
+    traced_bench = None
+    with open(os.path.join(src, "trace.log")) as fh:
+        for line in fh:
+            if line.startswith("{"):
+                traced_bench = json.loads(line)
+    if traced_bench is not None:
+        with open(os.path.join(dst, "bench_under_trace.json"), "w") as fh:
+            json.dump(traced_bench, fh, indent=1)
     pmc = {}
     for f in sorted(glob.glob(os.path.join(src, "pmc*", "p_counter_collection.csv"))):
         per = {}
@@ -52,6 +63,7 @@ def main(tag="r01", roots=98304, iterations=1000):
         "iterations": iterations,
         "trace_avg_ns": sum(durs) / len(durs) if durs else None,
         "trace_launches": len(durs),
+        "bench_search_kernel_ms_same_run": traced_bench.get("search_kernel_ms") if traced_bench else None,
         "pmc_per_launch": vals,
         "fetch_bytes_raw": fetch_kb * 1024 if fetch_kb is not None else None,
         "write_bytes": write_kb * 1024 if write_kb is not None else None,
