@@ -36,11 +36,13 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--workload", choices=["c3", "c2"], default="c3")
+    p.add_argument("--workload", choices=["c3", "c2", "c2d"], default="c3",
+                   help="c3: rs-full-doko + CAP (default, the metric's config); c2: rs-doko roots after 4x Healthy; "
+                        "c2d: rs-doko infostates determinized by the rule-based sampler")
     p.add_argument("--iterations", type=int, default=1000)
     p.add_argument("--infostates", type=int, default=4096,
                    help="infostates per GPU (c3): 4096 x 64 samples = 262,144 roots, streamed through the resident waves' node pools (131,072 roots)")
-    p.add_argument("--samples", type=int, default=64, help="CAP samples per infostate (c3)")
+    p.add_argument("--samples", type=int, default=64, help="samples per infostate (c3, c2d)")
     p.add_argument("--roots", type=int, default=32768, help="roots per GPU (c2)")
     p.add_argument("--c", type=float, default=2.5)
     p.add_argument("--fusion", choices=["maxn", "avg"], default="maxn")
@@ -65,7 +67,9 @@ def make_workload(args, dk, L, dev, sp, rank, world, local_rank, dist=None):
     iters = args.iterations
     fuse_mode = dk.FUSE_MAXN if args.fusion == "maxn" else dk.FUSE_AVG
 
-    if args.workload == "c3":
+    determinized = args.workload in ("c3", "c2d")
+    game = dk.GAME_FULL_DOKO if args.workload == "c3" else dk.GAME_DOKO
+    if determinized:
         if args.samples % world:
             raise SystemExit("samples must be divisible by the number of GPUs")
         I = args.infostates * world          # global infostates
@@ -82,10 +86,10 @@ def make_workload(args, dk, L, dev, sp, rank, world, local_rank, dist=None):
         for _ in range(4):
             ck(L.dk_env_step_batch_async(eng.ctx, ptr(states_t), ptr(a), n, sp))
 
-    if args.workload == "c3":
+    if determinized:
         info_seeds = torch.tensor(np.arange(I, dtype=np.uint64) + np.uint64(0xC3000000), device=dev)
         info = torch.zeros((I, 128), dtype=torch.uint8, device=dev)
-        ck(L.dk_new_game_batch_async(eng.ctx, dk.GAME_FULL_DOKO, ptr(info_seeds), I, ptr(info), sp))
+        ck(L.dk_new_game_batch_async(eng.ctx, game, ptr(info_seeds), I, ptr(info), sp))
         healthy_round(info, I)
         plies = torch.tensor(np.array([[0, 8, 20, 32][j % 4] for j in range(I)], dtype=np.uint32).view(np.int32), device=dev)
         ply_rng = torch.tensor(dk.splitmix_rng_states(np.arange(I, dtype=np.uint64) + np.uint64(0xC3100000)).view(np.int64), device=dev)
@@ -115,9 +119,9 @@ def make_workload(args, dk, L, dev, sp, rank, world, local_rank, dist=None):
     ck(L.dk_sync(eng.ctx, sp))
 
     def step():
-        if args.workload == "c3":
+        if determinized:
             ck(L.dk_determinize_batch_async(eng.ctx, ptr(info), I, S_r, ptr(d_samp), ptr(roots), sp))
-            ck(L.dk_search_batch_async(eng.ctx, dk.GAME_FULL_DOKO, ptr(roots), ptr(d_srch), n_roots, iters, args.c,
+            ck(L.dk_search_batch_async(eng.ctx, game, ptr(roots), ptr(d_srch), n_roots, iters, args.c,
                                        ptr(visits), ptr(values), ptr(best), sp))
             ck(L.dk_fuse_accumulate_async(eng.ctx, ptr(visits), I, S_r, ptr(allowed), fuse_mode, ptr(acc_u), ptr(acc_f), sp))
             if world > 1:
@@ -128,7 +132,7 @@ def make_workload(args, dk, L, dev, sp, rank, world, local_rank, dist=None):
                                        ptr(visits), ptr(values), ptr(best), sp))
 
     return eng, step, n_roots, {"visits": visits, "values": values, "best": best, "roots": roots, "I": I, "S_r": S_r,
-                                "actions": actions if args.workload == "c3" else None}
+                                "actions": actions if determinized else None}
 
 
 def main():
@@ -167,6 +171,7 @@ def main():
             raise RuntimeError("doko_amd error %d: %s" % (rc, L.dk_status_string(rc).decode()))
 
     eng, step, n_roots, bufs = make_workload(args, dk, L, dev, sp, rank, world, local_rank, dist)
+    determinized = args.workload in ("c3", "c2d")
     search_ms = []
     iters = args.iterations
     visits = bufs["visits"]
@@ -208,6 +213,18 @@ def main():
         b_sim = alg_bytes_per_sim(args.workload)
         achieved = n_roots * iters * b_sim / (kernel_ms / 1e3) / 1e9 if b_sim else None
         traffic = pmc_traffic(n_roots, iters) if args.workload == "c3" else None
+        workload_desc = {
+            "c3": "C3 rs-full-doko determinized UCT: %d infostates x %d CAP samples/GPU-share, %d roots x %d sims per GPU"
+                  % (I, args.samples, n_roots, iters),
+            "c2d": "C2 determinized: rs-doko, %d infostates x %d rule-based samples/GPU-share "
+                   "(rs-doko-assignment), %d roots x %d sims per GPU" % (I, args.samples, n_roots, iters),
+            "c2": "C2 rs-doko random-rollout UCT: %d roots x %d sims per GPU" % (n_roots, iters),
+        }[args.workload]
+        data = {"c3": "synthetic: seeded deals (SmallRng::seed_from_u64), 4x Healthy, k in {0,8,20,32} random plies; "
+                      "determinized on the GPU by CAP",
+                "c2d": "synthetic: seeded rs-doko deals, 4x Healthy, k in {0,8,20,32} random plies; determinized "
+                       "on the GPU by the rs-doko-assignment sampler",
+                "c2": "synthetic: seeded rs-doko deals (SmallRng::seed_from_u64(0xD0C00000+i)), 4x Healthy"}[args.workload]
         stream_peak = stream_copy_gbs(torch, dev)
         result = {
             "metric": METRIC,
@@ -221,16 +238,13 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u64+f64",
-            "data": "synthetic: seeded deals (SmallRng::seed_from_u64), 4x Healthy, k in {0,8,20,32} random plies; "
-                    "determinized on the GPU by CAP",
+            "data": data,
             "config": {
-                "workload": ("C3 rs-full-doko determinized UCT: %d infostates x %d CAP samples/GPU-share, %d roots x %d sims per GPU"
-                             % (I, args.samples, n_roots, iters)) if args.workload == "c3" else
-                            ("C2 rs-doko random-rollout UCT: %d roots x %d sims per GPU" % (n_roots, iters)),
+                "workload": workload_desc,
                 "roots_per_gpu": n_roots,
                 "iterations": iters,
                 "uct_c": args.c,
-                "fusion": args.fusion if args.workload == "c3" else None,
+                "fusion": args.fusion if determinized else None,
                 "parallelism": "dp%d (samples split over GPUs, RCCL all-reduce of fusion accumulators)" % world,
             },
             "kernel_only_rollouts_per_s": n_roots * iters * world / (kernel_ms / 1e3),
@@ -244,8 +258,9 @@ def main():
                 "traffic": traffic,
                 "alg_bytes_per_sim": b_sim,
                 "stream_copy_peak_measured_gbs": stream_peak,
-                "note": "the search is VALU/SALU-issue bound (one 32-root wave per SIMD, PMC: ~65% of wave cycles "
-                        "issuing); HBM bytes are the SURVEY 8(d) algorithmic model from the oracle's counters, "
+                "note": "the search is bound by VALU issue and dependent-load latency (64-root waves, two per SIMD; "
+                        "PMC: VALU busy ~51% of the launch, 41% of wave cycles waiting on memory); achieved = the "
+                        "SURVEY 8(d) algorithmic bytes from the oracle's counters / event-timed kernel; "
                         "traffic = 2*FETCH_SIZE+WRITE_SIZE from profiles/pmc_search.json scaled per launch",
             },
             "cpu_baseline": cpu,
@@ -269,23 +284,34 @@ def cpu_baseline(args, dk):
     iters = args.iterations
     roots = []
     seeds = []
-    if args.workload == "c3":
+    if args.workload in ("c3", "c2d"):
+        do = args.workload == "c2d"
         for k in range(n):
             j, s = k % args.infostates, k // args.infostates
-            st = ol.FdoState.new_game(0xC3000000 + j)
+            st = (ol.DoState if do else ol.FdoState).new_game(0xC3000000 + j)
             for _ in range(4):
                 st.play(24)
             rng = ol.arr(ctypes.c_uint64, 4, [int(x) for x in dk.splitmix_rng_states(np.array([0xC3100000 + j], dtype=np.uint64))[0]])
-            st.random_plies(rng, [0, 8, 20, 32][j % 4], True)
-            smp = st.card_matching(ol.rng_seed(0xC3200000 + j * args.samples + s))
+            if do:
+                st.random_plies(rng, [0, 8, 20, 32][j % 4])
+                smp = st.sample_assignment_full(ol.rng_seed(0xC3200000 + j * args.samples + s))
+            else:
+                st.random_plies(rng, [0, 8, 20, 32][j % 4], True)
+                smp = st.card_matching(ol.rng_seed(0xC3200000 + j * args.samples + s))
             roots.append(smp)
             seeds.append(0xC3300000 + j * args.samples + s)
         handles = (ctypes.c_void_p * n)(*[r.h for r in roots])
         vis = (ctypes.c_uint32 * (39 * n))()
         sd = ol.arr(ctypes.c_uint64, n, seeds)
-        secs = ol.lib().or_fdo_search_many(None, handles, sd, n, iters, args.c, vis, threads)
+        if do:
+            secs = ol.lib().or_do_search_many(handles, sd, n, iters, args.c, vis, threads)
+        else:
+            secs = ol.lib().or_fdo_search_many(None, handles, sd, n, iters, args.c, vis, threads)
         n1 = min(n, 64)
-        secs1 = ol.lib().or_fdo_search_many(None, handles, sd, n1, iters, args.c, vis, 1)
+        if do:
+            secs1 = ol.lib().or_do_search_many(handles, sd, n1, iters, args.c, vis, 1)
+        else:
+            secs1 = ol.lib().or_fdo_search_many(None, handles, sd, n1, iters, args.c, vis, 1)
     else:
         for k in range(n):
             st = ol.DoState.new_game(0xD0C00000 + k)

@@ -197,9 +197,15 @@ int dk_search_batch_async(dk_ctx* ctx, int game, const dk_state* d_roots, const 
                           uint32_t iterations, double c, uint32_t* d_visits, double* d_values, uint8_t* d_best,
                           void* stream);
 
-/* ---- CAPSampling::sample -> card_matching_full ------------------------------
- * (compare_impi.rs:64-81 -> rs-full-doko/src/matching/card_matching.rs:469-497)
- * out[i*samples + s] = card_matching_full(infostates[i], SmallRng::seed_from_u64(seeds[i*samples+s]))
+/* ---- determinization: SamplingFn::sample ------------------------------------
+ * out[i*samples + s] = sample(infostates[i], SmallRng::seed_from_u64(seeds[i*samples+s])), by game:
+ *   DK_GAME_FULL_DOKO: CAPSampling -> card_matching_full
+ *       (compare_impi.rs:64-81 -> rs-full-doko/src/matching/card_matching.rs:469-497)
+ *   DK_GAME_DOKO:      sample_assignment_full(state, &state.observation_for_current_player(), rng)
+ *       (rs-doko-assignment/src/assignment.rs:472-580; observation rs-doko/src/state/state.rs:336-410)
+ * Any other game, or a finished rs-full-doko infostate, is DK_E_STATE. An rs-doko
+ * infostate on which the reference sampler panics (a hidden card that no player
+ * with open slots may hold, assignment.rs:430-433) is DK_E_STATE as well.
  */
 int dk_determinize_batch(dk_ctx* ctx, const dk_state* infostates, uint32_t n_info, uint32_t samples,
                          const uint64_t* seeds, dk_state* out);

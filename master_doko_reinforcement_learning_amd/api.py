@@ -6,6 +6,7 @@ Names follow the Rust types they replace:
 * ``McEnv``                       — McEnvState (rs-doko-mcts/src/env/env_state.rs:7-28), batched
 * ``CachedMCTS``                  — CachedMCTS::monte_carlo_tree_search (mcts.rs:284-315), batched over roots
 * ``card_matching_full``          — CAP determinization (rs-full-doko/src/matching/card_matching.rs:469-497)
+* ``sample_assignment_full``      — rs-doko rule-based determinization (rs-doko-assignment/src/assignment.rs:472-580)
 * ``PolicyFusionMaxN`` / ``PolicyFusionAverageStrategy`` — policy_fusion.rs:18-123
 * ``DefaultImpiPolicy``           — sample -> search -> fuse (compare_impi.rs:212-371)
 
@@ -178,6 +179,14 @@ def card_matching_full(engine, infostates, samples, seeds):
     return out
 
 
+def sample_assignment_full(engine, infostates, samples, seeds):
+    """rs-doko `sample_assignment_full(state, &state.observation_for_current_player(), rng)`
+    for each rs-doko infostate, `samples` times (rng i*samples+s =
+    SmallRng::seed_from_u64(seeds[i*samples+s])): returns (n_info*samples, 128)
+    determinized states.  Raises DokoError where the reference panics."""
+    return card_matching_full(engine, infostates, samples, seeds)
+
+
 class _Fusion:
     mode = None
 
@@ -200,7 +209,10 @@ class PolicyFusionAverageStrategy(_Fusion):
 
 
 class DefaultImpiPolicy:
-    """Determinized decision: `num_samples` CAP samples -> UCT each -> fusion."""
+    """Determinized decision: `num_samples` samples -> UCT each -> fusion.
+    rs-full-doko infostates are sampled by CAP (compare_impi.rs:64-81), rs-doko
+    infostates by the rule-based sampler (assignment.rs:472-580); one call
+    holds infostates of one game."""
 
     def __init__(self, engine, uct_exploration_constant=2.5, iterations=1000, num_samples=64, fusion=FUSE_MAXN):
         self.engine = engine

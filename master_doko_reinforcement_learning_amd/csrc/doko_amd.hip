@@ -17,6 +17,7 @@
 
 #include "../../include/doko_amd.h"
 #include "engine/adapters.h"
+#include "engine/assign_engine.h"
 #include "engine/cap_engine.h"
 #include "engine/search_core.h"
 
@@ -341,14 +342,17 @@ __global__ void __launch_bounds__(WAVE) determinize_kernel(const dk_state* info,
                                                            const uint64_t* seeds, dk_state* out, int* err) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_info * samples) return;
-    const dk_state s = info[i / samples];
+    const dk_state& s = info[i / samples];
     dk_state o;
-    if (s.raw[127] != DK_GAME_FULL_DOKO || s.fdo.current_player == DK_NONE) {
+    dk::Rng rng = dk::Rng::seed_from_u64(seeds[i]);
+    if (s.raw[127] == DK_GAME_FULL_DOKO && s.fdo.current_player != DK_NONE) {
+        dk::cap::card_matching_full(s.fdo, rng, o.fdo);          // CAPSampling (rs-full-doko)
+    } else if (s.raw[127] == DK_GAME_DOKO) {
+        if (dk::asg::sample_assignment_full(s.dk, rng, o.dk))    // rule-based sampler (rs-doko)
+            atomicOr(err, 2);
+    } else {
         atomicOr(err, 2);
         o = s;
-    } else {
-        dk::Rng rng = dk::Rng::seed_from_u64(seeds[i]);
-        dk::cap::card_matching_full(s.fdo, rng, o.fdo);
     }
     out[i] = o;
 }
@@ -896,6 +900,10 @@ int dk_decide_batch(dk_ctx* ctx, const dk_state* infostates, uint32_t n_info, ui
     const size_t n = (size_t)n_info * samples;
     if (n == 0) return DK_OK;
     if (n > ctx->max_roots || iterations > ctx->max_iters) return ctx->last_error = DK_E_CAPACITY;
+    const int game = infostates[0].raw[127];
+    if (game != DK_GAME_FULL_DOKO && game != DK_GAME_DOKO) return ctx->last_error = DK_E_INVALID;
+    for (uint32_t j = 1; j < n_info; ++j)
+        if (infostates[j].raw[127] != game) return ctx->last_error = DK_E_INVALID;
     dk_state* d_i = (dk_state*)scratch(ctx, 0, n_info * sizeof(dk_state));
     uint64_t* d_seeds = (uint64_t*)scratch(ctx, 1, 2 * n * sizeof(uint64_t));
     dk_state* d_roots = (dk_state*)scratch(ctx, 2, n * sizeof(dk_state));
@@ -911,7 +919,7 @@ int dk_decide_batch(dk_ctx* ctx, const dk_state* infostates, uint32_t n_info, ui
     DK_HIP(hipMemcpyAsync(d_seeds, seeds, 2 * n * sizeof(uint64_t), hipMemcpyHostToDevice, ctx->stream));
     int rc = dk_determinize_batch_async(ctx, d_i, n_info, samples, d_seeds, d_roots, ctx->stream);
     if (rc) return rc;
-    rc = dk_search_batch_async(ctx, DK_GAME_FULL_DOKO, d_roots, d_seeds + n, (uint32_t)n, iterations, c, d_v, d_val, d_b, ctx->stream);
+    rc = dk_search_batch_async(ctx, game, d_roots, d_seeds + n, (uint32_t)n, iterations, c, d_v, d_val, d_b, ctx->stream);
     if (rc) return rc;
     hipLaunchKernelGGL(legal_kernel, dim3(grid_for(n_info, 64)), dim3(64), 0, ctx->stream, d_i, n_info, d_allowed);
     DK_HIP(hipGetLastError());

@@ -8,7 +8,6 @@ namespace oracle {
 namespace dko {
 
 static void panic(const char* m) { fprintf(stderr, "oracle(dko) panic: %s\n", m); abort(); }
-enum Color { Trump = 0, Heart, Spade, Club };
 
 // hand/hand.rs:28-35
 uint64_t hand_add(uint64_t h, int c) {

@@ -43,7 +43,8 @@ struct State {
 
 uint64_t hand_add(uint64_t h, int c);
 uint64_t hand_remove(uint64_t h, int c);   // removes the LOW copy first (hand/hand.rs:38-46)
-int card_color(int c);                      // 0 trump, 2 heart, 3 spade, 4 club (DoColor order differs; see .cpp)
+enum Color { Trump = 0, Heart, Spade, Club };
+int card_color(int c);                      // card/card_to_color.rs (normal game)
 uint64_t calculate_allowed_actions(int phase, int trick_color, uint64_t hand);
 int winning_player_in_trick(const Trick& t);
 State new_game(SmallRng& rng);

@@ -13,6 +13,7 @@
 #include "../include/doko_amd.h"
 #include "card_matching.hpp"
 #include "doko.hpp"
+#include "assignment.hpp"
 #include "full_doko.hpp"
 #include "fusion.hpp"
 #include "mcts.hpp"
@@ -244,6 +245,45 @@ double or_do_search_many(void** roots, const uint64_t* seeds, uint32_t n, uint32
     }
     for (auto& th : pool) th.join();
     return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
+// ---------------------------------------------------------------- rs-doko sampler
+// tricks: 12 x {start player (-1 = None), card0..card3 (-1 = None)}
+static void tricks_from(const int32_t* t, dko::Trick out[12]) {
+    for (int i = 0; i < 12; ++i) {
+        out[i] = dko::Trick();
+        out[i].present = t[5 * i] >= 0;
+        out[i].start = t[5 * i] < 0 ? 0 : t[5 * i];
+        for (int k = 0; k < 4; ++k) out[i].cards[k] = t[5 * i + 1 + k];
+    }
+}
+uint64_t or_do_remaining_cards(const int32_t* tricks, uint64_t hand) {
+    dko::Trick t[12]; tricks_from(tricks, t); return dko::calc_remaining_cards(t, hand);
+}
+// out: 4 x 48 card ids (-1 padded), lens: 4
+void or_do_allowed_to_have(int marriage, const int32_t* tricks, uint64_t hand, int obs, int32_t* out, int32_t* lens) {
+    dko::Trick t[12]; tricks_from(tricks, t);
+    dko::CardVec v[4]; dko::player_allowed_to_have(marriage, t, hand, obs, v);
+    for (int i = 0; i < 4; ++i) {
+        lens[i] = (int32_t)v[i].size();
+        for (int k = 0; k < 48; ++k) out[48 * i + k] = k < (int)v[i].size() ? v[i][(size_t)k] : -1;
+    }
+}
+int or_do_sample_assignment(int marriage, const int32_t* tricks, uint64_t hand, const int32_t* lengths, int obs,
+                            uint64_t* rng_state, uint64_t* hands_out) {
+    dko::Trick t[12]; tricks_from(tricks, t);
+    int len[4] = {lengths[0], lengths[1], lengths[2], lengths[3]};
+    SmallRng r = rng_from(rng_state); dko::CardVec v[4];
+    const bool ok = dko::sample_assignment(marriage, t, hand, len, obs, r, v);
+    rng_to(r, rng_state);
+    if (ok) for (int i = 0; i < 4; ++i) hands_out[i] = dko::hand_from_vec(v[i]);
+    return ok ? 1 : 0;
+}
+void* or_do_sample_full(void* sp, uint64_t* rng_state) {
+    SmallRng r = rng_from(rng_state); dko::State out;
+    const bool ok = dko::sample_assignment_full(*(dko::State*)sp, r, out);
+    rng_to(r, rng_state);
+    return ok ? new dko::State(out) : nullptr;
 }
 
 // ---------------------------------------------------------------- tic-tac-toe

@@ -14,6 +14,7 @@ reference. The output files are data only (inputs + expected outputs):
 * bitflag_select_rank.json — rs-game-utils/src/bit_flag.rs:186-192.
 * ttt_kats.json — rs-doko-mcts/src/example/tic_tac_toe.rs tests (finish states).
 * fusion_kats.json — rs-doko-py-bridge/src/compare_impi/policy_fusion.rs:130-311.
+* do_assignment_kats.json — rs-doko-assignment/src/assignment.rs:593-1190 (rule-based sampler).
 
 Usage: python tests/golden/make_fixtures.py
 """
@@ -227,6 +228,122 @@ def fusion_kats():
     return {"source": "rs-doko-py-bridge/src/compare_impi/policy_fusion.rs:130-311", "cases": cases}
 
 
+def _strip_line_comments(text):
+    return "\n".join(ln.split("//")[0] for ln in text.split("\n"))
+
+
+def _paren(text, start):
+    """Return the content of the balanced (...) whose '(' is at text[start]."""
+    depth = 0
+    for i in range(start, len(text)):
+        if text[i] in "([":
+            depth += 1
+        elif text[i] in ")]":
+            depth -= 1
+            if depth == 0:
+                return text[start + 1:i]
+    raise ValueError("unbalanced")
+
+
+def _split_top(args):
+    out, depth, cur = [], 0, ""
+    for ch in args:
+        if ch in "([":
+            depth += 1
+        elif ch in ")]":
+            depth -= 1
+        if ch == "," and depth == 0:
+            out.append(cur.strip())
+            cur = ""
+        else:
+            cur += ch
+    if cur.strip():
+        out.append(cur.strip())
+    return out
+
+
+def _player(tok):
+    tok = tok.strip()
+    if tok.isdigit():
+        return int(tok)
+    return PLAYERS[tok.split("_")[1]]
+
+
+def _cards(tok):
+    return [CARD_NAMES.index(c.strip().split("::")[-1]) for c in tok.split(",") if c.strip()]
+
+
+def _vec_cards(tok):
+    m = re.match(r"\s*vec!\[(.*)\]\s*$", tok, re.S)
+    return _cards(m.group(1))
+
+
+def _tricks(tok):
+    body = tok.strip()[2:-1]  # &[ ... ]
+    tricks = []
+    for t in _split_top(body):
+        if t == "None":
+            tricks.append(None)
+            continue
+        m = re.match(r"Some\(DoTrick::existing\(\s*(\w+)\s*,\s*vec!\[(.*)\]\s*\)\)$", t, re.S)
+        tricks.append({"start": _player(m.group(1)), "cards": _cards(m.group(2))})
+    assert len(tricks) == 12
+    return tricks
+
+
+def _hand(tok):
+    tok = tok.strip()
+    if tok.isdigit():
+        return int(tok)
+    m = re.match(r"hand_from_vec\((.*)\)$", tok, re.S)
+    h = 0
+    for c in _vec_cards(m.group(1)):
+        h |= (1 << (c + 24)) if (h >> c) & 1 else (1 << c)
+    return h
+
+
+def _marriage(tok):
+    tok = tok.strip()
+    return -1 if tok == "None" else _player(re.match(r"Some\((\w+)\)", tok).group(1))
+
+
+def do_assignment_kats():
+    """rs-doko-assignment/src/assignment.rs:593-1190: player_allowed_to_have
+    lists, calc_remaining_cards, and the support sets of 1000 seeded samples."""
+    path = os.path.join(REF, "rs-doko-assignment/src/assignment.rs")
+    with open(path, encoding="utf-8") as fh:
+        text = fh.read()
+    tests = _strip_line_comments(text[text.find("#[cfg(test)]"):])
+    calls = []
+    for m in re.finditer(r"(?<!fn )\b(player_allowed_to_have|calc_remaining_cards|brute_force_assignments)\(", tests):
+        calls.append((m.start(), m.group(1), m.end() - 1))
+    allowed, remaining, support = [], [], []
+    for k, (pos, name, par) in enumerate(calls):
+        args = _split_top(_paren(tests, par))
+        tail = tests[par:calls[k + 1][0] if k + 1 < len(calls) else len(tests)]
+        if name == "player_allowed_to_have":
+            exp = {}
+            for i, v in re.findall(r"assert_eq!\(result\[(\d)\], vec!\[([^\]]*)\]\);", tail):
+                exp[int(i)] = _cards(v)
+            allowed.append({"marriage": _marriage(args[0]), "tricks": _tricks(args[1]), "hand": _hand(args[2]),
+                            "observer": _player(args[3]), "expect": [exp[i] for i in range(4)]})
+        elif name == "calc_remaining_cards":
+            v = re.search(r"assert_eq!\(remaining_cards_as_vec, vec!\[([^\]]*)\]\)", tail, re.S).group(1)
+            remaining.append({"tricks": _tricks(args[0]), "hand": _hand(args[1]), "expect": _cards(v)})
+        elif name == "brute_force_assignments":
+            n = re.search(r"assert_eq!\(result\.len\(\), (\d+)\)", tail)
+            sets = [[_cards(h) for h in re.findall(r"vec!\[([^\]]*)\]", blk)]
+                    for blk in re.findall(r"result\.contains\(&\[(.*?)\]\)\);", tail, re.S)]
+            support.append({"marriage": _marriage(args[0]), "tricks": _tricks(args[1]), "hand": _hand(args[2]),
+                            "lengths": [int(x) for x in re.findall(r"\d+", args[3])], "observer": _player(args[4]),
+                            "seed": 42, "draws": 1000, "expect_len": int(n.group(1)) if n else None,
+                            "expect_contains": sets})
+    return {"source": "rs-doko-assignment/src/assignment.rs:593-1190",
+            "note": "support cases draw 1000 samples from ONE SmallRng::seed_from_u64(42) stream; expect_len is the "
+                    "number of distinct (sorted) assignments; a case without expect_len must only not panic",
+            "allowed_to_have": allowed, "remaining": remaining, "support": support}
+
+
 def main():
     with open(os.path.join(OUT, "fdo_traces.json"), "w") as fh:
         json.dump(fdo_traces(), fh, indent=0)
@@ -240,6 +357,8 @@ def main():
         json.dump(ttt_kats(), fh, indent=1)
     with open(os.path.join(OUT, "fusion_kats.json"), "w") as fh:
         json.dump(fusion_kats(), fh, indent=1)
+    with open(os.path.join(OUT, "do_assignment_kats.json"), "w") as fh:
+        json.dump(do_assignment_kats(), fh, indent=None)
     print("wrote fixtures to", OUT)
 
 

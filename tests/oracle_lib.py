@@ -74,6 +74,11 @@ def lib():
             "or_do_search": (ctypes.c_int, [vp, u64p, ctypes.c_uint32, ctypes.c_double, u32p, f64p, u64p]),
             "or_do_search_many": (ctypes.c_double, [ctypes.POINTER(vp), u64p, ctypes.c_uint32, ctypes.c_uint32,
                                                     ctypes.c_double, u32p, ctypes.c_int]),
+            "or_do_remaining_cards": (ctypes.c_uint64, [i32p, ctypes.c_uint64]),
+            "or_do_allowed_to_have": (None, [ctypes.c_int, i32p, ctypes.c_uint64, ctypes.c_int, i32p, i32p]),
+            "or_do_sample_assignment": (ctypes.c_int, [ctypes.c_int, i32p, ctypes.c_uint64, i32p, ctypes.c_int,
+                                                       u64p, u64p]),
+            "or_do_sample_full": (vp, [vp, u64p]),
             "or_ttt_finish": (ctypes.c_int, [i32p]),
             "or_ttt_rollout": (None, [i32p, u64p, f64p]),
             "or_ttt_search": (ctypes.c_int, [i32p, u64p, ctypes.c_uint32, ctypes.c_double, u32p, f64p]),
@@ -230,12 +235,50 @@ class DoState:
         lib().or_do_rollout(self.h, rng, o)
         return list(o)
 
+    def sample_assignment_full(self, rng):
+        """rs-doko-assignment sample_assignment_full for the current player's
+        observation (assignment.rs:472-505); None where the reference panics."""
+        h = lib().or_do_sample_full(self.h, rng)
+        return DoState(h) if h else None
+
     def search(self, rng, iters, c):
         v = arr(ctypes.c_uint32, 39)
         val = arr(ctypes.c_double, 39)
         ctr = arr(ctypes.c_uint64, 8)
         best = lib().or_do_search(self.h, rng, iters, c, v, val, ctr)
         return best, list(v), list(val), list(ctr)
+
+
+def _tricks_arr(tricks):
+    flat = []
+    for t in tricks:
+        if t is None:
+            flat += [-1, -1, -1, -1, -1]
+        else:
+            cs = list(t["cards"]) + [-1] * (4 - len(t["cards"]))
+            flat += [t["start"]] + cs
+    return arr(ctypes.c_int32, 60, flat)
+
+
+def do_remaining_cards(tricks, hand):
+    """assignment.rs:13-39 (tricks: 12 x None | {"start", "cards"})."""
+    return lib().or_do_remaining_cards(_tricks_arr(tricks), hand)
+
+
+def do_allowed_to_have(marriage, tricks, hand, observer):
+    """assignment.rs:79-287 -> four card lists in the reference's order."""
+    out = arr(ctypes.c_int32, 4 * 48)
+    lens = arr(ctypes.c_int32, 4)
+    lib().or_do_allowed_to_have(marriage, _tricks_arr(tricks), hand, observer, out, lens)
+    return [list(out[48 * i:48 * i + lens[i]]) for i in range(4)]
+
+
+def do_sample_assignment(marriage, tricks, hand, lengths, observer, rng):
+    """assignment.rs:507-580 -> four hands (u64), or None where the reference panics."""
+    out = arr(ctypes.c_uint64, 4)
+    ok = lib().or_do_sample_assignment(marriage, _tricks_arr(tricks), hand, arr(ctypes.c_int32, 4, lengths),
+                                       observer, rng, out)
+    return list(out) if ok else None
 
 
 def ttt_pack(board, last_action=-1):

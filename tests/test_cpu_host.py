@@ -54,6 +54,13 @@ def test_engine_cap_vs_oracle(native_bins):
     assert _run("cap_check", 120, 3) > 5000
 
 
+def test_engine_assignment_vs_oracle(native_bins):
+    """assign_engine.h (host build) = oracle rs-doko sample_assignment_full
+    (rs-doko-assignment/src/assignment.rs:472-580): hands, packed state, RNG stream
+    position and panic cases at every decision point, weddings included."""
+    assert _run("assign_check", 200, 3) > 40000
+
+
 def test_fusion_kats():
     """rs-doko-py-bridge/src/compare_impi/policy_fusion.rs:130-311."""
     with open(os.path.join(GOLD, "fusion_kats.json")) as fh:

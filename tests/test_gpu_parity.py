@@ -374,3 +374,117 @@ def test_full_size_properties(eng):
     assert np.all((v1 > 0) <= (bits == 1))
     v2, val2, b2 = mcts.monte_carlo_tree_search(roots, 2.5, 1000, seeds)
     assert np.array_equal(v1, v2) and np.array_equal(val1.view(np.uint64), val2.view(np.uint64)) and np.array_equal(b1, b2)
+
+
+# ---------------------------------------------------------------- rs-doko rule-based sampler
+def do_states(n_games, seed):
+    """Random rs-doko positions from oracle trajectories (every third game a wedding when possible)."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for g in range(n_games):
+        s = ol.DoState.new_game(int(seed * 1000 + g))
+        while True:
+            out.append(s.clone())
+            info = s.info()
+            if info["phase"] == 2:
+                break
+            legal = s.allowed()
+            if info["phase"] == 0:
+                a = 25 if (g % 3 == 1 and (legal >> 25) & 1) else 24
+            else:
+                a = int(rng.choice([a for a in range(24) if legal >> a & 1]))
+            s.play(a)
+    return out
+
+
+def test_do_sample_assignment_parity(eng):
+    """sample_assignment_full (rs-doko-assignment/src/assignment.rs:472-580) on the GPU
+    == the oracle, all 128 bytes of every sample, at every phase of random games."""
+    import master_doko_reinforcement_learning_amd as dk
+    info = do_states(24, 5)[::2]
+    samples = 8
+    seeds = np.arange(len(info) * samples, dtype=np.uint64) * 977 + 11
+    got = dk.sample_assignment_full(eng, pack_all(info), samples, seeds)
+    for i, s in enumerate(info):
+        for k in range(samples):
+            smp = s.sample_assignment_full(ol.rng_seed(int(seeds[i * samples + k])))
+            assert smp is not None
+            assert got[i * samples + k].tobytes() == smp.pack()
+
+
+def _card_counts(hands):
+    """(n, 4) u64 hands -> (n, 4, 24) card multiplicities."""
+    bits = (hands[..., None] >> np.arange(48, dtype=np.uint64)) & np.uint64(1)
+    return (bits[..., :24] + bits[..., 24:]).astype(np.int32)
+
+
+def test_do_sample_assignment_full_size_properties(eng):
+    """4096 rs-doko infostates x 64 samples: hand sizes kept, the observer's cards
+    kept, the hidden cards redistributed exactly, and every sampled hand
+    consistent with the colours its player failed to follow."""
+    import master_doko_reinforcement_learning_amd as dk
+    n_info, S = 4096, 64
+    seeds = np.arange(n_info, dtype=np.uint64) + 77
+    info = eng.new_games(dk.GAME_DOKO, seeds)
+    env = dk.McEnv(eng)
+    for _ in range(4):
+        info = env.by_action(info, np.full(n_info, np.uint64(1) << np.uint64(24)))
+    plies = np.array([[0, 8, 20, 33][j % 4] for j in range(n_info)], dtype=np.uint32)
+    info, _ = env.random_plies(info, dk.splitmix_rng_states(seeds * np.uint64(3)), plies)
+    smp = dk.sample_assignment_full(eng, info, S, np.arange(n_info * S, dtype=np.uint64) * 3 + 5)
+    h_in = np.repeat(info[:, :32].copy().view(np.uint64), S, axis=0)
+    h_out = smp[:, :32].copy().view(np.uint64)
+    assert np.array_equal(smp[:, 32:], np.repeat(info[:, 32:], S, axis=0))   # only the hands change
+    c_in, c_out = _card_counts(h_in), _card_counts(h_out)
+    assert np.array_equal(c_in.sum(axis=2), c_out.sum(axis=2))
+    obs = info[:, 100].astype(np.int64)
+    obs = np.where(obs == 255, 0, obs)
+    obs = np.repeat(obs, S)
+    rows = np.arange(n_info * S)
+    assert np.array_equal(c_in[rows, obs], c_out[rows, obs])
+    assert np.array_equal(c_in.sum(axis=1), c_out.sum(axis=1))
+    # colour voids (normal-game colours): nobody holds a colour they failed to follow
+    for j in range(0, n_info, 97):
+        st = info[j]
+        nc, start = int(st[98]), int(st[96])
+        tw = int(st[88:92].copy().view(np.uint32)[0])
+        trump = set(range(6)) | {7, 8, 9, 14, 15, 20, 21}
+        color = lambda c: "T" if c in trump else "HCS"[c // 6 - 1]
+        voids = [set() for _ in range(4)]
+        for t in range(0, (nc + 3) // 4):
+            lead = color(int(st[32 + 4 * t]))
+            p0 = start if t == 0 else (tw >> (2 * (t - 1))) & 3
+            for k in range(min(4, nc - 4 * t)):
+                if color(int(st[32 + 4 * t + k])) != lead:
+                    voids[(p0 + k) % 4].add(lead)
+        for s_ in range(S):
+            for p in range(4):
+                held = {color(c) for c in range(24) if c_out[j * S + s_, p, c] > 0}
+                assert not (held & voids[p]) or p == obs[j * S]
+
+
+def test_decide_end_to_end_doko(eng):
+    """DefaultImpiPolicy on rs-doko infostates: rule-based samples -> UCT -> MaxN fusion
+    (the determinized C2 variant), against the oracle pipeline."""
+    import master_doko_reinforcement_learning_amd as dk
+    info = []
+    for j in range(6):
+        s = ol.DoState.new_game(0xD0C00000 + 40 + j)
+        for _ in range(4):
+            s.play(24)
+        s.random_plies(ol.rng_seed(700 + j), [0, 8, 20, 33][j % 4])
+        info.append(s)
+    S, iters = 8, 200
+    seeds = np.arange(2 * len(info) * S, dtype=np.uint64) * 19 + 5
+    pol = dk.DefaultImpiPolicy(eng, 2.5, iters, S, dk.FUSE_MAXN)
+    actions, visits = pol.execute(pack_all(info), seeds, return_visits=True)
+    n = len(info) * S
+    for j, s in enumerate(info):
+        rows = []
+        for k in range(S):
+            smp = s.sample_assignment_full(ol.rng_seed(int(seeds[j * S + k])))
+            _, v, _, _ = smp.search(ol.rng_seed(int(seeds[n + j * S + k])), iters, 2.5)
+            rows.append(v)
+            assert list(visits[j * S + k]) == v
+        exp, _ = ol.fuse_maxn(rows, s.allowed())
+        assert int(actions[j]) == exp

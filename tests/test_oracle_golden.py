@@ -154,3 +154,49 @@ def test_ttt_finish_states():
     for c in load("ttt_kats.json")["cases"]:
         board = [sym[ch] for ch in c["board"]]
         assert ol.lib().or_ttt_finish(ol.arr(ol.ctypes.c_int32, 9, board)) == c["finish"]
+
+
+# ---------------------------------------------------------------- rs-doko sampler
+def test_do_allowed_to_have_golden():
+    """rs-doko-assignment/src/assignment.rs:593-771 — the per-player card lists
+    (order included) of player_allowed_to_have."""
+    g = load("do_assignment_kats.json")
+    assert len(g["allowed_to_have"]) == 4
+    for case in g["allowed_to_have"]:
+        got = ol.do_allowed_to_have(case["marriage"], case["tricks"], case["hand"], case["observer"])
+        assert got == case["expect"]
+
+
+def test_do_remaining_cards_golden():
+    """assignment.rs:773-853 — calc_remaining_cards then hand_to_vec."""
+    g = load("do_assignment_kats.json")
+    for case in g["remaining"]:
+        rem = ol.do_remaining_cards(case["tricks"], case["hand"])
+        got = [c for c in range(24) for _ in range((rem >> c & 1) + (rem >> (c + 24) & 1))]
+        assert got == case["expect"]
+
+
+def _sorted_hand(h):
+    return [c for c in range(24) for _ in range((h >> c & 1) + (h >> (c + 24) & 1))]
+
+
+def test_do_sample_assignment_support_golden():
+    """assignment.rs:909-1190 — 1000 samples from one SmallRng::seed_from_u64(42)
+    stream: the set of distinct assignments equals the reference's listed set
+    (9 and 12 assignments); the third case (assignment.rs:1110-1190) must not panic."""
+    g = load("do_assignment_kats.json")
+    assert len(g["support"]) == 3
+    for case in g["support"]:
+        rng = ol.rng_seed(case["seed"])
+        seen = set()
+        for _ in range(case["draws"]):
+            hands = ol.do_sample_assignment(case["marriage"], case["tricks"], case["hand"], case["lengths"],
+                                            case["observer"], rng)
+            assert hands is not None
+            for i in range(4):
+                assert bin(hands[i]).count("1") == case["lengths"][i]
+            seen.add(tuple(tuple(_sorted_hand(h)) for h in hands))
+        if case["expect_len"] is not None:
+            assert len(seen) == case["expect_len"]
+            for exp in case["expect_contains"]:
+                assert tuple(tuple(sorted(h)) for h in exp) in seen
