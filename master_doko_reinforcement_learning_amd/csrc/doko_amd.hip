@@ -147,7 +147,7 @@ __global__ void DK_SEARCH_BOUNDS search_kernel(const dk_state* __restrict__ root
     const uint32_t T = iters + 1;
     const uint32_t n_ln = LN_LDS ? T : 0u;
     for (uint32_t i = lane; i < n_ln; i += WAVE) dk_lds[i] = (uint64_t)__double_as_longlong(ln_table[i]);
-    if (E::GAME == DK_GAME_FULL_DOKO) dk::fdo::card_table_init();   // ends with a barrier
+    if (E::GAME != DK_GAME_TTT) dk::fdo::card_table_init();   // ends with a barrier
     __syncthreads();
     const uint32_t n_ln16 = (n_ln + 1u) & ~1u;                           // keep the next region 16-B aligned
     const uint32_t path_st_base = n_ln16;
@@ -434,7 +434,8 @@ struct dk_ctx {
     bool timed = false;
     int last_error = DK_OK;
     uint64_t pool_bytes = 0;
-    uint32_t roots_per_wave = 64;   // DK_ROOTS_PER_WAVE
+    uint32_t roots_per_wave = 64;   // pool region width; DK_ROOTS_PER_WAVE fixes the launch width too
+    bool rpw_fixed = false;
     bool ln_in_lds = false;         // DK_LN_LDS=1: ln(N) table copied into every workgroup's LDS (8 KB at
                                     // 1000 iterations); by default it is read through the L1/L2 caches
     int lds_path = 16;              // DK_LDS_PATH (path entries kept in LDS, <= MAX_PATH; deeper ones
@@ -477,11 +478,24 @@ int finish(dk_ctx* ctx, hipStream_t st) {
     return ctx->last_error = DK_OK;
 }
 
+// Roots per wave of one launch.  A wave64 instruction costs the same whatever its
+// exec mask, so full 64-root waves do the most work per instruction; but a batch
+// too small to give every SIMD a wave leaves SIMDs idle.  Take the widest wave
+// (a multiple of 16) that still puts one wave on every SIMD: 32,768 roots on 256
+// CUs run as 1,024 waves of 32 (756 M/s for C2, against 679 M/s as 512 waves of
+// 64 and 646 M/s as 2,048 waves of 16).  Results do not depend on the width.
+uint32_t launch_rpw(const dk_ctx* ctx, uint32_t n) {
+    if (ctx->rpw_fixed) return ctx->roots_per_wave;
+    const uint32_t simds = 4u * (uint32_t)ctx->cu_count;
+    uint32_t r = (n + simds - 1) / simds;
+    r = (r + 15u) & ~15u;
+    return r < 16u ? 16u : (r > ctx->roots_per_wave ? ctx->roots_per_wave : r);
+}
+
 template <class E, bool LN>
 hipError_t launch_search_t(dk_ctx* ctx, const dk_state* roots, const uint64_t* seeds, uint32_t n, uint32_t iters,
                            double c, uint32_t* visits, double* values, uint8_t* best, hipStream_t st,
-                           size_t lds_bytes) {
-    const uint32_t rpw = ctx->roots_per_wave;
+                           size_t lds_bytes, uint32_t rpw) {
     const auto kern = search_kernel<E, LN>;
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, WAVE, lds_bytes) != hipSuccess || per_cu < 1)
@@ -504,9 +518,10 @@ template <class E>
 hipError_t launch_search(dk_ctx* ctx, const dk_state* roots, const uint64_t* seeds, uint32_t n, uint32_t iters,
                          double c, uint32_t* visits, double* values, uint8_t* best, hipStream_t st) {
     const bool ln = iters + 1 <= LN_LDS_MAX && ctx->ln_in_lds;
-    const size_t lds_bytes = (ln ? (size_t)((iters + 2) & ~1u) * 8 : 0) + (size_t)ctx->lds_path * ctx->roots_per_wave * 12;
-    return ln ? launch_search_t<E, true>(ctx, roots, seeds, n, iters, c, visits, values, best, st, lds_bytes)
-              : launch_search_t<E, false>(ctx, roots, seeds, n, iters, c, visits, values, best, st, lds_bytes);
+    const uint32_t rpw = launch_rpw(ctx, n);
+    const size_t lds_bytes = (ln ? (size_t)((iters + 2) & ~1u) * 8 : 0) + (size_t)ctx->lds_path * rpw * 12;
+    return ln ? launch_search_t<E, true>(ctx, roots, seeds, n, iters, c, visits, values, best, st, lds_bytes, rpw)
+              : launch_search_t<E, false>(ctx, roots, seeds, n, iters, c, visits, values, best, st, lds_bytes, rpw);
 }
 
 }  // namespace
@@ -549,7 +564,7 @@ dk_ctx* dk_create(const dk_config* cfg) {
     ctx->cu_count = prop.multiProcessorCount;
     if (const char* e = getenv("DK_ROOTS_PER_WAVE")) {
         const int v = atoi(e);
-        if (v >= 1 && v <= WAVE) ctx->roots_per_wave = (uint32_t)v;
+        if (v >= 1 && v <= WAVE) { ctx->roots_per_wave = (uint32_t)v; ctx->rpw_fixed = true; }
     }
     if (const char* e = getenv("DK_LN_LDS")) ctx->ln_in_lds = atoi(e) != 0;
     if (const char* e = getenv("DK_LDS_PATH")) {

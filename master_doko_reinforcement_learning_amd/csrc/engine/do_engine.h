@@ -129,7 +129,9 @@ DK_HD void score(const Work& w, int pts[4]) {
     for (int p = 0; p < 4; ++p) pts[p] = ((w.re_players >> p) & 1) ? rp : kp;
 }
 
-DK_HD int rollout(Work w, Rng& rng, int pts[4]) {
+// Generic stepwise rollout (random_action_for_current_player until finished,
+// state.rs:315-334); kept as the host-side cross-check of rollout_cards.
+DK_HD int rollout_stepwise(Work w, Rng& rng, int pts[4]) {
     int plies = 0;
     while (w.phase != PH_FINISHED) {
         const uint64_t a = legal_actions(w);
@@ -138,6 +140,97 @@ DK_HD int rollout(Work w, Rng& rng, int pts[4]) {
     }
     score(w, pts);
     return plies;
+}
+
+// Card phase to the end (w.phase == PH_PLAYCARD), the rs-doko counterpart of
+// fdo::rollout_cards: hands as "kinds held" / "kinds held twice" 24-bit masks
+// (which copy a removal takes is invisible to the rewards), per-player values
+// selected without register-array indexing, and the trick evaluated
+// incrementally as its cards are played (first strict maximum, eyes).  One
+// range draw per card, as random_single draws one even for a single option.
+DK_HD int rollout_cards(const Work& w0, Rng& rng, int pts[4]) {
+    uint32_t any0, any1, any2, any3, two0, two1, two2, two3;
+    {
+        const uint32_t M = 0xFFFFFFu;
+        const uint64_t h0 = w0.h[0], h1 = w0.h[1], h2 = w0.h[2], h3 = w0.h[3];
+        any0 = ((uint32_t)h0 | (uint32_t)(h0 >> 24)) & M; two0 = ((uint32_t)h0 & (uint32_t)(h0 >> 24)) & M;
+        any1 = ((uint32_t)h1 | (uint32_t)(h1 >> 24)) & M; two1 = ((uint32_t)h1 & (uint32_t)(h1 >> 24)) & M;
+        any2 = ((uint32_t)h2 | (uint32_t)(h2 >> 24)) & M; two2 = ((uint32_t)h2 & (uint32_t)(h2 >> 24)) & M;
+        any3 = ((uint32_t)h3 | (uint32_t)(h3 >> 24)) & M; two3 = ((uint32_t)h3 & (uint32_t)(h3 >> 24)) & M;
+    }
+    const uint32_t tm = fdo::trump_mask(fdo::GT_NORMAL);
+    uint32_t team_kind = w0.team_kind, re_players = w0.re_players;
+    const uint32_t wedding_player = w0.wedding_player;
+    uint32_t cur = w0.cur, trick_start = w0.trick_start, trick_len = w0.trick_len, t_idx = w0.trick_index;
+    uint32_t eyes = w0.eyes, ntr = w0.ntricks;
+    uint32_t lead = 0xFFFFFFu, best_pos = 0, t_eyes = 0;
+    int best_key = -2;
+    for (uint32_t i = 0; i < trick_len; ++i) {
+        const uint32_t c = (w0.trick_cards >> (8u * i)) & 0xFFu;
+        if (i == 0) lead = fdo::class_mask(c, tm);
+        const int k = fdo::key_fast(c, tm, lead);
+        if (k > best_key) { best_key = k; best_pos = i; }
+        t_eyes += fdo::eyes_fast(c);
+    }
+    int plies = 0;
+    for (;;) {
+        const uint32_t a = fdo::sel4u(any0, any1, any2, any3, cur);
+        const uint32_t t2 = fdo::sel4u(two0, two1, two2, two3, cur);
+        const uint32_t f = a & (trick_len == 0u ? 0xFFFFFFu : lead);
+        const uint32_t legal = f ? f : a;
+        const uint32_t r = rng.range_u32((uint32_t)popc32(legal));
+        uint32_t k = (uint32_t)popc32(legal) - 1u - r, pos = 0;   // rank r from the MSB
+#pragma unroll
+        for (int wdt = 16; wdt >= 1; wdt >>= 1) {
+            const uint32_t cnt = (uint32_t)popc32((legal >> pos) & ((1u << wdt) - 1u));
+            const bool hi = k >= cnt;
+            k = hi ? k - cnt : k;
+            pos = hi ? pos + (uint32_t)wdt : pos;
+        }
+        const uint32_t card = pos, bit = 1u << card;
+        const bool dup = (t2 & bit) != 0u;
+        const uint32_t na = dup ? a : (a ^ bit), nt = dup ? (t2 ^ bit) : t2;
+        any0 = cur == 0u ? na : any0; any1 = cur == 1u ? na : any1; any2 = cur == 2u ? na : any2; any3 = cur == 3u ? na : any3;
+        two0 = cur == 0u ? nt : two0; two1 = cur == 1u ? nt : two1; two2 = cur == 2u ? nt : two2; two3 = cur == 3u ? nt : two3;
+        const fdo::CardInfo ci = fdo::card_info(fdo::GT_NORMAL, card);
+        const bool first = trick_len == 0u;
+        lead = first ? (ci.x & 0xFFFFFFu) : lead;
+        const int key = (((ci.x >> 28) & 1u) || ((lead >> card) & 1u)) ? (int)ci.y : -1;
+        const bool better = first || key > best_key;
+        best_key = better ? key : best_key;
+        best_pos = better ? trick_len : best_pos;
+        t_eyes = (first ? 0u : t_eyes) + ((ci.x >> 24) & 15u);
+        trick_len += 1u;
+        cur = (cur + 1u) & 3u;
+        plies += 1;
+        if (trick_len == 4u) {
+            const uint32_t winner = (trick_start + best_pos) & 3u;
+            eyes += t_eyes << (8u * winner);
+            ntr += 1u << (8u * winner);
+            if (team_kind == fdo::TK_WED_UNSOLVED && t_idx < 3u && (winner != wedding_player || t_idx == 2u)) {
+                team_kind = fdo::TK_WED_SOLVED;
+                re_players = (1u << wedding_player) | (winner != wedding_player ? 1u << winner : 0u);
+            }
+            t_idx += 1u;
+            if (t_idx == 12u) break;
+            cur = winner; trick_start = winner; trick_len = 0;
+        }
+    }
+    Work fin = w0;
+    fin.eyes = eyes; fin.ntricks = ntr; fin.re_players = (uint8_t)re_players;
+    score(fin, pts);
+    return plies;
+}
+
+DK_HD int rollout(Work w, Rng& rng, int pts[4]) {
+    int plies = 0;
+    while (w.phase == PH_RESERVATION) {
+        const uint64_t a = legal_actions(w);
+        play_action(w, ctz64(random_single(a, rng)));
+        plies++;
+    }
+    if (w.phase == PH_FINISHED) { score(w, pts); return plies; }
+    return plies + rollout_cards(w, rng, pts);
 }
 
 DK_HD void unpack(const dk_do_state& s, Work& w) {

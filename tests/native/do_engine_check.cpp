@@ -1,0 +1,72 @@
+// TEST INFRASTRUCTURE: host build of the rs-doko engine (do_engine.h) checked
+// against the ORACLE on random rs-doko trajectories (weddings included): at every
+// position the packed state, the legal mask, and a random rollout from it
+// (rewards and the RNG stream position) of the fast card-phase rollout
+// (rollout_cards) and of the stepwise rollout equal the oracle's
+// McDokoEnvState::random_rollout.
+// Usage: do_engine_check <games> <seed>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+
+#include "../../master_doko_reinforcement_learning_amd/csrc/engine/do_engine.h"
+#include "../../oracle/doko.hpp"
+
+using namespace oracle;
+extern "C" void or_do_pack(void* sp, uint8_t* out);
+
+int main(int argc, char** argv) {
+    const int games = argc > 1 ? atoi(argv[1]) : 100;
+    const uint64_t seed = argc > 2 ? strtoull(argv[2], 0, 10) : 1;
+    std::mt19937_64 pol(seed);
+    long n = 0;
+    for (int g = 0; g < games; ++g) {
+        SmallRng deal = SmallRng::seed_from_u64(seed * 9001 + g);
+        dko::State s = dko::new_game(deal);
+        const bool wedding = g % 3 != 0;
+        for (;;) {
+            dk_do_state pk; or_do_pack(&s, (uint8_t*)&pk);
+            dk::dko::Work w; dk::dko::unpack(pk, w);
+            if (dk::dko::legal_actions(w) != dko::observation_allowed(s)) { printf("MISMATCH legal game %d\n", g); return 1; }
+            for (int rep = 0; rep < 3; ++rep) {
+                const uint64_t sd = pol();
+                SmallRng r = SmallRng::seed_from_u64(sd);
+                dko::Env e; e.doko = s;
+                double want[4]; e.random_rollout(r, want);
+                dk::Rng d1 = dk::Rng::seed_from_u64(sd), d2 = dk::Rng::seed_from_u64(sd);
+                int p1[4], p2[4];
+                dk::dko::rollout(w, d1, p1);
+                dk::dko::rollout_stepwise(w, d2, p2);
+                for (int p = 0; p < 4; ++p)
+                    if ((double)p1[p] != want[p] || (double)p2[p] != want[p]) {
+                        printf("MISMATCH rewards game %d card %d p %d: %d %d vs %g\n", g, pk.card_index, p, p1[p], p2[p], want[p]);
+                        return 1;
+                    }
+                if (d1.s0 != r.s[0] || d1.s1 != r.s[1] || d1.s2 != r.s[2] || d1.s3 != r.s[3] ||
+                    d2.s0 != r.s[0] || d2.s1 != r.s[1] || d2.s2 != r.s[2] || d2.s3 != r.s[3]) {
+                    printf("MISMATCH rng game %d card %d\n", g, pk.card_index); return 1;
+                }
+                n++;
+            }
+            if (s.phase == dko::Finished) break;
+            const uint64_t legal = dko::observation_allowed(s);
+            int a;
+            if (s.phase == dko::Reservation) {
+                a = dko::A_Healthy;
+                if (wedding && (legal >> dko::A_Wedding & 1)) a = dko::A_Wedding;
+            } else {
+                int k = (int)(pol() % (uint64_t)__builtin_popcountll(legal));
+                a = 0;
+                for (int b = 0; b < 24; ++b) if (legal >> b & 1) { if (k-- == 0) { a = b; break; } }
+            }
+            // stepping on the wire format equals the oracle's transition
+            dk_do_state nx = pk; dk::dko::step_packed(nx, a);
+            dko::play_action(s, a);
+            dk_do_state want_pk; or_do_pack(&s, (uint8_t*)&want_pk);
+            if (memcmp(&nx, &want_pk, sizeof(nx)) != 0) { printf("MISMATCH step game %d action %d\n", g, a); return 1; }
+        }
+    }
+    printf("OK %ld rollouts\n", n);
+    return 0;
+}

@@ -37,6 +37,12 @@ def test_engine_rules_vs_oracle(native_bins):
     assert _run("fdo_engine_check", 300, 11) > 20000
 
 
+def test_do_engine_vs_oracle(native_bins):
+    """do_engine.h (host build) = oracle rs-doko: legal masks, wire-format steps, and
+    rollouts (fast card phase and stepwise; rewards + RNG stream position), weddings included."""
+    assert _run("do_engine_check", 200, 7) > 30000
+
+
 def test_engine_search_vs_oracle(native_bins):
     """search_core.h (host build) = oracle UCT: visits, f64 values bitwise, best, RNG stream."""
     assert _run("search_check", 6, 400, 5) > 10
