@@ -237,6 +237,43 @@ int dk_decide_batch(dk_ctx* ctx, const dk_state* infostates, uint32_t n_info, ui
                     const uint64_t* seeds, uint32_t iterations, double c, int fuse_mode, uint8_t* actions,
                     uint32_t* visits);
 
+/* ---- AlphaZero PUCT search: mcts_search (rs-doko-alpha-zero/src/alpha_zero/mcts/async_mcts.rs:224-406)
+ * over FdoAzEnvState (rs-doko-alpha-zero/src/env/envs/full_doko/full_doko.rs:15-172), batched over
+ * n_games independent games.  The reference awaits its batch processor (the network) once for the
+ * root and once per iteration; here the caller runs the network between the launches, on the
+ * same stream, over the packed leaf states the search writes:
+ *
+ *   dk_az_begin_async   roots -> d_eval[g] = root state                  (new_root_node, node.rs:209-244)
+ *   network(d_eval)     -> value[n][4] (POV of each state's current player), logits[n][39]
+ *   dk_az_root_async    priors = softmax(logits) mixed with the Dirichlet noise d_noise[n][39]
+ *                       (1 - eps, eps), restricted to the root's allowed actions and renormalised;
+ *                       announcements are offered at the root iff epoch >= 10
+ *                                                                        (expand_root_node, async_mcts.rs:71-196)
+ *   repeat `iterations` times:
+ *     dk_az_select_async  PUCT descent, leaf expansion; d_eval[g] = leaf state,
+ *                         d_need_eval[g] = 0 for a terminal leaf (its network row is ignored)
+ *                                                                        (mcts.rs:23-74, 306-420)
+ *     network(d_eval)
+ *     dk_az_backup_async  leaf priors = softmax over its allowed actions' logits; backpropagate
+ *                         the value (or the terminal rewards player_points/8)  (async_mcts.rs:280-345, mcts.rs:250-280)
+ *   dk_az_finish_async  random_bool(1/5000), then select_action: temperature_mode 0 = None
+ *                       (greedy, last maximum), 1 = infinite (uniform), 2 = finite `temperature`
+ *                       (visits^(1/T) WeightedIndex); d_visits[n][39] = root child visits
+ *                                                                        (async_mcts.rs:347-405, mcts.rs:185-248)
+ * seeds[g] seeds game g's SmallRng (used by the final draws).  The Dirichlet noise is an input:
+ * the reference samples it from the search's SmallRng (rand_distr 0.5.1), which is not restated.
+ * One AZ search batch per context at a time; node/state pools grow on demand (48 B per node,
+ * 1 + 12 (iterations + 1) + 39 nodes and iterations + 2 packed states per game).
+ */
+int dk_az_begin_async(dk_ctx* ctx, const dk_state* d_roots, const uint64_t* d_seeds, uint32_t n_games,
+                      uint32_t iterations, int epoch, dk_state* d_eval, void* stream);
+int dk_az_root_async(dk_ctx* ctx, const float* d_value, const float* d_logits, const float* d_noise,
+                     float dirichlet_epsilon, void* stream);
+int dk_az_select_async(dk_ctx* ctx, float c, dk_state* d_eval, uint8_t* d_need_eval, void* stream);
+int dk_az_backup_async(dk_ctx* ctx, const float* d_value, const float* d_logits, void* stream);
+int dk_az_finish_async(dk_ctx* ctx, int temperature_mode, float temperature, uint32_t* d_visits, uint8_t* d_action,
+                       void* stream);
+
 /* ---- completion / errors / timing of *_async work -------------------------------
  * dk_sync: waits for the stream and returns the first device-side error
  * (DK_E_CAPACITY when a search ran out of child slots) since the last dk_sync.

@@ -5,12 +5,12 @@ rs-full-doko / rs-doko rules, CAP and rule-based determinization, policy fusion)
 for gfx950 behind the C-ABI of include/doko_amd.h.  See DESIGN.md.
 """
 from . import _native
-from .api import (FUSE_AVG, FUSE_MAXN, GAME_DOKO, GAME_FULL_DOKO, GAME_TTT, NUM_ACTIONS, CachedMCTS,
+from .api import (FUSE_AVG, AlphaZeroSearch, FUSE_MAXN, GAME_DOKO, GAME_FULL_DOKO, GAME_TTT, NUM_ACTIONS, CachedMCTS,
                   DefaultImpiPolicy, DokoError, Engine, McEnv, PolicyFusionAverageStrategy, PolicyFusionMaxN,
                   card_matching_full, sample_assignment_full, splitmix_rng_states)
 
 __all__ = ["Engine", "McEnv", "CachedMCTS", "card_matching_full", "sample_assignment_full", "PolicyFusionMaxN", "PolicyFusionAverageStrategy",
-           "DefaultImpiPolicy", "DokoError", "splitmix_rng_states", "GAME_FULL_DOKO", "GAME_DOKO", "GAME_TTT",
+           "DefaultImpiPolicy", "AlphaZeroSearch", "DokoError", "splitmix_rng_states", "GAME_FULL_DOKO", "GAME_DOKO", "GAME_TTT",
            "FUSE_MAXN", "FUSE_AVG", "NUM_ACTIONS", "build"]
 
 

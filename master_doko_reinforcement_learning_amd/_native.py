@@ -82,6 +82,11 @@ def lib():
         "dk_env_step_batch_async": (ctypes.c_int, [vp, vp, vp, u32, vp]),
         "dk_env_random_plies_batch_async": (ctypes.c_int, [vp, vp, vp, vp, u32, vp]),
         "dk_decide_batch": (ctypes.c_int, [vp, vp, u32, u32, vp, u32, ctypes.c_double, ctypes.c_int, vp, vp]),
+        "dk_az_begin_async": (ctypes.c_int, [vp, vp, vp, u32, u32, ctypes.c_int, vp, vp]),
+        "dk_az_root_async": (ctypes.c_int, [vp, vp, vp, vp, ctypes.c_float, vp]),
+        "dk_az_select_async": (ctypes.c_int, [vp, ctypes.c_float, vp, vp, vp]),
+        "dk_az_backup_async": (ctypes.c_int, [vp, vp, vp, vp]),
+        "dk_az_finish_async": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_float, vp, vp, vp]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(L, name)
@@ -99,4 +104,5 @@ EXPORTED = [
     "dk_search_batch_async", "dk_determinize_batch", "dk_determinize_batch_async", "dk_fuse",
     "dk_fuse_accumulate_async", "dk_fuse_select_async", "dk_decide_batch", "dk_sync", "dk_last_search_ms",
     "dk_pool_bytes", "dk_legal_actions_async", "dk_env_step_batch_async", "dk_env_random_plies_batch_async",
+    "dk_az_begin_async", "dk_az_root_async", "dk_az_select_async", "dk_az_backup_async", "dk_az_finish_async",
 ]

@@ -9,6 +9,8 @@ Names follow the Rust types they replace:
 * ``sample_assignment_full``      — rs-doko rule-based determinization (rs-doko-assignment/src/assignment.rs:472-580)
 * ``PolicyFusionMaxN`` / ``PolicyFusionAverageStrategy`` — policy_fusion.rs:18-123
 * ``DefaultImpiPolicy``           — sample -> search -> fuse (compare_impi.rs:212-371)
+* ``AlphaZeroSearch``             — AlphaZero PUCT mcts_search (rs-doko-alpha-zero/src/alpha_zero/mcts/async_mcts.rs:224-406),
+                                    batched over games, network evaluated between launches
 
 States are ``numpy.uint8`` arrays of shape (n, 128) in the dk_state wire format
 of include/doko_amd.h.  Every call runs on the GPU; errors raise DokoError
@@ -234,3 +236,69 @@ class DefaultImpiPolicy:
                                              self.iterations, self.c, self.fusion, _ptr(actions),
                                              _ptr(visits) if return_visits else None))
         return (actions, visits) if return_visits else actions
+
+
+class AlphaZeroSearch:
+    """`mcts_search` of rs-doko-alpha-zero (async_mcts.rs:224-406) over FdoAzEnvState,
+    batched over games: every iteration runs one PUCT selection per game on the GPU,
+    then `network` on all leaves at once (the reference's batch processor), then the
+    backup.  Everything stays on the device (torch tensors on the current stream).
+
+    network(states) -> (value, logits): states = uint8 [n, 128] packed dk_state on the
+    GPU; value = float32 [n, 4] from each state's current player's point of view;
+    logits = float32 [n, 39].
+    temperature: None (greedy), float('inf') (uniform) or a finite T (select_action,
+    mcts.rs:185-248)."""
+
+    def __init__(self, engine, puct_exploration_constant=1.0, dirichlet_epsilon=0.25, epoch=10, temperature=None):
+        self.engine = engine
+        self.c = float(puct_exploration_constant)
+        self.eps = float(dirichlet_epsilon)
+        self.epoch = int(epoch)
+        self.temperature = temperature
+
+    def mcts_search(self, roots, network, noise, iterations, seeds):
+        """roots: uint8 [n, 128] (GPU); noise: float32 [n, 39] Dirichlet samples (GPU);
+        seeds: uint64 [n] (SmallRng per game).  Returns (actions uint8 [n], visits int32 [n, 39])."""
+        import torch
+        dev = roots.device
+        # the launches need a real stream handle shared with torch (handle 0 would
+        # select the library's own stream, unordered with the network's kernels)
+        caller = torch.cuda.current_stream(dev)
+        if caller.cuda_stream != 0:
+            return self._search(roots, network, noise, iterations, seeds, caller.cuda_stream)
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(caller)
+        with torch.cuda.stream(side):
+            out = self._search(roots, network, noise, iterations, seeds, side.cuda_stream)
+        caller.wait_stream(side)
+        return out
+
+    def _search(self, roots, network, noise, iterations, seeds, st):
+        import torch
+        L = _native.lib()
+        ctx = self.engine.ctx
+        n = roots.shape[0]
+        dev = roots.device
+        seeds_t = torch.as_tensor(np.ascontiguousarray(seeds, dtype=np.uint64).view(np.int64), device=dev)
+        roots = roots.contiguous()
+        noise = noise.contiguous().float()
+        ev = torch.empty((n, STATE_BYTES), dtype=torch.uint8, device=dev)
+        need = torch.empty(n, dtype=torch.uint8, device=dev)
+        _check(L.dk_az_begin_async(ctx, roots.data_ptr(), seeds_t.data_ptr(), n, iterations, self.epoch,
+                                   ev.data_ptr(), st))
+        value, logits = network(ev)
+        value, logits = value.float().contiguous(), logits.float().contiguous()
+        _check(L.dk_az_root_async(ctx, value.data_ptr(), logits.data_ptr(), noise.data_ptr(), self.eps, st))
+        for _ in range(iterations):
+            _check(L.dk_az_select_async(ctx, self.c, ev.data_ptr(), need.data_ptr(), st))
+            value, logits = network(ev)
+            value, logits = value.float().contiguous(), logits.float().contiguous()
+            _check(L.dk_az_backup_async(ctx, value.data_ptr(), logits.data_ptr(), st))
+        visits = torch.empty((n, NUM_ACTIONS), dtype=torch.int32, device=dev)
+        actions = torch.empty(n, dtype=torch.uint8, device=dev)
+        t = self.temperature
+        mode, temp = (0, 1.0) if t is None else ((1, 1.0) if np.isinf(t) else (2, float(t)))
+        _check(L.dk_az_finish_async(ctx, mode, temp, visits.data_ptr(), actions.data_ptr(), st))
+        _check(L.dk_sync(ctx, st))
+        return actions, visits

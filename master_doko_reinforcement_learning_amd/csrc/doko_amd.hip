@@ -18,6 +18,7 @@
 #include "../../include/doko_amd.h"
 #include "engine/adapters.h"
 #include "engine/assign_engine.h"
+#include "engine/az_core.h"
 #include "engine/cap_engine.h"
 #include "engine/search_core.h"
 
@@ -357,6 +358,81 @@ __global__ void __launch_bounds__(WAVE) determinize_kernel(const dk_state* info,
     out[i] = o;
 }
 
+// ---------------------------------------------------------------- AlphaZero PUCT (az_core.h)
+// One lane per game; game g owns nodes [g*cap_nodes, (g+1)*cap_nodes) and states
+// [g*cap_states, ...).  The network runs between the launches on the same stream.
+__device__ inline dk::az::Mem az_mem(dk::az::Node* nodes, dk_state* states, uint32_t g, uint32_t cap_nodes,
+                                     uint32_t cap_states) {
+    dk::az::Mem m;
+    m.nodes = nodes + (size_t)g * cap_nodes;
+    m.states = states + (size_t)g * cap_states;
+    m.cap_nodes = cap_nodes; m.cap_states = cap_states;
+    return m;
+}
+
+__global__ void az_init_kernel(const dk_state* roots, const uint64_t* seeds, uint32_t n, dk::az::Node* nodes,
+                               dk_state* states, dk::az::Game* games, uint32_t cap_nodes, uint32_t cap_states,
+                               dk_state* eval, int* err) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n) return;
+    const dk_state r = roots[g];
+    if (r.raw[127] != DK_GAME_FULL_DOKO) { atomicOr(err, 2); return; }
+    dk::az::Mem m = az_mem(nodes, states, g, cap_nodes, cap_states);
+    dk::az::Game gm;
+    dk::az::init(r, gm, m, seeds[g]);
+    games[g] = gm;
+    eval[g] = r;
+}
+
+__global__ void az_root_kernel(const float* value, const float* logits, const float* noise, float eps, int epoch,
+                               uint32_t n, dk::az::Node* nodes, dk_state* states, dk::az::Game* games,
+                               uint32_t cap_nodes, uint32_t cap_states, int* err) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n) return;
+    dk::az::Mem m = az_mem(nodes, states, g, cap_nodes, cap_states);
+    dk::az::Game gm = games[g];
+    dk::az::root_expand(gm, m, value + 4 * (size_t)g, logits + 39 * (size_t)g, noise + 39 * (size_t)g, eps, epoch);
+    if (gm.status) atomicOr(err, 1);
+    games[g] = gm;
+}
+
+__global__ void az_select_kernel(float c, int epoch, uint32_t n, dk::az::Node* nodes, dk_state* states,
+                                 dk::az::Game* games, uint32_t cap_nodes, uint32_t cap_states, dk_state* eval,
+                                 uint8_t* need_eval, int* err) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n) return;
+    dk::az::Mem m = az_mem(nodes, states, g, cap_nodes, cap_states);
+    dk::az::Game gm = games[g];
+    if (gm.status == 0) dk::az::select(gm, m, c, epoch, eval + g);
+    if (gm.status) atomicOr(err, 1);
+    if (need_eval) need_eval[g] = (uint8_t)gm.need_eval;
+    games[g] = gm;
+}
+
+__global__ void az_backup_kernel(const float* value, const float* logits, uint32_t n, dk::az::Node* nodes,
+                                 dk_state* states, dk::az::Game* games, uint32_t cap_nodes, uint32_t cap_states) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n) return;
+    dk::az::Mem m = az_mem(nodes, states, g, cap_nodes, cap_states);
+    dk::az::Game gm = games[g];
+    dk::az::backup(gm, m, value + 4 * (size_t)g, logits + 39 * (size_t)g);
+    games[g] = gm;
+}
+
+__global__ void az_finish_kernel(int temp_mode, float temperature, uint32_t n, dk::az::Node* nodes, dk_state* states,
+                                 dk::az::Game* games, uint32_t cap_nodes, uint32_t cap_states, uint32_t* visits,
+                                 uint8_t* action) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n) return;
+    dk::az::Mem m = az_mem(nodes, states, g, cap_nodes, cap_states);
+    dk::az::Game gm = games[g];
+    uint32_t v[39];
+    const int a = dk::az::finish(gm, m, temp_mode, temperature, v);
+    for (int k = 0; k < 39; ++k) visits[39 * (size_t)g + k] = v[k];
+    action[g] = a < 0 ? (uint8_t)DK_NONE : (uint8_t)a;
+    games[g] = gm;
+}
+
 // PolicyFusionMaxN / PolicyFusionAverageStrategy accumulators (policy_fusion.rs:23-123).
 // One thread per (infostate, action).
 __global__ void fuse_accumulate_kernel(const uint32_t* visits, uint32_t n_info, uint32_t samples,
@@ -442,6 +518,14 @@ struct dk_ctx {
                                     // spill to global).  16 keeps a workgroup at 12 KB of LDS so that
                                     // 8 single-wave workgroups (2 per SIMD) fit a CU's 160 KB.
     uint64_t* prof = nullptr;       // phase timers (DK_PHASE_PROF builds only)
+    // AlphaZero PUCT search (dk_az_*): per-game node / state regions, allocated on first use
+    dk::az::Node* az_nodes = nullptr;
+    dk_state* az_states = nullptr;
+    dk::az::Game* az_games = nullptr;
+    size_t az_bytes = 0;
+    uint32_t az_n = 0, az_iters = 0, az_cap_nodes = 0, az_cap_states = 0, az_done = 0;
+    int az_epoch = 0;
+    bool az_root_done = false;
     std::vector<void*> scratch;
     std::vector<size_t> scratch_size;
     std::mutex mu;
@@ -622,6 +706,9 @@ void dk_destroy(dk_ctx* ctx) {
     if (ctx->err) (void)hipFree(ctx->err);
     if (ctx->queue) (void)hipFree(ctx->queue);
     if (ctx->prof) (void)hipFree(ctx->prof);
+    if (ctx->az_nodes) (void)hipFree(ctx->az_nodes);
+    if (ctx->az_states) (void)hipFree(ctx->az_states);
+    if (ctx->az_games) (void)hipFree(ctx->az_games);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -945,6 +1032,77 @@ int dk_decide_batch(dk_ctx* ctx, const dk_state* infostates, uint32_t n_info, ui
     DK_HIP(hipMemcpyAsync(actions, d_b + n, n_info, hipMemcpyDeviceToHost, ctx->stream));
     if (visits) DK_HIP(hipMemcpyAsync(visits, d_v, n * 39 * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
     return finish(ctx, ctx->stream);
+}
+
+// ---------------------------------------------------------------- AlphaZero PUCT search
+int dk_az_begin_async(dk_ctx* ctx, const dk_state* d_roots, const uint64_t* d_seeds, uint32_t n_games,
+                      uint32_t iterations, int epoch, dk_state* d_eval, void* stream) {
+    if (!ctx || !d_roots || !d_seeds || !d_eval || n_games == 0) return DK_E_INVALID;
+    if (iterations >= dk::NI_MAX_STATES) return ctx->last_error = DK_E_CAPACITY;
+    const uint32_t cap_nodes = 1u + 12u * (iterations + 1u) + 39u, cap_states = iterations + 2u;
+    const size_t need = (size_t)n_games * ((size_t)cap_nodes * sizeof(dk::az::Node) + (size_t)cap_states * sizeof(dk_state) +
+                                           sizeof(dk::az::Game));
+    if (need > ctx->az_bytes) {
+        hipStream_t st = pick(ctx, stream);
+        (void)hipStreamSynchronize(st);
+        if (ctx->az_nodes) (void)hipFree(ctx->az_nodes);
+        if (ctx->az_states) (void)hipFree(ctx->az_states);
+        if (ctx->az_games) (void)hipFree(ctx->az_games);
+        ctx->az_nodes = nullptr; ctx->az_states = nullptr; ctx->az_games = nullptr; ctx->az_bytes = 0;
+        bool ok = hipMalloc(&ctx->az_nodes, (size_t)n_games * cap_nodes * sizeof(dk::az::Node)) == hipSuccess;
+        ok = ok && hipMalloc(&ctx->az_states, (size_t)n_games * cap_states * sizeof(dk_state)) == hipSuccess;
+        ok = ok && hipMalloc(&ctx->az_games, (size_t)n_games * sizeof(dk::az::Game)) == hipSuccess;
+        if (!ok) return ctx->last_error = DK_E_CAPACITY;
+        ctx->az_bytes = need;
+    }
+    ctx->az_n = n_games; ctx->az_iters = iterations; ctx->az_epoch = epoch; ctx->az_done = 0; ctx->az_root_done = false;
+    ctx->az_cap_nodes = cap_nodes; ctx->az_cap_states = cap_states;
+    hipLaunchKernelGGL(az_init_kernel, dim3(grid_for(n_games, 64)), dim3(64), 0, pick(ctx, stream), d_roots, d_seeds,
+                       n_games, ctx->az_nodes, ctx->az_states, ctx->az_games, cap_nodes, cap_states, d_eval, ctx->err);
+    DK_HIP(hipGetLastError());
+    return DK_OK;
+}
+
+int dk_az_root_async(dk_ctx* ctx, const float* d_value, const float* d_logits, const float* d_noise,
+                     float dirichlet_epsilon, void* stream) {
+    if (!ctx || !ctx->az_n || !d_value || !d_logits || !d_noise) return DK_E_INVALID;
+    hipLaunchKernelGGL(az_root_kernel, dim3(grid_for(ctx->az_n, 64)), dim3(64), 0, pick(ctx, stream), d_value, d_logits,
+                       d_noise, dirichlet_epsilon, ctx->az_epoch, ctx->az_n, ctx->az_nodes, ctx->az_states,
+                       ctx->az_games, ctx->az_cap_nodes, ctx->az_cap_states, ctx->err);
+    DK_HIP(hipGetLastError());
+    ctx->az_root_done = true;
+    return DK_OK;
+}
+
+int dk_az_select_async(dk_ctx* ctx, float c, dk_state* d_eval, uint8_t* d_need_eval, void* stream) {
+    if (!ctx || !ctx->az_n || !ctx->az_root_done || !d_eval) return DK_E_INVALID;
+    if (ctx->az_done >= ctx->az_iters) return DK_E_INVALID;
+    hipLaunchKernelGGL(az_select_kernel, dim3(grid_for(ctx->az_n, 64)), dim3(64), 0, pick(ctx, stream), c,
+                       ctx->az_epoch, ctx->az_n, ctx->az_nodes, ctx->az_states, ctx->az_games, ctx->az_cap_nodes,
+                       ctx->az_cap_states, d_eval, d_need_eval, ctx->err);
+    DK_HIP(hipGetLastError());
+    return DK_OK;
+}
+
+int dk_az_backup_async(dk_ctx* ctx, const float* d_value, const float* d_logits, void* stream) {
+    if (!ctx || !ctx->az_n || !d_value || !d_logits) return DK_E_INVALID;
+    hipLaunchKernelGGL(az_backup_kernel, dim3(grid_for(ctx->az_n, 64)), dim3(64), 0, pick(ctx, stream), d_value,
+                       d_logits, ctx->az_n, ctx->az_nodes, ctx->az_states, ctx->az_games, ctx->az_cap_nodes,
+                       ctx->az_cap_states);
+    DK_HIP(hipGetLastError());
+    ctx->az_done += 1;
+    return DK_OK;
+}
+
+int dk_az_finish_async(dk_ctx* ctx, int temperature_mode, float temperature, uint32_t* d_visits, uint8_t* d_action,
+                       void* stream) {
+    if (!ctx || !ctx->az_n || !d_visits || !d_action || temperature_mode < 0 || temperature_mode > 2) return DK_E_INVALID;
+    if (ctx->az_done != ctx->az_iters) return DK_E_INVALID;
+    hipLaunchKernelGGL(az_finish_kernel, dim3(grid_for(ctx->az_n, 64)), dim3(64), 0, pick(ctx, stream), temperature_mode,
+                       temperature, ctx->az_n, ctx->az_nodes, ctx->az_states, ctx->az_games, ctx->az_cap_nodes,
+                       ctx->az_cap_states, d_visits, d_action);
+    DK_HIP(hipGetLastError());
+    return DK_OK;
 }
 
 }  // extern "C"

@@ -14,6 +14,8 @@
 #include "card_matching.hpp"
 #include "doko.hpp"
 #include "assignment.hpp"
+#include "az_eval.hpp"
+#include "az_mcts.hpp"
 #include "full_doko.hpp"
 #include "fusion.hpp"
 #include "mcts.hpp"
@@ -285,6 +287,25 @@ void* or_do_sample_full(void* sp, uint64_t* rng_state) {
     rng_to(r, rng_state);
     return ok ? new dko::State(out) : nullptr;
 }
+
+// ---------------------------------------------------------------- AlphaZero PUCT (synthetic network)
+void or_az_hash_eval(const uint8_t* packed, float* value, float* logits) { az::hash_eval(packed, value, logits); }
+// temp_mode: 0 None, 1 infinite, 2 finite `temp`.  Returns the chosen action.
+int or_az_search(void* sp, const float* noise, uint32_t iters, float c, float eps, int epoch, int temp_mode, float temp,
+                 uint64_t* rng_state, uint32_t* visits, float* root_priors) {
+    az::Env e; e.doko = *(fdo::State*)sp;
+    az::Options o; o.c = c; o.dirichlet_epsilon = eps; o.epoch = epoch;
+    o.has_temperature = temp_mode != 0; o.temperature = temp_mode == 1 ? INFINITY : temp;
+    auto eval = [](const az::Env& st, float v[4], float l[39]) {
+        uint8_t b[128]; or_fdo_pack((void*)&st.doko, b); az::hash_eval(b, v, l);
+    };
+    SmallRng r = rng_from(rng_state);
+    az::Search s;
+    const int a = s.search(e, eval, noise, iters, o, r, visits, root_priors);
+    rng_to(r, rng_state);
+    return a;
+}
+void or_az_take_action(void* sp, int a) { az::Env e; e.doko = *(fdo::State*)sp; *(fdo::State*)sp = e.take_action(a, true).doko; }
 
 // ---------------------------------------------------------------- tic-tac-toe
 int or_ttt_finish(const int32_t* board) { int b[9]; for (int i = 0; i < 9; ++i) b[i] = board[i]; return ttt::calc_finish_state(b); }

@@ -79,6 +79,10 @@ def lib():
             "or_do_sample_assignment": (ctypes.c_int, [ctypes.c_int, i32p, ctypes.c_uint64, i32p, ctypes.c_int,
                                                        u64p, u64p]),
             "or_do_sample_full": (vp, [vp, u64p]),
+            "or_az_hash_eval": (None, [u8p, f32p, f32p]),
+            "or_az_search": (ctypes.c_int, [vp, f32p, ctypes.c_uint32, ctypes.c_float, ctypes.c_float, ctypes.c_int,
+                                            ctypes.c_int, ctypes.c_float, u64p, u32p, f32p]),
+            "or_az_take_action": (None, [vp, ctypes.c_int]),
             "or_ttt_finish": (ctypes.c_int, [i32p]),
             "or_ttt_rollout": (None, [i32p, u64p, f64p]),
             "or_ttt_search": (ctypes.c_int, [i32p, u64p, ctypes.c_uint32, ctypes.c_double, u32p, f64p]),
@@ -176,6 +180,18 @@ class FdoState:
 
     def card_matching(self, rng):
         return FdoState(lib().or_fdo_card_matching(self.h, rng))
+
+    def az_search(self, noise, iters, c, eps, epoch, temp_mode, temp, rng):
+        """AlphaZero mcts_search (async_mcts.rs:224-406) with the synthetic hash
+        network of oracle/az_eval.hpp -> (action, visits[39], root priors[39])."""
+        v = arr(ctypes.c_uint32, 39)
+        pr = arr(ctypes.c_float, 39, [-1.0] * 39)
+        a = lib().or_az_search(self.h, arr(ctypes.c_float, 39, noise), iters, c, eps, epoch, temp_mode, temp, rng, v, pr)
+        return a, list(v), list(pr)
+
+    def az_take_action(self, a):
+        """FdoAzEnvState::take_action_by_action_index(a, skip_single=true)."""
+        lib().or_az_take_action(self.h, a)
 
     def consistent_sample(self, sample):
         return bool(lib().or_fdo_sample_consistent(self.h, sample.h))
@@ -306,3 +322,23 @@ def fuse_avg(visits_rows):
     flat = arr(ctypes.c_uint32, 39 * S, [x for row in visits_rows for x in row])
     probs = arr(ctypes.c_float, 39)
     return lib().or_fuse_avg(flat, S, probs), list(probs)
+
+
+def az_hash_eval_np(packed):
+    """numpy twin of oracle/az_eval.hpp hash_eval: (n, 128) uint8 -> value (n, 4), logits (n, 39) float32."""
+    import numpy as np
+    b = np.asarray(packed, dtype=np.uint8)
+    h = np.full(b.shape[0], 0xCBF29CE484222325, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        for i in range(117):
+            h ^= b[:, i].astype(np.uint64)
+            h *= np.uint64(0x100000001B3)
+        value = np.stack([((h >> np.uint64(8 * k)) & np.uint64(15)).astype(np.int64) - 8 for k in range(4)], axis=1)
+        logits = []
+        for a in range(39):
+            z = h + np.uint64(a) + np.uint64(0x9E3779B97F4A7C15)
+            z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+            z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+            z = z ^ (z >> np.uint64(31))
+            logits.append((z & np.uint64(31)).astype(np.int64) - 16)
+    return (value.astype(np.float32) * np.float32(0.125)), (np.stack(logits, axis=1).astype(np.float32) * np.float32(0.25))

@@ -67,6 +67,12 @@ def test_engine_assignment_vs_oracle(native_bins):
     assert _run("assign_check", 200, 3) > 40000
 
 
+def test_az_core_vs_oracle(native_bins):
+    """az_core.h (host build, driven batch-wise like the GPU) = oracle AlphaZero
+    mcts_search: root priors, visits, chosen action and RNG position, three temperature modes."""
+    assert _run("az_check", 120, 300, 5) == 360
+
+
 def test_fusion_kats():
     """rs-doko-py-bridge/src/compare_impi/policy_fusion.rs:130-311."""
     with open(os.path.join(GOLD, "fusion_kats.json")) as fh:

@@ -488,3 +488,34 @@ def test_decide_end_to_end_doko(eng):
             assert list(visits[j * S + k]) == v
         exp, _ = ol.fuse_maxn(rows, s.allowed())
         assert int(actions[j]) == exp
+
+
+# ---------------------------------------------------------------- AlphaZero PUCT search
+@pytest.mark.parametrize("temp_mode", [0, 1, 2])
+def test_az_search_parity(eng, temp_mode):
+    """AlphaZero mcts_search (rs-doko-alpha-zero async_mcts.rs:224-406) on the GPU ==
+    the oracle restatement, with the synthetic hash network (oracle/az_eval.hpp) on both
+    sides: root child visits, chosen action (greedy / uniform / T = 1) for every game."""
+    import torch
+    import master_doko_reinforcement_learning_amd as dk
+    pool = [s for s in fdo_states(24, 31) if s.info()["phase"] != 3]
+    info = pool[::max(1, len(pool) // 64)][:64]
+    n, iters, c, eps = len(info), 150, 2.5, 0.25
+    epoch = 3 if temp_mode == 1 else 12
+    rng = np.random.default_rng(temp_mode)
+    noise = (rng.integers(0, 1000, size=(n, 39)) / 4000.0).astype(np.float32)
+    seeds = rng.integers(0, 2**63, size=n, dtype=np.uint64)
+    dev = torch.device("cuda", 0)
+
+    def network(states):
+        v, l = ol.az_hash_eval_np(states.cpu().numpy())
+        return torch.from_numpy(v).to(dev), torch.from_numpy(l).to(dev)
+
+    roots = torch.from_numpy(pack_all(info)).to(dev)
+    az = dk.AlphaZeroSearch(eng, c, eps, epoch, [None, float("inf"), 1.0][temp_mode])
+    actions, visits = az.mcts_search(roots, network, torch.from_numpy(noise).to(dev), iters, seeds)
+    actions, visits = actions.cpu().numpy(), visits.cpu().numpy()
+    for g, s in enumerate(info):
+        a, v, _ = s.az_search(list(noise[g]), iters, c, eps, epoch, temp_mode, 1.0, ol.rng_seed(int(seeds[g])))
+        assert list(visits[g]) == v
+        assert int(actions[g]) == a
