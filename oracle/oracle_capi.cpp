@@ -16,6 +16,7 @@
 #include "assignment.hpp"
 #include "az_eval.hpp"
 #include "az_mcts.hpp"
+#include "encode_pi.hpp"
 #include "full_doko.hpp"
 #include "fusion.hpp"
 #include "mcts.hpp"
@@ -306,6 +307,34 @@ int or_az_search(void* sp, const float* noise, uint32_t iters, float c, float ep
     return a;
 }
 void or_az_take_action(void* sp, int a) { az::Env e; e.doko = *(fdo::State*)sp; *(fdo::State*)sp = e.take_action(a, true).doko; }
+
+// ---------------------------------------------------------------- encode_state_pi
+void or_encode_pi(void* sp, int64_t* out) { enc::encode_state_pi(*(fdo::State*)sp, out); }
+// A state from the fields encode_state_pi reads (the reference test builds its FdoState the same way):
+// f[0] res_start, f[1] res_len, f[2..5] res, f[6] n_tricks, f[7 + 6t ..] = {start, len, c0..c3} for t < 12,
+// f[79] ann_n, f[80 + 3k ..] = {card_index, player, announcement bit} for k < 12,
+// f[116] current_player, f[117] phase, f[118] re_players.
+void or_encode_pi_fields(const int32_t* f, const uint64_t* hands, int64_t* out) {
+    fdo::State s;
+    s.res_start = f[0]; s.res_len = f[1];
+    for (int i = 0; i < 4; ++i) s.res[i] = f[2 + i];
+    s.n_tricks = f[6];
+    for (int t = 0; t < 12; ++t) {
+        const int32_t* q = f + 7 + 6 * t;
+        s.tricks[t].start = q[0]; s.tricks[t].len = q[1];
+        for (int i = 0; i < 4; ++i) s.tricks[t].cards[i] = q[2 + i];
+    }
+    for (int p = 0; p < 4; ++p) s.hands[p].bits = hands[p];
+    s.announcements.n = f[79];
+    for (int k = 0; k < 12; ++k) {
+        s.announcements.list[k].card_index = f[80 + 3 * k];
+        s.announcements.list[k].player = f[81 + 3 * k];
+        s.announcements.list[k].announcement = (uint32_t)f[82 + 3 * k];
+    }
+    s.current_player = f[116]; s.phase = f[117];
+    s.team_state.kind = fdo::NoWedding; s.team_state.re_players = (uint8_t)f[118];
+    enc::encode_state_pi(s, out);
+}
 
 // ---------------------------------------------------------------- tic-tac-toe
 int or_ttt_finish(const int32_t* board) { int b[9]; for (int i = 0; i < 9; ++i) b[i] = board[i]; return ttt::calc_finish_state(b); }

@@ -15,6 +15,7 @@ reference. The output files are data only (inputs + expected outputs):
 * ttt_kats.json — rs-doko-mcts/src/example/tic_tac_toe.rs tests (finish states).
 * fusion_kats.json — rs-doko-py-bridge/src/compare_impi/policy_fusion.rs:130-311.
 * do_assignment_kats.json — rs-doko-assignment/src/assignment.rs:593-1190 (rule-based sampler).
+* encode_pi_kat.json — rs-doko-networks/src/full_doko/var1/encode_pi.rs:237-797 (AlphaZero network input).
 
 Usage: python tests/golden/make_fixtures.py
 """
@@ -344,6 +345,98 @@ def do_assignment_kats():
             "allowed_to_have": allowed, "remaining": remaining, "support": support}
 
 
+def _var2_tables():
+    """Token tables of the encoder helpers, read from their match arms
+    (rs-doko-networks/src/full_doko/var2/encode_reservation_or_card_or_none.rs)."""
+    path = os.path.join(REF, "rs-doko-networks/src/full_doko/var2/encode_reservation_or_card_or_none.rs")
+    with open(path, encoding="utf-8") as fh:
+        text = fh.read()
+    def arms(fn, enum):
+        body = text[text.find("pub fn " + fn):]
+        body = body[:body.find("\npub fn ", 10) if "\npub fn " in body[10:] else len(body)]
+        return {k: int(v) for k, v in re.findall(enum + r"::(\w+) => \[(\d+)\]", body)}, \
+               int(re.search(r"None => \[(\d+)\]", body).group(1)) if re.search(r"None => \[(\d+)\]", body) else None
+    return {"card": arms("encode_reservation_or_card_or_none_card", "FdoCard"),
+            "pi_ann": arms("encode_reservation_or_card_or_pi_announcement", "FdoAnnouncement"),
+            "pi_res": arms("encode_reservation_or_card_or_pi_reservation", "FdoReservation"),
+            "vis_res": arms("encode_reservation_or_card_or_reservation", "FdoVisibleReservation")}
+
+
+FDO_RES = ["Healthy", "Wedding", "DiamondsSolo", "HeartsSolo", "SpadesSolo", "ClubsSolo", "QueensSolo", "JacksSolo",
+           "TrumplessSolo"]
+ANN_BITS = {"ReContra": 1, "No90": 2, "No60": 4, "No30": 8, "Black": 16, "CounterReContra": 32}
+
+
+def encode_pi_kat():
+    """rs-doko-networks/src/full_doko/var1/encode_pi.rs:237-797 (test_encode_state):
+    the state's fields and the expected 311 tokens, the latter evaluated from the
+    test's 311 helper-call assertions with the helpers' own token tables."""
+    path = os.path.join(REF, "rs-doko-networks/src/full_doko/var1/encode_pi.rs")
+    with open(path, encoding="utf-8") as fh:
+        text = fh.read()
+    t = text[text.find("fn test_encode_state"):]
+    card = lambda n: CARD_NAMES.index(n.split("::")[-1].strip())
+    pl = lambda n: PLAYERS[n.split("::")[-1].strip()]
+    m = re.search(r"reservations: PlayerOrientedVec::from_full\(FdoPlayer::(\w+), vec!\[(.*?)\]\)", t, re.S)
+    res_start = PLAYERS[m.group(1)]
+    res = [FDO_RES.index(x.strip().split("::")[-1]) for x in m.group(2).split(",") if x.strip()]
+    tricks = []
+    for sp, cs in re.findall(r"FdoTrick \{\s*cards: PlayerOrientedVec::from_full\(FdoPlayer::(\w+), vec!\[(.*?)\]\)", t, re.S):
+        tricks.append({"start": PLAYERS[sp], "cards": [card(x) for x in cs.split(",") if x.strip()]})
+    hm = re.search(r"hands: PlayerZeroOrientedArr::from_full\(\[(.*?)\]\),\s*announcements", t, re.S).group(1)
+    hands = []
+    for cs in re.findall(r"FdoHand::from_vec\(vec!\[(.*?)\]\)", hm, re.S):
+        h = 0
+        for c in [card(x) for x in cs.split(",") if x.strip()]:
+            h |= (1 << (c + 24)) if (h >> c) & 1 else (1 << c)
+        hands.append(h)
+    anns = [{"card_index": int(ci), "player": PLAYERS[p], "bit": ANN_BITS[a]}
+            for ci, p, a in re.findall(r"FdoAnnouncementOccurrence \{\s*card_index: (\d+),\s*player: FdoPlayer::(\w+),\s*"
+                                       r"announcement: (\w+),", t, re.S)]
+    cur = PLAYERS[re.search(r"current_player: Some\(FdoPlayer::(\w+)\)", t).group(1)]
+    phase = PHASES[re.search(r"current_phase: FdoPhase::(\w+)", t).group(1)]
+    re_players = 0
+    for p in re.findall(r"FdoPlayer::(\w+)", re.search(r"re_players: FdoPlayerSet::from_vec\(vec!\[(.*?)\]\)", t).group(1)):
+        re_players |= 1 << PLAYERS[p]
+    tab = _var2_tables()
+
+    def ev(fn, arg):
+        arg = arg.strip()
+        a0 = arg.split(",")[0].strip()
+        if fn == "encode_reservation_or_card_or_reservation":
+            return tab["vis_res"][0][re.search(r"FdoVisibleReservation::(\w+)", arg).group(1)]
+        if fn == "encode_reservation_or_card_or_none_card":
+            return tab["card"][0][re.search(r"FdoCard::(\w+)", arg).group(1)] if "Some" in arg else tab["card"][1]
+        if fn == "encode_reservation_or_card_or_pi_announcement":
+            return tab["pi_ann"][0][re.search(r"Some\((\w+)\)", arg).group(1)] if "Some" in arg else tab["pi_ann"][1]
+        if fn == "encode_position_or_unknown_int":
+            return int(a0) + 1
+        if fn == "encode_position_or_unknown_hand":
+            if a0 == "None":
+                return 0
+            return (pl(re.search(r"Some\(FdoPlayer::(\w+)\)", arg).group(1)) - pl(arg.split(",")[1])) % 4 + 1 + 52
+        if fn == "encode_player_or_none":
+            if a0 == "None":
+                return 0
+            return (pl(re.search(r"Some\(FdoPlayer::(\w+)\)", arg).group(1)) - pl(arg.split(",")[1])) % 4 + 1
+        if fn == "encode_subposition_card":
+            return 0 if a0 == "None" else {0: 11, 1: 12}[int(re.search(r"Some\((\d+)\)", arg).group(1))]
+        if fn == "encode_subposition_pos":
+            return 0 if a0 == "None" else int(re.search(r"Some\((\d+)\)", arg).group(1)) + 1
+        if fn == "encode_announcement_team":
+            return 0 if a0 == "None" else {"Re": 1, "Kontra": 2}[re.search(r"FdoTeam::(\w+)", arg).group(1)]
+        if fn == "encode_phase":
+            return PHASES[re.search(r"FdoPhase::(\w+)", arg).group(1)]
+        raise ValueError(fn)
+
+    calls = re.findall(r"assert_eq_inc!\(result\[i\.\.i\+1\], (\w+)\((.*?)\)\);", t)
+    tokens = [ev(fn, arg) for fn, arg in calls]
+    assert len(tokens) == 311
+    return {"source": "rs-doko-networks/src/full_doko/var1/encode_pi.rs:237-797",
+            "res_start": res_start, "res": res, "tricks": tricks, "hands": hands, "announcements": anns,
+            "current_player": cur, "phase": phase, "re_players": re_players, "expect": tokens}
+
+
 def main():
     with open(os.path.join(OUT, "fdo_traces.json"), "w") as fh:
         json.dump(fdo_traces(), fh, indent=0)
@@ -359,6 +452,8 @@ def main():
         json.dump(fusion_kats(), fh, indent=1)
     with open(os.path.join(OUT, "do_assignment_kats.json"), "w") as fh:
         json.dump(do_assignment_kats(), fh, indent=None)
+    with open(os.path.join(OUT, "encode_pi_kat.json"), "w") as fh:
+        json.dump(encode_pi_kat(), fh, indent=None)
     print("wrote fixtures to", OUT)
 
 

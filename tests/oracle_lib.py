@@ -83,6 +83,8 @@ def lib():
             "or_az_search": (ctypes.c_int, [vp, f32p, ctypes.c_uint32, ctypes.c_float, ctypes.c_float, ctypes.c_int,
                                             ctypes.c_int, ctypes.c_float, u64p, u32p, f32p]),
             "or_az_take_action": (None, [vp, ctypes.c_int]),
+            "or_encode_pi": (None, [vp, ctypes.POINTER(ctypes.c_int64)]),
+            "or_encode_pi_fields": (None, [i32p, u64p, ctypes.POINTER(ctypes.c_int64)]),
             "or_ttt_finish": (ctypes.c_int, [i32p]),
             "or_ttt_rollout": (None, [i32p, u64p, f64p]),
             "or_ttt_search": (ctypes.c_int, [i32p, u64p, ctypes.c_uint32, ctypes.c_double, u32p, f64p]),
@@ -188,6 +190,12 @@ class FdoState:
         pr = arr(ctypes.c_float, 39, [-1.0] * 39)
         a = lib().or_az_search(self.h, arr(ctypes.c_float, 39, noise), iters, c, eps, epoch, temp_mode, temp, rng, v, pr)
         return a, list(v), list(pr)
+
+    def encode_pi(self):
+        """encode_state_pi (rs-doko-networks/src/full_doko/var1/encode_pi.rs:27-214) -> 311 tokens."""
+        o = arr(ctypes.c_int64, 311)
+        lib().or_encode_pi(self.h, o)
+        return list(o)
 
     def az_take_action(self, a):
         """FdoAzEnvState::take_action_by_action_index(a, skip_single=true)."""
@@ -342,3 +350,22 @@ def az_hash_eval_np(packed):
             z = z ^ (z >> np.uint64(31))
             logits.append((z & np.uint64(31)).astype(np.int64) - 16)
     return (value.astype(np.float32) * np.float32(0.125)), (np.stack(logits, axis=1).astype(np.float32) * np.float32(0.25))
+
+
+def encode_pi_fields(res_start, res, tricks, hands, announcements, current_player, phase, re_players):
+    """encode_state_pi of a state given by the fields the encoder reads (the encode_pi.rs test layout)."""
+    f = [0] * 119
+    f[0], f[1] = res_start, len(res)
+    for i, r in enumerate(res):
+        f[2 + i] = r
+    f[6] = len(tricks)
+    for t, tr in enumerate(tricks):
+        cs = list(tr["cards"]) + [-1] * (4 - len(tr["cards"]))
+        f[7 + 6 * t:13 + 6 * t] = [tr["start"], len(tr["cards"])] + cs
+    f[79] = len(announcements)
+    for k, a in enumerate(announcements):
+        f[80 + 3 * k:83 + 3 * k] = [a["card_index"], a["player"], a["bit"]]
+    f[116], f[117], f[118] = current_player, phase, re_players
+    o = arr(ctypes.c_int64, 311)
+    lib().or_encode_pi_fields(arr(ctypes.c_int32, 119, f), arr(ctypes.c_uint64, 4, hands), o)
+    return list(o)

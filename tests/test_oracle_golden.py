@@ -200,3 +200,13 @@ def test_do_sample_assignment_support_golden():
             assert len(seen) == case["expect_len"]
             for exp in case["expect_contains"]:
                 assert tuple(tuple(sorted(h)) for h in exp) in seen
+
+
+# ---------------------------------------------------------------- AlphaZero network input
+def test_encode_state_pi_golden():
+    """rs-doko-networks/src/full_doko/var1/encode_pi.rs:237-797 — all 311 tokens of the
+    reference's encoder test (a clubs solo after 43 cards with five announcements)."""
+    g = load("encode_pi_kat.json")
+    got = ol.encode_pi_fields(g["res_start"], g["res"], g["tricks"], g["hands"], g["announcements"],
+                              g["current_player"], g["phase"], g["re_players"])
+    assert got == g["expect"]
