@@ -36,9 +36,12 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--workload", choices=["c3", "c2", "c2d"], default="c3",
+    p.add_argument("--workload", choices=["c3", "c2", "c2d", "c5"], default="c3",
                    help="c3: rs-full-doko + CAP (default, the metric's config); c2: rs-doko roots after 4x Healthy; "
-                        "c2d: rs-doko infostates determinized by the rule-based sampler")
+                        "c2d: rs-doko infostates determinized by the rule-based sampler; "
+                        "c5: AlphaZero self-play moves (PUCT + policy/value network)")
+    p.add_argument("--games", type=int, default=8192, help="concurrent self-play games per GPU (c5)")
+    p.add_argument("--az-iterations", type=int, default=200, help="PUCT iterations per move (c5)")
     p.add_argument("--iterations", type=int, default=1000)
     p.add_argument("--infostates", type=int, default=4096,
                    help="infostates per GPU (c3): 4096 x 64 samples = 262,144 roots, streamed through the resident waves' node pools (131,072 roots)")
@@ -170,6 +173,8 @@ def main():
         if rc != 0:
             raise RuntimeError("doko_amd error %d: %s" % (rc, L.dk_status_string(rc).decode()))
 
+    if args.workload == "c5":
+        return run_c5(args, dk, L, dev, stream, rank, world, local_rank, dist)
     eng, step, n_roots, bufs = make_workload(args, dk, L, dev, sp, rank, world, local_rank, dist)
     determinized = args.workload in ("c3", "c2d")
     search_ms = []
@@ -264,6 +269,131 @@ def main():
                         "traffic = 2*FETCH_SIZE+WRITE_SIZE from profiles/pmc_search.json scaled per launch",
             },
             "cpu_baseline": cpu,
+        }
+        print(json.dumps(result))
+    if world > 1:
+        dist.destroy_process_group()
+    eng.close()
+    return result
+
+
+AZ_FLOP_PER_EVAL = None
+
+
+def az_flop_per_eval(d=160, seq=62, blocks=6, classes=43):
+    """Algorithmic FLOPs of one DokoAzNet evaluation (multiply-add = 2): per block the
+    projections 2*S*d*d*(3+1+1+4+4) and attention 4*S*S*d; the class heads 4*C*S*d + 2*C*d*d + 2*C*d."""
+    return blocks * (26 * seq * d * d + 4 * seq * seq * d) + 4 * classes * seq * d + 2 * classes * d * d + 2 * classes * d
+
+
+def run_c5(args, dk, L, dev, stream, rank, world, local_rank, dist):
+    """Config 5: AlphaZero self-play.  One step = one move decision of every concurrent
+    game: root evaluation, `az_iterations` x (PUCT select on the GPU -> encode_state_pi on
+    the GPU -> DokoAzNet in bf16 -> backup), the temperature pick, the move
+    (take_action with skip_single), and fresh deals for finished games.  Run parameters
+    of the reference (az_doko.py:579-614): 8192 concurrent games, 200 iterations,
+    Dirichlet alpha 0.8 / epsilon 0.3, c_puct 4.0, temperature 0.5.  Games are
+    independent, so N GPUs run N replicas (weak scaling, no collective)."""
+    import torch
+    from master_doko_reinforcement_learning_amd.az_network import AzEvaluator, DokoAzNet
+    torch.manual_seed(1234 + rank)
+    G, iters = args.games, args.az_iterations
+    eng = dk.Engine(device=local_rank, max_roots=64, max_iterations=max(1, iters))
+    sp = stream.cuda_stream
+
+    def ck(rc):
+        if rc != 0:
+            raise RuntimeError("doko_amd error %d: %s" % (rc, L.dk_status_string(rc).decode()))
+
+    seeds = np.arange(G, dtype=np.uint64) + np.uint64(0xA2000000 + rank * G)
+    st = torch.zeros((G, 128), dtype=torch.uint8, device=dev)
+    ck(L.dk_new_game_batch_async(eng.ctx, dk.GAME_FULL_DOKO, torch.tensor(seeds.view(np.int64), device=dev).data_ptr(),
+                                 G, st.data_ptr(), sp))
+    records = dk.az_records(eng, st)
+    net = DokoAzNet().to(dev)
+    ev_time = [0.0]
+
+    class TimedEval(AzEvaluator):
+        def __call__(self, recs):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            out = super().__call__(recs)
+            e1.record()
+            ev_time.append((e0, e1))
+            return out
+
+    evaluator = TimedEval(eng, net)
+    search = dk.AlphaZeroSearch(eng, 4.0, 0.3, 10, 0.5)
+    dirichlet = torch.distributions.Dirichlet(torch.full((39,), 0.8, device=dev))
+    next_seed = [int(seeds[-1]) + 1]
+    moves = [0, 0]
+
+    def step():
+        noise = dirichlet.sample((G,)).float()
+        srch = np.arange(G, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15) + np.uint64(next_seed[0])
+        actions, _ = search.mcts_search(records, evaluator, noise, iters, srch)
+        dk.az_step(eng, records, actions)
+        fin = (records[:, 99] == 3).nonzero().flatten()      # phase byte: Finished -> a fresh deal
+        moves[0] += int((actions != 255).sum().item())
+        if fin.numel():
+            k = fin.numel()
+            fs = torch.tensor((np.arange(k, dtype=np.uint64) + np.uint64(next_seed[0])).view(np.int64), device=dev)
+            next_seed[0] += k
+            fresh = torch.zeros((k, 128), dtype=torch.uint8, device=dev)
+            ck(L.dk_new_game_batch_async(eng.ctx, dk.GAME_FULL_DOKO, fs.data_ptr(), k, fresh.data_ptr(), sp))
+            records[fin] = dk.az_records(eng, fresh)
+            moves[1] += k
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    ev_time[:] = [0.0]
+    moves[:] = [0, 0]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    net_ms = sum(e0.elapsed_time(e1) for e0, e1 in ev_time[1:])
+    evals = G * (iters + 1) * args.steps
+    flop = az_flop_per_eval()
+    result = None
+    if rank == 0:
+        achieved = flop * evals / (net_ms / 1e3) / 1e12
+        result = {
+            "metric": "AlphaZero self-play PUCT simulations/sec (one policy/value network leaf evaluation each)",
+            "value": G * iters * args.steps * world / elapsed,
+            "unit": "simulations/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16 network, f32 tree statistics",
+            "data": "synthetic: seeded full-doko deals, random-initialised DokoAzNet (d 160, 6 blocks); Dirichlet "
+                    "noise from torch",
+            "config": {"workload": "C5 AlphaZero self-play: %d concurrent games x %d PUCT iterations per move per GPU"
+                                   % (G, iters),
+                       "c_puct": 4.0, "dirichlet": [0.8, 0.3], "temperature": 0.5,
+                       "moves_per_step": G, "games_finished": moves[1], "parallelism": "replicas x%d" % world},
+            "network_ms_per_step": net_ms / args.steps,
+            "search_ms_per_step": elapsed / args.steps * 1e3 - net_ms / args.steps,
+            "roofline": {"bound": "mfma", "achieved": achieved, "peak": 2500.0, "unit": "TFLOP/s",
+                         "frac": achieved / 2500.0, "traffic": None,
+                         "note": "network GEMMs/attention: %.1f MFLOP per leaf evaluation (algorithmic), bf16 dense "
+                                 "peak; achieved over the network's event-timed share of the step" % (flop / 1e6)},
+            "cpu_baseline": None,
         }
         print(json.dumps(result))
     if world > 1:

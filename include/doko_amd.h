@@ -135,6 +135,20 @@ typedef union dk_state {
     dk_ttt_state ttt;
 } dk_state;
 
+/* AlphaZero game record: the packed rs-full-doko state plus its announcement
+ * occurrence list (FdoAnnouncements.announcements, announcement/announcement.rs:47-59),
+ * which the network's encoder reads (encode_pi.rs:135-170) and dk_fdo_state has no room for.
+ * ann_code[k] = player << 4 | (announcement action - 33): 0 ReContra, 1 No90, 2 No60,
+ * 3 No30, 4 Black (FdoAction::AnnouncementReContra always records FdoAnnouncement::ReContra,
+ * action/action.rs:295-310). */
+typedef struct dk_az_state {
+    dk_state state;          /*   0                                                          */
+    uint8_t ann_card[12];    /* 128: card_index of each occurrence                           */
+    uint8_t ann_code[12];    /* 140                                                          */
+    uint8_t ann_n;           /* 152                                                          */
+    uint8_t reserved[7];     /* 153                                                          */
+} dk_az_state;
+
 /* ---- context ---------------------------------------------------------------- */
 typedef struct dk_config {
     int32_t device;          /* HIP device ordinal                                          */
@@ -241,9 +255,9 @@ int dk_decide_batch(dk_ctx* ctx, const dk_state* infostates, uint32_t n_info, ui
  * over FdoAzEnvState (rs-doko-alpha-zero/src/env/envs/full_doko/full_doko.rs:15-172), batched over
  * n_games independent games.  The reference awaits its batch processor (the network) once for the
  * root and once per iteration; here the caller runs the network between the launches, on the
- * same stream, over the packed leaf states the search writes:
+ * same stream, over the leaf records (dk_az_state) the search writes:
  *
- *   dk_az_begin_async   roots -> d_eval[g] = root state                  (new_root_node, node.rs:209-244)
+ *   dk_az_begin_async   roots (dk_az_state records) -> d_eval[g] = root  (new_root_node, node.rs:209-244)
  *   network(d_eval)     -> value[n][4] (POV of each state's current player), logits[n][39]
  *   dk_az_root_async    priors = softmax(logits) mixed with the Dirichlet noise d_noise[n][39]
  *                       (1 - eps, eps), restricted to the root's allowed actions and renormalised;
@@ -265,14 +279,35 @@ int dk_decide_batch(dk_ctx* ctx, const dk_state* infostates, uint32_t n_info, ui
  * One AZ search batch per context at a time; node/state pools grow on demand (48 B per node,
  * 1 + 12 (iterations + 1) + 39 nodes and iterations + 2 packed states per game).
  */
-int dk_az_begin_async(dk_ctx* ctx, const dk_state* d_roots, const uint64_t* d_seeds, uint32_t n_games,
-                      uint32_t iterations, int epoch, dk_state* d_eval, void* stream);
+int dk_az_begin_async(dk_ctx* ctx, const dk_az_state* d_roots, const uint64_t* d_seeds, uint32_t n_games,
+                      uint32_t iterations, int epoch, dk_az_state* d_eval, void* stream);
 int dk_az_root_async(dk_ctx* ctx, const float* d_value, const float* d_logits, const float* d_noise,
                      float dirichlet_epsilon, void* stream);
-int dk_az_select_async(dk_ctx* ctx, float c, dk_state* d_eval, uint8_t* d_need_eval, void* stream);
+int dk_az_select_async(dk_ctx* ctx, float c, dk_az_state* d_eval, uint8_t* d_need_eval, void* stream);
 int dk_az_backup_async(dk_ctx* ctx, const float* d_value, const float* d_logits, void* stream);
 int dk_az_finish_async(dk_ctx* ctx, int temperature_mode, float temperature, uint32_t* d_visits, uint8_t* d_action,
                        void* stream);
+/* Game records for self-play.  dk_az_records_async: records of packed rs-full-doko states
+ * without announcements (new games, DK_E_STATE otherwise).  dk_az_step_async:
+ * take_action_by_action_index(action, skip_single = true) (full_doko.rs:121-157) on every
+ * record whose action is not DK_NONE (a self-play move).  dk_az_encode_async: the network
+ * input encode_state_pi (rs-doko-networks/src/full_doko/var1/encode_pi.rs:27-214),
+ * tokens[n][311] int32. */
+int dk_az_records_async(dk_ctx* ctx, const dk_state* d_states, uint32_t n, dk_az_state* d_out, void* stream);
+int dk_az_step_async(dk_ctx* ctx, dk_az_state* d_records, const uint8_t* d_actions, uint32_t n, void* stream);
+int dk_az_encode_async(dk_ctx* ctx, const dk_az_state* d_records, uint32_t n, int32_t* d_tokens, void* stream);
+
+/* ---- AlphaZero network row kernels (bf16 activations [rows, d], d % 32 == 0, d <= 512) ----
+ * The network itself (az_network.py) is PyTorch; these fuse its memory-bound row passes:
+ * dk_net_embed_ln_bf16_async: x = sum of the six token embeddings of encode_state_pi
+ *   (tables = 6 device pointers: object, position, player, subposition, team, phase; the sum in
+ *   that order with bf16 rounding after each add, as torch), h = LayerNorm(x; gamma, beta, eps).
+ * dk_net_add_ln_bf16_async: x += delta (delta may be NULL), h = LayerNorm(x).
+ * `stream` is the caller's stream (torch's current stream). */
+int dk_net_embed_ln_bf16_async(const int32_t* d_tokens, uint32_t batch, const void* const* tables, uint32_t d,
+                               const void* gamma, const void* beta, float eps, void* x_out, void* h_out, void* stream);
+int dk_net_add_ln_bf16_async(void* x_io, const void* delta, uint32_t rows, uint32_t d, const void* gamma, const void* beta,
+                             float eps, void* h_out, void* stream);
 
 /* ---- completion / errors / timing of *_async work -------------------------------
  * dk_sync: waits for the stream and returns the first device-side error

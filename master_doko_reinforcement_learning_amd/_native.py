@@ -87,6 +87,11 @@ def lib():
         "dk_az_select_async": (ctypes.c_int, [vp, ctypes.c_float, vp, vp, vp]),
         "dk_az_backup_async": (ctypes.c_int, [vp, vp, vp, vp]),
         "dk_az_finish_async": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_float, vp, vp, vp]),
+        "dk_az_records_async": (ctypes.c_int, [vp, vp, u32, vp, vp]),
+        "dk_az_step_async": (ctypes.c_int, [vp, vp, vp, u32, vp]),
+        "dk_az_encode_async": (ctypes.c_int, [vp, vp, u32, vp, vp]),
+        "dk_net_embed_ln_bf16_async": (ctypes.c_int, [vp, u32, ctypes.POINTER(vp), u32, vp, vp, ctypes.c_float, vp, vp, vp]),
+        "dk_net_add_ln_bf16_async": (ctypes.c_int, [vp, vp, u32, u32, vp, vp, ctypes.c_float, vp, vp]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(L, name)
@@ -105,4 +110,6 @@ EXPORTED = [
     "dk_fuse_accumulate_async", "dk_fuse_select_async", "dk_decide_batch", "dk_sync", "dk_last_search_ms",
     "dk_pool_bytes", "dk_legal_actions_async", "dk_env_step_batch_async", "dk_env_random_plies_batch_async",
     "dk_az_begin_async", "dk_az_root_async", "dk_az_select_async", "dk_az_backup_async", "dk_az_finish_async",
+    "dk_az_records_async", "dk_az_step_async", "dk_az_encode_async", "dk_net_embed_ln_bf16_async",
+    "dk_net_add_ln_bf16_async",
 ]

@@ -29,6 +29,8 @@ FUSE_MAXN = 0
 FUSE_AVG = 1
 NUM_ACTIONS = 39
 STATE_BYTES = 128
+AZ_STATE_BYTES = 160   # dk_az_state: packed state + announcement occurrence list
+AZ_TOKENS = 311        # encode_state_pi
 
 
 class DokoError(RuntimeError):
@@ -244,9 +246,9 @@ class AlphaZeroSearch:
     then `network` on all leaves at once (the reference's batch processor), then the
     backup.  Everything stays on the device (torch tensors on the current stream).
 
-    network(states) -> (value, logits): states = uint8 [n, 128] packed dk_state on the
-    GPU; value = float32 [n, 4] from each state's current player's point of view;
-    logits = float32 [n, 39].
+    network(records) -> (value, logits): records = uint8 [n, 160] dk_az_state on the
+    GPU (az_encode turns them into the 311-token network input); value = float32
+    [n, 4] from each state's current player's point of view; logits = float32 [n, 39].
     temperature: None (greedy), float('inf') (uniform) or a finite T (select_action,
     mcts.rs:185-248)."""
 
@@ -258,7 +260,7 @@ class AlphaZeroSearch:
         self.temperature = temperature
 
     def mcts_search(self, roots, network, noise, iterations, seeds):
-        """roots: uint8 [n, 128] (GPU); noise: float32 [n, 39] Dirichlet samples (GPU);
+        """roots: uint8 [n, 160] dk_az_state records (GPU); noise: float32 [n, 39] Dirichlet samples (GPU);
         seeds: uint64 [n] (SmallRng per game).  Returns (actions uint8 [n], visits int32 [n, 39])."""
         import torch
         dev = roots.device
@@ -283,7 +285,7 @@ class AlphaZeroSearch:
         seeds_t = torch.as_tensor(np.ascontiguousarray(seeds, dtype=np.uint64).view(np.int64), device=dev)
         roots = roots.contiguous()
         noise = noise.contiguous().float()
-        ev = torch.empty((n, STATE_BYTES), dtype=torch.uint8, device=dev)
+        ev = torch.empty((n, AZ_STATE_BYTES), dtype=torch.uint8, device=dev)
         need = torch.empty(n, dtype=torch.uint8, device=dev)
         _check(L.dk_az_begin_async(ctx, roots.data_ptr(), seeds_t.data_ptr(), n, iterations, self.epoch,
                                    ev.data_ptr(), st))
@@ -302,3 +304,42 @@ class AlphaZeroSearch:
         _check(L.dk_az_finish_async(ctx, mode, temp, visits.data_ptr(), actions.data_ptr(), st))
         _check(L.dk_sync(ctx, st))
         return actions, visits
+
+
+def _stream(t):
+    import torch
+    st = torch.cuda.current_stream(t.device).cuda_stream
+    return st
+
+
+def az_records(engine, states):
+    """dk_az_state records (uint8 [n, 160], GPU) of packed rs-full-doko states without
+    announcements (new games): the AlphaZero game records."""
+    import torch
+    states = states.contiguous()
+    out = torch.empty((states.shape[0], AZ_STATE_BYTES), dtype=torch.uint8, device=states.device)
+    st = _stream(states)
+    _check(_native.lib().dk_az_records_async(engine.ctx, states.data_ptr(), states.shape[0], out.data_ptr(), st))
+    _check(_native.lib().dk_sync(engine.ctx, st))
+    return out
+
+
+def az_step(engine, records, actions):
+    """take_action_by_action_index(a, skip_single=true) (full_doko.rs:121-157) in place on
+    every record whose action (uint8, GPU) is not 255: one self-play move."""
+    st = _stream(records)
+    _check(_native.lib().dk_az_step_async(engine.ctx, records.data_ptr(), actions.contiguous().data_ptr(),
+                                          records.shape[0], st))
+    _check(_native.lib().dk_sync(engine.ctx, st))
+    return records
+
+
+def az_encode(engine, records, out=None):
+    """encode_state_pi (rs-doko-networks/src/full_doko/var1/encode_pi.rs:27-214) of each
+    record: int32 [n, 311] tokens on the GPU (asynchronous on the current stream)."""
+    import torch
+    n = records.shape[0]
+    if out is None:
+        out = torch.empty((n, AZ_TOKENS), dtype=torch.int32, device=records.device)
+    _check(_native.lib().dk_az_encode_async(engine.ctx, records.data_ptr(), n, out.data_ptr(), _stream(records)))
+    return out

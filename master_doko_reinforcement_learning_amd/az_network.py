@@ -1,0 +1,206 @@
+"""The AlphaZero policy/value network for full Doppelkopf, inference side.
+
+Architecture of rs-doko-py-bridge/python/az_doko.py:28-138 (AlphaZeroTicTacToeNetwork
+with TransformerBlock.py / SelfAttention.py), default config n_embd 160, 4 heads,
+4 shared blocks + 1 policy block + 1 value block:
+
+    tokens [B, 311] = 5 x 62 token rows + phase (encode_state_pi, see az_encode)
+    x = E_obj[t0] + E_pos[t1] + E_player[t2] + E_subpos[t3] + E_team[t4] + E_phase[t5]   [B, 62, d]
+    blocks: x += c_proj(MHA(LN1 x));  x += W2 GELU(W1 LN2 x)
+    heads : per-class attention pooling (learned class queries over the 62 positions),
+            then a per-class LN -> Linear(d, d) -> GELU -> Linear(d, 1)
+    value [B, 4], policy logits [B, 39]
+
+Re-expressed for MI355X rather than translated:
+  * the attention core is torch's fused scaled_dot_product_attention over a fused
+    qkv projection (the reference's nn.MultiheadAttention in_proj has the same
+    [q; k; v] weight layout, see load_reference_state_dict);
+  * the 4 + 39 per-class MLPs of the heads run as ONE batched GEMM per layer
+    (class-stacked weights [C, d, d]) instead of 43 small launches;
+  * inference runs in bf16 (hipBLASLt GEMMs on the matrix cores); the tokens come
+    straight from the device encoder, no host round trip.
+Weights are random-initialised here (no checkpoint ships with the reference);
+load_reference_state_dict maps a reference state_dict onto this module.
+"""
+import ctypes
+import math
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+ctypes_vp = ctypes.c_void_p
+VOCAB = (43, 57, 5, 13, 3, 3)   # object, position, player, subposition, team, phase (az_doko.py:85-90)
+SEQ = 62
+
+
+class Block(nn.Module):
+    def __init__(self, d, heads):
+        super().__init__()
+        self.heads = heads
+        self.ln_1 = nn.LayerNorm(d)
+        self.qkv = nn.Linear(d, 3 * d)          # MultiheadAttention.in_proj
+        self.out = nn.Linear(d, d)              # MultiheadAttention.out_proj
+        self.c_proj = nn.Linear(d, d)           # SelfAttention.c_proj
+        self.ln_2 = nn.LayerNorm(d)
+        self.fc = nn.Linear(d, 4 * d)
+        self.proj = nn.Linear(4 * d, d)
+
+    def attn_delta(self, h):                     # h = ln_1(x)
+        b, s, d = h.shape
+        q, k, v = self.qkv(h).view(b, s, 3, self.heads, d // self.heads).permute(2, 0, 3, 1, 4)
+        y = F.scaled_dot_product_attention(q, k, v).transpose(1, 2).reshape(b, s, d)
+        return self.c_proj(self.out(y))
+
+    def mlp_delta(self, h):                      # h = ln_2(x)
+        return self.proj(F.gelu(self.fc(h)))
+
+    def forward(self, x):
+        x = x + self.attn_delta(self.ln_1(x))
+        return x + self.mlp_delta(self.ln_2(x))
+
+
+class ClassHead(nn.Module):
+    """PerClassAttentionMLPHead (az_doko.py:28-56) with class-stacked MLP weights."""
+
+    def __init__(self, d, classes):
+        super().__init__()
+        self.queries = nn.Parameter(torch.randn(classes, d))
+        self.scale = d ** -0.5
+        self.ln_w = nn.Parameter(torch.ones(classes, d))
+        self.ln_b = nn.Parameter(torch.zeros(classes, d))
+        self.w1 = nn.Parameter(torch.empty(classes, d, d))
+        self.b1 = nn.Parameter(torch.empty(classes, d))
+        self.w2 = nn.Parameter(torch.empty(classes, d))
+        self.b2 = nn.Parameter(torch.empty(classes))
+        bound = 1.0 / math.sqrt(d)
+        for p in (self.w1, self.b1, self.w2, self.b2):
+            nn.init.uniform_(p, -bound, bound)
+
+    def forward(self, x):                                        # x [B, S, d]
+        w = torch.softmax(torch.einsum("cd,bsd->bcs", self.queries, x) * self.scale, dim=-1)
+        a = torch.einsum("bcs,bsd->bcd", w, x)                  # [B, C, d]
+        a = F.layer_norm(a, a.shape[-1:]) * self.ln_w + self.ln_b
+        h = F.gelu(torch.einsum("bci,coi->bco", a, self.w1) + self.b1)
+        return torch.einsum("bco,co->bc", h, self.w2) + self.b2
+
+
+class DokoAzNet(nn.Module):
+    def __init__(self, d=160, heads=4, layers=4, policy_layers=1, value_layers=1):
+        super().__init__()
+        self.emb = nn.ModuleList([nn.Embedding(v, d) for v in VOCAB])
+        self.blocks = nn.ModuleList([Block(d, heads) for _ in range(layers)])
+        self.p_blocks = nn.ModuleList([Block(d, heads) for _ in range(policy_layers)])
+        self.v_blocks = nn.ModuleList([Block(d, heads) for _ in range(value_layers)])
+        self.p_ln = nn.LayerNorm(d)
+        self.v_ln = nn.LayerNorm(d)
+        self.value_head = ClassHead(d, 4)
+        self.policy_head = ClassHead(d, 39)
+
+    def forward(self, tokens):                                   # int32/int64 [B, 311]
+        if tokens.is_cuda and self.emb[0].weight.dtype == torch.bfloat16:
+            return self.forward_fused(tokens)
+        t = tokens.long()
+        x = sum(self.emb[i](t[:, SEQ * i:SEQ * (i + 1)]) for i in range(5)) + self.emb[5](t[:, 310:311])
+        for blk in self.blocks:
+            x = blk(x)
+        xp, xv = x, x
+        for blk in self.p_blocks:
+            xp = blk(xp)
+        for blk in self.v_blocks:
+            xv = blk(xv)
+        return self.value_head(self.v_ln(xv)), self.policy_head(self.p_ln(xp))
+
+    def forward_fused(self, tokens):
+        """bf16 forward on the GPU with the row passes fused in HIP kernels
+        (csrc/az_net_kernels.h): the embedding sum + first LayerNorm in one pass,
+        and every residual add fused with the LayerNorm that follows it."""
+        from . import _native
+        L = _native.lib()
+        st = torch.cuda.current_stream(tokens.device).cuda_stream
+        tok = tokens.int().contiguous()
+        B, d = tok.shape[0], self.emb[0].weight.shape[1]
+        rows = B * SEQ
+        if not (self.blocks and self.p_blocks and self.v_blocks):
+            raise ValueError("the fused forward needs shared, policy and value blocks")
+
+        def ck(rc):
+            if rc != 0:
+                raise RuntimeError("doko_amd network kernel error %d" % rc)
+
+        def add_ln(x, delta, ln):
+            h = torch.empty_like(x)
+            ck(L.dk_net_add_ln_bf16_async(x.data_ptr(), delta.data_ptr() if delta is not None else None, rows, d,
+                                          ln.weight.data_ptr(), ln.bias.data_ptr(), ln.eps, h.data_ptr(), st))
+            return h
+
+        x = torch.empty((B, SEQ, d), dtype=torch.bfloat16, device=tok.device)
+        h = torch.empty_like(x)
+        tables = (ctypes_vp * 6)(*[e.weight.data_ptr() for e in self.emb])
+        ln0 = self.blocks[0].ln_1
+        ck(L.dk_net_embed_ln_bf16_async(tok.data_ptr(), B, tables, d, ln0.weight.data_ptr(), ln0.bias.data_ptr(),
+                                        ln0.eps, x.data_ptr(), h.data_ptr(), st))
+
+        def run(x, h, blocks, final_ln):
+            for i, blk in enumerate(blocks):
+                h = add_ln(x, blk.attn_delta(h), blk.ln_2)
+                nxt = blocks[i + 1].ln_1 if i + 1 < len(blocks) else final_ln
+                h = add_ln(x, blk.mlp_delta(h), nxt)
+            return h
+
+        hp = run(x, h, self.blocks, self.p_blocks[0].ln_1)       # x now holds the shared trunk's output
+        xv = x.clone()
+        hv = add_ln(xv, None, self.v_blocks[0].ln_1)
+        hp = run(x, hp, self.p_blocks, self.p_ln)
+        hv = run(xv, hv, self.v_blocks, self.v_ln)
+        return self.value_head(hv), self.policy_head(hp)
+
+    @torch.no_grad()
+    def load_reference_state_dict(self, sd):
+        """Map a state_dict of the reference AlphaZeroTicTacToeNetwork onto this module
+        (load it with torch.load(path, weights_only=True))."""
+        names = ["game_object_e", "position_e", "player_played_e", "subposition_e", "team_e", "phase_e"]
+        for i, n in enumerate(names):
+            self.emb[i].weight.copy_(sd["transformer.%s.weight" % n])
+
+        def blk(dst, pre):
+            dst.ln_1.weight.copy_(sd[pre + "ln_1.weight"]); dst.ln_1.bias.copy_(sd[pre + "ln_1.bias"])
+            dst.qkv.weight.copy_(sd[pre + "attn.attn.in_proj_weight"]); dst.qkv.bias.copy_(sd[pre + "attn.attn.in_proj_bias"])
+            dst.out.weight.copy_(sd[pre + "attn.attn.out_proj.weight"]); dst.out.bias.copy_(sd[pre + "attn.attn.out_proj.bias"])
+            dst.c_proj.weight.copy_(sd[pre + "attn.c_proj.weight"]); dst.c_proj.bias.copy_(sd[pre + "attn.c_proj.bias"])
+            dst.ln_2.weight.copy_(sd[pre + "ln_2.weight"]); dst.ln_2.bias.copy_(sd[pre + "ln_2.bias"])
+            dst.fc.weight.copy_(sd[pre + "mlp.c_fc.weight"]); dst.fc.bias.copy_(sd[pre + "mlp.c_fc.bias"])
+            dst.proj.weight.copy_(sd[pre + "mlp.c_proj.weight"]); dst.proj.bias.copy_(sd[pre + "mlp.c_proj.bias"])
+        for group, mods in (("h", self.blocks), ("p_h", self.p_blocks), ("v_h", self.v_blocks)):
+            for i, m in enumerate(mods):
+                blk(m, "transformer.%s.%d." % (group, i))
+        for ln, n in ((self.p_ln, "p_ln_f"), (self.v_ln, "v_ln_f")):
+            ln.weight.copy_(sd["transformer.%s.weight" % n]); ln.bias.copy_(sd["transformer.%s.bias" % n])
+        for head, n in ((self.value_head, "value_head"), (self.policy_head, "policy_head")):
+            head.queries.copy_(sd[n + ".card_queries"])
+            for c in range(head.queries.shape[0]):
+                pre = "%s.mlps.%d." % (n, c)
+                head.ln_w[c].copy_(sd[pre + "0.weight"]); head.ln_b[c].copy_(sd[pre + "0.bias"])
+                head.w1[c].copy_(sd[pre + "1.weight"]); head.b1[c].copy_(sd[pre + "1.bias"])
+                head.w2[c].copy_(sd[pre + "3.weight"][0]); head.b2[c].copy_(sd[pre + "3.bias"][0])
+
+
+class AzEvaluator:
+    """The network as AlphaZeroSearch's `network` callable: dk_az_state records ->
+    device encoder (az_encode) -> DokoAzNet (bf16) -> (value f32 [n, 4], logits f32 [n, 39])."""
+
+    def __init__(self, engine, net, dtype=torch.bfloat16):
+        self.engine = engine
+        self.net = net.eval().to(dtype)
+        self.dtype = dtype
+        self._tok = None
+
+    @torch.inference_mode()
+    def __call__(self, records):
+        from .api import az_encode
+        n = records.shape[0]
+        if self._tok is None or self._tok.shape[0] < n:
+            self._tok = torch.empty((n, 311), dtype=torch.int32, device=records.device)
+        tok = az_encode(self.engine, records, self._tok[:n])
+        v, p = self.net(tok)
+        return v.float(), p.float()

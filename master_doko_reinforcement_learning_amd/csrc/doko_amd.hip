@@ -19,6 +19,8 @@
 #include "engine/adapters.h"
 #include "engine/assign_engine.h"
 #include "engine/az_core.h"
+#include "engine/encode_pi.h"
+#include "az_net_kernels.h"
 #include "engine/cap_engine.h"
 #include "engine/search_core.h"
 
@@ -361,7 +363,7 @@ __global__ void __launch_bounds__(WAVE) determinize_kernel(const dk_state* info,
 // ---------------------------------------------------------------- AlphaZero PUCT (az_core.h)
 // One lane per game; game g owns nodes [g*cap_nodes, (g+1)*cap_nodes) and states
 // [g*cap_states, ...).  The network runs between the launches on the same stream.
-__device__ inline dk::az::Mem az_mem(dk::az::Node* nodes, dk_state* states, uint32_t g, uint32_t cap_nodes,
+__device__ inline dk::az::Mem az_mem(dk::az::Node* nodes, dk_az_state* states, uint32_t g, uint32_t cap_nodes,
                                      uint32_t cap_states) {
     dk::az::Mem m;
     m.nodes = nodes + (size_t)g * cap_nodes;
@@ -370,13 +372,13 @@ __device__ inline dk::az::Mem az_mem(dk::az::Node* nodes, dk_state* states, uint
     return m;
 }
 
-__global__ void az_init_kernel(const dk_state* roots, const uint64_t* seeds, uint32_t n, dk::az::Node* nodes,
-                               dk_state* states, dk::az::Game* games, uint32_t cap_nodes, uint32_t cap_states,
-                               dk_state* eval, int* err) {
+__global__ void az_init_kernel(const dk_az_state* roots, const uint64_t* seeds, uint32_t n, dk::az::Node* nodes,
+                               dk_az_state* states, dk::az::Game* games, uint32_t cap_nodes, uint32_t cap_states,
+                               dk_az_state* eval, int* err) {
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= n) return;
-    const dk_state r = roots[g];
-    if (r.raw[127] != DK_GAME_FULL_DOKO) { atomicOr(err, 2); return; }
+    const dk_az_state r = roots[g];
+    if (r.state.raw[127] != DK_GAME_FULL_DOKO) { atomicOr(err, 2); return; }
     dk::az::Mem m = az_mem(nodes, states, g, cap_nodes, cap_states);
     dk::az::Game gm;
     dk::az::init(r, gm, m, seeds[g]);
@@ -385,7 +387,7 @@ __global__ void az_init_kernel(const dk_state* roots, const uint64_t* seeds, uin
 }
 
 __global__ void az_root_kernel(const float* value, const float* logits, const float* noise, float eps, int epoch,
-                               uint32_t n, dk::az::Node* nodes, dk_state* states, dk::az::Game* games,
+                               uint32_t n, dk::az::Node* nodes, dk_az_state* states, dk::az::Game* games,
                                uint32_t cap_nodes, uint32_t cap_states, int* err) {
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= n) return;
@@ -396,8 +398,8 @@ __global__ void az_root_kernel(const float* value, const float* logits, const fl
     games[g] = gm;
 }
 
-__global__ void az_select_kernel(float c, int epoch, uint32_t n, dk::az::Node* nodes, dk_state* states,
-                                 dk::az::Game* games, uint32_t cap_nodes, uint32_t cap_states, dk_state* eval,
+__global__ void az_select_kernel(float c, int epoch, uint32_t n, dk::az::Node* nodes, dk_az_state* states,
+                                 dk::az::Game* games, uint32_t cap_nodes, uint32_t cap_states, dk_az_state* eval,
                                  uint8_t* need_eval, int* err) {
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= n) return;
@@ -410,7 +412,7 @@ __global__ void az_select_kernel(float c, int epoch, uint32_t n, dk::az::Node* n
 }
 
 __global__ void az_backup_kernel(const float* value, const float* logits, uint32_t n, dk::az::Node* nodes,
-                                 dk_state* states, dk::az::Game* games, uint32_t cap_nodes, uint32_t cap_states) {
+                                 dk_az_state* states, dk::az::Game* games, uint32_t cap_nodes, uint32_t cap_states) {
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= n) return;
     dk::az::Mem m = az_mem(nodes, states, g, cap_nodes, cap_states);
@@ -419,7 +421,7 @@ __global__ void az_backup_kernel(const float* value, const float* logits, uint32
     games[g] = gm;
 }
 
-__global__ void az_finish_kernel(int temp_mode, float temperature, uint32_t n, dk::az::Node* nodes, dk_state* states,
+__global__ void az_finish_kernel(int temp_mode, float temperature, uint32_t n, dk::az::Node* nodes, dk_az_state* states,
                                  dk::az::Game* games, uint32_t cap_nodes, uint32_t cap_states, uint32_t* visits,
                                  uint8_t* action) {
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
@@ -431,6 +433,42 @@ __global__ void az_finish_kernel(int temp_mode, float temperature, uint32_t n, d
     for (int k = 0; k < 39; ++k) visits[39 * (size_t)g + k] = v[k];
     action[g] = a < 0 ? (uint8_t)DK_NONE : (uint8_t)a;
     games[g] = gm;
+}
+
+// records of packed states that have no announcements yet
+__global__ void az_records_kernel(const dk_state* states, uint32_t n, dk_az_state* out, int* err) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    dk_az_state r;
+    r.state = states[i];
+    for (int k = 0; k < 12; ++k) { r.ann_card[k] = 0; r.ann_code[k] = 0; }
+    r.ann_n = 0;
+    for (int k = 0; k < 7; ++k) r.reserved[k] = 0;
+    if (r.state.raw[127] != DK_GAME_FULL_DOKO || r.state.fdo.ann_count != 0) atomicOr(err, 2);
+    out[i] = r;
+}
+
+// take_action_by_action_index(a, skip_single = true) on game records (self-play moves);
+// DK_NONE leaves a record unchanged
+__global__ void az_step_kernel(dk_az_state* records, const uint8_t* actions, uint32_t n, int* err) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint8_t a = actions[i];
+    if (a == DK_NONE) return;
+    dk_az_state r = records[i];
+    dk::fdo::Work w; dk::fdo::unpack(r.state.fdo, w);
+    if (a >= 39 || !((dk::fdo::legal_actions(w) >> a) & 1)) { atomicOr(err, 2); return; }
+    dk::az::take_action(r, a);
+    records[i] = r;
+}
+
+// encode_state_pi: one lane per record, 311 int32 tokens
+__global__ void az_encode_kernel(const dk_az_state* records, uint32_t n, int32_t* tokens) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int32_t* o = tokens + 311 * (size_t)i;
+    auto put = [o](uint32_t k, uint32_t v) { o[k] = (int32_t)v; };
+    dk::enc::encode_state_pi(records[i], put);
 }
 
 // PolicyFusionMaxN / PolicyFusionAverageStrategy accumulators (policy_fusion.rs:23-123).
@@ -520,7 +558,7 @@ struct dk_ctx {
     uint64_t* prof = nullptr;       // phase timers (DK_PHASE_PROF builds only)
     // AlphaZero PUCT search (dk_az_*): per-game node / state regions, allocated on first use
     dk::az::Node* az_nodes = nullptr;
-    dk_state* az_states = nullptr;
+    dk_az_state* az_states = nullptr;
     dk::az::Game* az_games = nullptr;
     size_t az_bytes = 0;
     uint32_t az_n = 0, az_iters = 0, az_cap_nodes = 0, az_cap_states = 0, az_done = 0;
@@ -1035,12 +1073,12 @@ int dk_decide_batch(dk_ctx* ctx, const dk_state* infostates, uint32_t n_info, ui
 }
 
 // ---------------------------------------------------------------- AlphaZero PUCT search
-int dk_az_begin_async(dk_ctx* ctx, const dk_state* d_roots, const uint64_t* d_seeds, uint32_t n_games,
-                      uint32_t iterations, int epoch, dk_state* d_eval, void* stream) {
+int dk_az_begin_async(dk_ctx* ctx, const dk_az_state* d_roots, const uint64_t* d_seeds, uint32_t n_games,
+                      uint32_t iterations, int epoch, dk_az_state* d_eval, void* stream) {
     if (!ctx || !d_roots || !d_seeds || !d_eval || n_games == 0) return DK_E_INVALID;
     if (iterations >= dk::NI_MAX_STATES) return ctx->last_error = DK_E_CAPACITY;
     const uint32_t cap_nodes = 1u + 12u * (iterations + 1u) + 39u, cap_states = iterations + 2u;
-    const size_t need = (size_t)n_games * ((size_t)cap_nodes * sizeof(dk::az::Node) + (size_t)cap_states * sizeof(dk_state) +
+    const size_t need = (size_t)n_games * ((size_t)cap_nodes * sizeof(dk::az::Node) + (size_t)cap_states * sizeof(dk_az_state) +
                                            sizeof(dk::az::Game));
     if (need > ctx->az_bytes) {
         hipStream_t st = pick(ctx, stream);
@@ -1050,7 +1088,7 @@ int dk_az_begin_async(dk_ctx* ctx, const dk_state* d_roots, const uint64_t* d_se
         if (ctx->az_games) (void)hipFree(ctx->az_games);
         ctx->az_nodes = nullptr; ctx->az_states = nullptr; ctx->az_games = nullptr; ctx->az_bytes = 0;
         bool ok = hipMalloc(&ctx->az_nodes, (size_t)n_games * cap_nodes * sizeof(dk::az::Node)) == hipSuccess;
-        ok = ok && hipMalloc(&ctx->az_states, (size_t)n_games * cap_states * sizeof(dk_state)) == hipSuccess;
+        ok = ok && hipMalloc(&ctx->az_states, (size_t)n_games * cap_states * sizeof(dk_az_state)) == hipSuccess;
         ok = ok && hipMalloc(&ctx->az_games, (size_t)n_games * sizeof(dk::az::Game)) == hipSuccess;
         if (!ok) return ctx->last_error = DK_E_CAPACITY;
         ctx->az_bytes = need;
@@ -1074,7 +1112,7 @@ int dk_az_root_async(dk_ctx* ctx, const float* d_value, const float* d_logits, c
     return DK_OK;
 }
 
-int dk_az_select_async(dk_ctx* ctx, float c, dk_state* d_eval, uint8_t* d_need_eval, void* stream) {
+int dk_az_select_async(dk_ctx* ctx, float c, dk_az_state* d_eval, uint8_t* d_need_eval, void* stream) {
     if (!ctx || !ctx->az_n || !ctx->az_root_done || !d_eval) return DK_E_INVALID;
     if (ctx->az_done >= ctx->az_iters) return DK_E_INVALID;
     hipLaunchKernelGGL(az_select_kernel, dim3(grid_for(ctx->az_n, 64)), dim3(64), 0, pick(ctx, stream), c,
@@ -1094,6 +1132,30 @@ int dk_az_backup_async(dk_ctx* ctx, const float* d_value, const float* d_logits,
     return DK_OK;
 }
 
+int dk_az_records_async(dk_ctx* ctx, const dk_state* d_states, uint32_t n, dk_az_state* d_out, void* stream) {
+    if (!ctx || !d_states || !d_out) return DK_E_INVALID;
+    if (n == 0) return DK_OK;
+    hipLaunchKernelGGL(az_records_kernel, dim3(grid_for(n, 64)), dim3(64), 0, pick(ctx, stream), d_states, n, d_out, ctx->err);
+    DK_HIP(hipGetLastError());
+    return DK_OK;
+}
+
+int dk_az_step_async(dk_ctx* ctx, dk_az_state* d_records, const uint8_t* d_actions, uint32_t n, void* stream) {
+    if (!ctx || !d_records || !d_actions) return DK_E_INVALID;
+    if (n == 0) return DK_OK;
+    hipLaunchKernelGGL(az_step_kernel, dim3(grid_for(n, 64)), dim3(64), 0, pick(ctx, stream), d_records, d_actions, n, ctx->err);
+    DK_HIP(hipGetLastError());
+    return DK_OK;
+}
+
+int dk_az_encode_async(dk_ctx* ctx, const dk_az_state* d_records, uint32_t n, int32_t* d_tokens, void* stream) {
+    if (!ctx || !d_records || !d_tokens) return DK_E_INVALID;
+    if (n == 0) return DK_OK;
+    hipLaunchKernelGGL(az_encode_kernel, dim3(grid_for(n, 64)), dim3(64), 0, pick(ctx, stream), d_records, n, d_tokens);
+    DK_HIP(hipGetLastError());
+    return DK_OK;
+}
+
 int dk_az_finish_async(dk_ctx* ctx, int temperature_mode, float temperature, uint32_t* d_visits, uint8_t* d_action,
                        void* stream) {
     if (!ctx || !ctx->az_n || !d_visits || !d_action || temperature_mode < 0 || temperature_mode > 2) return DK_E_INVALID;
@@ -1101,6 +1163,51 @@ int dk_az_finish_async(dk_ctx* ctx, int temperature_mode, float temperature, uin
     hipLaunchKernelGGL(az_finish_kernel, dim3(grid_for(ctx->az_n, 64)), dim3(64), 0, pick(ctx, stream), temperature_mode,
                        temperature, ctx->az_n, ctx->az_nodes, ctx->az_states, ctx->az_games, ctx->az_cap_nodes,
                        ctx->az_cap_states, d_visits, d_action);
+    DK_HIP(hipGetLastError());
+    return DK_OK;
+}
+
+// ---------------------------------------------------------------- AlphaZero network row kernels
+namespace {
+int ln_per(uint32_t d) { return (d % 32u == 0u && d >= 32u && d <= 32u * (uint32_t)dk::net::LN_MAX_PER_LANE) ? (int)(d / 32u) : 0; }
+}  // namespace
+
+#define DK_LN_CASES(M) M(1) M(2) M(3) M(4) M(5) M(6) M(7) M(8) M(9) M(10) M(11) M(12) M(13) M(14) M(15) M(16)
+
+int dk_net_embed_ln_bf16_async(const int32_t* d_tokens, uint32_t batch, const void* const* tables, uint32_t d,
+                               const void* gamma, const void* beta, float eps, void* x_out, void* h_out, void* stream) {
+    const int per = ln_per(d);
+    if (!tables || !d_tokens || !x_out || !h_out || !gamma || !beta || per == 0) return DK_E_INVALID;
+    if (batch == 0) return DK_OK;
+    const uint32_t rows = batch * 62u;
+    const dim3 grid((rows + 7u) / 8u), block(256);
+    hipStream_t st = (hipStream_t)stream;
+    const uint16_t* const* t = (const uint16_t* const*)tables;
+    switch (per) {
+#define M(P) case P: hipLaunchKernelGGL(dk::net::embed_ln_kernel<P>, grid, block, 0, st, d_tokens, batch, t[0], t[1], t[2], \
+                                        t[3], t[4], t[5], (const uint16_t*)gamma, (const uint16_t*)beta, eps,            \
+                                        (uint16_t*)x_out, (uint16_t*)h_out); break;
+        DK_LN_CASES(M)
+#undef M
+    }
+    DK_HIP(hipGetLastError());
+    return DK_OK;
+}
+
+int dk_net_add_ln_bf16_async(void* x_io, const void* delta, uint32_t rows, uint32_t d, const void* gamma, const void* beta,
+                             float eps, void* h_out, void* stream) {
+    const int per = ln_per(d);
+    if (!x_io || !h_out || !gamma || !beta || per == 0) return DK_E_INVALID;
+    if (rows == 0) return DK_OK;
+    const dim3 grid((rows + 7u) / 8u), block(256);
+    hipStream_t st = (hipStream_t)stream;
+    switch (per) {
+#define M(P) case P: hipLaunchKernelGGL(dk::net::add_ln_kernel<P>, grid, block, 0, st, (uint16_t*)x_io,                  \
+                                        (const uint16_t*)delta, rows, (const uint16_t*)gamma, (const uint16_t*)beta, eps, \
+                                        (uint16_t*)h_out); break;
+        DK_LN_CASES(M)
+#undef M
+    }
     DK_HIP(hipGetLastError());
     return DK_OK;
 }

@@ -24,8 +24,9 @@
 // node are one block in ascending action order (the reference's
 // children[action] array order).  win[] is the RotArr win_score by absolute
 // player (every RotArr access is get_for_i/index_for_i, so the rotation is
-// only a storage convention).  States are kept packed (dk_fdo_state, card
-// history included): they are the network's input.
+// only a storage convention).  States are kept as dk_az_state records (the
+// packed state, card history included, plus the announcement occurrence list):
+// they are the network's input (encode_pi.h).
 #pragma once
 #include <math.h>
 #include "fdo_engine.h"
@@ -79,17 +80,30 @@ DK_HD uint64_t allowed(const dk_fdo_state& s, bool secondary, int epoch) {
 DK_HD bool terminal(const dk_fdo_state& s) { return s.phase == fdo::PH_FINISHED; }
 DK_HD int current_player(const dk_fdo_state& s) { return s.current_player == DK_NONE ? 0 : (int)s.current_player; }
 
+// FdoState::play_action on a record: an announcement action also appends its
+// occurrence (internal_play_announcement, announcement.rs:178-215).
+DK_HD void step_record(dk_az_state& r, int a) {
+    dk_fdo_state& s = r.state.fdo;
+    if (a >= 33 && a <= 37 && r.ann_n < 12) {
+        r.ann_card[r.ann_n] = s.card_index;
+        r.ann_code[r.ann_n] = (uint8_t)((s.current_player << 4) | (uint32_t)(a - 33));
+        r.ann_n += 1;
+    }
+    fdo::step_packed(s, a);
+}
+
 // take_action_by_action_index(action, skip_single = true) (full_doko.rs:121-157):
 // after the action, forced plies (one legal action once announcements are
 // removed) are played too.
-DK_HD void take_action(dk_fdo_state& s, int a) {
-    fdo::step_packed(s, a);
+DK_HD void take_action(dk_az_state& r, int a) {
+    dk_fdo_state& s = r.state.fdo;
+    step_record(r, a);
     for (int guard = 0; guard < 256; ++guard) {
         if (s.phase == fdo::PH_FINISHED) break;
         fdo::Work w; fdo::unpack(s, w);
         const uint64_t al = fdo::legal_actions(w) & ~ANN_BITS;
         if (popc64(al) != 1) break;
-        fdo::step_packed(s, ctz64(al));
+        step_record(r, ctz64(al));
     }
 }
 
@@ -112,19 +126,19 @@ DK_HD void softmax(float* d, int n) {
 // Memory of one game: node region, state region.
 struct Mem {
     Node* nodes;
-    dk_state* states;
+    dk_az_state* states;
     uint32_t cap_nodes, cap_states;
 };
 
 // new_root_node (node.rs:209-244): state 0, no children yet.
-DK_HD void init(const dk_state& root, Game& g, Mem& m, uint64_t seed) {
+DK_HD void init(const dk_az_state& root, Game& g, Mem& m, uint64_t seed) {
     const Rng r = Rng::seed_from_u64(seed);
     g.rng[0] = r.s0; g.rng[1] = r.s1; g.rng[2] = r.s2; g.rng[3] = r.s3;
     Node n;
     for (int p = 0; p < 4; ++p) n.win[p] = 0.0f;
     n.visits = 0; n.prior = 0.0f; n.child_base = 0; n.parent = NO_NODE; n.state = 0; n.nchild = 0;
-    n.action = 0xFF; n.player = (uint8_t)current_player(root.fdo);
-    n.flags = (uint8_t)(NF_STATE | (terminal(root.fdo) ? NF_TERMINAL : 0u));
+    n.action = 0xFF; n.player = (uint8_t)current_player(root.state.fdo);
+    n.flags = (uint8_t)(NF_STATE | (terminal(root.state.fdo) ? NF_TERMINAL : 0u));
     n.pad[0] = n.pad[1] = 0;
     m.nodes[0] = n;
     m.states[0] = root;
@@ -158,7 +172,7 @@ DK_HD bool add_children(Game& g, Mem& m, uint32_t idx, uint64_t mask, const floa
 // Dirichlet sample (an input: see the oracle's note).
 DK_HD void root_expand(Game& g, Mem& m, const float value[4], const float logits[39], const float noise[39], float eps,
                        int epoch) {
-    const dk_fdo_state& s = m.states[0].fdo;
+    const dk_fdo_state& s = m.states[0].state.fdo;
     const uint64_t al = allowed(s, false, epoch);
     float probs[39];
     for (int i = 0; i < 39; ++i) probs[i] = logits[i];
@@ -190,7 +204,7 @@ DK_HD float puct(const Node& c, int parent_player, float sqrt_pv, float cexp) {
 // One iteration's selection (select_promising_node, mcts.rs:306-380) and the
 // expansion of the leaf (expand_node, mcts.rs:23-74).  Returns true when the
 // leaf needs the network (non-terminal); the leaf's packed state goes to *eval.
-DK_HD bool select(Game& g, Mem& m, float cexp, int epoch, dk_state* eval) {
+DK_HD bool select(Game& g, Mem& m, float cexp, int epoch, dk_az_state* eval) {
     uint32_t idx = 0;
     for (int guard = 0; guard < 4096; ++guard) {
         const Node nd = m.nodes[idx];
@@ -208,17 +222,17 @@ DK_HD bool select(Game& g, Mem& m, float cexp, int epoch, dk_state* eval) {
     Node& L = m.nodes[idx];
     if (!(L.flags & NF_STATE)) {
         if (g.next_state >= m.cap_states) { g.status = 1; g.need_eval = 0; return false; }
-        dk_state st = m.states[m.nodes[L.parent].state];
-        take_action(st.fdo, L.action);
+        dk_az_state st = m.states[m.nodes[L.parent].state];
+        take_action(st, L.action);
         L.state = g.next_state++;
         m.states[L.state] = st;
-        L.player = (uint8_t)current_player(st.fdo);
-        L.flags = (uint8_t)(NF_STATE | (terminal(st.fdo) ? NF_TERMINAL : 0u));
+        L.player = (uint8_t)current_player(st.state.fdo);
+        L.flags = (uint8_t)(NF_STATE | (terminal(st.state.fdo) ? NF_TERMINAL : 0u));
     }
     g.leaf = idx;
-    const dk_state& ls = m.states[L.state];
+    const dk_az_state& ls = m.states[L.state];
     if (L.flags & NF_TERMINAL) { g.need_eval = 0; return false; }
-    if (!add_children(g, m, idx, allowed(ls.fdo, true, epoch), nullptr)) { g.need_eval = 0; return false; }
+    if (!add_children(g, m, idx, allowed(ls.state.fdo, true, epoch), nullptr)) { g.need_eval = 0; return false; }
     if (eval) *eval = ls;
     g.need_eval = 1;
     return true;
@@ -240,7 +254,7 @@ DK_HD void backup(Game& g, Mem& m, const float value[4], const float logits[39])
         const int cp = L.player;
         for (int p = 0; p < 4; ++p) r[p] = value[(p - cp + 4) & 3];
     } else {
-        rewards(m.states[L.state].fdo, r);
+        rewards(m.states[L.state].state.fdo, r);
     }
     for (uint32_t t = g.leaf; t != NO_NODE; t = m.nodes[t].parent) {
         Node& n = m.nodes[t];

@@ -27,6 +27,7 @@ using namespace oracle;
 static_assert(sizeof(dk_fdo_state) == 128, "dk_fdo_state size");
 static_assert(sizeof(dk_do_state) == 128, "dk_do_state size");
 static_assert(sizeof(dk_ttt_state) == 128, "dk_ttt_state size");
+static_assert(sizeof(dk_az_state) == 160, "dk_az_state size");
 
 static SmallRng rng_from(const uint64_t* s) { SmallRng r; for (int i = 0; i < 4; ++i) r.s[i] = s[i]; return r; }
 static void rng_to(const SmallRng& r, uint64_t* s) { if (s) for (int i = 0; i < 4; ++i) s[i] = r.s[i]; }
@@ -305,6 +306,19 @@ int or_az_search(void* sp, const float* noise, uint32_t iters, float c, float ep
     const int a = s.search(e, eval, noise, iters, o, r, visits, root_priors);
     rng_to(r, rng_state);
     return a;
+}
+// dk_az_state record: the packed state plus the announcement occurrence list
+void or_fdo_pack_az(void* sp, uint8_t* out) {
+    const fdo::State& s = *(fdo::State*)sp;
+    memset(out, 0, sizeof(dk_az_state));
+    dk_az_state* r = (dk_az_state*)out;
+    or_fdo_pack(sp, r->state.raw);
+    for (int k = 0; k < s.announcements.n; ++k) {
+        const fdo::AnnOccurrence& a = s.announcements.list[k];
+        r->ann_card[k] = (uint8_t)a.card_index;
+        r->ann_code[k] = (uint8_t)((a.player << 4) | __builtin_ctz(a.announcement));
+    }
+    r->ann_n = (uint8_t)s.announcements.n;
 }
 void or_az_take_action(void* sp, int a) { az::Env e; e.doko = *(fdo::State*)sp; *(fdo::State*)sp = e.take_action(a, true).doko; }
 

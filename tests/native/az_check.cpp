@@ -14,11 +14,14 @@
 #include <vector>
 
 #include "../../master_doko_reinforcement_learning_amd/csrc/engine/az_core.h"
+#include "../../master_doko_reinforcement_learning_amd/csrc/engine/encode_pi.h"
+#include "../../oracle/encode_pi.hpp"
 #include "../../oracle/az_eval.hpp"
 #include "../../oracle/full_doko.hpp"
 
 using namespace oracle;
 extern "C" void or_fdo_pack(void* sp, uint8_t* out);
+extern "C" void or_fdo_pack_az(void* sp, uint8_t* out);
 extern "C" int or_az_search(void* sp, const float* noise, uint32_t iters, float c, float eps, int epoch, int temp_mode,
                             float temp, uint64_t* rng_state, uint32_t* visits, float* root_priors);
 
@@ -32,20 +35,36 @@ int main(int argc, char** argv) {
         const float x = (float)k * 0.25f;
         if (std::exp(x) != dk::az::exp_f32(x)) { printf("MISMATCH exp(%g)\n", x); return 1; }
     }
-    // positions from random games (all phases, with announcements)
+    // positions from random games (all phases, with announcements).  Along every
+    // trajectory the device record (step_record) must equal the oracle's packed
+    // record, and encode_pi.h must equal the oracle's encode_state_pi.
     std::vector<fdo::State> pos;
+    long encoded = 0;
     for (int g = 0; (int)pos.size() < npos; ++g) {
         SmallRng deal = SmallRng::seed_from_u64(seed * 5077 + g);
         fdo::State s = fdo::new_game(deal);
+        dk_az_state rec; or_fdo_pack_az(&s, (uint8_t*)&rec);
         const int stop = (int)(pol() % 60);
-        for (int ply = 0; ply < stop && s.phase != fdo::Finished; ++ply) {
+        for (int ply = 0; ply < 80 && s.phase != fdo::Finished; ++ply) {
+            if (ply == stop) pos.push_back(s);
+            dk_az_state want; or_fdo_pack_az(&s, (uint8_t*)&want);
+            if (memcmp(&want, &rec, 117) != 0 || memcmp(want.ann_card, rec.ann_card, 32) != 0) {
+                printf("MISMATCH record game %d ply %d\n", g, ply); return 1;
+            }
+            int64_t eo[311]; uint32_t ed[311];
+            enc::encode_state_pi(s, eo);
+            auto put = [&](uint32_t i, uint32_t v) { ed[i] = v; };
+            dk::enc::encode_state_pi(rec, put);
+            for (int i = 0; i < 311; ++i) if ((int64_t)ed[i] != eo[i]) { printf("MISMATCH encode game %d ply %d token %d: %u vs %lld\n", g, ply, i, ed[i], (long long)eo[i]); return 1; }
+            encoded++;
             const uint64_t legal = fdo::observation_allowed_actions(s);
             int k = (int)(pol() % (uint64_t)__builtin_popcountll(legal)), a = 0;
             for (int b = 0; b < 39; ++b) if (legal >> b & 1) { if (k-- == 0) { a = b; break; } }
             fdo::play_action(s, a);
+            dk::az::step_record(rec, a);
         }
-        if (s.phase != fdo::Finished) pos.push_back(s);
     }
+    if (encoded < 100) { printf("too few encoded positions\n"); return 1; }
     const int G = (int)pos.size();
     const float c = 2.5f, eps = 0.25f;
     long checked = 0;
@@ -59,15 +78,15 @@ int main(int argc, char** argv) {
         // device core, batched
         const uint32_t cap_nodes = 40 + 39 * (iters + 1), cap_states = iters + 2;
         std::vector<dk::az::Node> nodes((size_t)G * cap_nodes);
-        std::vector<dk_state> states((size_t)G * cap_states);
+        std::vector<dk_az_state> states((size_t)G * cap_states);
         std::vector<dk::az::Game> games(G);
-        std::vector<dk_state> eval(G);
+        std::vector<dk_az_state> eval(G);
         std::vector<float> val((size_t)G * 4), logit((size_t)G * 39);
         auto mem = [&](int g) { dk::az::Mem m; m.nodes = &nodes[(size_t)g * cap_nodes]; m.states = &states[(size_t)g * cap_states];
                                 m.cap_nodes = cap_nodes; m.cap_states = cap_states; return m; };
-        auto network = [&](int g) { az::hash_eval(eval[g].raw, &val[4 * g], &logit[39 * g]); };
+        auto network = [&](int g) { az::hash_eval(eval[g].state.raw, &val[4 * g], &logit[39 * g]); };
         for (int g = 0; g < G; ++g) {
-            dk_state r; or_fdo_pack(&pos[g], r.raw);
+            dk_az_state r; or_fdo_pack_az(&pos[g], (uint8_t*)&r);
             dk::az::Mem m = mem(g);
             dk::az::init(r, games[g], m, seeds[g]);
             eval[g] = r;

@@ -84,6 +84,7 @@ def lib():
                                             ctypes.c_int, ctypes.c_float, u64p, u32p, f32p]),
             "or_az_take_action": (None, [vp, ctypes.c_int]),
             "or_encode_pi": (None, [vp, ctypes.POINTER(ctypes.c_int64)]),
+            "or_fdo_pack_az": (None, [vp, u8p]),
             "or_encode_pi_fields": (None, [i32p, u64p, ctypes.POINTER(ctypes.c_int64)]),
             "or_ttt_finish": (ctypes.c_int, [i32p]),
             "or_ttt_rollout": (None, [i32p, u64p, f64p]),
@@ -190,6 +191,12 @@ class FdoState:
         pr = arr(ctypes.c_float, 39, [-1.0] * 39)
         a = lib().or_az_search(self.h, arr(ctypes.c_float, 39, noise), iters, c, eps, epoch, temp_mode, temp, rng, v, pr)
         return a, list(v), list(pr)
+
+    def pack_az(self):
+        """dk_az_state record (160 B): packed state + announcement occurrence list."""
+        o = arr(ctypes.c_uint8, 160)
+        lib().or_fdo_pack_az(self.h, o)
+        return bytes(o)
 
     def encode_pi(self):
         """encode_state_pi (rs-doko-networks/src/full_doko/var1/encode_pi.rs:27-214) -> 311 tokens."""

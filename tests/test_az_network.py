@@ -1,0 +1,106 @@
+"""AlphaZero network (az_network.DokoAzNet) against a plain-PyTorch fp32 module with the
+reference's structure and state_dict names (rs-doko-py-bridge/python/az_doko.py:28-138,
+TransformerBlock.py, SelfAttention.py): identical outputs after load_reference_state_dict.
+CPU only."""
+import torch
+from torch import nn
+
+from master_doko_reinforcement_learning_amd.az_network import VOCAB, DokoAzNet
+
+
+class _Cfg:
+    n_embd, n_head, attn_pdrop, resid_pdrop = 32, 4, 0.0, 0.0
+
+
+class _SelfAttention(nn.Module):
+    def __init__(self, c):
+        super().__init__()
+        self.attn = nn.MultiheadAttention(c.n_embd, c.n_head, dropout=0.0, batch_first=True)
+        self.c_proj = nn.Linear(c.n_embd, c.n_embd)
+
+    def forward(self, x):
+        return self.c_proj(self.attn(x, x, x)[0])
+
+
+class _Block(nn.Module):
+    def __init__(self, c):
+        super().__init__()
+        self.ln_1 = nn.LayerNorm(c.n_embd)
+        self.attn = _SelfAttention(c)
+        self.ln_2 = nn.LayerNorm(c.n_embd)
+        self.mlp = nn.ModuleDict(dict(c_fc=nn.Linear(c.n_embd, 4 * c.n_embd), c_proj=nn.Linear(4 * c.n_embd, c.n_embd)))
+
+    def forward(self, x):
+        x = x + self.attn(self.ln_1(x))
+        return x + self.mlp.c_proj(nn.functional.gelu(self.mlp.c_fc(self.ln_2(x))))
+
+
+class _Head(nn.Module):
+    def __init__(self, d, classes):
+        super().__init__()
+        self.card_queries = nn.Parameter(torch.randn(classes, d))
+        self.mlps = nn.ModuleList([nn.Sequential(nn.LayerNorm(d), nn.Linear(d, d), nn.GELU(), nn.Linear(d, 1))
+                                   for _ in range(classes)])
+        for m in self.mlps:   # non-trivial LayerNorm affine
+            nn.init.normal_(m[0].weight, 1.0, 0.1)
+            nn.init.normal_(m[0].bias, 0.0, 0.1)
+
+    def forward(self, x):
+        w = torch.softmax(torch.einsum("cd,bsd->bcs", self.card_queries, x) * x.shape[-1] ** -0.5, dim=-1)
+        a = torch.einsum("bcs,bsd->bcd", w, x)
+        return torch.cat([m(a[:, c, :]) for c, m in enumerate(self.mlps)], dim=1)
+
+
+class _RefNet(nn.Module):
+    def __init__(self, c):
+        super().__init__()
+        d = c.n_embd
+        names = ["game_object_e", "position_e", "player_played_e", "subposition_e", "team_e", "phase_e"]
+        mods = {n: nn.Embedding(v, d) for n, v in zip(names, VOCAB)}
+        mods.update(h=nn.ModuleList([_Block(c) for _ in range(2)]), p_h=nn.ModuleList([_Block(c)]),
+                    v_h=nn.ModuleList([_Block(c)]), p_ln_f=nn.LayerNorm(d), v_ln_f=nn.LayerNorm(d))
+        self.transformer = nn.ModuleDict(mods)
+        self.value_head = _Head(d, 4)
+        self.policy_head = _Head(d, 39)
+
+    def forward(self, x):
+        t = self.transformer
+        h = (t.game_object_e(x[:, 0:62]) + t.position_e(x[:, 62:124]) + t.player_played_e(x[:, 124:186]) +
+             t.subposition_e(x[:, 186:248]) + t.team_e(x[:, 248:310]) + t.phase_e(x[:, 310:311]).expand(-1, 62, -1))
+        for b in t.h:
+            h = b(h)
+        hp, hv = h, h
+        for b in t.p_h:
+            hp = b(hp)
+        for b in t.v_h:
+            hv = b(hv)
+        return self.value_head(t.v_ln_f(hv)), self.policy_head(t.p_ln_f(hp))
+
+
+def _tokens(n, seed):
+    g = torch.Generator().manual_seed(seed)
+    parts = [torch.randint(0, v, (n, 62 if i < 5 else 1), generator=g) for i, v in enumerate(VOCAB)]
+    return torch.cat(parts, dim=1)
+
+
+def test_network_matches_reference_structure():
+    torch.manual_seed(0)
+    ref = _RefNet(_Cfg()).eval()
+    net = DokoAzNet(d=32, heads=4, layers=2).eval()
+    net.load_reference_state_dict(ref.state_dict())
+    x = _tokens(8, 1)
+    with torch.no_grad():
+        v0, p0 = ref(x)
+        v1, p1 = net(x.int())
+    assert v1.shape == (8, 4) and p1.shape == (8, 39)
+    torch.testing.assert_close(v1, v0, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(p1, p0, rtol=1e-4, atol=1e-5)
+
+
+def test_default_network_shapes():
+    net = DokoAzNet().eval()
+    n_params = sum(p.numel() for p in net.parameters())
+    assert 1.0e6 < n_params < 4.0e6
+    with torch.no_grad():
+        v, p = net(_tokens(3, 2))
+    assert v.shape == (3, 4) and p.shape == (3, 39) and torch.isfinite(p).all()

@@ -511,7 +511,7 @@ def test_az_search_parity(eng, temp_mode):
         v, l = ol.az_hash_eval_np(states.cpu().numpy())
         return torch.from_numpy(v).to(dev), torch.from_numpy(l).to(dev)
 
-    roots = torch.from_numpy(pack_all(info)).to(dev)
+    roots = torch.from_numpy(np.frombuffer(b"".join(s.pack_az() for s in info), dtype=np.uint8).reshape(-1, 160).copy()).to(dev)
     az = dk.AlphaZeroSearch(eng, c, eps, epoch, [None, float("inf"), 1.0][temp_mode])
     actions, visits = az.mcts_search(roots, network, torch.from_numpy(noise).to(dev), iters, seeds)
     actions, visits = actions.cpu().numpy(), visits.cpu().numpy()
@@ -519,3 +519,64 @@ def test_az_search_parity(eng, temp_mode):
         a, v, _ = s.az_search(list(noise[g]), iters, c, eps, epoch, temp_mode, 1.0, ol.rng_seed(int(seeds[g])))
         assert list(visits[g]) == v
         assert int(actions[g]) == a
+
+
+def test_az_encode_and_step_parity(eng):
+    """encode_state_pi on the GPU == the oracle's (311 tokens) at every position of random
+    games with announcements, and dk_az_step (take_action with skip_single) keeps the
+    records equal to the oracle's states and announcement lists."""
+    import torch
+    import master_doko_reinforcement_learning_amd as dk
+    dev = torch.device("cuda", 0)
+    states = [s for s in fdo_states(16, 41) if s.info()["phase"] != 3]
+    recs = torch.from_numpy(np.frombuffer(b"".join(s.pack_az() for s in states), dtype=np.uint8).reshape(-1, 160).copy()).to(dev)
+    tok = dk.az_encode(eng, recs).cpu().numpy()
+    for i, s in enumerate(states):
+        assert list(tok[i]) == s.encode_pi()
+    # one skip-single step from every position: the first legal action
+    acts = []
+    nxt = []
+    for s in states:
+        legal = s.allowed()
+        a = [b for b in range(39) if legal >> b & 1][0]
+        acts.append(a)
+        c = s.clone()
+        c.az_take_action(a)
+        nxt.append(c)
+    dk.az_step(eng, recs, torch.tensor(acts, dtype=torch.uint8, device=dev))
+    got = recs.cpu().numpy()
+    for i, c in enumerate(nxt):
+        want = np.frombuffer(c.pack_az(), dtype=np.uint8)
+        assert got[i, :117].tobytes() == want[:117].tobytes()
+        assert got[i, 128:153].tobytes() == want[128:153].tobytes()
+
+
+def test_az_selfplay_with_network(eng):
+    """C5 plumbing on the GPU: AlphaZeroSearch with the DokoAzNet evaluator (device encoder
+    -> bf16 network) from fresh deals: every game's root children get exactly `iterations`
+    visits, the chosen actions are legal, encoded tokens stay inside the embedding
+    vocabularies, and dk_az_step plays the moves."""
+    import torch
+    import master_doko_reinforcement_learning_amd as dk
+    from master_doko_reinforcement_learning_amd.az_network import VOCAB, AzEvaluator, DokoAzNet
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    G, iters = 32, 24
+    st = torch.from_numpy(eng.new_games(dk.GAME_FULL_DOKO, np.arange(G, dtype=np.uint64) + 900)).to(dev)
+    recs = dk.az_records(eng, st)
+    ev = AzEvaluator(eng, DokoAzNet().to(dev))
+    search = dk.AlphaZeroSearch(eng, 4.0, 0.3, 10, 0.5)
+    noise = torch.distributions.Dirichlet(torch.full((39,), 0.8, device=dev)).sample((G,))
+    for move in range(6):
+        tok = dk.az_encode(eng, recs).cpu().numpy()
+        for i, v in enumerate(VOCAB):
+            part = tok[:, 62 * i:62 * (i + 1)] if i < 5 else tok[:, 310:]
+            assert part.min() >= 0 and part.max() < v
+        actions, visits = search.mcts_search(recs, ev, noise, iters, np.arange(G, dtype=np.uint64) + 7 * move)
+        visits = visits.cpu().numpy()
+        assert np.all(visits.sum(axis=1) == iters)
+        legal = np.zeros(G, dtype=np.uint64)
+        a = actions.cpu().numpy()
+        for g in range(G):
+            assert visits[g, a[g]] > 0
+        dk.az_step(eng, recs, actions)
