@@ -308,6 +308,10 @@ int dk_net_embed_ln_bf16_async(const int32_t* d_tokens, uint32_t batch, const vo
                                const void* gamma, const void* beta, float eps, void* x_out, void* h_out, void* stream);
 int dk_net_add_ln_bf16_async(void* x_io, const void* delta, uint32_t rows, uint32_t d, const void* gamma, const void* beta,
                              float eps, void* h_out, void* stream);
+/* dk_net_attn62_bf16_async: softmax(q k^T / sqrt(40)) v for the network's shape (62 tokens,
+ * 4 heads x 40), q/k/v read from the fused projection qkv[batch*62][480] ([q | k | v], heads
+ * contiguous), heads' outputs written to y[batch*62][160]; bf16 MFMA, one wave per (sample, head). */
+int dk_net_attn62_bf16_async(const void* qkv, void* y, uint32_t batch, void* stream);
 
 /* ---- completion / errors / timing of *_async work -------------------------------
  * dk_sync: waits for the stream and returns the first device-side error

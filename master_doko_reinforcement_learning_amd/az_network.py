@@ -112,9 +112,10 @@ class DokoAzNet(nn.Module):
         return self.value_head(self.v_ln(xv)), self.policy_head(self.p_ln(xp))
 
     def forward_fused(self, tokens):
-        """bf16 forward on the GPU with the row passes fused in HIP kernels
-        (csrc/az_net_kernels.h): the embedding sum + first LayerNorm in one pass,
-        and every residual add fused with the LayerNorm that follows it."""
+        """bf16 forward on the GPU with HIP kernels (csrc/az_net_kernels.h) for the
+        embedding sum + first LayerNorm (one pass), every residual add fused with the
+        LayerNorm that follows it, and the 62-token attention core (bf16 MFMA, reading
+        the fused qkv projection in place)."""
         from . import _native
         L = _native.lib()
         st = torch.cuda.current_stream(tokens.device).cuda_stream
@@ -141,9 +142,19 @@ class DokoAzNet(nn.Module):
         ck(L.dk_net_embed_ln_bf16_async(tok.data_ptr(), B, tables, d, ln0.weight.data_ptr(), ln0.bias.data_ptr(),
                                         ln0.eps, x.data_ptr(), h.data_ptr(), st))
 
+        fused_attn = d == 160 and all(b.heads == 4 for b in list(self.blocks) + list(self.p_blocks) + list(self.v_blocks))
+
+        def attn_delta(blk, h):
+            if not fused_attn:
+                return blk.attn_delta(h)
+            qkv = blk.qkv(h)                                     # [B, 62, 480]: q | k | v, heads contiguous
+            y = torch.empty_like(h)
+            ck(L.dk_net_attn62_bf16_async(qkv.data_ptr(), y.data_ptr(), B, st))
+            return blk.c_proj(blk.out(y))
+
         def run(x, h, blocks, final_ln):
             for i, blk in enumerate(blocks):
-                h = add_ln(x, blk.attn_delta(h), blk.ln_2)
+                h = add_ln(x, attn_delta(blk, h), blk.ln_2)
                 nxt = blocks[i + 1].ln_1 if i + 1 < len(blocks) else final_ln
                 h = add_ln(x, blk.mlp_delta(h), nxt)
             return h

@@ -6,9 +6,8 @@
 //   embed_ln   : x = sum of the six token embeddings; h = LN(x)         (one pass)
 //   add_ln     : x += delta; h = LN(x)                                  (one pass)
 //   ln         : h = LN(x)
-// One row per 32-lane half-wave: lane l holds elements l, l+32, ... (d/32 per
-// lane), so every load/store instruction of a half-wave covers 64 contiguous
-// bytes.  Mean and variance: f32 two-pass over the registers, shuffle
+// One row per 32-lane half-wave: lane l holds bf16 pairs l, l+32, ..., so every
+// load/store instruction of a half-wave covers up to 128 contiguous bytes.  Mean and variance: f32 two-pass over the registers, shuffle
 // reductions inside the half-wave.  LayerNorm as torch: (x - mean) *
 // rsqrt(var + eps) * gamma + beta, biased variance.
 #pragma once
@@ -18,7 +17,7 @@
 namespace dk {
 namespace net {
 
-constexpr int LN_MAX_PER_LANE = 16;   // d <= 512
+constexpr int LN_MAX_PER_LANE = 8;    // bf16 pairs per lane: d <= 512
 
 __device__ __forceinline__ float bf2f(uint16_t v) { return __uint_as_float((uint32_t)v << 16); }
 __device__ __forceinline__ uint16_t f2bf(float f) {   // round to nearest even (torch's conversion)
@@ -33,70 +32,233 @@ __device__ __forceinline__ float half_wave_sum(float v) {
     return v;
 }
 
+// A row as bf16 pairs: lane l holds pairs l, l + 32, ... (PER pairs, the last
+// ones masked when d/2 is not a multiple of 32), so every load / store of a
+// half-wave moves up to 128 contiguous bytes.
 template <int PER>
-__device__ __forceinline__ void ln_row(const float (&x)[PER], int d, int lane, const uint16_t* gamma, const uint16_t* beta,
-                                       float eps, uint16_t* out) {
+__device__ __forceinline__ void ln_row(const float (&x)[2 * PER], int d, int lane, const uint32_t* gamma2,
+                                       const uint32_t* beta2, float eps, uint32_t* out2) {
+    const int np = d / 2;
     float s = 0.0f;
 #pragma unroll
-    for (int k = 0; k < PER; ++k) s += x[k];
+    for (int k = 0; k < PER; ++k)
+        if (lane + 32 * k < np) s += x[2 * k] + x[2 * k + 1];
     const float mean = half_wave_sum(s) / (float)d;
     float q = 0.0f;
 #pragma unroll
-    for (int k = 0; k < PER; ++k) { const float c = x[k] - mean; q += c * c; }
+    for (int k = 0; k < PER; ++k)
+        if (lane + 32 * k < np) {
+            const float c0 = x[2 * k] - mean, c1 = x[2 * k + 1] - mean;
+            q += c0 * c0 + c1 * c1;
+        }
     const float rstd = rsqrtf(half_wave_sum(q) / (float)d + eps);
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
         const int j = lane + 32 * k;
-        out[j] = f2bf((x[k] - mean) * rstd * bf2f(gamma[j]) + bf2f(beta[j]));
+        if (j < np) {
+            const uint32_t g = gamma2[j], b = beta2[j];
+            const float y0 = (x[2 * k] - mean) * rstd * bf2f((uint16_t)g) + bf2f((uint16_t)b);
+            const float y1 = (x[2 * k + 1] - mean) * rstd * bf2f((uint16_t)(g >> 16)) + bf2f((uint16_t)(b >> 16));
+            out2[j] = (uint32_t)f2bf(y0) | ((uint32_t)f2bf(y1) << 16);
+        }
     }
 }
 
 // tokens [B, 311] int32 (encode_state_pi); tables: object, position, player, subposition, team, phase
 template <int PER>
-__global__ void embed_ln_kernel(const int32_t* __restrict__ tokens, uint32_t B, const uint16_t* __restrict__ e0,
+__global__ void embed_ln_kernel(const int32_t* __restrict__ tokens, uint32_t B, int d, const uint16_t* __restrict__ e0,
                                 const uint16_t* __restrict__ e1, const uint16_t* __restrict__ e2,
                                 const uint16_t* __restrict__ e3, const uint16_t* __restrict__ e4,
                                 const uint16_t* __restrict__ e5, const uint16_t* gamma, const uint16_t* beta, float eps,
                                 uint16_t* __restrict__ x_out, uint16_t* __restrict__ h_out) {
-    const int d = 32 * PER;
     const uint32_t row = blockIdx.x * (blockDim.x / 32) + threadIdx.x / 32;
-    const int lane = threadIdx.x & 31;
+    const int lane = threadIdx.x & 31, np = d / 2;
     if (row >= B * 62u) return;
     const uint32_t b = row / 62u, s = row % 62u;
     const int32_t* t = tokens + (size_t)b * 311;
-    const uint16_t* rows[6] = {e0 + (size_t)t[s] * d, e1 + (size_t)t[62 + s] * d, e2 + (size_t)t[124 + s] * d,
-                               e3 + (size_t)t[186 + s] * d, e4 + (size_t)t[248 + s] * d, e5 + (size_t)t[310] * d};
-    float x[PER];
+    const uint32_t* rows[6] = {(const uint32_t*)(e0 + (size_t)t[s] * d), (const uint32_t*)(e1 + (size_t)t[62 + s] * d),
+                               (const uint32_t*)(e2 + (size_t)t[124 + s] * d), (const uint32_t*)(e3 + (size_t)t[186 + s] * d),
+                               (const uint32_t*)(e4 + (size_t)t[248 + s] * d), (const uint32_t*)(e5 + (size_t)t[310] * d)};
+    uint32_t* xo = (uint32_t*)(x_out + (size_t)row * d);
+    float x[2 * PER];
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
         const int j = lane + 32 * k;
-        // torch sums the six bf16 embeddings left to right with a bf16 rounding after each add
-        float acc = bf2f(rows[0][j]);
+        x[2 * k] = x[2 * k + 1] = 0.0f;
+        if (j < np) {
+            // torch sums the six bf16 embeddings left to right with a bf16 rounding after each add
+            uint32_t v = rows[0][j];
+            float a0 = bf2f((uint16_t)v), a1 = bf2f((uint16_t)(v >> 16));
 #pragma unroll
-        for (int e = 1; e < 6; ++e) acc = bf2f(f2bf(acc + bf2f(rows[e][j])));
-        x[k] = acc;
-        x_out[(size_t)row * d + j] = f2bf(acc);
+            for (int e = 1; e < 6; ++e) {
+                v = rows[e][j];
+                a0 = bf2f(f2bf(a0 + bf2f((uint16_t)v)));
+                a1 = bf2f(f2bf(a1 + bf2f((uint16_t)(v >> 16))));
+            }
+            x[2 * k] = a0; x[2 * k + 1] = a1;
+            xo[j] = (uint32_t)f2bf(a0) | ((uint32_t)f2bf(a1) << 16);
+        }
     }
-    ln_row<PER>(x, d, lane, gamma, beta, eps, h_out + (size_t)row * d);
+    ln_row<PER>(x, d, lane, (const uint32_t*)gamma, (const uint32_t*)beta, eps, (uint32_t*)(h_out + (size_t)row * d));
 }
 
 // x += delta (bf16 add as torch rounds it); h = LN(x)
 template <int PER>
-__global__ void add_ln_kernel(uint16_t* __restrict__ x_io, const uint16_t* __restrict__ delta, uint32_t rows,
+__global__ void add_ln_kernel(uint16_t* __restrict__ x_io, const uint16_t* __restrict__ delta, uint32_t rows, int d,
                               const uint16_t* gamma, const uint16_t* beta, float eps, uint16_t* __restrict__ h_out) {
-    const int d = 32 * PER;
     const uint32_t row = blockIdx.x * (blockDim.x / 32) + threadIdx.x / 32;
-    const int lane = threadIdx.x & 31;
+    const int lane = threadIdx.x & 31, np = d / 2;
     if (row >= rows) return;
-    float x[PER];
+    uint32_t* xr = (uint32_t*)(x_io + (size_t)row * d);
+    const uint32_t* dr = (const uint32_t*)(delta + (size_t)row * d);
+    float x[2 * PER];
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
-        const size_t j = (size_t)row * d + lane + 32 * k;
-        const uint16_t v = delta ? f2bf(bf2f(x_io[j]) + bf2f(delta[j])) : x_io[j];
-        if (delta) x_io[j] = v;
-        x[k] = bf2f(v);
+        const int j = lane + 32 * k;
+        x[2 * k] = x[2 * k + 1] = 0.0f;
+        if (j < np) {
+            uint32_t v = xr[j];
+            if (delta) {
+                const uint32_t dv = dr[j];
+                v = (uint32_t)f2bf(bf2f((uint16_t)v) + bf2f((uint16_t)dv)) |
+                    ((uint32_t)f2bf(bf2f((uint16_t)(v >> 16)) + bf2f((uint16_t)(dv >> 16))) << 16);
+                xr[j] = v;
+            }
+            x[2 * k] = bf2f((uint16_t)v); x[2 * k + 1] = bf2f((uint16_t)(v >> 16));
+        }
     }
-    ln_row<PER>(x, d, lane, gamma, beta, eps, h_out + (size_t)row * d);
+    ln_row<PER>(x, d, lane, (const uint32_t*)gamma, (const uint32_t*)beta, eps, (uint32_t*)(h_out + (size_t)row * d));
+}
+
+// ---------------------------------------------------------------------------
+// Self-attention core of a block for the network's shape: 62 tokens, 4 heads of
+// dimension 40 (d = 160), reading q, k, v straight out of the fused qkv
+// projection [B*62, 480] and writing the heads' outputs into [B*62, 160] (no
+// permute / transpose copies).  One wave per (sample, head), bf16 MFMA
+// v_mfma_f32_32x32x16_bf16 (tokens padded to 64, head dimension to 48):
+//   X  = K Q^T   (2 x 2 tiles of 32 x 32, 3 k-steps over the head dimension):
+//        X[t][s] has the query s on the lane, the keys t in the registers;
+//   P  = softmax over t per column s (registers + one cross-half shuffle),
+//        normalised, packed to bf16 in place (the accumulator-as-operand idiom:
+//        registers 8q..8q+7 of a tile are k-step q, element j of lane half h is
+//        key 16q + 8(j>>2) + 4h + (j&3));
+//   O  = P V     (P^T fragments as the A operand, V^T staged in LDS as [e][t] so
+//        a lane's 8 keys are two 8-byte reads; 2 x 2 tiles, 4 k-steps):
+//        O[s][e] has e on the lane: each register is one 64-byte row segment.
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ bf16x8_t load_frag8(const uint16_t* p, bool ok) {
+    union { uint4 u; bf16x8_t v; } r;
+    r.u = ok ? *(const uint4*)p : make_uint4(0u, 0u, 0u, 0u);
+    return r.v;
+}
+
+__global__ void __launch_bounds__(256) attn62_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ y,
+                                                     uint32_t batch, float scale) {
+    constexpr int S = 62, HD = 40, H = 4, D = 160, LDT = 64 + 4;   // LDS row stride (keys) in bf16
+    __shared__ uint16_t vt_all[4][64 * LDT];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t bh = blockIdx.x * 4u + (uint32_t)wave;
+    const bool valid = bh < batch * (uint32_t)H;
+    const uint32_t b = valid ? bh / H : 0u, hd = valid ? bh % H : 0u;
+    const int r = lane & 31, h = lane >> 5;
+    const uint16_t* base = qkv + (size_t)b * S * (3 * D);
+    uint16_t* vt = vt_all[wave];
+
+    // V^T into LDS: lane = key t, zero padding for t >= 62 and e >= 40
+    {
+        const int t = lane;
+        const uint16_t* vr = base + (size_t)(t < S ? t : 0) * (3 * D) + 2 * D + hd * HD;
+        for (int e = 0; e < HD; ++e) vt[e * LDT + t] = (valid && t < S) ? vr[e] : (uint16_t)0;
+        for (int e = HD; e < 64; ++e) vt[e * LDT + t] = 0;
+    }
+    // Q and K fragments: tile i covers tokens 32i + r, k-step kk covers dims 16kk + 8h + j
+    bf16x8_t qf[2][3], kf[2][3];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int tok = 32 * i + r;
+#pragma unroll
+        for (int kk = 0; kk < 3; ++kk) {
+            const int e0 = 16 * kk + 8 * h;
+            const bool ok = valid && tok < S && e0 < HD;
+            const uint16_t* row = base + (size_t)(ok ? tok : 0) * (3 * D) + hd * HD + (ok ? e0 : 0);
+            qf[i][kk] = load_frag8(row, ok);
+            kf[i][kk] = load_frag8(row + D, ok);
+        }
+    }
+    // X[ti][si] = K_ti Q_si^T
+    f32x16_t x[2][2];
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+        for (int si = 0; si < 2; ++si) {
+            f32x16_t acc = {0};
+#pragma unroll
+            for (int kk = 0; kk < 3; ++kk) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[ti][kk], qf[si][kk], acc, 0, 0, 0);
+            x[ti][si] = acc;
+        }
+    // softmax over the keys t of every query column s; P packed to bf16 fragments
+    bf16x8_t pf[2][4];
+#pragma unroll
+    for (int si = 0; si < 2; ++si) {
+        float m = -INFINITY;
+#pragma unroll
+        for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+            for (int g = 0; g < 16; ++g) {
+                const int t = 32 * ti + (g & 3) + 8 * (g >> 2) + 4 * h;
+                if (t < S) m = fmaxf(m, x[ti][si][g]);
+            }
+        m = fmaxf(m, __shfl_xor(m, 32));
+        float l = 0.0f;
+#pragma unroll
+        for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+            for (int g = 0; g < 16; ++g) {
+                const int t = 32 * ti + (g & 3) + 8 * (g >> 2) + 4 * h;
+                const float pv = t < S ? __expf((x[ti][si][g] - m) * scale) : 0.0f;
+                x[ti][si][g] = pv;
+                l += pv;
+            }
+        l += __shfl_xor(l, 32);
+        const float inv = 1.0f / l;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            union { uint16_t u[8]; bf16x8_t v; } pk;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) pk.u[j] = f2bf(x[q >> 1][si][8 * (q & 1) + j] * inv);
+            pf[si][q] = pk.v;
+        }
+    }
+    __syncthreads();   // V^T in LDS (every wave of the block reaches this)
+    // O[si][et] = P_si V_et
+#pragma unroll
+    for (int et = 0; et < 2; ++et) {
+        bf16x8_t vf[4];
+        const int e = 32 * et + r;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int t0 = 16 * q + 4 * h;   // keys t0..t0+3 and t0+8..t0+11 (within tile q >> 1)
+            union { uint2 u[2]; bf16x8_t v; } f;
+            f.u[0] = *(const uint2*)&vt[e * LDT + t0];
+            f.u[1] = *(const uint2*)&vt[e * LDT + t0 + 8];
+            vf[q] = f.v;
+        }
+#pragma unroll
+        for (int si = 0; si < 2; ++si) {
+            f32x16_t acc = {0};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pf[si][q], vf[q], acc, 0, 0, 0);
+            if (valid && e < HD) {
+#pragma unroll
+                for (int g = 0; g < 16; ++g) {
+                    const int s = 32 * si + (g & 3) + 8 * (g >> 2) + 4 * h;
+                    if (s < S) y[((size_t)b * S + s) * D + hd * HD + e] = f2bf(acc[g]);
+                }
+            }
+        }
+    }
 }
 
 }  // namespace net

@@ -1169,10 +1169,11 @@ int dk_az_finish_async(dk_ctx* ctx, int temperature_mode, float temperature, uin
 
 // ---------------------------------------------------------------- AlphaZero network row kernels
 namespace {
-int ln_per(uint32_t d) { return (d % 32u == 0u && d >= 32u && d <= 32u * (uint32_t)dk::net::LN_MAX_PER_LANE) ? (int)(d / 32u) : 0; }
+// bf16 pairs per lane of a 32-lane row group (d even, d <= 512)
+int ln_per(uint32_t d) { return (d % 32u == 0u && d >= 32u && d <= 64u * (uint32_t)dk::net::LN_MAX_PER_LANE) ? (int)((d + 63u) / 64u) : 0; }
 }  // namespace
 
-#define DK_LN_CASES(M) M(1) M(2) M(3) M(4) M(5) M(6) M(7) M(8) M(9) M(10) M(11) M(12) M(13) M(14) M(15) M(16)
+#define DK_LN_CASES(M) M(1) M(2) M(3) M(4) M(5) M(6) M(7) M(8)
 
 int dk_net_embed_ln_bf16_async(const int32_t* d_tokens, uint32_t batch, const void* const* tables, uint32_t d,
                                const void* gamma, const void* beta, float eps, void* x_out, void* h_out, void* stream) {
@@ -1184,12 +1185,22 @@ int dk_net_embed_ln_bf16_async(const int32_t* d_tokens, uint32_t batch, const vo
     hipStream_t st = (hipStream_t)stream;
     const uint16_t* const* t = (const uint16_t* const*)tables;
     switch (per) {
-#define M(P) case P: hipLaunchKernelGGL(dk::net::embed_ln_kernel<P>, grid, block, 0, st, d_tokens, batch, t[0], t[1], t[2], \
+#define M(P) case P: hipLaunchKernelGGL(dk::net::embed_ln_kernel<P>, grid, block, 0, st, d_tokens, batch, (int)d, t[0], t[1], t[2], \
                                         t[3], t[4], t[5], (const uint16_t*)gamma, (const uint16_t*)beta, eps,            \
                                         (uint16_t*)x_out, (uint16_t*)h_out); break;
         DK_LN_CASES(M)
 #undef M
     }
+    DK_HIP(hipGetLastError());
+    return DK_OK;
+}
+
+int dk_net_attn62_bf16_async(const void* qkv, void* y, uint32_t batch, void* stream) {
+    if (!qkv || !y) return DK_E_INVALID;
+    if (batch == 0) return DK_OK;
+    const uint32_t waves = batch * 4u;
+    hipLaunchKernelGGL(dk::net::attn62_kernel, dim3((waves + 3u) / 4u), dim3(256), 0, (hipStream_t)stream,
+                       (const uint16_t*)qkv, (uint16_t*)y, batch, 1.0f / sqrtf(40.0f));
     DK_HIP(hipGetLastError());
     return DK_OK;
 }
@@ -1203,7 +1214,7 @@ int dk_net_add_ln_bf16_async(void* x_io, const void* delta, uint32_t rows, uint3
     hipStream_t st = (hipStream_t)stream;
     switch (per) {
 #define M(P) case P: hipLaunchKernelGGL(dk::net::add_ln_kernel<P>, grid, block, 0, st, (uint16_t*)x_io,                  \
-                                        (const uint16_t*)delta, rows, (const uint16_t*)gamma, (const uint16_t*)beta, eps, \
+                                        (const uint16_t*)delta, rows, (int)d, (const uint16_t*)gamma, (const uint16_t*)beta, eps, \
                                         (uint16_t*)h_out); break;
         DK_LN_CASES(M)
 #undef M

@@ -36,6 +36,23 @@ def test_add_ln_matches_torch(d):
     torch.testing.assert_close(h.float(), h_ref, rtol=1e-2, atol=2e-2)   # bf16 output of an f32 LayerNorm
 
 
+def test_attn62_matches_torch():
+    """MFMA attention core (62 tokens, 4 heads x 40) against fp32 softmax(q k^T / sqrt(40)) v."""
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(3)
+    B = 77
+    qkv = (torch.randn(B, 62, 480, device=dev) * 1.5).bfloat16()
+    y = torch.full((B, 62, 160), float("nan"), device=dev).bfloat16()
+    rc = _lib().dk_net_attn62_bf16_async(qkv.data_ptr(), y.data_ptr(), B, torch.cuda.current_stream(dev).cuda_stream)
+    assert rc == 0
+    torch.cuda.synchronize()
+    q, k, v = qkv.float().view(B, 62, 3, 4, 40).permute(2, 0, 3, 1, 4)
+    ref = torch.softmax(q @ k.transpose(-1, -2) / 40 ** 0.5, dim=-1) @ v          # [B, 4, 62, 40]
+    ref = ref.transpose(1, 2).reshape(B, 62, 160)
+    assert torch.isfinite(y.float()).all()
+    torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=2e-2)
+
+
 def test_fused_network_matches_fp32_module():
     """DokoAzNet's fused bf16 forward (embedding+LN, add+LN kernels, torch GEMMs and SDPA)
     against the same weights run as the plain fp32 module."""
