@@ -20,10 +20,11 @@ namespace net {
 constexpr int LN_MAX_PER_LANE = 8;    // bf16 pairs per lane: d <= 512
 
 __device__ __forceinline__ float bf2f(uint16_t v) { return __uint_as_float((uint32_t)v << 16); }
-__device__ __forceinline__ uint16_t f2bf(float f) {   // round to nearest even (torch's conversion)
+__device__ __forceinline__ uint16_t f2bf(float f) {   // round to nearest even (torch's conversion), branch-free
     const uint32_t u = __float_as_uint(f);
-    if ((u & 0x7F800000u) == 0x7F800000u && (u & 0x7FFFFFu)) return (uint16_t)((u >> 16) | 0x40u);   // NaN
-    return (uint16_t)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+    const uint32_t rne = (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
+    const uint32_t nan = (u >> 16) | 0x40u;
+    return (uint16_t)(((u & 0x7FFFFFFFu) > 0x7F800000u) ? nan : rne);
 }
 
 __device__ __forceinline__ float half_wave_sum(float v) {
