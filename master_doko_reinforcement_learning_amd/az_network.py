@@ -52,6 +52,20 @@ class Block(nn.Module):
         y = F.scaled_dot_product_attention(q, k, v).transpose(1, 2).reshape(b, s, d)
         return self.c_proj(self.out(y))
 
+    def folded_proj(self):
+        """c_proj(out(y)) = (Wc Wo) y + (Wc bo + bc): the two back-to-back projections of
+        the reference's SelfAttention (MultiheadAttention.out_proj, then c_proj) folded
+        into one GEMM for inference (products in f32, cached until the weights change)."""
+        key = (self.out.weight.data_ptr(), self.c_proj.weight.data_ptr(), self.out.weight._version,
+               self.c_proj.weight._version, self.out.weight.dtype)
+        if getattr(self, "_fold_key", None) != key:
+            wo, bo = self.out.weight.float(), self.out.bias.float()
+            wc, bc = self.c_proj.weight.float(), self.c_proj.bias.float()
+            dt = self.out.weight.dtype
+            self._fold = ((wc @ wo).to(dt), (wc @ bo + bc).to(dt))
+            self._fold_key = key
+        return self._fold
+
     def mlp_delta(self, h):                      # h = ln_2(x)
         return self.proj(F.gelu(self.fc(h)))
 
@@ -150,7 +164,8 @@ class DokoAzNet(nn.Module):
             qkv = blk.qkv(h)                                     # [B, 62, 480]: q | k | v, heads contiguous
             y = torch.empty_like(h)
             ck(L.dk_net_attn62_bf16_async(qkv.data_ptr(), y.data_ptr(), B, st))
-            return blk.c_proj(blk.out(y))
+            w, b = blk.folded_proj()
+            return F.linear(y, w, b)
 
         def run(x, h, blocks, final_ln):
             for i, blk in enumerate(blocks):

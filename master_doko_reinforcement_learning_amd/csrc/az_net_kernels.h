@@ -103,32 +103,47 @@ __global__ void embed_ln_kernel(const int32_t* __restrict__ tokens, uint32_t B, 
     ln_row<PER>(x, d, lane, (const uint32_t*)gamma, (const uint32_t*)beta, eps, (uint32_t*)(h_out + (size_t)row * d));
 }
 
-// x += delta (bf16 add as torch rounds it); h = LN(x)
+// x += delta (bf16 add as torch rounds it); h = LN(x).  A half-wave handles ADD_LN_ROWS
+// consecutive rows and issues all of their loads before any arithmetic, so each wave
+// keeps ADD_LN_ROWS times more bytes in flight (and the grid has that many fewer waves).
+constexpr int ADD_LN_ROWS = 4;
 template <int PER>
 __global__ void add_ln_kernel(uint16_t* __restrict__ x_io, const uint16_t* __restrict__ delta, uint32_t rows, int d,
                               const uint16_t* gamma, const uint16_t* beta, float eps, uint16_t* __restrict__ h_out) {
-    const uint32_t row = blockIdx.x * (blockDim.x / 32) + threadIdx.x / 32;
+    const uint32_t row0 = (blockIdx.x * (blockDim.x / 32) + threadIdx.x / 32) * ADD_LN_ROWS;
     const int lane = threadIdx.x & 31, np = d / 2;
-    if (row >= rows) return;
-    uint32_t* xr = (uint32_t*)(x_io + (size_t)row * d);
-    const uint32_t* dr = (const uint32_t*)(delta + (size_t)row * d);
-    float x[2 * PER];
+    if (row0 >= rows) return;
+    uint32_t xv[ADD_LN_ROWS][PER], dv[ADD_LN_ROWS][PER];
 #pragma unroll
-    for (int k = 0; k < PER; ++k) {
-        const int j = lane + 32 * k;
-        x[2 * k] = x[2 * k + 1] = 0.0f;
-        if (j < np) {
-            uint32_t v = xr[j];
+    for (int q = 0; q < ADD_LN_ROWS; ++q)
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int j = lane + 32 * k;
+            const bool ok = row0 + q < rows && j < np;
+            const size_t at = (size_t)(row0 + q) * (d / 2) + j;
+            xv[q][k] = ok ? ((const uint32_t*)x_io)[at] : 0u;
+            dv[q][k] = (ok && delta) ? ((const uint32_t*)delta)[at] : 0u;
+        }
+#pragma unroll
+    for (int q = 0; q < ADD_LN_ROWS; ++q) {
+        if (row0 + q >= rows) break;
+        uint32_t* xr = (uint32_t*)(x_io + (size_t)(row0 + q) * d);
+        float x[2 * PER];
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int j = lane + 32 * k;
+            uint32_t v = xv[q][k];
             if (delta) {
-                const uint32_t dv = dr[j];
-                v = (uint32_t)f2bf(bf2f((uint16_t)v) + bf2f((uint16_t)dv)) |
-                    ((uint32_t)f2bf(bf2f((uint16_t)(v >> 16)) + bf2f((uint16_t)(dv >> 16))) << 16);
-                xr[j] = v;
+                const uint32_t e = dv[q][k];
+                v = (uint32_t)f2bf(bf2f((uint16_t)v) + bf2f((uint16_t)e)) |
+                    ((uint32_t)f2bf(bf2f((uint16_t)(v >> 16)) + bf2f((uint16_t)(e >> 16))) << 16);
+                if (j < np) xr[j] = v;
             }
             x[2 * k] = bf2f((uint16_t)v); x[2 * k + 1] = bf2f((uint16_t)(v >> 16));
         }
+        ln_row<PER>(x, d, lane, (const uint32_t*)gamma, (const uint32_t*)beta, eps,
+                    (uint32_t*)(h_out + (size_t)(row0 + q) * d));
     }
-    ln_row<PER>(x, d, lane, (const uint32_t*)gamma, (const uint32_t*)beta, eps, (uint32_t*)(h_out + (size_t)row * d));
 }
 
 // ---------------------------------------------------------------------------
@@ -167,12 +182,22 @@ __global__ void __launch_bounds__(256) attn62_kernel(const uint16_t* __restrict_
     const uint16_t* base = qkv + (size_t)b * S * (3 * D);
     uint16_t* vt = vt_all[wave];
 
-    // V^T into LDS: lane = key t, zero padding for t >= 62 and e >= 40
+    // V^T into LDS as [e][t]: the 62 x 40 tile is read as 310 16-byte pieces (8 dims of
+    // one key each, 5 per lane) and scattered transposed; zero padding for t >= 62, e >= 40
     {
-        const int t = lane;
-        const uint16_t* vr = base + (size_t)(t < S ? t : 0) * (3 * D) + 2 * D + hd * HD;
-        for (int e = 0; e < HD; ++e) vt[e * LDT + t] = (valid && t < S) ? vr[e] : (uint16_t)0;
-        for (int e = HD; e < 64; ++e) vt[e * LDT + t] = 0;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            const int v = lane + 64 * i;          // piece v: key v / 5, dims 8 (v % 5) .. +8
+            const int t = v / 5, e0 = 8 * (v % 5);
+            const bool ok = valid && v < S * 5;
+            union { uint4 u; uint16_t s[8]; } pc;
+            pc.u = ok ? *(const uint4*)(base + (size_t)t * (3 * D) + 2 * D + hd * HD + e0) : make_uint4(0u, 0u, 0u, 0u);
+            if (v < 64 * 5) {
+#pragma unroll
+                for (int m = 0; m < 8; ++m) vt[(e0 + m) * LDT + t] = pc.s[m];
+            }
+        }
+        for (int e = HD; e < 64; ++e) vt[e * LDT + lane] = 0;
     }
     // Q and K fragments: tile i covers tokens 32i + r, k-step kk covers dims 16kk + 8h + j
     bf16x8_t qf[2][3], kf[2][3];

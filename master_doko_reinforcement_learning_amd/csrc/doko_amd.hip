@@ -1210,7 +1210,8 @@ int dk_net_add_ln_bf16_async(void* x_io, const void* delta, uint32_t rows, uint3
     const int per = ln_per(d);
     if (!x_io || !h_out || !gamma || !beta || per == 0) return DK_E_INVALID;
     if (rows == 0) return DK_OK;
-    const dim3 grid((rows + 7u) / 8u), block(256);
+    const uint32_t rows_per_block = 8u * (uint32_t)dk::net::ADD_LN_ROWS;
+    const dim3 grid((rows + rows_per_block - 1u) / rows_per_block), block(256);
     hipStream_t st = (hipStream_t)stream;
     switch (per) {
 #define M(P) case P: hipLaunchKernelGGL(dk::net::add_ln_kernel<P>, grid, block, 0, st, (uint16_t*)x_io,                  \
