@@ -56,12 +56,13 @@ constexpr uint32_t LN_LDS_MAX = 2048;   // ln(N) entries staged in LDS (16 KB)
 
 // ---------------------------------------------------------------- node pool access
 // Node pool of one root, root-major: [root][slot] so that a node's child block
-// is one contiguous run of 16-byte hot records (one or a few cache lines).
+// is one contiguous run of 16- or 32-byte hot records (one or a few cache lines).
 // Only the owning lane ever touches a root's tree, so plain loads and stores
 // (L1-cacheable, program-ordered within the lane) are sufficient.
-template <class W, bool LN_LDS>
+template <class W, bool LN_LDS, class H>
 struct GpuMem {
-    dk::NodeHot* hot;
+    using Hot = H;
+    H* hot;
     dk::NodeCold* cold;
     W* states;
     // LDS regions are addressed as offsets into dk_lds (u64 words) so that the
@@ -84,17 +85,11 @@ struct GpuMem {
         if constexpr (LN_LDS) return __longlong_as_double((long long)dk_lds[v]);
         else return ln_glob[v];
     }
-    __device__ dk::NodeHot load_hot(uint32_t s) const { return hot[s]; }
-    __device__ void store_hot(uint32_t s, const dk::NodeHot& h) const { hot[s] = h; }
+    __device__ H load_hot(uint32_t s) const { return hot[s]; }
+    __device__ void store_hot(uint32_t s, const H& h) const { hot[s] = h; }
     __device__ void store_stats(uint32_t s, uint64_t v) const { hot[s].stats = v; }
     __device__ void store_backup(uint32_t s, uint64_t v, double q, float isv) const {
-        hot[s].stats = v;
-#if DK_HOT16
-        (void)q; (void)isv;
-#else
-        hot[s].q = q;
-        hot[s].isv = isv;
-#endif
+        dk::hot_backup(hot[s], v, q, isv);
     }
     __device__ void store_child_base(uint32_t s, uint32_t child_base) const { hot[s].child_base = child_base; }
     __device__ void store_node_tail(uint32_t s, uint32_t child_base, uint32_t info) const {
@@ -137,11 +132,11 @@ struct GpuMem {
 // next group instead of idling until the slowest wave of the launch ends, and the pools
 // are sized for the resident waves, not for the batch.  The LDS holds each lane's
 // selection path: lds_n x (u32 slot|player, u64 stats).
-template <class E, bool LN_LDS>
+template <class E, bool LN_LDS, class H>
 __global__ void DK_SEARCH_BOUNDS search_kernel(const dk_state* __restrict__ roots,
                                                       const uint64_t* __restrict__ seeds, uint32_t n,
                                                       uint32_t iters, double c, const double* __restrict__ ln_table,
-                                                      dk::NodeHot* hot, dk::NodeCold* cold, typename E::Work* states,
+                                                      void* hot_pool, dk::NodeCold* cold, typename E::Work* states,
                                                       uint32_t* ovf, uint64_t* ovf_st,
                                                       uint32_t cap_slots, uint32_t rpw, int lds_n,
                                                       uint32_t* visits, double* values,
@@ -167,8 +162,8 @@ __global__ void DK_SEARCH_BOUNDS search_kernel(const dk_state* __restrict__ root
         typename E::Work w;
         E::load(roots[root], w);
         dk::Rng rng = dk::Rng::seed_from_u64(seeds[root]);
-        GpuMem<typename E::Work, LN_LDS> mem;
-        mem.hot = hot + pr * cap_slots;
+        GpuMem<typename E::Work, LN_LDS, H> mem;
+        mem.hot = reinterpret_cast<H*>(hot_pool) + pr * cap_slots;
         mem.cold = cold + pr * cap_slots;
         mem.states = states + pr * T;
         mem.path_st_off = path_st_base + lane;
@@ -537,7 +532,7 @@ struct dk_ctx {
                                     // the resident capacity: CUs x 8 single-wave workgroups x 64 lanes))
     int cu_count = 0;
     uint32_t* queue = nullptr;      // root-group counter of the persistent search grid
-    dk::NodeHot* hot = nullptr;
+    void* hot = nullptr;            // hot records, 32 B per slot (NodeHot16 launches use half)
     dk::NodeCold* cold = nullptr;
     uint32_t* ovf = nullptr;
     uint64_t* ovf_st = nullptr;
@@ -550,6 +545,7 @@ struct dk_ctx {
     uint64_t pool_bytes = 0;
     uint32_t roots_per_wave = 64;   // pool region width; DK_ROOTS_PER_WAVE fixes the launch width too
     bool rpw_fixed = false;
+    int hot_layout = 0;             // DK_HOT_RECORD=16|32 fixes the hot-record layout; 0 = per launch
     bool ln_in_lds = false;         // DK_LN_LDS=1: ln(N) table copied into every workgroup's LDS (8 KB at
                                     // 1000 iterations); by default it is read through the L1/L2 caches
     int lds_path = 16;              // DK_LDS_PATH (path entries kept in LDS, <= MAX_PATH; deeper ones
@@ -614,11 +610,11 @@ uint32_t launch_rpw(const dk_ctx* ctx, uint32_t n) {
     return r < 16u ? 16u : (r > ctx->roots_per_wave ? ctx->roots_per_wave : r);
 }
 
-template <class E, bool LN>
+template <class E, bool LN, class H>
 hipError_t launch_search_t(dk_ctx* ctx, const dk_state* roots, const uint64_t* seeds, uint32_t n, uint32_t iters,
                            double c, uint32_t* visits, double* values, uint8_t* best, hipStream_t st,
                            size_t lds_bytes, uint32_t rpw) {
-    const auto kern = search_kernel<E, LN>;
+    const auto kern = search_kernel<E, LN, H>;
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, WAVE, lds_bytes) != hipSuccess || per_cu < 1)
         per_cu = 1;
@@ -642,8 +638,15 @@ hipError_t launch_search(dk_ctx* ctx, const dk_state* roots, const uint64_t* see
     const bool ln = iters + 1 <= LN_LDS_MAX && ctx->ln_in_lds;
     const uint32_t rpw = launch_rpw(ctx, n);
     const size_t lds_bytes = (ln ? (size_t)((iters + 2) & ~1u) * 8 : 0) + (size_t)ctx->lds_path * rpw * 12;
-    return ln ? launch_search_t<E, true>(ctx, roots, seeds, n, iters, c, visits, values, best, st, lds_bytes, rpw)
-              : launch_search_t<E, false>(ctx, roots, seeds, n, iters, c, visits, values, best, st, lds_bytes, rpw);
+    // hot-record layout (search_core.h): 16 B once the batch gives every SIMD two waves,
+    // 32 B (cached means) when a single wave per SIMD leaves the pick's latency exposed
+    const uint32_t simds = 4u * (uint32_t)ctx->cu_count;
+    const bool h16 = ctx->hot_layout ? ctx->hot_layout == 16 : grid_for(n, rpw) >= 2u * simds;
+    if (h16)
+        return ln ? launch_search_t<E, true, dk::NodeHot16>(ctx, roots, seeds, n, iters, c, visits, values, best, st, lds_bytes, rpw)
+                  : launch_search_t<E, false, dk::NodeHot16>(ctx, roots, seeds, n, iters, c, visits, values, best, st, lds_bytes, rpw);
+    return ln ? launch_search_t<E, true, dk::NodeHot32>(ctx, roots, seeds, n, iters, c, visits, values, best, st, lds_bytes, rpw)
+              : launch_search_t<E, false, dk::NodeHot32>(ctx, roots, seeds, n, iters, c, visits, values, best, st, lds_bytes, rpw);
 }
 
 }  // namespace
@@ -688,6 +691,10 @@ dk_ctx* dk_create(const dk_config* cfg) {
         const int v = atoi(e);
         if (v >= 1 && v <= WAVE) { ctx->roots_per_wave = (uint32_t)v; ctx->rpw_fixed = true; }
     }
+    if (const char* e = getenv("DK_HOT_RECORD")) {
+        const int v = atoi(e);
+        if (v == 16 || v == 32) ctx->hot_layout = v;
+    }
     if (const char* e = getenv("DK_LN_LDS")) ctx->ln_in_lds = atoi(e) != 0;
     if (const char* e = getenv("DK_LDS_PATH")) {
         const int v = atoi(e);
@@ -705,7 +712,7 @@ dk_ctx* dk_create(const dk_config* cfg) {
     ctx->pool_roots = (uint32_t)((pool + rpw - 1) / rpw * rpw);   // whole regions of rpw roots
     const size_t R = ctx->pool_roots, S = ctx->cap_slots, T = (size_t)cfg->max_iterations + 1;
     bool ok = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) == hipSuccess;
-    ok = ok && hipMalloc(&ctx->hot, R * S * sizeof(dk::NodeHot)) == hipSuccess;
+    ok = ok && hipMalloc(&ctx->hot, R * S * sizeof(dk::NodeHot32)) == hipSuccess;
     ok = ok && hipMalloc(&ctx->cold, R * S * sizeof(dk::NodeCold)) == hipSuccess;
     ok = ok && hipMalloc(&ctx->ovf, R * dk::MAX_DEPTH * sizeof(uint32_t)) == hipSuccess;
     ok = ok && hipMalloc(&ctx->ovf_st, R * dk::MAX_DEPTH * sizeof(uint64_t)) == hipSuccess;
@@ -725,7 +732,7 @@ dk_ctx* dk_create(const dk_config* cfg) {
         ok = hipMemcpy(ctx->ln_table, ln.data(), ln.size() * sizeof(double), hipMemcpyHostToDevice) == hipSuccess;
         ok = ok && hipMemset(ctx->err, 0, sizeof(int)) == hipSuccess;
     }
-    ctx->pool_bytes = R * S * (sizeof(dk::NodeHot) + sizeof(dk::NodeCold)) + R * T * STATE_SLOT_BYTES;
+    ctx->pool_bytes = R * S * (sizeof(dk::NodeHot32) + sizeof(dk::NodeCold)) + R * T * STATE_SLOT_BYTES;
     if (!ok) { dk_destroy(ctx); return nullptr; }
     return ctx;
 }

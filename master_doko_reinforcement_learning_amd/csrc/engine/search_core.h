@@ -56,29 +56,37 @@ namespace dk {
 #define DK_STAMP_DRAINED(t) [[maybe_unused]] const uint64_t t = 0
 #endif
 
-// Hot records are 32 B and cache the exact mean and 1/sqrt(visits) written by the backup.
-// DK_HOT16=1 builds 16-B records that derive both from the stats at selection time (half
-// the bytes per scanned child and per backed-up node): measured 7-11 % slower, since
-// the kernel is bound by VALU issue and the twelve f64 divisions per pick cost more than
-// the halved traffic saves.
-#ifndef DK_HOT16
-#define DK_HOT16 0
-#endif
-#if DK_HOT16
-struct alignas(16) NodeHot {
+// Two hot-record layouts; the launch picks one per batch (doko_amd.hip, hot_layout):
+//  NodeHot16 (16 B): stats, child_base, info.  The pick derives the sibling min / max
+//    exactly from 64-bit cross products of the stats and divides in f64 only for the
+//    candidates, so a scanned child and a backed-up node cost 16 B.  Faster when the
+//    launch has several waves per SIMD (C3: 6 %, C2d: 4 %): the halved bytes win.
+//  NodeHot32 (32 B): also the exact mean and an f32 1/sqrt(visits) written by the
+//    backup.  Faster at one wave per SIMD (C2's 32,768 roots: 7 %), where the pick's
+//    dependent chain is exposed and a cached mean shortens it.
+struct alignas(16) NodeHot16 {
     uint64_t stats;       // visits (low 32) | win_score (high 32, two's complement)
     uint32_t child_base;  // first slot of the child block (valid when nchild > 0)
     uint32_t info;        // nchild:6 | player:2 | has_unexpanded:1 | chain_head:1 | state_idx:22
+    static constexpr bool CACHED_MEAN = false;
 };
-#else
-struct alignas(32) NodeHot {
-    uint64_t stats;       // visits (low 32) | win_score (high 32, two's complement)
-    uint32_t child_base;  // first slot of the child block (valid when nchild > 0)
-    uint32_t info;        // nchild:6 | player:2 | has_unexpanded:1 | chain_head:1 | state_idx:22
+struct alignas(32) NodeHot32 {
+    uint64_t stats;
+    uint32_t child_base;
+    uint32_t info;
     double q;             // win_score / visits exactly as the reference computes it (0 if unvisited)
     float isv;            // ~1/sqrt(visits) (f32 estimate for the UCT filter)
     uint32_t pad;
+    static constexpr bool CACHED_MEAN = true;
 };
+// the layout of host builds (test harnesses); -DDK_HOT16=0 selects the 32-B one
+#ifndef DK_HOT16
+#define DK_HOT16 1
+#endif
+#if DK_HOT16
+using NodeHot = NodeHot16;
+#else
+using NodeHot = NodeHot32;
 #endif
 struct alignas(16) NodeCold {
     uint64_t unexpanded;  // actions not yet expanded
@@ -133,29 +141,27 @@ DK_HD float sqrt_approx(float x) { return sqrtf(x); }
 DK_HD float rsqrt_approx(float x) { return 1.0f / sqrtf(x); }
 #endif
 
-DK_HD NodeHot make_hot(uint64_t stats, uint32_t child_base, uint32_t info) {
-    NodeHot h;
+template <class H>
+DK_HD H make_hot(uint64_t stats, uint32_t child_base, uint32_t info) {
+    H h;
     h.stats = stats; h.child_base = child_base; h.info = info;
-#if !DK_HOT16
-    h.q = mean_of(stats); h.isv = (uint32_t)stats ? rsqrt_approx((float)(uint32_t)stats) : 0.0f; h.pad = 0;
-#endif
+    if constexpr (H::CACHED_MEAN) {
+        h.q = mean_of(stats); h.isv = (uint32_t)stats ? rsqrt_approx((float)(uint32_t)stats) : 0.0f; h.pad = 0;
+    }
     return h;
 }
+// the backup's store: stats, plus the cached mean of a 32-B record
+template <class H>
+DK_HD void hot_backup(H& h, uint64_t stats, double q, float isv) {
+    h.stats = stats;
+    if constexpr (H::CACHED_MEAN) { h.q = q; h.isv = isv; }
+    else { (void)q; (void)isv; }
+}
 // the exact mean (mean_of) and the f32 1/sqrt(visits) estimate of a hot record
-DK_HD double hot_q(const NodeHot& h) {
-#if DK_HOT16
-    return mean_of(h.stats);
-#else
-    return h.q;
-#endif
-}
-DK_HD float hot_isv(const NodeHot& h) {
-#if DK_HOT16
-    return (uint32_t)h.stats ? rsqrt_approx((float)(uint32_t)h.stats) : 0.0f;
-#else
-    return h.isv;
-#endif
-}
+DK_HD double hot_q(const NodeHot16& h) { return mean_of(h.stats); }
+DK_HD double hot_q(const NodeHot32& h) { return h.q; }
+DK_HD float hot_isv(const NodeHot16& h) { return (uint32_t)h.stats ? rsqrt_approx((float)(uint32_t)h.stats) : 0.0f; }
+DK_HD float hot_isv(const NodeHot32& h) { return h.isv; }
 
 // Child block of n <= SCAN_REG records held in registers, structure of arrays
 // (constant indices only, so everything stays in VGPRs).
@@ -166,7 +172,7 @@ struct Block {
     float isv[SCAN_REG];
 };
 
-// UCT pick over a register block; returns the index and the picked node's
+// UCT pick over a register block (32-B records); returns the index and the picked node's
 // stats / child_base / info.  Bit-exact with the reference's first-strict-
 // maximum over f64 UCT values:
 //  1. sibling min / max over the stored exact means (the reference's values);
@@ -185,7 +191,7 @@ struct Block {
 // *end holds the picked child's chain end.
 template <class Mem>
 DK_HD uint32_t pick_child_reg(const Block& b, uint32_t n, double lnN, double c, Mem& mem, uint64_t* p_st, uint32_t* p_cb,
-                              uint32_t* p_inf, NodeHot* end, bool* end_ok) {
+                              uint32_t* p_inf, NodeHot32* end, bool* end_ok) {
     double min_q = INFINITY, max_q = -INFINITY;
 #pragma unroll
     for (int j = 0; j < SCAN_REG; ++j) {
@@ -224,7 +230,7 @@ DK_HD uint32_t pick_child_reg(const Block& b, uint32_t n, double lnN, double c, 
     // prefetch the chain ends of forced candidates (their child_base is the chain end)
     const bool f1 = ni_nchild(in1) == 1 && !ni_open(in1);
     const bool f2 = nc >= 2 && ni_nchild(in2) == 1 && !ni_open(in2);
-    NodeHot e1, e2;
+    NodeHot32 e1, e2;
     if (f1) e1 = mem.load_hot(cb1);
     if (f2) e2 = mem.load_hot(cb2);
     // a single candidate is the unique maximum: no exact evaluation needed
@@ -258,16 +264,111 @@ DK_HD uint32_t pick_child_reg(const Block& b, uint32_t n, double lnN, double c, 
     return pick;
 }
 
+// The pick for 16-B hot records (no stored mean): the sibling min / max are found
+// EXACTLY by comparing the means w/v as 64-bit cross products w_a v_b < w_b v_a
+// (division-free; rounding to f64 is monotone, so the winner's f64 mean is the
+// reference's f64 min / max), and only min, max and the candidates' means are
+// divided in f64.  The f32 estimate of every child's normalised mean is
+// (w * rcp(v) - min) * 2 / range - 1; its error now also scales with
+// |q|max / range (the f32 means carry a relative error), so the candidate margin
+// grows with that ratio and a nearly flat block falls back to the full exact pass.
+template <class Mem>
+DK_HD uint32_t pick_child_reg(const Block& b, uint32_t n, double lnN, double c, Mem& mem, uint64_t* p_st, uint32_t* p_cb,
+                              uint32_t* p_inf, NodeHot16* end, bool* end_ok) {
+    int32_t w[SCAN_REG];
+    uint32_t v[SCAN_REG];
+#pragma unroll
+    for (int j = 0; j < SCAN_REG; ++j) {
+        const uint32_t vv = (uint32_t)b.st[j];
+        w[j] = vv ? (int32_t)(b.st[j] >> 32) : 0;
+        v[j] = vv ? vv : 1u;   // an unvisited child's mean is 0 = 0/1
+    }
+    int32_t wmin = w[0], wmax = w[0];
+    uint32_t vmin = v[0], vmax = v[0];
+#pragma unroll
+    for (int j = 1; j < SCAN_REG; ++j) {
+        if ((uint32_t)j < n) {
+            const bool lt = (int64_t)w[j] * (int64_t)vmin < (int64_t)wmin * (int64_t)v[j];
+            const bool gt = (int64_t)w[j] * (int64_t)vmax > (int64_t)wmax * (int64_t)v[j];
+            wmin = lt ? w[j] : wmin; vmin = lt ? v[j] : vmin;
+            wmax = gt ? w[j] : wmax; vmax = gt ? v[j] : vmax;
+        }
+    }
+    const double min_q = (double)wmin / (double)vmin, max_q = (double)wmax / (double)vmax;
+    const double range = max_q - min_q;
+    const bool flat = fabs(range) < DK_F64_EPSILON;
+    const float inv_r = flat ? 0.0f : 2.0f * rcp_approx((float)range);
+    const float minf = (float)min_q;
+    const float qabs = fmaxf(fabsf(minf), fabsf((float)max_q));
+    const float ex = (float)c * sqrt_approx((float)lnN);
+    float ue[SCAN_REG];
+    float umax = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < SCAN_REG; ++j) {
+        const float qf = (float)w[j] * rcp_approx((float)v[j]);
+        const float nq = flat ? 1.0f : (qf - minf) * inv_r - 1.0f;
+        const uint32_t vis = (uint32_t)b.st[j];
+        const float u = vis == 0 ? INFINITY : nq + ex * rsqrt_approx((float)vis);
+        ue[j] = (uint32_t)j < n ? u : -INFINITY;
+        umax = ue[j] > umax ? ue[j] : umax;
+    }
+    const float cut = umax - (3e-6f * (3.0f + fabsf(ex)) + 4e-6f * qabs * inv_r);
+    uint64_t s1 = b.st[0], s2 = b.st[0];
+    uint32_t j1 = 0, j2 = 0, nc = 0, cb1 = b.cb[0], cb2 = b.cb[0], in1 = b.inf[0], in2 = b.inf[0];
+#pragma unroll
+    for (int j = 0; j < SCAN_REG; ++j) {
+        const bool cj = ue[j] >= cut;   // implies j < n
+        const bool first = cj && nc == 0, second = cj && nc == 1;
+        s1 = first ? b.st[j] : s1; j1 = first ? (uint32_t)j : j1; cb1 = first ? b.cb[j] : cb1; in1 = first ? b.inf[j] : in1;
+        s2 = second ? b.st[j] : s2; j2 = second ? (uint32_t)j : j2; cb2 = second ? b.cb[j] : cb2; in2 = second ? b.inf[j] : in2;
+        nc += cj ? 1u : 0u;
+    }
+    const bool f1 = ni_nchild(in1) == 1 && !ni_open(in1);
+    const bool f2 = nc >= 2 && ni_nchild(in2) == 1 && !ni_open(in2);
+    NodeHot16 e1, e2;
+    if (f1) e1 = mem.load_hot(cb1);
+    if (f2) e2 = mem.load_hot(cb2);
+    uint32_t pick = j1;
+    if (nc == 2) {
+        const double u1 = uct_exact(s1, mean_of(s1), flat, min_q, max_q, lnN, c);
+        const double u2 = uct_exact(s2, mean_of(s2), flat, min_q, max_q, lnN, c);
+        if (u2 > u1) pick = j2;
+    } else if (nc > 2) {
+        double best = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < SCAN_REG; ++j) {
+            if (ue[j] >= cut) {
+                const double u = uct_exact(b.st[j], mean_of(b.st[j]), flat, min_q, max_q, lnN, c);
+                if (u > best) { best = u; pick = (uint32_t)j; }
+            }
+        }
+    }
+    uint64_t ps = b.st[0];
+    uint32_t pc = b.cb[0], pi = b.inf[0];
+#pragma unroll
+    for (int j = 1; j < SCAN_REG; ++j) {
+        ps = (uint32_t)j == pick ? b.st[j] : ps;
+        pc = (uint32_t)j == pick ? b.cb[j] : pc;
+        pi = (uint32_t)j == pick ? b.inf[j] : pi;
+    }
+    *p_st = ps; *p_cb = pc; *p_inf = pi;
+    *end_ok = (pick == j1 && f1) || (nc >= 2 && pick == j2 && f2);
+    if (pick == j1 && f1) *end = e1;
+    else if (nc >= 2 && pick == j2 && f2) *end = e2;
+    return pick;
+}
+
 template <class E, class Mem>
 DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, double c,
                       Mem& mem, uint32_t* visits39, double* values39, uint8_t* best_out, uint64_t* ctr_scanned) {
     using Work = typename E::Work;
+    using NodeHot = typename Mem::Hot;
     // the root's structure (child_base, info) lives in registers: it changes only
     // when the root itself is expanded, and its visits are the iteration count
     uint32_t root_cb = 0, root_info;
     {
         const uint64_t ra = E::allowed(root, true);
-        const NodeHot h = make_hot(0, 0, ni_make(0, (uint32_t)E::current_player(root), ra != 0, false, 0));
+        const NodeHot h = make_hot<NodeHot>(0, 0, ni_make(0, (uint32_t)E::current_player(root), ra != 0, false, 0));
         root_info = h.info;
         NodeCold cd;
         cd.unexpanded = ra; cd.parent = 0xFFFFFFFFu; cd.action = 0xFFu;
@@ -409,7 +510,7 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
             DK_STAMP_DRAINED(te1);
             DK_PROF(mem, 12, te1 - te0);
             const uint64_t ca = E::allowed(w, false);
-            const NodeHot ch = make_hot(0, 0, ni_make(0, (uint32_t)E::current_player(w), ca != 0, slot == 0 || block >= 2, next_state));
+            const NodeHot ch = make_hot<NodeHot>(0, 0, ni_make(0, (uint32_t)E::current_player(w), ca != 0, slot == 0 || block >= 2, next_state));
             NodeCold cc;
             cc.unexpanded = ca; cc.parent = slot; cc.action = (uint32_t)a;
             mem.store_hot(child, ch);

@@ -7,6 +7,7 @@
 
 template <class W>
 struct HostMem {
+    using Hot = dk::NodeHot;   // the host build's layout (DK_HOT16)
     uint32_t cap_slots, cap_states, max_path;
     std::vector<dk::NodeHot> hot;
     std::vector<dk::NodeCold> cold;
@@ -23,11 +24,8 @@ struct HostMem {
     dk::NodeHot load_hot(uint32_t s) { return hot[s]; }
     void store_hot(uint32_t s, const dk::NodeHot& h) { hot[s] = h; }
     void store_stats(uint32_t s, uint64_t v) { hot[s].stats = v; }
-    void store_backup(uint32_t s, uint64_t v, [[maybe_unused]] double q, [[maybe_unused]] float isv) {
-        hot[s].stats = v;
-#if !DK_HOT16
-        hot[s].q = q; hot[s].isv = isv;
-#endif
+    void store_backup(uint32_t s, uint64_t v, double q, float isv) {
+        dk::hot_backup(hot[s], v, q, isv);
     }
     void store_child_base(uint32_t s, uint32_t cb) { hot[s].child_base = cb; }
     void store_node_tail(uint32_t s, uint32_t cb, uint32_t info) { hot[s].child_base = cb; hot[s].info = info; }

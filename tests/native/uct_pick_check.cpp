@@ -67,7 +67,7 @@ int main(int argc, char** argv) {
             total += v;
         }
         if (r() % 50 == 0) rec[r() % n].stats = 0;   // an unvisited child
-        for (uint32_t j = 0; j < n; ++j) rec[j] = dk::make_hot(rec[j].stats, 0, 0);   // as the backup leaves it
+        for (uint32_t j = 0; j < n; ++j) rec[j] = dk::make_hot<dk::NodeHot>(rec[j].stats, 0, 0);   // as the backup leaves it
         const double lnN = std::log((double)(total + (uint32_t)(r() % 5)));
         const double c = (r() % 4 == 0) ? 0.7 + (double)(r() % 100) / 10.0 : 2.5;
         dk::Block blk;

@@ -55,6 +55,12 @@ def test_uct_pick_filter_exact(native_bins):
     assert _run("uct_pick_check", 1000000, 3) == 1000000
 
 
+def test_hot32_variant_exact(native_bins):
+    """The 32-B hot-record build (DK_HOT16=0, cached exact means) stays exact as well."""
+    assert _run("uct_pick_check32", 300000, 5) == 300000
+    assert _run("search_check32", 6, 400, 5) > 10
+
+
 def test_engine_cap_vs_oracle(native_bins):
     """cap_engine.h (host build) = oracle card_matching_full; samples always consistent."""
     assert _run("cap_check", 120, 3) > 5000

@@ -194,12 +194,16 @@ def test_search_parity_fdo(eng, iters):
 @pytest.mark.parametrize("env", [{"DK_LDS_PATH": "2"}, {"DK_ROOTS_PER_WAVE": "7"}, {"DK_ROOTS_PER_WAVE": "16"},
                                  {"DK_ROOTS_PER_WAVE": "32", "DK_LN_LDS": "1"},
                                  {"DK_POOL_ROOTS": "1", "DK_ROOTS_PER_WAVE": "4"},
-                                 {"DK_POOL_ROOTS": "16", "DK_ROOTS_PER_WAVE": "5"}])
+                                 {"DK_POOL_ROOTS": "16", "DK_ROOTS_PER_WAVE": "5"},
+                                 {"DK_HOT_RECORD": "16"}, {"DK_HOT_RECORD": "32"},
+                                 {"DK_HOT_RECORD": "16", "DK_LDS_PATH": "2"},
+                                 {"DK_HOT_RECORD": "16", "DK_POOL_ROOTS": "1", "DK_ROOTS_PER_WAVE": "4"}])
 def test_search_parity_fdo_launch_variants(env, monkeypatch):
     """Path overflow into global memory (2 LDS entries), partial / narrow waves, the LDS
     ln table, and batches larger than the node pools: with DK_POOL_ROOTS=1 one wave
     streams all six 4-root groups through a single pool region (stale trees of the
-    previous group stay in it), with 16 four waves share five groups."""
+    previous group stay in it), with 16 four waves share five groups.  DK_HOT_RECORD
+    forces either hot-record layout (small batches pick the 32-B one by themselves)."""
     import master_doko_reinforcement_learning_amd as dk
     for k, v in env.items():
         monkeypatch.setenv(k, v)
@@ -218,8 +222,12 @@ def test_search_parity_fdo_launch_variants(env, monkeypatch):
         e.close()
 
 
-def test_search_parity_doko(eng):
+@pytest.mark.parametrize("layout", [None, "16"])
+def test_search_parity_doko(eng, layout, monkeypatch):
     import master_doko_reinforcement_learning_amd as dk
+    if layout:
+        monkeypatch.setenv("DK_HOT_RECORD", layout)
+        eng = dk.Engine(device=0, max_roots=64, max_iterations=500)
     states = []
     for g in range(32):
         s = ol.DoState.new_game(0xD0C00000 + g)
@@ -229,6 +237,8 @@ def test_search_parity_doko(eng):
         states.append(s)
     seeds = np.arange(32, dtype=np.uint64) * 13 + 1
     visits, values, best = dk.CachedMCTS(eng, dk.GAME_DOKO).monte_carlo_tree_search(pack_all(states), 2.5, 500, seeds)
+    if layout:
+        eng.close()
     for i, (b, v, val) in enumerate(_oracle_search(states, seeds, 500, 2.5, "do")):
         assert list(visits[i]) == v
         assert values[i].tobytes() == np.array(val, dtype=np.float64).tobytes()
@@ -355,10 +365,10 @@ def test_decide_end_to_end(eng):
         assert int(actions[j]) == exp
 
 
-def test_full_size_properties(eng):
+def test_full_size_properties(eng, monkeypatch):
     """Bench-sized batch shape (4096 roots x 1000 iterations here): every root's
-    visits sum to the iteration count, only root-legal actions are visited, and
-    a repeat run is bit-identical."""
+    visits sum to the iteration count, only root-legal actions are visited, a
+    repeat run is bit-identical, and so is a run with the other hot-record layout."""
     import master_doko_reinforcement_learning_amd as dk
     n = 4096
     seeds = np.arange(n, dtype=np.uint64) + 1234
@@ -374,6 +384,13 @@ def test_full_size_properties(eng):
     assert np.all((v1 > 0) <= (bits == 1))
     v2, val2, b2 = mcts.monte_carlo_tree_search(roots, 2.5, 1000, seeds)
     assert np.array_equal(v1, v2) and np.array_equal(val1.view(np.uint64), val2.view(np.uint64)) and np.array_equal(b1, b2)
+    monkeypatch.setenv("DK_HOT_RECORD", "16")
+    e16 = dk.Engine(device=0, max_roots=n, max_iterations=1000)
+    try:
+        v3, val3, b3 = dk.CachedMCTS(e16, dk.GAME_FULL_DOKO).monte_carlo_tree_search(roots, 2.5, 1000, seeds)
+    finally:
+        e16.close()
+    assert np.array_equal(v1, v3) and np.array_equal(val1.view(np.uint64), val3.view(np.uint64)) and np.array_equal(b1, b3)
 
 
 # ---------------------------------------------------------------- rs-doko rule-based sampler
