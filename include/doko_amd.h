@@ -287,6 +287,36 @@ int dk_az_select_async(dk_ctx* ctx, float c, dk_az_state* d_eval, uint8_t* d_nee
 int dk_az_backup_async(dk_ctx* ctx, const float* d_value, const float* d_logits, void* stream);
 int dk_az_finish_async(dk_ctx* ctx, int temperature_mode, float temperature, uint32_t* d_visits, uint8_t* d_action,
                        void* stream);
+/* IMPI autoregressive determinization: forward_pred_process_with_mask
+ * (rs-doko-impi/src/forward.rs:392-661), the SamplingFn of ARSampling
+ * (rs-doko-py-bridge/src/compare_impi/compare_impi.rs:84-105), batched over
+ * n_info x samples lanes (lane = info * samples + sample, seed d_seeds[lane]).
+ * Every guess of every lane is one row of a network batch, run by the caller:
+ *   dk_ar_begin_async    lanes from the infostate records (dk_az_state: the packed
+ *                        state plus its announcement list); *d_rounds = the largest
+ *                        number of guesses of a lane (one network call each)
+ *   repeat *d_rounds times:
+ *     dk_ar_prepare_async  each running lane moves to its next guess (a card for
+ *                          the next player with open slots, 12 x 3 steps; then the
+ *                          hidden reservations) and writes its 311 encode_state_ipi
+ *                          tokens to d_tokens[lane] (other rows keep their content:
+ *                          start from a zeroed buffer); a lane with nothing left
+ *                          to guess runs _is_consistent and its log draw
+ *     (network: d_tokens [lanes][311] -> d_logits [lanes][33] f32)
+ *     dk_ar_choose_async   mask, softmax(temperature), normalize, choose_weighted
+ *   dk_ar_prepare_async  once more (finishes every lane)
+ *   dk_ar_output_async   d_out[lane] = the sample (clone_with_different_hands_and_
+ *                        reservations, state.rs:96-118) or the infostate itself;
+ *                        d_status 0 Consistent, 1 NotConsistent (d_reason =
+ *                        NotConsistentReason, is_consistent.rs:26-36), 2 where the
+ *                        reference panics, 3 unfinished.
+ * The infostate records must stay valid until dk_ar_output_async. */
+int dk_ar_begin_async(dk_ctx* ctx, const dk_az_state* d_infostates, uint32_t n_info, uint32_t samples,
+                      const uint64_t* d_seeds, float log_chance, uint32_t* d_rounds, void* stream);
+int dk_ar_prepare_async(dk_ctx* ctx, int32_t* d_tokens, void* stream);
+int dk_ar_choose_async(dk_ctx* ctx, const float* d_logits, float temperature, void* stream);
+int dk_ar_output_async(dk_ctx* ctx, dk_state* d_out, uint8_t* d_status, uint8_t* d_reason, void* stream);
+
 /* Game records for self-play.  dk_az_records_async: records of packed rs-full-doko states
  * without announcements (new games, DK_E_STATE otherwise).  dk_az_step_async:
  * take_action_by_action_index(action, skip_single = true) (full_doko.rs:121-157) on every

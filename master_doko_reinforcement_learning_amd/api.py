@@ -9,6 +9,8 @@ Names follow the Rust types they replace:
 * ``sample_assignment_full``      — rs-doko rule-based determinization (rs-doko-assignment/src/assignment.rs:472-580)
 * ``PolicyFusionMaxN`` / ``PolicyFusionAverageStrategy`` — policy_fusion.rs:18-123
 * ``DefaultImpiPolicy``           — sample -> search -> fuse (compare_impi.rs:212-371)
+* ``ARSampling``                  — IMPI autoregressive determinization (forward_pred_process_with_mask,
+                                    rs-doko-impi/src/forward.rs:392-661), batched, network between launches
 * ``AlphaZeroSearch``             — AlphaZero PUCT mcts_search (rs-doko-alpha-zero/src/alpha_zero/mcts/async_mcts.rs:224-406),
                                     batched over games, network evaluated between launches
 
@@ -31,6 +33,13 @@ NUM_ACTIONS = 39
 STATE_BYTES = 128
 AZ_STATE_BYTES = 160   # dk_az_state: packed state + announcement occurrence list
 AZ_TOKENS = 311        # encode_state_pi
+IPI_TOKENS = 311       # encode_state_ipi
+IPI_CLASSES = 33       # ImperfectInformationOutput::COUNT
+# ForwardPredResult / NotConsistentReason (rs-full-doko/src/matching/is_consistent.rs:26-36)
+AR_CONSISTENT, AR_NOT_CONSISTENT, AR_PANIC, AR_UNFINISHED = 0, 1, 2, 3
+NOT_CONSISTENT_REASONS = ("HandSizeMismatch", "NotInRemainingCards", "RemainingCardsLeft", "AlreadyDiscardedColor",
+                          "HasClubQueenButSomeoneElseAnnouncedWedding", "HasNoClubQueenButAnnouncedRe",
+                          "HasClubQueenButAnnouncedKontra", "WrongReservation", "WrongReservationClubQ")
 
 
 class DokoError(RuntimeError):
@@ -304,6 +313,69 @@ class AlphaZeroSearch:
         _check(L.dk_az_finish_async(ctx, mode, temp, visits.data_ptr(), actions.data_ptr(), st))
         _check(L.dk_sync(ctx, st))
         return actions, visits
+
+
+class ARSampling:
+    """The ARSampling SamplingFn (rs-doko-py-bridge/src/compare_impi/compare_impi.rs:84-105):
+    forward_pred_process_with_mask (rs-doko-impi/src/forward.rs:392-661) for `samples`
+    draws of every infostate at once.  Each network call of the reference (one card or
+    one hidden reservation of one player) is one row of a batched network evaluation;
+    all lanes advance in lockstep rounds between two kernels (engine/ar_engine.h).
+
+    network(tokens) -> logits: tokens = int32 [n, 311] encode_state_ipi rows on the GPU,
+    logits = float [n, 33] (ImperfectInformationOutput order: 9 reservations, 24 cards).
+    log_chance: the probability of the reference's log-file draw (one u64 per sample)."""
+
+    def __init__(self, engine, network, temperature=1.0, log_chance=1.0 / 30000.0):
+        self.engine = engine
+        self.network = network
+        self.temperature = float(temperature)
+        self.log_chance = float(log_chance)
+        self.rounds = 0
+
+    def sample(self, infostates, samples, seeds):
+        """infostates: uint8 [n_info, 160] dk_az_state records (GPU); seeds: uint64 [n_info * samples].
+        Returns (states uint8 [n, 128], status uint8 [n], reason uint8 [n]) with n = n_info * samples,
+        lane = info * samples + sample; status AR_CONSISTENT rows hold the sample, the others the
+        infostate (AR_NOT_CONSISTENT: reason = index into NOT_CONSISTENT_REASONS)."""
+        import torch
+        dev = infostates.device
+        caller = torch.cuda.current_stream(dev)
+        if caller.cuda_stream != 0:
+            return self._sample(infostates, samples, seeds, caller.cuda_stream)
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(caller)
+        with torch.cuda.stream(side):
+            out = self._sample(infostates, samples, seeds, side.cuda_stream)
+        caller.wait_stream(side)
+        return out
+
+    def _sample(self, infostates, samples, seeds, st):
+        import torch
+        L = _native.lib()
+        ctx = self.engine.ctx
+        info = infostates.contiguous()
+        dev = info.device
+        n = info.shape[0] * samples
+        seeds_t = torch.as_tensor(np.ascontiguousarray(seeds, dtype=np.uint64).view(np.int64), device=dev)
+        if seeds_t.shape[0] != n:
+            raise ValueError("need one seed per (infostate, sample)")
+        rounds = torch.zeros(1, dtype=torch.int32, device=dev)
+        tokens = torch.zeros((n, IPI_TOKENS), dtype=torch.int32, device=dev)
+        _check(L.dk_ar_begin_async(ctx, info.data_ptr(), info.shape[0], samples, seeds_t.data_ptr(),
+                                   self.log_chance, rounds.data_ptr(), st))
+        self.rounds = int(rounds.item())
+        for _ in range(self.rounds):
+            _check(L.dk_ar_prepare_async(ctx, tokens.data_ptr(), st))
+            logits = self.network(tokens).float().contiguous()
+            _check(L.dk_ar_choose_async(ctx, logits.data_ptr(), self.temperature, st))
+        _check(L.dk_ar_prepare_async(ctx, tokens.data_ptr(), st))
+        out = torch.empty((n, STATE_BYTES), dtype=torch.uint8, device=dev)
+        status = torch.empty(n, dtype=torch.uint8, device=dev)
+        reason = torch.empty(n, dtype=torch.uint8, device=dev)
+        _check(L.dk_ar_output_async(ctx, out.data_ptr(), status.data_ptr(), reason.data_ptr(), st))
+        _check(L.dk_sync(ctx, st))
+        return out, status, reason
 
 
 def _stream(t):

@@ -99,6 +99,55 @@ class ClassHead(nn.Module):
         return torch.einsum("bco,co->bc", h, self.w2) + self.b2
 
 
+class FusedTrunk:
+    """The bf16 GPU forward of a token trunk (shared by DokoAzNet and DokoImpiNet): HIP
+    kernels (csrc/az_net_kernels.h) for the embedding sum + first LayerNorm, every
+    residual add fused with the LayerNorm that follows it, and (d = 160, 4 heads) the
+    62-token attention core; the GEMMs are torch (hipBLASLt).  `x` is the residual
+    stream, `h` the current LayerNorm output."""
+
+    def __init__(self, tokens, emb, ln0):
+        from . import _native
+        self.L = _native.lib()
+        self.st = torch.cuda.current_stream(tokens.device).cuda_stream
+        tok = tokens.int().contiguous()
+        B, d = tok.shape[0], emb[0].weight.shape[1]
+        self.rows, self.d = B * SEQ, d
+        self.x = torch.empty((B, SEQ, d), dtype=torch.bfloat16, device=tok.device)
+        self.h = torch.empty_like(self.x)
+        tables = (ctypes_vp * 6)(*[e.weight.data_ptr() for e in emb])
+        self.ck(self.L.dk_net_embed_ln_bf16_async(tok.data_ptr(), B, tables, d, ln0.weight.data_ptr(), ln0.bias.data_ptr(),
+                                                  ln0.eps, self.x.data_ptr(), self.h.data_ptr(), self.st))
+
+    @staticmethod
+    def ck(rc):
+        if rc != 0:
+            raise RuntimeError("doko_amd network kernel error %d" % rc)
+
+    def add_ln(self, x, delta, ln):
+        h = torch.empty_like(x)
+        self.ck(self.L.dk_net_add_ln_bf16_async(x.data_ptr(), delta.data_ptr() if delta is not None else None, self.rows,
+                                                self.d, ln.weight.data_ptr(), ln.bias.data_ptr(), ln.eps, h.data_ptr(), self.st))
+        return h
+
+    def attn_delta(self, blk, h):
+        if not (self.d == 160 and blk.heads == 4):
+            return blk.attn_delta(h)
+        qkv = blk.qkv(h)                                     # [B, 62, 480]: q | k | v, heads contiguous
+        y = torch.empty_like(h)
+        self.ck(self.L.dk_net_attn62_bf16_async(qkv.data_ptr(), y.data_ptr(), h.shape[0], self.st))
+        w, b = blk.folded_proj()
+        return F.linear(y, w, b)
+
+    def run(self, h, blocks, final_ln, x=None):
+        x = self.x if x is None else x
+        for i, blk in enumerate(blocks):
+            h = self.add_ln(x, self.attn_delta(blk, h), blk.ln_2)
+            nxt = blocks[i + 1].ln_1 if i + 1 < len(blocks) else final_ln
+            h = self.add_ln(x, blk.mlp_delta(h), nxt)
+        return h
+
+
 class DokoAzNet(nn.Module):
     def __init__(self, d=160, heads=4, layers=4, policy_layers=1, value_layers=1):
         super().__init__()
@@ -130,55 +179,14 @@ class DokoAzNet(nn.Module):
         embedding sum + first LayerNorm (one pass), every residual add fused with the
         LayerNorm that follows it, and the 62-token attention core (bf16 MFMA, reading
         the fused qkv projection in place)."""
-        from . import _native
-        L = _native.lib()
-        st = torch.cuda.current_stream(tokens.device).cuda_stream
-        tok = tokens.int().contiguous()
-        B, d = tok.shape[0], self.emb[0].weight.shape[1]
-        rows = B * SEQ
         if not (self.blocks and self.p_blocks and self.v_blocks):
             raise ValueError("the fused forward needs shared, policy and value blocks")
-
-        def ck(rc):
-            if rc != 0:
-                raise RuntimeError("doko_amd network kernel error %d" % rc)
-
-        def add_ln(x, delta, ln):
-            h = torch.empty_like(x)
-            ck(L.dk_net_add_ln_bf16_async(x.data_ptr(), delta.data_ptr() if delta is not None else None, rows, d,
-                                          ln.weight.data_ptr(), ln.bias.data_ptr(), ln.eps, h.data_ptr(), st))
-            return h
-
-        x = torch.empty((B, SEQ, d), dtype=torch.bfloat16, device=tok.device)
-        h = torch.empty_like(x)
-        tables = (ctypes_vp * 6)(*[e.weight.data_ptr() for e in self.emb])
-        ln0 = self.blocks[0].ln_1
-        ck(L.dk_net_embed_ln_bf16_async(tok.data_ptr(), B, tables, d, ln0.weight.data_ptr(), ln0.bias.data_ptr(),
-                                        ln0.eps, x.data_ptr(), h.data_ptr(), st))
-
-        fused_attn = d == 160 and all(b.heads == 4 for b in list(self.blocks) + list(self.p_blocks) + list(self.v_blocks))
-
-        def attn_delta(blk, h):
-            if not fused_attn:
-                return blk.attn_delta(h)
-            qkv = blk.qkv(h)                                     # [B, 62, 480]: q | k | v, heads contiguous
-            y = torch.empty_like(h)
-            ck(L.dk_net_attn62_bf16_async(qkv.data_ptr(), y.data_ptr(), B, st))
-            w, b = blk.folded_proj()
-            return F.linear(y, w, b)
-
-        def run(x, h, blocks, final_ln):
-            for i, blk in enumerate(blocks):
-                h = add_ln(x, attn_delta(blk, h), blk.ln_2)
-                nxt = blocks[i + 1].ln_1 if i + 1 < len(blocks) else final_ln
-                h = add_ln(x, blk.mlp_delta(h), nxt)
-            return h
-
-        hp = run(x, h, self.blocks, self.p_blocks[0].ln_1)       # x now holds the shared trunk's output
-        xv = x.clone()
-        hv = add_ln(xv, None, self.v_blocks[0].ln_1)
-        hp = run(x, hp, self.p_blocks, self.p_ln)
-        hv = run(xv, hv, self.v_blocks, self.v_ln)
+        f = FusedTrunk(tokens, self.emb, self.blocks[0].ln_1)
+        hp = f.run(f.h, self.blocks, self.p_blocks[0].ln_1)       # f.x now holds the shared trunk's output
+        xv = f.x.clone()
+        hv = f.add_ln(xv, None, self.v_blocks[0].ln_1)
+        hp = f.run(hp, self.p_blocks, self.p_ln)
+        hv = f.run(hv, self.v_blocks, self.v_ln, x=xv)
         return self.value_head(hv), self.policy_head(hp)
 
     @torch.no_grad()

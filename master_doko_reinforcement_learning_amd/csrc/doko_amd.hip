@@ -18,6 +18,7 @@
 #include "../../include/doko_amd.h"
 #include "engine/adapters.h"
 #include "engine/assign_engine.h"
+#include "engine/ar_engine.h"
 #include "engine/az_core.h"
 #include "engine/encode_pi.h"
 #include "az_net_kernels.h"
@@ -466,6 +467,49 @@ __global__ void az_encode_kernel(const dk_az_state* records, uint32_t n, int32_t
     dk::enc::encode_state_pi(records[i], put);
 }
 
+// IMPI autoregressive determinization (engine/ar_engine.h), one thread per lane
+__global__ void ar_begin_kernel(const dk_az_state* info, uint32_t samples, const uint64_t* seeds, uint32_t n,
+                                dk::ar::Lane* lanes, uint32_t* rounds) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    dk::ar::Lane L;
+    const uint32_t g = dk::ar::init(info[i / samples], seeds[i], L);
+    lanes[i] = L;
+    atomicMax(rounds, g);
+}
+
+__global__ void ar_prepare_kernel(const dk_az_state* info, uint32_t samples, uint32_t n, dk::ar::Lane* lanes,
+                                  float log_chance, int32_t* tokens) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    dk::ar::Lane L = lanes[i];
+    if (L.status != dk::ar::RUNNING) return;
+    int32_t* o = tokens + (size_t)dk::ar::TOKENS * i;
+    auto put = [o](uint32_t k, uint32_t v) { o[k] = (int32_t)v; };
+    dk::ar::prepare(info[i / samples], L, log_chance, put);
+    lanes[i] = L;
+}
+
+__global__ void ar_choose_kernel(uint32_t n, dk::ar::Lane* lanes, const float* logits, float temperature) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    dk::ar::Lane L = lanes[i];
+    if (L.status != dk::ar::RUNNING || L.guess == DK_NONE) return;
+    dk::ar::choose(L, logits + (size_t)dk::ar::OUT * i, temperature);
+    lanes[i] = L;
+}
+
+__global__ void ar_output_kernel(const dk_az_state* info, uint32_t samples, uint32_t n, const dk::ar::Lane* lanes,
+                                 dk_state* out, uint8_t* status, uint8_t* reason) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const dk::ar::Lane L = lanes[i];
+    dk::ar::output(info[i / samples], L, out[i].fdo);
+    // lane status -> ABI status: 0 consistent, 1 not consistent, 2 reference panic, 3 unfinished
+    status[i] = L.status == dk::ar::CONSISTENT ? 0 : L.status == dk::ar::NOT_CONSISTENT ? 1 : L.status == dk::ar::PANIC ? 2 : 3;
+    reason[i] = L.reason;
+}
+
 // PolicyFusionMaxN / PolicyFusionAverageStrategy accumulators (policy_fusion.rs:23-123).
 // One thread per (infostate, action).
 __global__ void fuse_accumulate_kernel(const uint32_t* visits, uint32_t n_info, uint32_t samples,
@@ -558,6 +602,11 @@ struct dk_ctx {
     dk::az::Game* az_games = nullptr;
     size_t az_bytes = 0;
     uint32_t az_n = 0, az_iters = 0, az_cap_nodes = 0, az_cap_states = 0, az_done = 0;
+    // IMPI autoregressive determinization (dk_ar_*): one lane per (infostate, sample)
+    dk::ar::Lane* ar_lanes = nullptr;
+    const dk_az_state* ar_info = nullptr;
+    uint32_t ar_cap = 0, ar_n = 0, ar_samples = 0;
+    float ar_log_chance = 0.0f;
     int az_epoch = 0;
     bool az_root_done = false;
     std::vector<void*> scratch;
@@ -752,6 +801,7 @@ void dk_destroy(dk_ctx* ctx) {
     if (ctx->queue) (void)hipFree(ctx->queue);
     if (ctx->prof) (void)hipFree(ctx->prof);
     if (ctx->az_nodes) (void)hipFree(ctx->az_nodes);
+    if (ctx->ar_lanes) (void)hipFree(ctx->ar_lanes);
     if (ctx->az_states) (void)hipFree(ctx->az_states);
     if (ctx->az_games) (void)hipFree(ctx->az_games);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
@@ -1170,6 +1220,57 @@ int dk_az_finish_async(dk_ctx* ctx, int temperature_mode, float temperature, uin
     hipLaunchKernelGGL(az_finish_kernel, dim3(grid_for(ctx->az_n, 64)), dim3(64), 0, pick(ctx, stream), temperature_mode,
                        temperature, ctx->az_n, ctx->az_nodes, ctx->az_states, ctx->az_games, ctx->az_cap_nodes,
                        ctx->az_cap_states, d_visits, d_action);
+    DK_HIP(hipGetLastError());
+    return DK_OK;
+}
+
+// ---------------------------------------------------------------- IMPI autoregressive determinization
+int dk_ar_begin_async(dk_ctx* ctx, const dk_az_state* d_infostates, uint32_t n_info, uint32_t samples,
+                      const uint64_t* d_seeds, float log_chance, uint32_t* d_rounds, void* stream) {
+    if (!ctx || !d_infostates || !d_seeds || !d_rounds || samples == 0) return DK_E_INVALID;
+    const uint64_t n64 = (uint64_t)n_info * samples;
+    if (n64 > 0xFFFFFFFFull / dk::ar::TOKENS) return DK_E_INVALID;
+    const uint32_t n = (uint32_t)n64;
+    hipStream_t st = pick(ctx, stream);
+    if (n > ctx->ar_cap) {
+        (void)hipStreamSynchronize(st);
+        if (ctx->ar_lanes) (void)hipFree(ctx->ar_lanes);
+        ctx->ar_lanes = nullptr; ctx->ar_cap = 0;
+        if (hipMalloc(&ctx->ar_lanes, (size_t)n * sizeof(dk::ar::Lane)) != hipSuccess) return ctx->last_error = DK_E_CAPACITY;
+        ctx->ar_cap = n;
+    }
+    ctx->ar_info = d_infostates; ctx->ar_n = n; ctx->ar_samples = samples; ctx->ar_log_chance = log_chance;
+    DK_HIP(hipMemsetAsync(d_rounds, 0, sizeof(uint32_t), st));
+    if (n == 0) return DK_OK;
+    hipLaunchKernelGGL(ar_begin_kernel, dim3(grid_for(n, 64)), dim3(64), 0, st, d_infostates, samples, d_seeds, n,
+                       ctx->ar_lanes, d_rounds);
+    DK_HIP(hipGetLastError());
+    return DK_OK;
+}
+
+int dk_ar_prepare_async(dk_ctx* ctx, int32_t* d_tokens, void* stream) {
+    if (!ctx || !ctx->ar_info || !d_tokens) return DK_E_INVALID;
+    if (ctx->ar_n == 0) return DK_OK;
+    hipLaunchKernelGGL(ar_prepare_kernel, dim3(grid_for(ctx->ar_n, 64)), dim3(64), 0, pick(ctx, stream), ctx->ar_info,
+                       ctx->ar_samples, ctx->ar_n, ctx->ar_lanes, ctx->ar_log_chance, d_tokens);
+    DK_HIP(hipGetLastError());
+    return DK_OK;
+}
+
+int dk_ar_choose_async(dk_ctx* ctx, const float* d_logits, float temperature, void* stream) {
+    if (!ctx || !ctx->ar_info || !d_logits) return DK_E_INVALID;
+    if (ctx->ar_n == 0) return DK_OK;
+    hipLaunchKernelGGL(ar_choose_kernel, dim3(grid_for(ctx->ar_n, 64)), dim3(64), 0, pick(ctx, stream), ctx->ar_n,
+                       ctx->ar_lanes, d_logits, temperature);
+    DK_HIP(hipGetLastError());
+    return DK_OK;
+}
+
+int dk_ar_output_async(dk_ctx* ctx, dk_state* d_out, uint8_t* d_status, uint8_t* d_reason, void* stream) {
+    if (!ctx || !ctx->ar_info || !d_out || !d_status || !d_reason) return DK_E_INVALID;
+    if (ctx->ar_n == 0) return DK_OK;
+    hipLaunchKernelGGL(ar_output_kernel, dim3(grid_for(ctx->ar_n, 64)), dim3(64), 0, pick(ctx, stream), ctx->ar_info,
+                       ctx->ar_samples, ctx->ar_n, ctx->ar_lanes, d_out, d_status, d_reason);
     DK_HIP(hipGetLastError());
     return DK_OK;
 }

@@ -101,6 +101,26 @@ DK_HD int trick_start(const dk_fdo_state& s, int t) {
     return t == 0 ? (int)s.res_start : (int)((s.trick_winners >> (2 * (t - 1))) & 3);
 }
 
+// Per-player facts of the card history: club queens played, and the colours a
+// player failed to follow (gather_impossible_colors.rs:11-43; bit = FdoColor).
+DK_HD void history_facts(const dk_fdo_state& s, int played_q[4], uint32_t impossible[4]) {
+    for (int p = 0; p < 4; ++p) { played_q[p] = 0; impossible[p] = 0; }
+    const int gt = s.game_type;
+    for (int t = 0; t < s.n_tricks; ++t) {
+        const int start = trick_start(s, t);
+        const int first = 4 * t;
+        const int len = s.card_index - first < 4 ? s.card_index - first : 4;
+        if (len <= 0) continue;
+        const uint32_t tc = gt == DK_NONE ? 0xFF : fdo::card_color(s.cards[first], (uint32_t)gt);
+        for (int i = 0; i < len; ++i) {
+            const int c = s.cards[first + i];
+            const int p = (start + i) & 3;
+            if (c == fdo::CLUB_QUEEN) played_q[p] += 1;
+            if (gt != DK_NONE && fdo::card_color(c, (uint32_t)gt) != tc) impossible[p] |= 1u << tc;
+        }
+    }
+}
+
 // visible_reservations_logic.rs:7-66 (zero-oriented result in out[4])
 DK_HD void visible_reservations(const dk_fdo_state& s, int observing, uint8_t out[4]) {
     enum { V_WEDDING = 0, V_HEALTHY = 1, V_NOTREV = 2, V_NONE = 10 };
@@ -153,22 +173,10 @@ DK_HD void card_matching_full(const dk_fdo_state& s, Rng& rng, dk_fdo_state& out
     }
     st.possible[cur] = 0;
     // per-player history facts
-    int played_q[4] = {0, 0, 0, 0};
-    uint32_t impossible[4] = {0, 0, 0, 0};
+    int played_q[4];
+    uint32_t impossible[4];
+    history_facts(s, played_q, impossible);
     const int gt = s.game_type;
-    for (int t = 0; t < s.n_tricks; ++t) {
-        const int start = trick_start(s, t);
-        const int first = 4 * t;
-        const int len = s.card_index - first < 4 ? s.card_index - first : 4;
-        if (len <= 0) continue;
-        const uint32_t tc = gt == DK_NONE ? 0xFF : fdo::card_color(s.cards[first], (uint32_t)gt);
-        for (int i = 0; i < len; ++i) {
-            const int c = s.cards[first + i];
-            const int p = (start + i) & 3;
-            if (c == fdo::CLUB_QUEEN) played_q[p] += 1;
-            if (gt != DK_NONE && fdo::card_color(c, (uint32_t)gt) != tc) impossible[p] |= 1u << tc;
-        }
-    }
     if (gt != DK_NONE) {
         for (int p = 0; p < 4; ++p) {
             if (p == cur) continue;

@@ -17,6 +17,7 @@
 #include "az_eval.hpp"
 #include "az_mcts.hpp"
 #include "encode_pi.hpp"
+#include "impi.hpp"
 #include "full_doko.hpp"
 #include "fusion.hpp"
 #include "mcts.hpp"
@@ -328,7 +329,7 @@ void or_encode_pi(void* sp, int64_t* out) { enc::encode_state_pi(*(fdo::State*)s
 // f[0] res_start, f[1] res_len, f[2..5] res, f[6] n_tricks, f[7 + 6t ..] = {start, len, c0..c3} for t < 12,
 // f[79] ann_n, f[80 + 3k ..] = {card_index, player, announcement bit} for k < 12,
 // f[116] current_player, f[117] phase, f[118] re_players.
-void or_encode_pi_fields(const int32_t* f, const uint64_t* hands, int64_t* out) {
+static fdo::State state_from_fields(const int32_t* f, const uint64_t* hands) {
     fdo::State s;
     s.res_start = f[0]; s.res_len = f[1];
     for (int i = 0; i < 4; ++i) s.res[i] = f[2 + i];
@@ -347,7 +348,10 @@ void or_encode_pi_fields(const int32_t* f, const uint64_t* hands, int64_t* out) 
     }
     s.current_player = f[116]; s.phase = f[117];
     s.team_state.kind = fdo::NoWedding; s.team_state.re_players = (uint8_t)f[118];
-    enc::encode_state_pi(s, out);
+    return s;
+}
+void or_encode_pi_fields(const int32_t* f, const uint64_t* hands, int64_t* out) {
+    enc::encode_state_pi(state_from_fields(f, hands), out);
 }
 
 // ---------------------------------------------------------------- tic-tac-toe
@@ -374,4 +378,44 @@ void or_ttt_pack(const int32_t* board, int last_action, uint8_t* out) {
 int or_fuse_maxn(const uint32_t* visits, int S, uint64_t allowed, uint32_t* ranks) { return fuse_maxn(visits, S, allowed, ranks); }
 int or_fuse_avg(const uint32_t* visits, int S, float* probs) { return fuse_avg(visits, S, probs); }
 
+
+// ---------------------------------------------------------------- IMPI (autoregressive determinization)
+static void ipi_assumed(const uint64_t* ah, const int32_t* ar, fdo::Hand h[4], int r[4]) {
+    for (int p = 0; p < 4; ++p) { h[p].bits = ah[p]; r[p] = ar[p]; }
+}
+int or_ipi_encode(void* sp, const uint64_t* ah, const int32_t* ar, int guess, int64_t* out) {
+    fdo::Hand h[4]; int r[4]; ipi_assumed(ah, ar, h, r);
+    return impi::encode_state_ipi(*(fdo::State*)sp, h, r, guess, out);
+}
+int or_encode_ipi_fields(const int32_t* f, const uint64_t* hands, const uint64_t* ah, const int32_t* ar, int guess, int64_t* out) {
+    fdo::Hand h[4]; int r[4]; ipi_assumed(ah, ar, h, r);
+    return impi::encode_state_ipi(state_from_fields(f, hands), h, r, guess, out);
+}
+uint64_t or_ipi_next_card(void* sp, const uint64_t* ah, const int32_t* ar, int p) {
+    fdo::Hand h[4]; int r[4]; ipi_assumed(ah, ar, h, r);
+    return impi::next_possible_card(*(fdo::State*)sp, h, r, p).bits;
+}
+uint32_t or_ipi_next_reservation(void* sp, const uint64_t* ah, int p) {
+    fdo::Hand h[4]; int r[4]; const int32_t none[4] = {-1, -1, -1, -1}; ipi_assumed(ah, none, h, r);
+    return impi::next_possible_reservation(*(fdo::State*)sp, h, p);
+}
+int or_ipi_consistent(void* sp, const uint64_t* ah, const int32_t* ar) {
+    fdo::Hand h[4]; int r[4]; ipi_assumed(ah, ar, h, r);
+    return impi::is_consistent_reason(*(fdo::State*)sp, h, r);
+}
+void or_ipi_hash_eval(const int64_t* tok, float* logits) { impi::hash_eval(tok, logits); }
+// forward_pred_process_with_mask with the hash network.  Returns the status (0 consistent,
+// 1 not consistent, 2 reference panic); *reason, the packed sample (consistent only), and
+// the number of network evaluations.
+int or_ipi_sample(void* sp, uint64_t* rng_state, float temperature, float log_chance, int32_t* reason, uint8_t* out,
+                  int32_t* guesses) {
+    SmallRng r = rng_from(rng_state);
+    const impi::ArResult a = impi::forward_pred_process_with_mask(
+        *(fdo::State*)sp, temperature, log_chance, [](const int64_t* t, float* l) { impi::hash_eval(t, l); }, r);
+    rng_to(r, rng_state);
+    *reason = a.reason;
+    *guesses = a.guesses;
+    if (a.status == 0) or_fdo_pack((void*)&a.state, out);
+    return a.status;
+}
 }  // extern "C"

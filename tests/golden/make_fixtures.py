@@ -367,16 +367,9 @@ FDO_RES = ["Healthy", "Wedding", "DiamondsSolo", "HeartsSolo", "SpadesSolo", "Cl
 ANN_BITS = {"ReContra": 1, "No90": 2, "No60": 4, "No30": 8, "Black": 16, "CounterReContra": 32}
 
 
-def encode_pi_kat():
-    """rs-doko-networks/src/full_doko/var1/encode_pi.rs:237-797 (test_encode_state):
-    the state's fields and the expected 311 tokens, the latter evaluated from the
-    test's 311 helper-call assertions with the helpers' own token tables."""
-    path = os.path.join(REF, "rs-doko-networks/src/full_doko/var1/encode_pi.rs")
-    with open(path, encoding="utf-8") as fh:
-        text = fh.read()
-    t = text[text.find("fn test_encode_state"):]
+def _kat_state(t):
+    """Fields of the FdoState literal of an encoder test (tricks, hands, announcements ...)."""
     card = lambda n: CARD_NAMES.index(n.split("::")[-1].strip())
-    pl = lambda n: PLAYERS[n.split("::")[-1].strip()]
     m = re.search(r"reservations: PlayerOrientedVec::from_full\(FdoPlayer::(\w+), vec!\[(.*?)\]\)", t, re.S)
     res_start = PLAYERS[m.group(1)]
     res = [FDO_RES.index(x.strip().split("::")[-1]) for x in m.group(2).split(",") if x.strip()]
@@ -384,12 +377,7 @@ def encode_pi_kat():
     for sp, cs in re.findall(r"FdoTrick \{\s*cards: PlayerOrientedVec::from_full\(FdoPlayer::(\w+), vec!\[(.*?)\]\)", t, re.S):
         tricks.append({"start": PLAYERS[sp], "cards": [card(x) for x in cs.split(",") if x.strip()]})
     hm = re.search(r"hands: PlayerZeroOrientedArr::from_full\(\[(.*?)\]\),\s*announcements", t, re.S).group(1)
-    hands = []
-    for cs in re.findall(r"FdoHand::from_vec\(vec!\[(.*?)\]\)", hm, re.S):
-        h = 0
-        for c in [card(x) for x in cs.split(",") if x.strip()]:
-            h |= (1 << (c + 24)) if (h >> c) & 1 else (1 << c)
-        hands.append(h)
+    hands = _hands_of(hm)
     anns = [{"card_index": int(ci), "player": PLAYERS[p], "bit": ANN_BITS[a]}
             for ci, p, a in re.findall(r"FdoAnnouncementOccurrence \{\s*card_index: (\d+),\s*player: FdoPlayer::(\w+),\s*"
                                        r"announcement: (\w+),", t, re.S)]
@@ -398,6 +386,25 @@ def encode_pi_kat():
     re_players = 0
     for p in re.findall(r"FdoPlayer::(\w+)", re.search(r"re_players: FdoPlayerSet::from_vec\(vec!\[(.*?)\]\)", t).group(1)):
         re_players |= 1 << PLAYERS[p]
+    return {"res_start": res_start, "res": res, "tricks": tricks, "hands": hands, "announcements": anns,
+            "current_player": cur, "phase": phase, "re_players": re_players}
+
+
+def _hands_of(text):
+    """FdoHand::from_vec literals -> FdoHand bits (add: first copy, then second copy)."""
+    card = lambda n: CARD_NAMES.index(n.split("::")[-1].strip())
+    hands = []
+    for cs in re.findall(r"FdoHand::from_vec\(vec!\[(.*?)\]\)", text, re.S):
+        h = 0
+        for c in [card(x) for x in cs.split(",") if x.strip()]:
+            h |= (1 << (c + 24)) if (h >> c) & 1 else (1 << c)
+        hands.append(h)
+    return hands
+
+
+def _kat_tokens(t):
+    """The expected tokens: the test's assert_eq_inc! helper calls, evaluated with the helpers' tables."""
+    pl = lambda n: PLAYERS[n.split("::")[-1].strip()]
     tab = _var2_tables()
 
     def ev(fn, arg):
@@ -432,9 +439,43 @@ def encode_pi_kat():
     calls = re.findall(r"assert_eq_inc!\(result\[i\.\.i\+1\], (\w+)\((.*?)\)\);", t)
     tokens = [ev(fn, arg) for fn, arg in calls]
     assert len(tokens) == 311
-    return {"source": "rs-doko-networks/src/full_doko/var1/encode_pi.rs:237-797",
-            "res_start": res_start, "res": res, "tricks": tricks, "hands": hands, "announcements": anns,
-            "current_player": cur, "phase": phase, "re_players": re_players, "expect": tokens}
+    return tokens
+
+
+def encode_pi_kat():
+    """rs-doko-networks/src/full_doko/var1/encode_pi.rs:237-797 (test_encode_state):
+    the state's fields and the expected 311 tokens, the latter evaluated from the
+    test's 311 helper-call assertions with the helpers' own token tables."""
+    path = os.path.join(REF, "rs-doko-networks/src/full_doko/var1/encode_pi.rs")
+    with open(path, encoding="utf-8") as fh:
+        text = fh.read()
+    t = text[text.find("fn test_encode_state"):]
+    out = {"source": "rs-doko-networks/src/full_doko/var1/encode_pi.rs:237-797"}
+    out.update(_kat_state(t))
+    out["expect"] = _kat_tokens(t)
+    return out
+
+
+def encode_ipi_kat():
+    """rs-doko-networks/src/full_doko/var1/encode_ipi.rs:307-888 (test_encode_state): the
+    state, the assumed hands / reservations and the player to guess for, and the
+    expected 311 tokens (evaluated from the test's helper-call assertions)."""
+    path = os.path.join(REF, "rs-doko-networks/src/full_doko/var1/encode_ipi.rs")
+    with open(path, encoding="utf-8") as fh:
+        text = fh.read()
+    t = text[text.find("fn test_encode_state"):]
+    out = {"source": "rs-doko-networks/src/full_doko/var1/encode_ipi.rs:307-888"}
+    out.update(_kat_state(t))
+    call = t[t.find("let result = encode_state_ipi("):]
+    call = call[:call.find(");")]
+    out["assumed_hands"] = _hands_of(call)
+    rm = re.search(r"PlayerZeroOrientedArr::from_full\(\s*\[(.*?)\]\s*\),\s*FdoPlayer::(\w+)",
+                   call[call.rfind("PlayerZeroOrientedArr::from_full("):], re.S)
+    out["assumed_res"] = [-1 if x.strip() == "None" else FDO_RES.index(re.search(r"FdoReservation::(\w+)", x).group(1))
+                          for x in rm.group(1).split(",") if x.strip()]
+    out["guess"] = PLAYERS[rm.group(2)]
+    out["expect"] = _kat_tokens(t)
+    return out
 
 
 def main():
@@ -454,6 +495,8 @@ def main():
         json.dump(do_assignment_kats(), fh, indent=None)
     with open(os.path.join(OUT, "encode_pi_kat.json"), "w") as fh:
         json.dump(encode_pi_kat(), fh, indent=None)
+    with open(os.path.join(OUT, "encode_ipi_kat.json"), "w") as fh:
+        json.dump(encode_ipi_kat(), fh, indent=None)
     print("wrote fixtures to", OUT)
 
 

@@ -86,6 +86,13 @@ def lib():
             "or_encode_pi": (None, [vp, ctypes.POINTER(ctypes.c_int64)]),
             "or_fdo_pack_az": (None, [vp, u8p]),
             "or_encode_pi_fields": (None, [i32p, u64p, ctypes.POINTER(ctypes.c_int64)]),
+            "or_encode_ipi_fields": (ctypes.c_int, [i32p, u64p, u64p, i32p, ctypes.c_int, ctypes.POINTER(ctypes.c_int64)]),
+            "or_ipi_encode": (ctypes.c_int, [vp, u64p, i32p, ctypes.c_int, ctypes.POINTER(ctypes.c_int64)]),
+            "or_ipi_next_card": (ctypes.c_uint64, [vp, u64p, i32p, ctypes.c_int]),
+            "or_ipi_next_reservation": (ctypes.c_uint32, [vp, u64p, ctypes.c_int]),
+            "or_ipi_consistent": (ctypes.c_int, [vp, u64p, i32p]),
+            "or_ipi_hash_eval": (None, [ctypes.POINTER(ctypes.c_int64), f32p]),
+            "or_ipi_sample": (ctypes.c_int, [vp, u64p, ctypes.c_float, ctypes.c_float, i32p, u8p, i32p]),
             "or_ttt_finish": (ctypes.c_int, [i32p]),
             "or_ttt_rollout": (None, [i32p, u64p, f64p]),
             "or_ttt_search": (ctypes.c_int, [i32p, u64p, ctypes.c_uint32, ctypes.c_double, u32p, f64p]),
@@ -203,6 +210,34 @@ class FdoState:
         o = arr(ctypes.c_int64, 311)
         lib().or_encode_pi(self.h, o)
         return list(o)
+
+    def ipi_encode(self, hands, res, guess):
+        """encode_state_ipi (rs-doko-networks/src/full_doko/var1/encode_ipi.rs:48-282) -> 311 tokens
+        (None where the reference panics)."""
+        o = arr(ctypes.c_int64, 311)
+        ok = lib().or_ipi_encode(self.h, arr(ctypes.c_uint64, 4, hands), arr(ctypes.c_int32, 4, res), guess, o)
+        return list(o) if ok else None
+
+    def ipi_next_card(self, hands, res, p):
+        """next_possible_card (rs-doko-impi/src/next_consistent.rs:25-139) -> FdoHand bits."""
+        return lib().or_ipi_next_card(self.h, arr(ctypes.c_uint64, 4, hands), arr(ctypes.c_int32, 4, res), p)
+
+    def ipi_next_reservation(self, hands, p):
+        """next_possible_reservation (next_consistent.rs:141-193) -> bit set over FdoReservation."""
+        return lib().or_ipi_next_reservation(self.h, arr(ctypes.c_uint64, 4, hands), p)
+
+    def ipi_consistent(self, hands, res):
+        """_is_consistent (rs-full-doko/src/matching/is_consistent.rs:38-305) -> reason or -1."""
+        return lib().or_ipi_consistent(self.h, arr(ctypes.c_uint64, 4, hands), arr(ctypes.c_int32, 4, res))
+
+    def ipi_sample(self, rng, temperature, log_chance=1.0 / 30000.0):
+        """forward_pred_process_with_mask (rs-doko-impi/src/forward.rs:392-661) with the hash
+        network -> (status, reason, packed sample or None, network evaluations)."""
+        reason = arr(ctypes.c_int32, 1)
+        g = arr(ctypes.c_int32, 1)
+        o = arr(ctypes.c_uint8, 128)
+        st = lib().or_ipi_sample(self.h, rng, temperature, log_chance, reason, o, g)
+        return st, reason[0], (bytes(o) if st == 0 else None), g[0]
 
     def az_take_action(self, a):
         """FdoAzEnvState::take_action_by_action_index(a, skip_single=true)."""
@@ -359,8 +394,7 @@ def az_hash_eval_np(packed):
     return (value.astype(np.float32) * np.float32(0.125)), (np.stack(logits, axis=1).astype(np.float32) * np.float32(0.25))
 
 
-def encode_pi_fields(res_start, res, tricks, hands, announcements, current_player, phase, re_players):
-    """encode_state_pi of a state given by the fields the encoder reads (the encode_pi.rs test layout)."""
+def _state_fields(res_start, res, tricks, announcements, current_player, phase, re_players):
     f = [0] * 119
     f[0], f[1] = res_start, len(res)
     for i, r in enumerate(res):
@@ -373,6 +407,33 @@ def encode_pi_fields(res_start, res, tricks, hands, announcements, current_playe
     for k, a in enumerate(announcements):
         f[80 + 3 * k:83 + 3 * k] = [a["card_index"], a["player"], a["bit"]]
     f[116], f[117], f[118] = current_player, phase, re_players
+    return arr(ctypes.c_int32, 119, f)
+
+
+def encode_pi_fields(res_start, res, tricks, hands, announcements, current_player, phase, re_players):
+    """encode_state_pi of a state given by the fields the encoder reads (the encode_pi.rs test layout)."""
     o = arr(ctypes.c_int64, 311)
-    lib().or_encode_pi_fields(arr(ctypes.c_int32, 119, f), arr(ctypes.c_uint64, 4, hands), o)
+    lib().or_encode_pi_fields(_state_fields(res_start, res, tricks, announcements, current_player, phase, re_players),
+                              arr(ctypes.c_uint64, 4, hands), o)
     return list(o)
+
+
+def encode_ipi_fields(res_start, res, tricks, hands, announcements, current_player, phase, re_players,
+                      assumed_hands, assumed_res, guess):
+    """encode_state_ipi of a state given by its fields (the encode_ipi.rs test layout)."""
+    o = arr(ctypes.c_int64, 311)
+    ok = lib().or_encode_ipi_fields(_state_fields(res_start, res, tricks, announcements, current_player, phase, re_players),
+                                    arr(ctypes.c_uint64, 4, hands), arr(ctypes.c_uint64, 4, assumed_hands),
+                                    arr(ctypes.c_int32, 4, assumed_res), guess, o)
+    return list(o) if ok else None
+
+
+def ipi_hash_eval_np(tokens):
+    """The oracle's synthetic IMPI network (oracle/impi.hpp hash_eval) over [n, 311] tokens -> [n, 33] f32."""
+    import numpy as np
+    t = np.ascontiguousarray(tokens, dtype=np.int64).reshape(-1, 311)
+    out = np.zeros((t.shape[0], 33), dtype=np.float32)
+    for i in range(t.shape[0]):
+        lib().or_ipi_hash_eval(t[i].ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                               out[i].ctypes.data_as(ctypes.POINTER(ctypes.c_float)))
+    return out

@@ -148,3 +148,13 @@ def test_oracle_samples_consistent():
         for k in range(5):
             smp = s.card_matching(ol.rng_seed(1000 * g + k))
             assert s.consistent_sample(smp)
+
+
+def test_ar_engine_vs_oracle(native_bins):
+    """ar_engine.h (host build, driven in lockstep rounds like the GPU) = oracle
+    forward_pred_process_with_mask with the hash network: status, reason, sample, network
+    calls and RNG stream position per lane, at temperatures 1, 0.35 and 4."""
+    out = subprocess.run([os.path.join(NATIVE, "ar_check"), "200", "3", "9"], capture_output=True, text=True, check=True).stdout
+    assert out.startswith("OK"), out
+    lanes, ok, bad, panic = map(int, out.split()[1:5])
+    assert lanes == 1800 and ok > 1000 and bad > 20

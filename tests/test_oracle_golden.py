@@ -210,3 +210,76 @@ def test_encode_state_pi_golden():
     got = ol.encode_pi_fields(g["res_start"], g["res"], g["tricks"], g["hands"], g["announcements"],
                               g["current_player"], g["phase"], g["re_players"])
     assert got == g["expect"]
+
+
+def test_encode_state_ipi_golden():
+    """rs-doko-networks/src/full_doko/var1/encode_ipi.rs:307-888 — all 311 tokens of the
+    reference's IMPI encoder test (assumed hands with one unknown card, an assumed hidden
+    solo, guessing for RIGHT)."""
+    g = load("encode_ipi_kat.json")
+    got = ol.encode_ipi_fields(g["res_start"], g["res"], g["tricks"], g["hands"], g["announcements"],
+                               g["current_player"], g["phase"], g["re_players"], g["assumed_hands"],
+                               g["assumed_res"], g["guess"])
+    assert got == g["expect"]
+
+
+def _fdo_res_zero(packed):
+    """Zero-oriented real reservations (None = -1) from a packed dk_fdo_state."""
+    start, n = packed[96], packed[97]
+    out = [-1] * 4
+    for i in range(n):
+        out[(start + i) % 4] = packed[92 + i]
+    return out
+
+
+def _hand_cards(h):
+    return [(b if b < 24 else b - 24) for b in range(48) if (h >> b) & 1]
+
+
+def _hand_remove(h, c):   # FdoHand::remove: the second copy first (hand.rs:235-247)
+    return h & ~(1 << (c + 24)) if (h >> (c + 24)) & 1 else h & ~(1 << c)
+
+
+def test_ipi_next_possible_reverse_property():
+    """rs-doko-impi/src/next_consistent.rs:209-379 (test_next / reverse_pred_process) on the
+    oracle restatement: along random games over all legal actions, hide the other players'
+    reservations and then their true cards one at a time (players cp+3, cp+2, cp+1 per
+    round); every hidden true card must stay in next_possible_card and every true
+    reservation in next_possible_reservation.  The true deal is consistent (_is_consistent)."""
+    import random
+    rnd = random.Random(11)
+    checked = 0
+    for g in range(60):
+        s = ol.FdoState.new_game(0xA11CE + g)
+        while s.info()["phase"] != 3:
+            info = s.info()
+            cp = info["current_player"]
+            hands = s.hands()
+            res = _fdo_res_zero(s.pack())
+            assert s.ipi_consistent(hands, res) == -1
+            r = list(res)
+            for i in (3, 2, 1):
+                p = (cp + i) % 4
+                target = r[p]
+                r[p] = -1
+                if target >= 0:
+                    assert (s.ipi_next_reservation(hands, p) >> target) & 1
+            h = list(hands)
+            for _ in range(12):
+                for i in (3, 2, 1):
+                    p = (cp + i) % 4
+                    if h[p] == 0:
+                        continue
+                    target = rnd.choice(_hand_cards(h[p]))
+                    h[p] = _hand_remove(h[p], target)
+                    npo = s.ipi_next_card(h, r, p)
+                    hidden = [c for c in range(24) if ((hands[p] >> c) & 1) + ((hands[p] >> (c + 24)) & 1)
+                              > ((h[p] >> c) & 1) + ((h[p] >> (c + 24)) & 1)]
+                    assert target in hidden
+                    for c in hidden:
+                        assert (npo >> c) & 1 or (npo >> (c + 24)) & 1, (g, p, c)
+                    checked += 1
+            legal = s.allowed()
+            acts = [a for a in range(39) if legal >> a & 1]
+            s.play(rnd.choice(acts))
+    assert checked > 10000
