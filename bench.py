@@ -36,12 +36,15 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--workload", choices=["c3", "c2", "c2d", "c5"], default="c3",
+    p.add_argument("--workload", choices=["c3", "c2", "c2d", "c5", "impi"], default="c3",
                    help="c3: rs-full-doko + CAP (default, the metric's config); c2: rs-doko roots after 4x Healthy; "
                         "c2d: rs-doko infostates determinized by the rule-based sampler; "
-                        "c5: AlphaZero self-play moves (PUCT + policy/value network)")
+                        "c5: AlphaZero self-play moves (PUCT + policy/value network); "
+                        "impi: autoregressive (IMPI) determinization of the c3 infostates with the IMPI network")
     p.add_argument("--games", type=int, default=8192, help="concurrent self-play games per GPU (c5)")
     p.add_argument("--az-iterations", type=int, default=200, help="PUCT iterations per move (c5)")
+    p.add_argument("--ar-samples", type=int, default=4, help="AR samples per infostate (impi)")
+    p.add_argument("--ar-temperature", type=float, default=0.4, help="AR sampling temperature (impi; all_policies.rs:30)")
     p.add_argument("--iterations", type=int, default=1000)
     p.add_argument("--infostates", type=int, default=4096,
                    help="infostates per GPU (c3): 4096 x 64 samples = 262,144 roots, streamed through the resident waves' node pools (131,072 roots)")
@@ -175,6 +178,8 @@ def main():
 
     if args.workload == "c5":
         return run_c5(args, dk, L, dev, stream, rank, world, local_rank, dist)
+    if args.workload == "impi":
+        return run_impi(args, dk, L, dev, stream, rank, world, local_rank, dist)
     eng, step, n_roots, bufs = make_workload(args, dk, L, dev, sp, rank, world, local_rank, dist)
     determinized = args.workload in ("c3", "c2d")
     search_ms = []
@@ -393,6 +398,122 @@ def run_c5(args, dk, L, dev, stream, rank, world, local_rank, dist):
                          "frac": achieved / 2500.0, "traffic": None,
                          "note": "network GEMMs/attention: %.1f MFLOP per leaf evaluation (algorithmic), bf16 dense "
                                  "peak; achieved over the network's event-timed share of the step" % (flop / 1e6)},
+            "cpu_baseline": None,
+        }
+        print(json.dumps(result))
+    if world > 1:
+        dist.destroy_process_group()
+    eng.close()
+    return result
+
+
+def impi_flop_per_eval(d=256, seq=62, blocks=4, classes=33):
+    """Algorithmic FLOPs of one DokoImpiNet evaluation (create_ar.py:12-18 configuration)."""
+    return az_flop_per_eval(d=d, seq=seq, blocks=blocks, classes=classes)
+
+
+def run_impi(args, dk, L, dev, stream, rank, world, local_rank, dist):
+    """§8(f) row 4: the ARSampling SamplingFn (compare_impi.rs:84-105), i.e.
+    forward_pred_process_with_mask (rs-doko-impi/src/forward.rs:392-661), for
+    `ar_samples` draws of each of the C3 infostates (4096 per GPU, 4 x Healthy then
+    k in {0, 8, 20, 32} random plies).  One step = every card and hidden reservation
+    of every sample guessed by the IMPI network (DokoImpiNet, d 256, 4 blocks, bf16),
+    one batched network call per round, temperature 0.4 (all_policies.rs:30), then the
+    consistency check.  Infostates are independent: N GPUs run N replicas."""
+    import torch
+    from master_doko_reinforcement_learning_amd.impi_network import DokoImpiNet
+    torch.manual_seed(4321 + rank)
+    I, S = args.infostates, args.ar_samples
+    eng = dk.Engine(device=local_rank, max_roots=64, max_iterations=1)
+    sp = stream.cuda_stream
+
+    def ck(rc):
+        if rc != 0:
+            raise RuntimeError("doko_amd error %d: %s" % (rc, L.dk_status_string(rc).decode()))
+
+    info_seeds = torch.tensor((np.arange(I, dtype=np.uint64) + np.uint64(0xC3000000 + rank * I)).view(np.int64), device=dev)
+    info = torch.zeros((I, 128), dtype=torch.uint8, device=dev)
+    ck(L.dk_new_game_batch_async(eng.ctx, dk.GAME_FULL_DOKO, info_seeds.data_ptr(), I, info.data_ptr(), sp))
+    a = torch.full((I,), 1 << 24, dtype=torch.int64, device=dev)
+    for _ in range(4):
+        ck(L.dk_env_step_batch_async(eng.ctx, info.data_ptr(), a.data_ptr(), I, sp))
+    plies = torch.tensor(np.array([[0, 8, 20, 32][j % 4] for j in range(I)], dtype=np.uint32).view(np.int32), device=dev)
+    ply_rng = torch.tensor(dk.splitmix_rng_states(np.arange(I, dtype=np.uint64) + np.uint64(0xC3100000 + rank * I)).view(np.int64),
+                           device=dev)
+    ck(L.dk_env_random_plies_batch_async(eng.ctx, info.data_ptr(), ply_rng.data_ptr(), plies.data_ptr(), I, sp))
+    records = dk.az_records(eng, info)
+    net = DokoImpiNet().to(dev).eval().bfloat16()
+    ev = []
+
+    def network(tokens):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        out = net(tokens)
+        e1.record()
+        ev.append((e0, e1))
+        return out
+
+    ar = dk.ARSampling(eng, network, args.ar_temperature)
+    seeds = np.arange(I * S, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15) + np.uint64(0xA5000000 + rank)
+    stats = {"rows": 0, "consistent": 0, "lanes": 0}
+
+    def step():
+        with torch.inference_mode():
+            _, status, _ = ar.sample(records, S, seeds)
+        stats["rows"] += ar.rows
+        stats["consistent"] += int((status == 0).sum().item())
+        stats["lanes"] += I * S
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    ev.clear()
+    stats.update(rows=0, consistent=0, lanes=0)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    net_ms = sum(e0.elapsed_time(e1) for e0, e1 in ev)
+    flop = impi_flop_per_eval()
+    result = None
+    if rank == 0:
+        achieved = flop * stats["rows"] / (net_ms / 1e3) / 1e12
+        result = {
+            "metric": "IMPI autoregressive determinizations/sec (forward_pred_process_with_mask, one network call per guessed card)",
+            "value": I * S * args.steps * world / elapsed,
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16 network, f32 softmax / weighted draw",
+            "data": "synthetic: the C3 infostates (seeded deals, 4x Healthy, k in {0,8,20,32} random plies), "
+                    "random-initialised DokoImpiNet (d 256, 4 blocks, 4 heads)",
+            "config": {"workload": "IMPI AR determinization: %d infostates x %d samples per GPU" % (I, S),
+                       "temperature": args.ar_temperature, "network_rounds": ar.rounds,
+                       "network_rows_per_step": stats["rows"] // args.steps,
+                       "consistent_fraction": stats["consistent"] / max(1, stats["lanes"]),
+                       "parallelism": "replicas x%d" % world},
+            "network_ms_per_step": net_ms / args.steps,
+            "sampler_ms_per_step": elapsed / args.steps * 1e3 - net_ms / args.steps,
+            "roofline": {"bound": "mfma", "achieved": achieved, "peak": 2500.0, "unit": "TFLOP/s",
+                         "frac": achieved / 2500.0, "traffic": None,
+                         "note": "IMPI network: %.1f MFLOP per guess (algorithmic), rows = guesses actually needed "
+                                 "(infostates ordered by guess count, each round runs the prefix of lanes still "
+                                 "guessing); achieved over the network's event-timed share of the step" % (flop / 1e6)},
             "cpu_baseline": None,
         }
         print(json.dumps(result))

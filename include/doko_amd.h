@@ -310,9 +310,16 @@ int dk_az_finish_async(dk_ctx* ctx, int temperature_mode, float temperature, uin
  *                        d_status 0 Consistent, 1 NotConsistent (d_reason =
  *                        NotConsistentReason, is_consistent.rs:26-36), 2 where the
  *                        reference panics, 3 unfinished.
- * The infostate records must stay valid until dk_ar_output_async. */
+ * The infostate records must stay valid until dk_ar_output_async.
+ * dk_ar_guesses_async: per infostate, the number of guesses (network calls) a lane of it
+ * makes unless it stops early.  A lane with g guesses has a pending guess only in
+ * rounds 0..g-1, so with the infostates ordered by descending g the rows of round r
+ * are a prefix of the lanes and the network can run on that prefix alone (the
+ * choose kernel reads d_logits only for lanes with a pending guess). */
 int dk_ar_begin_async(dk_ctx* ctx, const dk_az_state* d_infostates, uint32_t n_info, uint32_t samples,
                       const uint64_t* d_seeds, float log_chance, uint32_t* d_rounds, void* stream);
+int dk_ar_guesses_async(dk_ctx* ctx, const dk_az_state* d_infostates, uint32_t n_info, uint32_t* d_counts,
+                        void* stream);
 int dk_ar_prepare_async(dk_ctx* ctx, int32_t* d_tokens, void* stream);
 int dk_ar_choose_async(dk_ctx* ctx, const float* d_logits, float temperature, void* stream);
 int dk_ar_output_async(dk_ctx* ctx, dk_state* d_out, uint8_t* d_status, uint8_t* d_reason, void* stream);
@@ -338,10 +345,12 @@ int dk_net_embed_ln_bf16_async(const int32_t* d_tokens, uint32_t batch, const vo
                                const void* gamma, const void* beta, float eps, void* x_out, void* h_out, void* stream);
 int dk_net_add_ln_bf16_async(void* x_io, const void* delta, uint32_t rows, uint32_t d, const void* gamma, const void* beta,
                              float eps, void* h_out, void* stream);
-/* dk_net_attn62_bf16_async: softmax(q k^T / sqrt(40)) v for the network's shape (62 tokens,
- * 4 heads x 40), q/k/v read from the fused projection qkv[batch*62][480] ([q | k | v], heads
- * contiguous), heads' outputs written to y[batch*62][160]; bf16 MFMA, one wave per (sample, head). */
-int dk_net_attn62_bf16_async(const void* qkv, void* y, uint32_t batch, void* stream);
+/* dk_net_attn62_bf16_async: softmax(q k^T / sqrt(head_dim)) v for the networks' shape (62
+ * tokens; heads x head_dim = 4 x 40 for the AlphaZero network, 4 x 64 for the IMPI network),
+ * q/k/v read from the fused projection qkv[batch*62][3d] ([q | k | v], heads contiguous), the
+ * heads' outputs written to y[batch*62][d]; bf16 MFMA, one wave per (sample, head). */
+int dk_net_attn62_bf16_async(const void* qkv, void* y, uint32_t batch, uint32_t heads, uint32_t head_dim,
+                             void* stream);
 
 /* ---- completion / errors / timing of *_async work -------------------------------
  * dk_sync: waits for the stream and returns the first device-side error

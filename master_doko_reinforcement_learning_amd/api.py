@@ -331,7 +331,8 @@ class ARSampling:
         self.network = network
         self.temperature = float(temperature)
         self.log_chance = float(log_chance)
-        self.rounds = 0
+        self.rounds = 0   # network rounds of the last sample() call
+        self.rows = 0     # network rows evaluated in it (the sum of the guesses, early stops aside)
 
     def sample(self, infostates, samples, seeds):
         """infostates: uint8 [n_info, 160] dk_az_state records (GPU); seeds: uint64 [n_info * samples].
@@ -356,24 +357,42 @@ class ARSampling:
         ctx = self.engine.ctx
         info = infostates.contiguous()
         dev = info.device
-        n = info.shape[0] * samples
-        seeds_t = torch.as_tensor(np.ascontiguousarray(seeds, dtype=np.uint64).view(np.int64), device=dev)
-        if seeds_t.shape[0] != n:
+        n_info = info.shape[0]
+        n = n_info * samples
+        seeds = np.ascontiguousarray(seeds, dtype=np.uint64)
+        if seeds.shape[0] != n:
             raise ValueError("need one seed per (infostate, sample)")
+        # order the infostates by descending number of guesses: the rows of round r are
+        # then the prefix of lanes whose infostate needs more than r guesses
+        counts = torch.empty(n_info, dtype=torch.int32, device=dev)
+        _check(L.dk_ar_guesses_async(ctx, info.data_ptr(), n_info, counts.data_ptr(), st))
+        counts = counts.cpu().numpy()
+        order = np.argsort(-counts, kind="stable")
+        sorted_counts = counts[order]
+        info_s = info[torch.as_tensor(order, device=dev)].contiguous()
+        seeds_s = seeds.reshape(n_info, samples)[order].reshape(-1)
+        seeds_t = torch.as_tensor(seeds_s.view(np.int64), device=dev)
         rounds = torch.zeros(1, dtype=torch.int32, device=dev)
         tokens = torch.zeros((n, IPI_TOKENS), dtype=torch.int32, device=dev)
-        _check(L.dk_ar_begin_async(ctx, info.data_ptr(), info.shape[0], samples, seeds_t.data_ptr(),
-                                   self.log_chance, rounds.data_ptr(), st))
-        self.rounds = int(rounds.item())
-        for _ in range(self.rounds):
+        _check(L.dk_ar_begin_async(ctx, info_s.data_ptr(), n_info, samples, seeds_t.data_ptr(), self.log_chance,
+                                   rounds.data_ptr(), st))
+        self.rounds = int(sorted_counts[0]) if n_info else 0
+        self.rows = 0
+        for r in range(self.rounds):
+            rows = samples * int(np.count_nonzero(sorted_counts > r))
             _check(L.dk_ar_prepare_async(ctx, tokens.data_ptr(), st))
-            logits = self.network(tokens).float().contiguous()
+            logits = self.network(tokens[:rows]).float().contiguous()
             _check(L.dk_ar_choose_async(ctx, logits.data_ptr(), self.temperature, st))
+            self.rows += rows
         _check(L.dk_ar_prepare_async(ctx, tokens.data_ptr(), st))
-        out = torch.empty((n, STATE_BYTES), dtype=torch.uint8, device=dev)
-        status = torch.empty(n, dtype=torch.uint8, device=dev)
-        reason = torch.empty(n, dtype=torch.uint8, device=dev)
-        _check(L.dk_ar_output_async(ctx, out.data_ptr(), status.data_ptr(), reason.data_ptr(), st))
+        out_s = torch.empty((n, STATE_BYTES), dtype=torch.uint8, device=dev)
+        status_s = torch.empty(n, dtype=torch.uint8, device=dev)
+        reason_s = torch.empty(n, dtype=torch.uint8, device=dev)
+        _check(L.dk_ar_output_async(ctx, out_s.data_ptr(), status_s.data_ptr(), reason_s.data_ptr(), st))
+        inv = torch.as_tensor(np.argsort(order), device=dev)
+        out = out_s.view(n_info, samples, STATE_BYTES)[inv].reshape(n, STATE_BYTES)
+        status = status_s.view(n_info, samples)[inv].reshape(n)
+        reason = reason_s.view(n_info, samples)[inv].reshape(n)
         _check(L.dk_sync(ctx, st))
         return out, status, reason
 

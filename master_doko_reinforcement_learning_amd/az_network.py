@@ -102,7 +102,7 @@ class ClassHead(nn.Module):
 class FusedTrunk:
     """The bf16 GPU forward of a token trunk (shared by DokoAzNet and DokoImpiNet): HIP
     kernels (csrc/az_net_kernels.h) for the embedding sum + first LayerNorm, every
-    residual add fused with the LayerNorm that follows it, and (d = 160, 4 heads) the
+    residual add fused with the LayerNorm that follows it, and (4 heads of 40 or 64) the
     62-token attention core; the GEMMs are torch (hipBLASLt).  `x` is the residual
     stream, `h` the current LayerNorm output."""
 
@@ -131,11 +131,11 @@ class FusedTrunk:
         return h
 
     def attn_delta(self, blk, h):
-        if not (self.d == 160 and blk.heads == 4):
+        if not (blk.heads == 4 and self.d // 4 in (40, 64) and self.d % 4 == 0):
             return blk.attn_delta(h)
-        qkv = blk.qkv(h)                                     # [B, 62, 480]: q | k | v, heads contiguous
+        qkv = blk.qkv(h)                                     # [B, 62, 3d]: q | k | v, heads contiguous
         y = torch.empty_like(h)
-        self.ck(self.L.dk_net_attn62_bf16_async(qkv.data_ptr(), y.data_ptr(), h.shape[0], self.st))
+        self.ck(self.L.dk_net_attn62_bf16_async(qkv.data_ptr(), y.data_ptr(), h.shape[0], 4, self.d // 4, self.st))
         w, b = blk.folded_proj()
         return F.linear(y, w, b)
 

@@ -147,12 +147,12 @@ __global__ void add_ln_kernel(uint16_t* __restrict__ x_io, const uint16_t* __res
 }
 
 // ---------------------------------------------------------------------------
-// Self-attention core of a block for the network's shape: 62 tokens, 4 heads of
-// dimension 40 (d = 160), reading q, k, v straight out of the fused qkv
-// projection [B*62, 480] and writing the heads' outputs into [B*62, 160] (no
-// permute / transpose copies).  One wave per (sample, head), bf16 MFMA
-// v_mfma_f32_32x32x16_bf16 (tokens padded to 64, head dimension to 48):
-//   X  = K Q^T   (2 x 2 tiles of 32 x 32, 3 k-steps over the head dimension):
+// Self-attention core of a block for the networks' shape: 62 tokens, H heads of
+// dimension HD (AlphaZero: 4 x 40, d = 160; IMPI: 4 x 64, d = 256), reading q, k, v
+// straight out of the fused qkv projection [B*62, 3d] and writing the heads' outputs
+// into [B*62, d] (no permute / transpose copies).  One wave per (sample, head), bf16
+// MFMA v_mfma_f32_32x32x16_bf16 (tokens padded to 64, head dimension to 16 KS):
+//   X  = K Q^T   (2 x 2 tiles of 32 x 32, KS k-steps over the head dimension):
 //        X[t][s] has the query s on the lane, the keys t in the registers;
 //   P  = softmax over t per column s (registers + one cross-half shuffle),
 //        normalised, packed to bf16 in place (the accumulator-as-operand idiom:
@@ -170,9 +170,13 @@ __device__ __forceinline__ bf16x8_t load_frag8(const uint16_t* p, bool ok) {
     return r.v;
 }
 
+template <int HD, int H>
 __global__ void __launch_bounds__(256) attn62_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ y,
                                                      uint32_t batch, float scale) {
-    constexpr int S = 62, HD = 40, H = 4, D = 160, LDT = 64 + 4;   // LDS row stride (keys) in bf16
+    static_assert(HD % 8 == 0 && HD <= 64, "head dimension: a multiple of 8, at most 64");
+    constexpr int S = 62, D = HD * H, LDT = 64 + 4;   // LDS row stride (keys) in bf16
+    constexpr int PC = HD / 8;                        // 16-byte pieces per key row of V
+    constexpr int KS = (HD + 15) / 16;                // k-steps over the head dimension
     __shared__ uint16_t vt_all[4][64 * LDT];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t bh = blockIdx.x * 4u + (uint32_t)wave;
@@ -182,30 +186,29 @@ __global__ void __launch_bounds__(256) attn62_kernel(const uint16_t* __restrict_
     const uint16_t* base = qkv + (size_t)b * S * (3 * D);
     uint16_t* vt = vt_all[wave];
 
-    // V^T into LDS as [e][t]: the 62 x 40 tile is read as 310 16-byte pieces (8 dims of
-    // one key each, 5 per lane) and scattered transposed; zero padding for t >= 62, e >= 40
+    // V^T into LDS as [e][t]: the 62 x HD tile is read as 62 * HD / 8 16-byte pieces (8
+    // dims of one key each, HD / 8 per lane) and scattered transposed; zero padding for
+    // t >= 62 and e >= HD
     {
 #pragma unroll
-        for (int i = 0; i < 5; ++i) {
-            const int v = lane + 64 * i;          // piece v: key v / 5, dims 8 (v % 5) .. +8
-            const int t = v / 5, e0 = 8 * (v % 5);
-            const bool ok = valid && v < S * 5;
+        for (int i = 0; i < PC; ++i) {
+            const int v = lane + 64 * i;          // piece v: key v / PC, dims 8 (v % PC) .. +8
+            const int t = v / PC, e0 = 8 * (v % PC);
+            const bool ok = valid && v < S * PC;
             union { uint4 u; uint16_t s[8]; } pc;
             pc.u = ok ? *(const uint4*)(base + (size_t)t * (3 * D) + 2 * D + hd * HD + e0) : make_uint4(0u, 0u, 0u, 0u);
-            if (v < 64 * 5) {
 #pragma unroll
-                for (int m = 0; m < 8; ++m) vt[(e0 + m) * LDT + t] = pc.s[m];
-            }
+            for (int m = 0; m < 8; ++m) vt[(e0 + m) * LDT + t] = pc.s[m];
         }
         for (int e = HD; e < 64; ++e) vt[e * LDT + lane] = 0;
     }
     // Q and K fragments: tile i covers tokens 32i + r, k-step kk covers dims 16kk + 8h + j
-    bf16x8_t qf[2][3], kf[2][3];
+    bf16x8_t qf[2][KS], kf[2][KS];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
         const int tok = 32 * i + r;
 #pragma unroll
-        for (int kk = 0; kk < 3; ++kk) {
+        for (int kk = 0; kk < KS; ++kk) {
             const int e0 = 16 * kk + 8 * h;
             const bool ok = valid && tok < S && e0 < HD;
             const uint16_t* row = base + (size_t)(ok ? tok : 0) * (3 * D) + hd * HD + (ok ? e0 : 0);
@@ -221,7 +224,7 @@ __global__ void __launch_bounds__(256) attn62_kernel(const uint16_t* __restrict_
         for (int si = 0; si < 2; ++si) {
             f32x16_t acc = {0};
 #pragma unroll
-            for (int kk = 0; kk < 3; ++kk) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[ti][kk], qf[si][kk], acc, 0, 0, 0);
+            for (int kk = 0; kk < KS; ++kk) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[ti][kk], qf[si][kk], acc, 0, 0, 0);
             x[ti][si] = acc;
         }
     // softmax over the keys t of every query column s; P packed to bf16 fragments

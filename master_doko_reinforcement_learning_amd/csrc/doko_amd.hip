@@ -478,6 +478,13 @@ __global__ void ar_begin_kernel(const dk_az_state* info, uint32_t samples, const
     atomicMax(rounds, g);
 }
 
+__global__ void ar_guesses_kernel(const dk_az_state* info, uint32_t n, uint32_t* counts) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    dk::ar::Lane L;
+    counts[i] = dk::ar::init(info[i], 0, L);
+}
+
 __global__ void ar_prepare_kernel(const dk_az_state* info, uint32_t samples, uint32_t n, dk::ar::Lane* lanes,
                                   float log_chance, int32_t* tokens) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1248,6 +1255,15 @@ int dk_ar_begin_async(dk_ctx* ctx, const dk_az_state* d_infostates, uint32_t n_i
     return DK_OK;
 }
 
+int dk_ar_guesses_async(dk_ctx* ctx, const dk_az_state* d_infostates, uint32_t n_info, uint32_t* d_counts, void* stream) {
+    if (!ctx || !d_infostates || !d_counts) return DK_E_INVALID;
+    if (n_info == 0) return DK_OK;
+    hipLaunchKernelGGL(ar_guesses_kernel, dim3(grid_for(n_info, 64)), dim3(64), 0, pick(ctx, stream), d_infostates, n_info,
+                       d_counts);
+    DK_HIP(hipGetLastError());
+    return DK_OK;
+}
+
 int dk_ar_prepare_async(dk_ctx* ctx, int32_t* d_tokens, void* stream) {
     if (!ctx || !ctx->ar_info || !d_tokens) return DK_E_INVALID;
     if (ctx->ar_n == 0) return DK_OK;
@@ -1303,12 +1319,18 @@ int dk_net_embed_ln_bf16_async(const int32_t* d_tokens, uint32_t batch, const vo
     return DK_OK;
 }
 
-int dk_net_attn62_bf16_async(const void* qkv, void* y, uint32_t batch, void* stream) {
-    if (!qkv || !y) return DK_E_INVALID;
+int dk_net_attn62_bf16_async(const void* qkv, void* y, uint32_t batch, uint32_t heads, uint32_t head_dim, void* stream) {
+    if (!qkv || !y || heads != 4u || (head_dim != 40u && head_dim != 64u)) return DK_E_INVALID;
     if (batch == 0) return DK_OK;
-    const uint32_t waves = batch * 4u;
-    hipLaunchKernelGGL(dk::net::attn62_kernel, dim3((waves + 3u) / 4u), dim3(256), 0, (hipStream_t)stream,
-                       (const uint16_t*)qkv, (uint16_t*)y, batch, 1.0f / sqrtf(40.0f));
+    if ((uint64_t)batch * heads > 0xFFFFFFFFull) return DK_E_INVALID;
+    const uint32_t waves = batch * heads;
+    const float scale = 1.0f / sqrtf((float)head_dim);
+    if (head_dim == 40u)
+        hipLaunchKernelGGL((dk::net::attn62_kernel<40, 4>), dim3((waves + 3u) / 4u), dim3(256), 0, (hipStream_t)stream,
+                           (const uint16_t*)qkv, (uint16_t*)y, batch, scale);
+    else
+        hipLaunchKernelGGL((dk::net::attn62_kernel<64, 4>), dim3((waves + 3u) / 4u), dim3(256), 0, (hipStream_t)stream,
+                           (const uint16_t*)qkv, (uint16_t*)y, batch, scale);
     DK_HIP(hipGetLastError());
     return DK_OK;
 }

@@ -36,19 +36,20 @@ def test_add_ln_matches_torch(d):
     torch.testing.assert_close(h.float(), h_ref, rtol=1e-2, atol=2e-2)   # bf16 output of an f32 LayerNorm
 
 
-def test_attn62_matches_torch():
-    """MFMA attention core (62 tokens, 4 heads x 40) against fp32 softmax(q k^T / sqrt(40)) v."""
+@pytest.mark.parametrize("hd", [40, 64])
+def test_attn62_matches_torch(hd):
+    """MFMA attention core (62 tokens, 4 heads x hd) against fp32 softmax(q k^T / sqrt(hd)) v."""
     dev = torch.device("cuda", 0)
     torch.manual_seed(3)
-    B = 77
-    qkv = (torch.randn(B, 62, 480, device=dev) * 1.5).bfloat16()
-    y = torch.full((B, 62, 160), float("nan"), device=dev).bfloat16()
-    rc = _lib().dk_net_attn62_bf16_async(qkv.data_ptr(), y.data_ptr(), B, torch.cuda.current_stream(dev).cuda_stream)
+    B, d = 77, 4 * hd
+    qkv = (torch.randn(B, 62, 3 * d, device=dev) * 1.5).bfloat16()
+    y = torch.full((B, 62, d), float("nan"), device=dev).bfloat16()
+    rc = _lib().dk_net_attn62_bf16_async(qkv.data_ptr(), y.data_ptr(), B, 4, hd, torch.cuda.current_stream(dev).cuda_stream)
     assert rc == 0
     torch.cuda.synchronize()
-    q, k, v = qkv.float().view(B, 62, 3, 4, 40).permute(2, 0, 3, 1, 4)
-    ref = torch.softmax(q @ k.transpose(-1, -2) / 40 ** 0.5, dim=-1) @ v          # [B, 4, 62, 40]
-    ref = ref.transpose(1, 2).reshape(B, 62, 160)
+    q, k, v = qkv.float().view(B, 62, 3, 4, hd).permute(2, 0, 3, 1, 4)
+    ref = torch.softmax(q @ k.transpose(-1, -2) / hd ** 0.5, dim=-1) @ v          # [B, 4, 62, hd]
+    ref = ref.transpose(1, 2).reshape(B, 62, d)
     assert torch.isfinite(y.float()).all()
     torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=2e-2)
 
