@@ -240,6 +240,11 @@ int dk_fuse(dk_ctx* ctx, const uint32_t* visits, uint32_t n_info, uint32_t sampl
             int mode, uint8_t* action);
 int dk_fuse_accumulate_async(dk_ctx* ctx, const uint32_t* d_visits, uint32_t n_info, uint32_t samples,
                              const uint64_t* d_allowed, int mode, uint32_t* d_acc_u32, float* d_acc_f32, void* stream);
+/* dk_fuse_accumulate_async with per-sample flags d_valid[n_info * samples]: samples with 0
+ * (failed determinizations, compare_impi.rs:276-288) take no part in the fusion. */
+int dk_fuse_accumulate_masked_async(dk_ctx* ctx, const uint32_t* d_visits, uint32_t n_info, uint32_t samples,
+                                    const uint8_t* d_valid, const uint64_t* d_allowed, int mode, uint32_t* d_acc_u32,
+                                    float* d_acc_f32, void* stream);
 int dk_fuse_select_async(dk_ctx* ctx, uint32_t n_info, int mode, const uint64_t* d_allowed, const uint32_t* d_acc_u32,
                          const float* d_acc_f32, uint8_t* d_action, void* stream);
 
@@ -323,6 +328,13 @@ int dk_ar_guesses_async(dk_ctx* ctx, const dk_az_state* d_infostates, uint32_t n
 int dk_ar_prepare_async(dk_ctx* ctx, int32_t* d_tokens, void* stream);
 int dk_ar_choose_async(dk_ctx* ctx, const float* d_logits, float temperature, void* stream);
 int dk_ar_output_async(dk_ctx* ctx, dk_state* d_out, uint8_t* d_status, uint8_t* d_reason, void* stream);
+/* The end of DefaultImpiPolicy::execute (compare_impi.rs:297-370) for AR samples:
+ * d_successes[i] = consistent samples of infostate i (d_status == 0); an infostate with none
+ * gets d_action[i] = FdoAllowedActions::random over its legal actions minus the five
+ * announcements (SmallRng::seed_from_u64(d_seeds[i])); other entries of d_action are
+ * left for the fusion to write. */
+int dk_ar_fallback_async(dk_ctx* ctx, uint32_t n_info, uint32_t samples, const uint8_t* d_status, const uint64_t* d_allowed,
+                         const uint64_t* d_seeds, uint8_t* d_action, uint32_t* d_successes, void* stream);
 
 /* Game records for self-play.  dk_az_records_async: records of packed rs-full-doko states
  * without announcements (new games, DK_E_STATE otherwise).  dk_az_step_async:

@@ -9,6 +9,7 @@ Names follow the Rust types they replace:
 * ``sample_assignment_full``      — rs-doko rule-based determinization (rs-doko-assignment/src/assignment.rs:472-580)
 * ``PolicyFusionMaxN`` / ``PolicyFusionAverageStrategy`` — policy_fusion.rs:18-123
 * ``DefaultImpiPolicy``           — sample -> search -> fuse (compare_impi.rs:212-371)
+* ``ArImpiPolicy``                — AR-determinized decision (mcts_ar_maxn/avg_policy, all_policies.rs:78-127)
 * ``ARSampling``                  — IMPI autoregressive determinization (forward_pred_process_with_mask,
                                     rs-doko-impi/src/forward.rs:392-661), batched, network between launches
 * ``AlphaZeroSearch``             — AlphaZero PUCT mcts_search (rs-doko-alpha-zero/src/alpha_zero/mcts/async_mcts.rs:224-406),
@@ -247,6 +248,77 @@ class DefaultImpiPolicy:
                                              self.iterations, self.c, self.fusion, _ptr(actions),
                                              _ptr(visits) if return_visits else None))
         return (actions, visits) if return_visits else actions
+
+
+class ArImpiPolicy:
+    """mcts_ar_maxn_policy / mcts_ar_avg_policy (rs-doko-py-bridge/src/compare_impi/all_policies.rs:78-127):
+    DefaultImpiPolicy::execute (compare_impi.rs:212-371) with the ARSampling sampler.  Per
+    infostate `num_samples` AR draws (network between launches), UCT on every draw, fusion
+    over the consistent ones only; an infostate without a consistent draw takes a random
+    legal non-announcement action.  Everything stays on the GPU (torch tensors).
+
+    The reference continues each sample's SmallRng from the sampler into the search; here
+    sampling, search and fallback take separate explicit seeds (production seeds are
+    from_os_rng, so only the seeding scheme differs, not the distribution)."""
+
+    def __init__(self, engine, network, uct_exploration_constant=2.5, iterations=1000, num_samples=64,
+                 fusion=FUSE_MAXN, temperature=0.4):
+        self.engine = engine
+        self.c = float(uct_exploration_constant)
+        self.iterations = iterations
+        self.num_samples = num_samples
+        self.fusion = fusion
+        self.sampler = ARSampling(engine, network, temperature)
+
+    def execute(self, infostates, seeds):
+        """infostates: uint8 [n, 160] dk_az_state records (GPU); seeds: uint64, n*S sampling seeds,
+        then n*S search seeds, then n fallback seeds.  Returns (actions uint8 [n], successes int32 [n],
+        visits int32 [n*S, 39]) as GPU tensors."""
+        import torch
+        dev = infostates.device
+        caller = torch.cuda.current_stream(dev)
+        if caller.cuda_stream != 0:
+            return self._execute(infostates, seeds, caller.cuda_stream)
+        side = torch.cuda.Stream(dev)   # a real handle: 0 would select the library's own stream
+        side.wait_stream(caller)
+        with torch.cuda.stream(side):
+            out = self._execute(infostates, seeds, side.cuda_stream)
+        caller.wait_stream(side)
+        return out
+
+    def _execute(self, infostates, seeds, st):
+        import torch
+        L = _native.lib()
+        ctx = self.engine.ctx
+        n, S = infostates.shape[0], self.num_samples
+        seeds = np.ascontiguousarray(seeds, dtype=np.uint64)
+        if seeds.shape[0] != 2 * n * S + n:
+            raise ValueError("need 2*n*num_samples + n seeds")
+        dev = infostates.device
+        samples, status, _ = self.sampler.sample(infostates, S, seeds[:n * S])
+        srch = torch.as_tensor(seeds[n * S:2 * n * S].view(np.int64), device=dev)
+        fb = torch.as_tensor(seeds[2 * n * S:].view(np.int64), device=dev)
+        visits = torch.empty((n * S, NUM_ACTIONS), dtype=torch.int32, device=dev)
+        values = torch.empty((n * S, NUM_ACTIONS), dtype=torch.float64, device=dev)
+        best = torch.empty(n * S, dtype=torch.uint8, device=dev)
+        _check(L.dk_search_batch_async(ctx, GAME_FULL_DOKO, samples.data_ptr(), srch.data_ptr(), n * S, self.iterations,
+                                       self.c, visits.data_ptr(), values.data_ptr(), best.data_ptr(), st))
+        info = infostates[:, :STATE_BYTES].contiguous()
+        allowed = torch.empty(n, dtype=torch.int64, device=dev)
+        _check(L.dk_legal_actions_async(ctx, info.data_ptr(), n, allowed.data_ptr(), st))
+        valid = (status == AR_CONSISTENT).to(torch.uint8)
+        acc_u = torch.zeros((n, NUM_ACTIONS), dtype=torch.int32, device=dev)
+        acc_f = torch.zeros((n, NUM_ACTIONS), dtype=torch.float32, device=dev)
+        actions = torch.empty(n, dtype=torch.uint8, device=dev)
+        _check(L.dk_fuse_accumulate_masked_async(ctx, visits.data_ptr(), n, S, valid.data_ptr(), allowed.data_ptr(),
+                                                 self.fusion, acc_u.data_ptr(), acc_f.data_ptr(), st))
+        _check(L.dk_fuse_select_async(ctx, n, self.fusion, allowed.data_ptr(), acc_u.data_ptr(), acc_f.data_ptr(),
+                                      actions.data_ptr(), st))
+        successes = torch.empty(n, dtype=torch.int32, device=dev)
+        _check(L.dk_ar_fallback_async(ctx, n, S, status.data_ptr(), allowed.data_ptr(), fb.data_ptr(), actions.data_ptr(),
+                                      successes.data_ptr(), st))
+        _check(L.dk_sync(ctx, st))
+        return actions, successes, visits
 
 
 class AlphaZeroSearch:

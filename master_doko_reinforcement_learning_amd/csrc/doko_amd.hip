@@ -506,6 +506,22 @@ __global__ void ar_choose_kernel(uint32_t n, dk::ar::Lane* lanes, const float* l
     lanes[i] = L;
 }
 
+// DefaultImpiPolicy::execute without one consistent sample (compare_impi.rs:355-370):
+// a random legal action other than the five announcements (FdoAllowedActions::random).
+__global__ void ar_fallback_kernel(uint32_t n_info, uint32_t samples, const uint8_t* status, const uint64_t* allowed,
+                                   const uint64_t* seeds, uint8_t* action, uint32_t* successes) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_info) return;
+    uint32_t ok = 0;
+    for (uint32_t s = 0; s < samples; ++s) ok += status[(size_t)i * samples + s] == 0 ? 1u : 0u;
+    successes[i] = ok;
+    if (ok) return;
+    const uint64_t m = allowed[i] & ~dk::fdo::ANN_ACTIONS;
+    if (m == 0) { action[i] = DK_NONE; return; }
+    dk::Rng rng = dk::Rng::seed_from_u64(seeds[i]);
+    action[i] = (uint8_t)dk::ctz64(dk::random_single(m, rng));
+}
+
 __global__ void ar_output_kernel(const dk_az_state* info, uint32_t samples, uint32_t n, const dk::ar::Lane* lanes,
                                  dk_state* out, uint8_t* status, uint8_t* reason) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -519,7 +535,9 @@ __global__ void ar_output_kernel(const dk_az_state* info, uint32_t samples, uint
 
 // PolicyFusionMaxN / PolicyFusionAverageStrategy accumulators (policy_fusion.rs:23-123).
 // One thread per (infostate, action).
-__global__ void fuse_accumulate_kernel(const uint32_t* visits, uint32_t n_info, uint32_t samples,
+// `valid` (nullable): per-sample flags; samples with valid == 0 (failed determinizations,
+// compare_impi.rs:276-288) take no part in the fusion.
+__global__ void fuse_accumulate_kernel(const uint32_t* visits, uint32_t n_info, uint32_t samples, const uint8_t* valid,
                                        const uint64_t* allowed, int mode, uint32_t* acc_u32, float* acc_f32) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n_info * 39) return;
@@ -529,6 +547,7 @@ __global__ void fuse_accumulate_kernel(const uint32_t* visits, uint32_t n_info, 
         if (!((al >> a) & 1)) { acc_u32[t] = 0u; return; }   // masked to UINT32_MAX in select (summable across ranks)
         uint32_t cum = 0;
         for (uint32_t s = 0; s < samples; ++s) {
+            if (valid && !valid[(size_t)info * samples + s]) continue;
             const uint32_t* row = visits + ((size_t)info * samples + s) * 39;
             const uint32_t va = row[a];
             uint32_t rank = 1;
@@ -543,6 +562,7 @@ __global__ void fuse_accumulate_kernel(const uint32_t* visits, uint32_t n_info, 
     } else {
         float sum = 0.0f;
         for (uint32_t s = 0; s < samples; ++s) {
+            if (valid && !valid[(size_t)info * samples + s]) continue;
             const uint32_t* row = visits + ((size_t)info * samples + s) * 39;
             uint64_t total = 0;
             for (uint32_t b = 0; b < 39; ++b) total += row[b];
@@ -1034,7 +1054,18 @@ int dk_fuse_accumulate_async(dk_ctx* ctx, const uint32_t* d_visits, uint32_t n_i
     if (!ctx || (mode != DK_FUSE_MAXN && mode != DK_FUSE_AVG)) return DK_E_INVALID;
     if (n_info == 0) return DK_OK;
     hipLaunchKernelGGL(fuse_accumulate_kernel, dim3(grid_for((size_t)n_info * 39, 64)), dim3(64), 0, pick(ctx, stream),
-                       d_visits, n_info, samples, d_allowed, mode, d_acc_u32, d_acc_f32);
+                       d_visits, n_info, samples, (const uint8_t*)nullptr, d_allowed, mode, d_acc_u32, d_acc_f32);
+    DK_HIP(hipGetLastError());
+    return DK_OK;
+}
+
+int dk_fuse_accumulate_masked_async(dk_ctx* ctx, const uint32_t* d_visits, uint32_t n_info, uint32_t samples,
+                                    const uint8_t* d_valid, const uint64_t* d_allowed, int mode, uint32_t* d_acc_u32,
+                                    float* d_acc_f32, void* stream) {
+    if (!ctx || !d_valid || (mode != DK_FUSE_MAXN && mode != DK_FUSE_AVG)) return DK_E_INVALID;
+    if (n_info == 0) return DK_OK;
+    hipLaunchKernelGGL(fuse_accumulate_kernel, dim3(grid_for((size_t)n_info * 39, 64)), dim3(64), 0, pick(ctx, stream),
+                       d_visits, n_info, samples, d_valid, d_allowed, mode, d_acc_u32, d_acc_f32);
     DK_HIP(hipGetLastError());
     return DK_OK;
 }
@@ -1278,6 +1309,16 @@ int dk_ar_choose_async(dk_ctx* ctx, const float* d_logits, float temperature, vo
     if (ctx->ar_n == 0) return DK_OK;
     hipLaunchKernelGGL(ar_choose_kernel, dim3(grid_for(ctx->ar_n, 64)), dim3(64), 0, pick(ctx, stream), ctx->ar_n,
                        ctx->ar_lanes, d_logits, temperature);
+    DK_HIP(hipGetLastError());
+    return DK_OK;
+}
+
+int dk_ar_fallback_async(dk_ctx* ctx, uint32_t n_info, uint32_t samples, const uint8_t* d_status, const uint64_t* d_allowed,
+                         const uint64_t* d_seeds, uint8_t* d_action, uint32_t* d_successes, void* stream) {
+    if (!ctx || !d_status || !d_allowed || !d_seeds || !d_action || !d_successes) return DK_E_INVALID;
+    if (n_info == 0) return DK_OK;
+    hipLaunchKernelGGL(ar_fallback_kernel, dim3(grid_for(n_info, 64)), dim3(64), 0, pick(ctx, stream), n_info, samples,
+                       d_status, d_allowed, d_seeds, d_action, d_successes);
     DK_HIP(hipGetLastError());
     return DK_OK;
 }

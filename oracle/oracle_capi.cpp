@@ -418,4 +418,18 @@ int or_ipi_sample(void* sp, uint64_t* rng_state, float temperature, float log_ch
     if (a.status == 0) or_fdo_pack((void*)&a.state, out);
     return a.status;
 }
+// the consistent sample as a new oracle state (nullptr otherwise)
+void* or_ipi_sample_state(void* sp, uint64_t* rng_state, float temperature, float log_chance, int32_t* status,
+                          int32_t* reason) {
+    SmallRng r = rng_from(rng_state);
+    const impi::ArResult a = impi::forward_pred_process_with_mask(
+        *(fdo::State*)sp, temperature, log_chance, [](const int64_t* t, float* l) { impi::hash_eval(t, l); }, r);
+    rng_to(r, rng_state);
+    *status = a.status;
+    *reason = a.reason;
+    return a.status == 0 ? new fdo::State(a.state) : nullptr;
+}
+uint64_t or_fdo_random_single(uint64_t mask, uint64_t* rng_state) {
+    SmallRng r = rng_from(rng_state); const uint64_t b = fdo::random_single(mask, r); rng_to(r, rng_state); return b;
+}
 }  // extern "C"

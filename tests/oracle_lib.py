@@ -92,6 +92,8 @@ def lib():
             "or_ipi_next_reservation": (ctypes.c_uint32, [vp, u64p, ctypes.c_int]),
             "or_ipi_consistent": (ctypes.c_int, [vp, u64p, i32p]),
             "or_ipi_hash_eval": (None, [ctypes.POINTER(ctypes.c_int64), f32p]),
+            "or_ipi_sample_state": (vp, [vp, u64p, ctypes.c_float, ctypes.c_float, i32p, i32p]),
+            "or_fdo_random_single": (ctypes.c_uint64, [ctypes.c_uint64, u64p]),
             "or_ipi_sample": (ctypes.c_int, [vp, u64p, ctypes.c_float, ctypes.c_float, i32p, u8p, i32p]),
             "or_ttt_finish": (ctypes.c_int, [i32p]),
             "or_ttt_rollout": (None, [i32p, u64p, f64p]),
@@ -238,6 +240,13 @@ class FdoState:
         o = arr(ctypes.c_uint8, 128)
         st = lib().or_ipi_sample(self.h, rng, temperature, log_chance, reason, o, g)
         return st, reason[0], (bytes(o) if st == 0 else None), g[0]
+
+    def ipi_sample_state(self, rng, temperature, log_chance=1.0 / 30000.0):
+        """forward_pred_process_with_mask with the hash network -> (status, reason, FdoState or None)."""
+        st = arr(ctypes.c_int32, 1)
+        rs = arr(ctypes.c_int32, 1)
+        h = lib().or_ipi_sample_state(self.h, rng, temperature, log_chance, st, rs)
+        return st[0], rs[0], (FdoState(h) if h else None)
 
     def az_take_action(self, a):
         """FdoAzEnvState::take_action_by_action_index(a, skip_single=true)."""
@@ -426,6 +435,11 @@ def encode_ipi_fields(res_start, res, tricks, hands, announcements, current_play
                                     arr(ctypes.c_uint64, 4, hands), arr(ctypes.c_uint64, 4, assumed_hands),
                                     arr(ctypes.c_int32, 4, assumed_res), guess, o)
     return list(o) if ok else None
+
+
+def random_single(mask, rng):
+    """Bitflag::random_single (rs-game-utils/src/bit_flag.rs:86-92) -> the chosen bit."""
+    return lib().or_fdo_random_single(mask, rng)
 
 
 def ipi_hash_eval_np(tokens):
