@@ -470,9 +470,14 @@ class ARSampling:
 
 
 def _stream(t):
+    """The caller's torch stream handle.  Handle 0 (torch's default stream) would select the
+    library's own stream, which is not ordered after the caller's queued work: wait for that
+    work first (the callers then dk_sync before returning)."""
     import torch
-    st = torch.cuda.current_stream(t.device).cuda_stream
-    return st
+    st = torch.cuda.current_stream(t.device)
+    if st.cuda_stream == 0:
+        st.synchronize()
+    return st.cuda_stream
 
 
 def az_records(engine, states):
@@ -504,5 +509,8 @@ def az_encode(engine, records, out=None):
     n = records.shape[0]
     if out is None:
         out = torch.empty((n, AZ_TOKENS), dtype=torch.int32, device=records.device)
-    _check(_native.lib().dk_az_encode_async(engine.ctx, records.data_ptr(), n, out.data_ptr(), _stream(records)))
+    st = _stream(records)
+    _check(_native.lib().dk_az_encode_async(engine.ctx, records.data_ptr(), n, out.data_ptr(), st))
+    if st == 0:
+        _check(_native.lib().dk_sync(engine.ctx, None))
     return out

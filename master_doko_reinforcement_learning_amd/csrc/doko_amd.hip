@@ -28,18 +28,10 @@
 namespace {
 
 constexpr int WAVE = 64;
-// register budget of the search kernel: by default the compiler's choice (~217 VGPRs, two
-// waves per SIMD, no spills).  With 64 roots per wave two full waves per SIMD beat three
-// half-filled ones at a 168-VGPR budget (which spills ~40 VGPRs); -DDK_SEARCH_MIN_WAVES=n
-// forces an n-wave budget for experiments.
-#ifndef DK_SEARCH_MIN_WAVES
-#define DK_SEARCH_MIN_WAVES 0
-#endif
-#if DK_SEARCH_MIN_WAVES > 0
-#define DK_SEARCH_BOUNDS __launch_bounds__(WAVE, DK_SEARCH_MIN_WAVES)
-#else
-#define DK_SEARCH_BOUNDS __launch_bounds__(WAVE)
-#endif
+// register budget of the search kernel: per hot-record layout (NodeHot16::MIN_WAVES = 3 waves
+// per SIMD, 167 VGPRs with a 24-B spill; NodeHot32: the compiler's choice, two waves).
+// Resident single-wave workgroups per CU at that budget (sizes the node pools):
+constexpr uint32_t RESIDENT_WG_PER_CU = 12;
 constexpr int MAX_PATH = 64;   // LDS path entries per lane (deeper paths spill to a global overflow)
 
 #define DK_HIP(call)                                              \
@@ -134,7 +126,7 @@ struct GpuMem {
 // are sized for the resident waves, not for the batch.  The LDS holds each lane's
 // selection path: lds_n x (u32 slot|player, u64 stats).
 template <class E, bool LN_LDS, class H>
-__global__ void DK_SEARCH_BOUNDS search_kernel(const dk_state* __restrict__ roots,
+__global__ void __launch_bounds__(WAVE, H::MIN_WAVES) search_kernel(const dk_state* __restrict__ roots,
                                                       const uint64_t* __restrict__ seeds, uint32_t n,
                                                       uint32_t iters, double c, const double* __restrict__ ln_table,
                                                       void* hot_pool, dk::NodeCold* cold, typename E::Work* states,
@@ -600,7 +592,7 @@ struct dk_ctx {
     hipStream_t stream = nullptr;
     uint32_t max_roots = 0, max_iters = 0, cap_slots = 0;
     uint32_t pool_roots = 0;        // roots the node pools hold at once (min(max_roots, DK_POOL_ROOTS or
-                                    // the resident capacity: CUs x 8 single-wave workgroups x 64 lanes))
+                                    // the resident capacity: CUs x 12 single-wave workgroups x 64 lanes))
     int cu_count = 0;
     uint32_t* queue = nullptr;      // root-group counter of the persistent search grid
     void* hot = nullptr;            // hot records, 32 B per slot (NodeHot16 launches use half)
@@ -621,7 +613,7 @@ struct dk_ctx {
                                     // 1000 iterations); by default it is read through the L1/L2 caches
     int lds_path = 16;              // DK_LDS_PATH (path entries kept in LDS, <= MAX_PATH; deeper ones
                                     // spill to global).  16 keeps a workgroup at 12 KB of LDS so that
-                                    // 8 single-wave workgroups (2 per SIMD) fit a CU's 160 KB.
+                                    // 12 single-wave workgroups (3 per SIMD) fit a CU's 160 KB.
     uint64_t* prof = nullptr;       // phase timers (DK_PHASE_PROF builds only)
     // AlphaZero PUCT search (dk_az_*): per-game node / state regions, allocated on first use
     dk::az::Node* az_nodes = nullptr;
@@ -778,7 +770,7 @@ dk_ctx* dk_create(const dk_config* cfg) {
     }
     // The search grid is persistent (search_kernel): the pools hold the resident waves'
     // roots, and a larger batch streams through them.
-    uint64_t pool = (uint64_t)prop.multiProcessorCount * 8u * WAVE;
+    uint64_t pool = (uint64_t)prop.multiProcessorCount * RESIDENT_WG_PER_CU * WAVE;
     if (const char* e = getenv("DK_POOL_ROOTS")) {
         const long long v = atoll(e);
         if (v >= 1) pool = (uint64_t)v;

@@ -69,6 +69,7 @@ struct alignas(16) NodeHot16 {
     uint32_t child_base;  // first slot of the child block (valid when nchild > 0)
     uint32_t info;        // nchild:6 | player:2 | has_unexpanded:1 | chain_head:1 | state_idx:22
     static constexpr bool CACHED_MEAN = false;
+    static constexpr int MIN_WAVES = 3;   // search-kernel register budget: 3 waves per SIMD (<= 168 VGPRs)
 };
 struct alignas(32) NodeHot32 {
     uint64_t stats;
@@ -78,6 +79,7 @@ struct alignas(32) NodeHot32 {
     float isv;            // ~1/sqrt(visits) (f32 estimate for the UCT filter)
     uint32_t pad;
     static constexpr bool CACHED_MEAN = true;
+    static constexpr int MIN_WAVES = 1;   // no budget (its launches have one wave per SIMD)
 };
 // the layout of host builds (test harnesses); -DDK_HOT16=0 selects the 32-B one
 #ifndef DK_HOT16
