@@ -51,9 +51,20 @@ int main(int argc, char** argv) {
         dk::NodeHot rec[dk::SCAN_REG];
         memset(rec, 0, sizeof(rec));
         const uint32_t n = 2 + (uint32_t)(r() % 11);
-        const int mode = (int)(r() % 6);
+        const int mode = (int)(r() % 7);
         const uint32_t vmax = mode == 5 ? 100000u : 1000u;
         uint32_t total = 0;
+        // mode 6: Farey neighbours a/b and c/d (|ad - bc| = 1, b, d in [500, 1000]) around a
+        // common integer part k differ by 1/(bd) ~ 1e-6, ~3e-8 relative at |mean| ~ 40:
+        // far below the f32 estimates' resolution, so the exact tie-break decides
+        int64_t fk = (int64_t)(r() % 81) - 40, fb = 500 + (int64_t)(r() % 501), fd = 500 + (int64_t)(r() % 501);
+        {
+            auto gcd = [](int64_t x, int64_t y) { while (y) { const int64_t t = x % y; x = y; y = t; } return x; };
+            while (gcd(fb, fd) != 1) ++fd;
+        }
+        int64_t fa = 0;
+        for (int64_t x = 0; x < fb; ++x) if ((x * fd + 1) % fb == 0) { fa = x; break; }
+        const int64_t fc = (fa * fd + 1) / fb;
         for (uint32_t j = 0; j < n; ++j) {
             uint32_t v = 1 + (uint32_t)(r() % vmax);
             int32_t s;
@@ -62,6 +73,11 @@ int main(int argc, char** argv) {
             else if (mode == 2) { s = (int32_t)(r() % 5) - 2; }                             // means near 0
             else if (mode == 3) { v = 1 + (uint32_t)(r() % 3); s = (int32_t)(r() % 9) - 4; } // tiny visits
             else if (mode == 4 && j > 0) { v = (uint32_t)rec[0].stats + (uint32_t)(r() % 3); s = (int32_t)(rec[0].stats >> 32) + (int32_t)(r() % 3) - 1; }
+            else if (mode == 6) {   // a near-tie pair (see below), alternating over the children
+                const bool first = (j % 2) == 0;
+                v = (uint32_t)(first ? fb : fd);
+                s = (int32_t)(first ? fa + fk * fb : fc + fk * fd);
+            }
             else s = (int32_t)(r() % (2 * 20 * v + 1)) - (int32_t)(20 * v);
             rec[j].stats = (uint64_t)v | ((uint64_t)(uint32_t)s << 32);
             total += v;
