@@ -357,6 +357,11 @@ int dk_net_embed_ln_bf16_async(const int32_t* d_tokens, uint32_t batch, const vo
                                const void* gamma, const void* beta, float eps, void* x_out, void* h_out, void* stream);
 int dk_net_add_ln_bf16_async(void* x_io, const void* delta, uint32_t rows, uint32_t d, const void* gamma, const void* beta,
                              float eps, void* h_out, void* stream);
+/* dk_net_fc_gelu_bf16_async: y[rows][n] = GELU(x[rows][k] w[n][k]^T + bias[n]) with the exact
+ * (erf) GELU of nn.GELU(): the first layer of a block's MLP (k = d = 160 or 256, n % 64 == 0),
+ * bf16 in and out, f32 accumulation, the activation written once. */
+int dk_net_fc_gelu_bf16_async(const void* x, const void* w, const void* bias, uint32_t rows, uint32_t k, uint32_t n,
+                              void* y, void* stream);
 /* dk_net_attn62_bf16_async: softmax(q k^T / sqrt(head_dim)) v for the networks' shape (62
  * tokens; heads x head_dim = 4 x 40 for the AlphaZero network, 4 x 64 for the IMPI network),
  * q/k/v read from the fused projection qkv[batch*62][3d] ([q | k | v], heads contiguous), the

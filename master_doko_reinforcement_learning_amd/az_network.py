@@ -102,9 +102,10 @@ class ClassHead(nn.Module):
 class FusedTrunk:
     """The bf16 GPU forward of a token trunk (shared by DokoAzNet and DokoImpiNet): HIP
     kernels (csrc/az_net_kernels.h) for the embedding sum + first LayerNorm, every
-    residual add fused with the LayerNorm that follows it, and (4 heads of 40 or 64) the
-    62-token attention core; the GEMMs are torch (hipBLASLt).  `x` is the residual
-    stream, `h` the current LayerNorm output."""
+    residual add fused with the LayerNorm that follows it, (4 heads of 40 or 64) the
+    62-token attention core, and (d = 160 or 256) the MLP's first layer with its exact
+    GELU; the other GEMMs are torch (hipBLASLt).  `x` is the residual stream, `h` the
+    current LayerNorm output."""
 
     def __init__(self, tokens, emb, ln0):
         from . import _native
@@ -139,12 +140,23 @@ class FusedTrunk:
         w, b = blk.folded_proj()
         return F.linear(y, w, b)
 
+    def mlp_delta(self, blk, h):
+        """proj(GELU(fc(h))): the first layer and its exact GELU in one kernel (the 4d-wide
+        activation is written once), the second layer on hipBLASLt."""
+        n = blk.fc.weight.shape[0]
+        if self.d not in (160, 256) or n % 64:
+            return blk.mlp_delta(h)
+        a = torch.empty(h.shape[:-1] + (n,), dtype=h.dtype, device=h.device)
+        self.ck(self.L.dk_net_fc_gelu_bf16_async(h.data_ptr(), blk.fc.weight.data_ptr(), blk.fc.bias.data_ptr(),
+                                                 self.rows, self.d, n, a.data_ptr(), self.st))
+        return blk.proj(a)
+
     def run(self, h, blocks, final_ln, x=None):
         x = self.x if x is None else x
         for i, blk in enumerate(blocks):
             h = self.add_ln(x, self.attn_delta(blk, h), blk.ln_2)
             nxt = blocks[i + 1].ln_1 if i + 1 < len(blocks) else final_ln
-            h = self.add_ln(x, blk.mlp_delta(h), nxt)
+            h = self.add_ln(x, self.mlp_delta(blk, h), nxt)
         return h
 
 

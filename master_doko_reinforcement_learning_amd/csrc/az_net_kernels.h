@@ -290,5 +290,141 @@ __global__ void __launch_bounds__(256) attn62_kernel(const uint16_t* __restrict_
     }
 }
 
+// ---------------------------------------------------------------------------
+// The MLP's first layer with its activation: y = GELU(x W^T + b), exact (erf) GELU as
+// the reference's nn.GELU(), for the networks' small K (= d: 160 AlphaZero, 256 IMPI).
+// hipBLASLt runs this GEMM at 160-320 TFLOP/s and the separate GELU pass re-reads and
+// re-writes the 4d-wide activation; here the activation is written once.
+//   workgroup: 4 waves x RT row tiles of 32 rows; a wave's x fragments (all K) stay in
+//   registers for the whole N loop;
+//   N loop: 64-column chunks of W staged in LDS (double-buffered, shared by the 4
+//   waves); per k-step RT x 2 tiles of v_mfma_f32_32x32x16_bf16 computing D^T = W x^T,
+//   so a lane holds one row and, per register quad, 4 consecutive columns;
+//   epilogue: bias + GELU on the f32 accumulators, 4 columns packed into one 8-byte store.
+// GELU(v) = v Phi(v) = 0.5 v (1 + erf(v / sqrt 2)).  erf by Abramowitz & Stegun 7.1.26
+// (|error| <= 1.5e-7, here about 3e-7 with the hardware rcp / exp2): 1 - erf(z) =
+// (a1 t + ... + a5 t^5) exp(-z^2), t = 1 / (1 + p z), z >= 0.  That is the size of f32's own
+// rounding of 1 + erf near -1 (6e-8) and far below the bf16 output's resolution; the
+// library erff costs several times as many instructions and bounded this kernel.
+__device__ __forceinline__ float gelu_erf(float v) {
+    const float z = fabsf(v) * 0.70710678118654752f;
+    const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
+    float p = fmaf(1.061405429f, t, -1.453152027f);
+    p = fmaf(p, t, 1.421413741f);
+    p = fmaf(p, t, -0.284496736f);
+    p = fmaf(p, t, 0.254829592f);
+    const float e = __builtin_amdgcn_exp2f(-z * z * 1.4426950408889634f);
+    const float c = p * t * e;                       // erfc(z) = 1 - erf(z)
+    const float phi = v >= 0.0f ? 1.0f - 0.5f * c : 0.5f * c;
+    return v * phi;
+}
+
+// the same on a pair, so that the FMAs / multiplies issue as packed f32 (v_pk_fma_f32)
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2_t gelu_erf2(f32x2_t v) {
+    const f32x2_t z = __builtin_elementwise_abs(v) * 0.70710678118654752f;
+    const f32x2_t d = __builtin_elementwise_fma(f32x2_t{0.3275911f, 0.3275911f}, z, f32x2_t{1.0f, 1.0f});
+    const f32x2_t t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+    f32x2_t p = __builtin_elementwise_fma(f32x2_t{1.061405429f, 1.061405429f}, t, f32x2_t{-1.453152027f, -1.453152027f});
+    p = __builtin_elementwise_fma(p, t, f32x2_t{1.421413741f, 1.421413741f});
+    p = __builtin_elementwise_fma(p, t, f32x2_t{-0.284496736f, -0.284496736f});
+    p = __builtin_elementwise_fma(p, t, f32x2_t{0.254829592f, 0.254829592f});
+    const f32x2_t a = -z * z * 1.4426950408889634f;
+    const f32x2_t e = {__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
+    const f32x2_t c = p * t * e;
+    const f32x2_t half_c = 0.5f * c;
+    const f32x2_t phi = {v.x >= 0.0f ? 1.0f - half_c.x : half_c.x, v.y >= 0.0f ? 1.0f - half_c.y : half_c.y};
+    return v * phi;
+}
+
+template <int K>
+__global__ void __launch_bounds__(256, 2) fc_gelu_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
+                                                         const uint16_t* __restrict__ bias, uint16_t* __restrict__ y,
+                                                         uint32_t rows, uint32_t n) {
+    static_assert(K % 16 == 0, "K: a multiple of 16");
+    // K = 160: 64-column chunks, 2 row tiles per wave; K = 256: 32-column chunks, 1 row tile
+    // (registers and LDS for two workgroups per CU)
+    constexpr int KS = K / 16, NC = K <= 160 ? 64 : 32, CT = NC / 32, LDW = K + 8, RT = K <= 160 ? 2 : 1, LDT = NC + 8;
+    __shared__ uint16_t ws[2][NC * LDW];
+    __shared__ uint16_t tile[4][32 * RT * LDT];   // per-wave output staging
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+    const uint32_t row0 = blockIdx.x * (128u * RT) + (uint32_t)wave * (32u * RT);
+    bf16x8_t af[RT][KS];
+#pragma unroll
+    for (int i = 0; i < RT; ++i) {
+        const uint32_t row = row0 + 32u * i + (uint32_t)r;
+        const bool ok = row < rows;
+        const uint16_t* xr = x + (size_t)(ok ? row : 0u) * K + 8 * h;
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk) af[i][kk] = load_frag8(xr + 16 * kk, ok);
+    }
+    auto stage = [&](uint32_t c, int buf) {
+        const uint16_t* src = w + (size_t)c * NC * K;
+        for (int v = threadIdx.x; v < NC * (K / 8); v += 256) {
+            const int col = v / (K / 8), k8 = v - col * (K / 8);
+            *(uint4*)&ws[buf][col * LDW + 8 * k8] = *(const uint4*)(src + (size_t)col * K + 8 * k8);
+        }
+    };
+    const uint32_t chunks = n / NC;
+    stage(0, 0);
+    __syncthreads();
+    for (uint32_t c = 0; c < chunks; ++c) {
+        const int buf = (int)(c & 1u);
+        if (c + 1 < chunks) stage(c + 1, buf ^ 1);
+        f32x16_t acc[RT][CT];
+#pragma unroll
+        for (int i = 0; i < RT; ++i)
+#pragma unroll
+            for (int j = 0; j < CT; ++j) acc[i][j] = f32x16_t{0};
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk) {
+            bf16x8_t bfr[CT];
+#pragma unroll
+            for (int j = 0; j < CT; ++j) bfr[j] = *(const bf16x8_t*)&ws[buf][(32 * j + r) * LDW + 16 * kk + 8 * h];
+#pragma unroll
+            for (int i = 0; i < RT; ++i)
+#pragma unroll
+                for (int j = 0; j < CT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[j], af[i][kk], acc[i][j], 0, 0, 0);
+        }
+        // acc[i][j][g]: row row0 + 32 i + r, column c*NC + 32 j + (g & 3) + 8 (g >> 2) + 4 h.
+        // bias + GELU, 4 columns packed per 8-byte LDS write into the wave's [32 RT][NC] tile,
+        // then written out as whole row segments of NC columns (NC / 8 lanes per row)
+        uint16_t* tw = tile[wave];
+#pragma unroll
+        for (int j = 0; j < CT; ++j) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int cl = 32 * j + 8 * q + 4 * h;
+                const uint2 bb = *(const uint2*)(bias + c * NC + cl);
+                const float b0 = bf2f((uint16_t)bb.x), b1 = bf2f((uint16_t)(bb.x >> 16));
+                const float b2 = bf2f((uint16_t)bb.y), b3 = bf2f((uint16_t)(bb.y >> 16));
+#pragma unroll
+                for (int i = 0; i < RT; ++i) {
+                    const f32x2_t g01 = gelu_erf2(f32x2_t{acc[i][j][4 * q + 0] + b0, acc[i][j][4 * q + 1] + b1});
+                    const f32x2_t g23 = gelu_erf2(f32x2_t{acc[i][j][4 * q + 2] + b2, acc[i][j][4 * q + 3] + b3});
+                    uint2 o;
+                    o.x = (uint32_t)f2bf(g01.x) | ((uint32_t)f2bf(g01.y) << 16);
+                    o.y = (uint32_t)f2bf(g23.x) | ((uint32_t)f2bf(g23.y) << 16);
+                    *(uint2*)&tw[(32 * i + r) * LDT + cl] = o;
+                }
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);   // this wave's LDS writes done (lgkmcnt(0))
+#pragma unroll
+        for (int p = 0; p < RT * NC / 16; ++p) {
+            const int v = 64 * p + lane, rl = v / (NC / 8), sg = v % (NC / 8);
+            const uint32_t row = row0 + (uint32_t)rl;
+            const uint4 o = *(const uint4*)&tw[rl * LDT + 8 * sg];
+            if (row < rows) *(uint4*)(y + (size_t)row * n + c * NC + 8 * sg) = o;
+        }
+        // LDS-only barrier: the next chunk's W is in LDS and this chunk's reads of the other
+        // buffer are done; the output stores stay in flight (__syncthreads would wait for them)
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0), vmcnt / expcnt untouched
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    }
+}
+
 }  // namespace net
 }  // namespace dk

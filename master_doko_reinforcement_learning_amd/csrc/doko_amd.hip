@@ -1352,6 +1352,22 @@ int dk_net_embed_ln_bf16_async(const int32_t* d_tokens, uint32_t batch, const vo
     return DK_OK;
 }
 
+int dk_net_fc_gelu_bf16_async(const void* x, const void* w, const void* bias, uint32_t rows, uint32_t k, uint32_t n,
+                              void* y, void* stream) {
+    if (!x || !w || !bias || !y || (k != 160u && k != 256u) || n == 0 || n % (k == 160u ? 64u : 32u)) return DK_E_INVALID;
+    if (rows == 0) return DK_OK;
+    const uint32_t wg_rows = k == 160u ? 256u : 128u;   // 4 waves x (2 or 1) row tiles of 32
+    const dim3 grid((rows + wg_rows - 1u) / wg_rows), block(256);
+    if (k == 160u)
+        hipLaunchKernelGGL(dk::net::fc_gelu_kernel<160>, grid, block, 0, (hipStream_t)stream, (const uint16_t*)x,
+                           (const uint16_t*)w, (const uint16_t*)bias, (uint16_t*)y, rows, n);
+    else
+        hipLaunchKernelGGL(dk::net::fc_gelu_kernel<256>, grid, block, 0, (hipStream_t)stream, (const uint16_t*)x,
+                           (const uint16_t*)w, (const uint16_t*)bias, (uint16_t*)y, rows, n);
+    DK_HIP(hipGetLastError());
+    return DK_OK;
+}
+
 int dk_net_attn62_bf16_async(const void* qkv, void* y, uint32_t batch, uint32_t heads, uint32_t head_dim, void* stream) {
     if (!qkv || !y || heads != 4u || (head_dim != 40u && head_dim != 64u)) return DK_E_INVALID;
     if (batch == 0) return DK_OK;

@@ -74,3 +74,22 @@ def test_fused_network_matches_fp32_module():
     assert (p16.float() - p32).abs().max().item() < 0.05 * scale_p + 0.02
     # the policy argmax agrees on almost every row
     assert (p16.float().argmax(1) == p32.argmax(1)).float().mean().item() > 0.9
+
+
+@pytest.mark.parametrize("k,n", [(160, 640), (256, 1024)])
+def test_fc_gelu_matches_torch(k, n):
+    """Fused MLP first layer: GELU(x W^T + b) (exact erf GELU) against fp32 torch."""
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(5)
+    rows = 62 * 37 + 5                                   # not a multiple of the 256-row tile
+    x = torch.randn(rows, k, device=dev).bfloat16()
+    w = (torch.randn(n, k, device=dev) / k ** 0.5).bfloat16()
+    b = (torch.randn(n, device=dev) * 0.1).bfloat16()
+    y = torch.full((rows, n), float("nan"), device=dev).bfloat16()
+    rc = _lib().dk_net_fc_gelu_bf16_async(x.data_ptr(), w.data_ptr(), b.data_ptr(), rows, k, n, y.data_ptr(),
+                                          torch.cuda.current_stream(dev).cuda_stream)
+    assert rc == 0
+    torch.cuda.synchronize()
+    ref = F.gelu(F.linear(x.float(), w.float(), b.float()))
+    assert torch.isfinite(y.float()).all()
+    torch.testing.assert_close(y.float(), ref, rtol=1e-2, atol=1e-2)
