@@ -224,6 +224,7 @@ def main():
         b_sim = alg_bytes_per_sim(args.workload)
         achieved = n_roots * iters * b_sim / (kernel_ms / 1e3) / 1e9 if b_sim else None
         traffic = pmc_traffic(n_roots, iters) if args.workload == "c3" else None
+        valu_busy, mem_wait = pmc_valu_busy() if args.workload == "c3" else (None, None)
         workload_desc = {
             "c3": "C3 rs-full-doko determinized UCT: %d infostates x %d CAP samples/GPU-share, %d roots x %d sims per GPU"
                   % (I, args.samples, n_roots, iters),
@@ -269,9 +270,12 @@ def main():
                 "traffic": traffic,
                 "alg_bytes_per_sim": b_sim,
                 "stream_copy_peak_measured_gbs": stream_peak,
+                "valu_busy_pmc": valu_busy,
                 "note": "the search is bound by VALU issue and dependent-load latency (64-root waves, three per SIMD; "
-                        "PMC: VALU busy ~51% of the launch, 41% of wave cycles waiting on memory); achieved = the "
+                        "PMC: VALU busy %s of the launch, %s of wave cycles waiting on memory); achieved = the "
                         "SURVEY 8(d) algorithmic bytes from the oracle's counters / event-timed kernel; "
+                        % ("%.0f%%" % (100 * valu_busy) if valu_busy else "n/a",
+                           "%.0f%%" % (100 * mem_wait) if mem_wait else "n/a") +
                         "traffic = 2*FETCH_SIZE+WRITE_SIZE from profiles/pmc_search.json scaled per launch",
             },
             "cpu_baseline": cpu,
@@ -616,6 +620,18 @@ def stream_copy_gbs(torch, dev, nbytes=1 << 31, reps=10):
     gbs = 2.0 * nbytes * reps / (e0.elapsed_time(e1) / 1e3) / 1e9
     del a, b
     return gbs
+
+
+def pmc_valu_busy():
+    """VALU busy fraction of the search launch from the committed PMC summary:
+    SQ_INSTS_VALU x 4 cycles per wave64 instruction / SIMDs over GRBM_GUI_ACTIVE per XCD."""
+    path = os.path.join(ROOT, "profiles", "pmc_search.json")
+    try:
+        with open(path) as fh:
+            c = json.load(fh)["pmc_per_launch"]
+        return c["SQ_INSTS_VALU"] * 4.0 / 1024.0 / (c["GRBM_GUI_ACTIVE"] / 8.0), c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"]
+    except Exception:
+        return None, None
 
 
 def pmc_traffic(n_roots, iters):
