@@ -133,7 +133,8 @@ __global__ void __launch_bounds__(WAVE, H::MIN_WAVES) search_kernel(const dk_sta
                                                       uint32_t* ovf, uint64_t* ovf_st,
                                                       uint32_t cap_slots, uint32_t rpw, int lds_n,
                                                       uint32_t* visits, double* values,
-                                                      uint8_t* best, int* err, uint32_t* queue, uint64_t* prof) {
+                                                      uint8_t* best, int* err, uint32_t* queue, uint64_t* prof,
+                                                      const uint32_t* __restrict__ order) {
     const uint32_t lane = threadIdx.x;
     const uint32_t T = iters + 1;
     const uint32_t n_ln = LN_LDS ? T : 0u;
@@ -150,6 +151,7 @@ __global__ void __launch_bounds__(WAVE, H::MIN_WAVES) search_kernel(const dk_sta
         if (lane == 0) g = atomicAdd(queue, 1u);
         g = __shfl(g, 0);
         if (g >= groups) break;                                         // every wave reaches this
+        if (order) g = order[g];                                        // longest groups first
         const uint32_t root = g * rpw + lane;
         if (lane >= rpw || root >= n) continue;
         typename E::Work w;
@@ -527,6 +529,30 @@ __global__ void ar_output_kernel(const dk_az_state* info, uint32_t samples, uint
 
 // PolicyFusionMaxN / PolicyFusionAverageStrategy accumulators (policy_fusion.rs:23-123).
 // One thread per (infostate, action).
+// Queue order of the search's root groups: descending cards left to play (the group's first
+// root), so the longest trees start first and the persistent grid's tail is made of short
+// groups (longest-processing-time-first).  Roots are independent, so the order changes no
+// result.  One workgroup: a 64-bin counting sort (order within a bin is arbitrary).
+__global__ void __launch_bounds__(1024) group_order_kernel(const dk_state* roots, uint32_t n, uint32_t rpw,
+                                                           uint32_t groups, uint32_t* order) {
+    __shared__ uint32_t hist[64];
+    if (threadIdx.x < 64) hist[threadIdx.x] = 0;
+    __syncthreads();
+    auto key = [&](uint32_t g) {
+        const uint32_t ci = roots[(size_t)g * rpw].fdo.card_index;
+        return 63u - (ci < 48u ? 48u - ci : 0u);   // ascending key = descending cards left
+    };
+    for (uint32_t g = threadIdx.x; g < groups; g += blockDim.x) atomicAdd(&hist[key(g)], 1u);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t sum = 0;
+        for (int b = 0; b < 64; ++b) { const uint32_t c = hist[b]; hist[b] = sum; sum += c; }
+    }
+    __syncthreads();
+    for (uint32_t g = threadIdx.x; g < groups; g += blockDim.x) order[atomicAdd(&hist[key(g)], 1u)] = g;
+    (void)n;
+}
+
 // `valid` (nullable): per-sample flags; samples with valid == 0 (failed determinizations,
 // compare_impi.rs:276-288) take no part in the fusion.
 __global__ void fuse_accumulate_kernel(const uint32_t* visits, uint32_t n_info, uint32_t samples, const uint8_t* valid,
@@ -595,6 +621,8 @@ struct dk_ctx {
                                     // the resident capacity: CUs x 12 single-wave workgroups x 64 lanes))
     int cu_count = 0;
     uint32_t* queue = nullptr;      // root-group counter of the persistent search grid
+    uint32_t* order = nullptr;      // queue order of the root groups (group_order_kernel)
+    int group_order = -1;           // DK_GROUP_ORDER=0 / 1 forces index order / longest-first; -1: per engine
     void* hot = nullptr;            // hot records, 32 B per slot (NodeHot16 launches use half)
     dk::NodeCold* cold = nullptr;
     uint32_t* ovf = nullptr;
@@ -694,9 +722,18 @@ hipError_t launch_search_t(dk_ctx* ctx, const dk_state* roots, const uint64_t* s
     if (grid == 0) return hipErrorInvalidValue;
     hipError_t e = hipMemsetAsync(ctx->queue, 0, sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
+    // group order only matters when waves take several groups each
+    const bool want = ctx->group_order < 0 ? E::ORDER_GROUPS : ctx->group_order == 1;
+    const bool ordered = want && E::GAME != DK_GAME_TTT && groups > grid;
+    if (ordered) {
+        hipLaunchKernelGGL(group_order_kernel, dim3(1), dim3(1024), 0, st, roots, n, rpw, groups, ctx->order);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
     hipLaunchKernelGGL(kern, dim3(grid), dim3(WAVE), lds_bytes, st, roots, seeds, n, iters, c, ctx->ln_table,
                        ctx->hot, ctx->cold, (typename E::Work*)ctx->states, ctx->ovf, ctx->ovf_st, ctx->cap_slots,
-                       rpw, ctx->lds_path, visits, values, best, ctx->err, ctx->queue, ctx->prof);
+                       rpw, ctx->lds_path, visits, values, best, ctx->err, ctx->queue, ctx->prof,
+                       ordered ? (const uint32_t*)ctx->order : (const uint32_t*)nullptr);
     return hipGetLastError();
 }
 
@@ -759,6 +796,7 @@ dk_ctx* dk_create(const dk_config* cfg) {
         const int v = atoi(e);
         if (v >= 1 && v <= WAVE) { ctx->roots_per_wave = (uint32_t)v; ctx->rpw_fixed = true; }
     }
+    if (const char* e = getenv("DK_GROUP_ORDER")) ctx->group_order = atoi(e) != 0 ? 1 : 0;
     if (const char* e = getenv("DK_HOT_RECORD")) {
         const int v = atoi(e);
         if (v == 16 || v == 32) ctx->hot_layout = v;
@@ -788,6 +826,7 @@ dk_ctx* dk_create(const dk_config* cfg) {
     ok = ok && hipMalloc(&ctx->ln_table, (T + 1) * sizeof(double)) == hipSuccess;
     ok = ok && hipMalloc(&ctx->err, sizeof(int)) == hipSuccess;
     ok = ok && hipMalloc(&ctx->queue, sizeof(uint32_t)) == hipSuccess;
+    ok = ok && hipMalloc(&ctx->order, ((size_t)cfg->max_roots + 1) * sizeof(uint32_t)) == hipSuccess;
     ok = ok && hipEventCreate(&ctx->ev0) == hipSuccess && hipEventCreate(&ctx->ev1) == hipSuccess;
 #ifdef DK_PHASE_PROF
     ok = ok && hipMalloc(&ctx->prof, (size_t)cfg->max_roots * 16 * sizeof(uint64_t)) == hipSuccess;
@@ -818,6 +857,7 @@ void dk_destroy(dk_ctx* ctx) {
     if (ctx->ln_table) (void)hipFree(ctx->ln_table);
     if (ctx->err) (void)hipFree(ctx->err);
     if (ctx->queue) (void)hipFree(ctx->queue);
+    if (ctx->order) (void)hipFree(ctx->order);
     if (ctx->prof) (void)hipFree(ctx->prof);
     if (ctx->az_nodes) (void)hipFree(ctx->az_nodes);
     if (ctx->ar_lanes) (void)hipFree(ctx->ar_lanes);

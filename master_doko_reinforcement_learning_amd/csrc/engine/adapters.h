@@ -10,6 +10,9 @@ struct FdoE {
     using Work = fdo::Work;
     using Packed = dk_fdo_state;
     static constexpr int GAME = DK_GAME_FULL_DOKO;
+    // search queue in root-index order: longest-first ordering measured 5 % slower on C3
+    // (heavy groups started together contend for the caches)
+    static constexpr bool ORDER_GROUPS = false;
     DK_HD static void load(const dk_state& s, Work& w) { fdo::unpack(s.fdo, w); }
     DK_HD static uint64_t allowed(const Work& w, bool first) { return fdo::env_allowed(w, first); }
     DK_HD static int current_player(const Work& w) { return fdo::env_current_player(w); }
@@ -28,6 +31,8 @@ struct DoE {
     using Work = dko::Work;
     using Packed = dk_do_state;
     static constexpr int GAME = DK_GAME_DOKO;
+    // search queue longest-first (group_order_kernel): 4 % faster on C2d
+    static constexpr bool ORDER_GROUPS = true;
     DK_HD static void load(const dk_state& s, Work& w) { dko::unpack(s.dk, w); }
     DK_HD static uint64_t allowed(const Work& w, bool first) { return dko::env_allowed(w, first); }
     DK_HD static int current_player(const Work& w) { return dko::env_current_player(w); }
@@ -42,6 +47,7 @@ struct TttE {
     using Work = ttt::Work;
     using Packed = dk_ttt_state;
     static constexpr int GAME = DK_GAME_TTT;
+    static constexpr bool ORDER_GROUPS = false;
     DK_HD static void load(const dk_state& s, Work& w) { ttt::unpack(s.ttt, w); }
     DK_HD static uint64_t allowed(const Work& w, bool first) { return ttt::env_allowed(w, first); }
     DK_HD static int current_player(const Work& w) { return ttt::env_current_player(w); }
