@@ -36,11 +36,12 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--workload", choices=["c3", "c2", "c2d", "c5", "impi"], default="c3",
+    p.add_argument("--workload", choices=["c3", "c2", "c2d", "c5", "impi", "impid"], default="c3",
                    help="c3: rs-full-doko + CAP (default, the metric's config); c2: rs-doko roots after 4x Healthy; "
                         "c2d: rs-doko infostates determinized by the rule-based sampler; "
                         "c5: AlphaZero self-play moves (PUCT + policy/value network); "
-                        "impi: autoregressive (IMPI) determinization of the c3 infostates with the IMPI network")
+                        "impi: autoregressive (IMPI) determinization of the c3 infostates with the IMPI network; "
+                        "impid: the AR-determinized decision (mcts_ar_maxn_policy: AR samples -> UCT -> MaxN)")
     p.add_argument("--games", type=int, default=8192, help="concurrent self-play games per GPU (c5)")
     p.add_argument("--az-iterations", type=int, default=200, help="PUCT iterations per move (c5)")
     p.add_argument("--ar-samples", type=int, default=4, help="AR samples per infostate (impi)")
@@ -179,7 +180,7 @@ def main():
 
     if args.workload == "c5":
         return run_c5(args, dk, L, dev, stream, rank, world, local_rank, dist)
-    if args.workload == "impi":
+    if args.workload in ("impi", "impid"):
         return run_impi(args, dk, L, dev, stream, rank, world, local_rank, dist)
     eng, step, n_roots, bufs = make_workload(args, dk, L, dev, sp, rank, world, local_rank, dist)
     determinized = args.workload in ("c3", "c2d")
@@ -424,12 +425,16 @@ def run_impi(args, dk, L, dev, stream, rank, world, local_rank, dist):
     k in {0, 8, 20, 32} random plies).  One step = every card and hidden reservation
     of every sample guessed by the IMPI network (DokoImpiNet, d 256, 4 blocks, bf16),
     one batched network call per round, temperature 0.4 (all_policies.rs:30), then the
-    consistency check.  Infostates are independent: N GPUs run N replicas."""
+    consistency check.  Infostates are independent: N GPUs run N replicas.
+    impid: the whole mcts_ar_maxn_policy decision (all_policies.rs:78-101) per step: the AR
+    samples, then UCT (`iterations`, c) on each sample, MaxN fusion over the consistent ones
+    and the random fallback (ArImpiPolicy)."""
     import torch
     from master_doko_reinforcement_learning_amd.impi_network import DokoImpiNet
     torch.manual_seed(4321 + rank)
     I, S = args.infostates, args.ar_samples
-    eng = dk.Engine(device=local_rank, max_roots=64, max_iterations=1)
+    decide = args.workload == "impid"
+    eng = dk.Engine(device=local_rank, max_roots=I * S if decide else 64, max_iterations=args.iterations if decide else 1)
     sp = stream.cuda_stream
 
     def ck(rc):
@@ -460,13 +465,20 @@ def run_impi(args, dk, L, dev, stream, rank, world, local_rank, dist):
 
     ar = dk.ARSampling(eng, network, args.ar_temperature)
     seeds = np.arange(I * S, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15) + np.uint64(0xA5000000 + rank)
+    policy = dk.ArImpiPolicy(eng, network, args.c, args.iterations, S, dk.FUSE_MAXN, args.ar_temperature) if decide else None
+    pol_seeds = np.arange(2 * I * S + I, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15) + np.uint64(0xA6000000 + rank)
     stats = {"rows": 0, "consistent": 0, "lanes": 0}
 
     def step():
         with torch.inference_mode():
-            _, status, _ = ar.sample(records, S, seeds)
-        stats["rows"] += ar.rows
-        stats["consistent"] += int((status == 0).sum().item())
+            if decide:
+                _, succ, _ = policy.execute(records, pol_seeds)
+                stats["rows"] += policy.sampler.rows
+                stats["consistent"] += int(succ.sum().item())
+            else:
+                _, status, _ = ar.sample(records, S, seeds)
+                stats["rows"] += ar.rows
+                stats["consistent"] += int((status == 0).sum().item())
         stats["lanes"] += I * S
 
     for _ in range(args.warmup):
@@ -494,9 +506,11 @@ def run_impi(args, dk, L, dev, stream, rank, world, local_rank, dist):
     if rank == 0:
         achieved = flop * stats["rows"] / (net_ms / 1e3) / 1e12
         result = {
-            "metric": "IMPI autoregressive determinizations/sec (forward_pred_process_with_mask, one network call per guessed card)",
-            "value": I * S * args.steps * world / elapsed,
-            "unit": "samples/s",
+            "metric": ("AR-determinized decisions/sec (mcts_ar_maxn_policy: %d AR samples x %d UCT simulations each)"
+                       % (S, args.iterations)) if decide else
+                      "IMPI autoregressive determinizations/sec (forward_pred_process_with_mask, one network call per guessed card)",
+            "value": (I if decide else I * S) * args.steps * world / elapsed,
+            "unit": "decisions/s" if decide else "samples/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -504,16 +518,18 @@ def run_impi(args, dk, L, dev, stream, rank, world, local_rank, dist):
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16 network, f32 softmax / weighted draw",
+            "dtype": "bf16 network, f32 softmax / weighted draw" + (", u64+f64 search" if decide else ""),
             "data": "synthetic: the C3 infostates (seeded deals, 4x Healthy, k in {0,8,20,32} random plies), "
                     "random-initialised DokoImpiNet (d 256, 4 blocks, 4 heads)",
-            "config": {"workload": "IMPI AR determinization: %d infostates x %d samples per GPU" % (I, S),
-                       "temperature": args.ar_temperature, "network_rounds": ar.rounds,
+            "config": {"workload": ("IMPI AR decision: %d infostates x %d AR samples x %d sims per GPU" % (I, S, args.iterations))
+                                   if decide else "IMPI AR determinization: %d infostates x %d samples per GPU" % (I, S),
+                       "temperature": args.ar_temperature, "network_rounds": ar.rounds if not decide else policy.sampler.rounds,
                        "network_rows_per_step": stats["rows"] // args.steps,
                        "consistent_fraction": stats["consistent"] / max(1, stats["lanes"]),
                        "parallelism": "replicas x%d" % world},
             "network_ms_per_step": net_ms / args.steps,
-            "sampler_ms_per_step": elapsed / args.steps * 1e3 - net_ms / args.steps,
+            ("search_sampler_fusion_ms_per_step" if decide else "sampler_ms_per_step"):
+                elapsed / args.steps * 1e3 - net_ms / args.steps,
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": 2500.0, "unit": "TFLOP/s",
                          "frac": achieved / 2500.0, "traffic": None,
                          "note": "IMPI network: %.1f MFLOP per guess (algorithmic), rows = guesses actually needed "
