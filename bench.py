@@ -2,11 +2,11 @@
 
 One step = one determinized decision batch of BASELINE.json config 3 on every
 GPU, entirely on the device:
-    CAP determinization (card_matching_full)  -> 6144 infostates x 64 samples = 393,216 roots
+    CAP determinization (card_matching_full)  -> 12288 infostates x 64 samples = 786,432 roots
     UCT search, 1000 simulations per root (select/expand/random rollout/backup)
     policy fusion (MaxN) of the per-sample visit counts per infostate
-With N GPUs (config 4) the global batch holds 6144*N infostates; the 64 samples
-of every infostate are split evenly over the ranks (393,216 roots per GPU, weak
+With N GPUs (config 4) the global batch holds 12288*N infostates; the 64 samples
+of every infostate are split evenly over the ranks (786,432 roots per GPU, weak
 scaling) and the per-infostate fusion accumulators are summed with one RCCL
 all-reduce over xGMI before the fused action is selected.
 
@@ -47,9 +47,9 @@ def parse():
     p.add_argument("--ar-samples", type=int, default=4, help="AR samples per infostate (impi)")
     p.add_argument("--ar-temperature", type=float, default=0.4, help="AR sampling temperature (impi; all_policies.rs:30)")
     p.add_argument("--iterations", type=int, default=1000)
-    p.add_argument("--infostates", type=int, default=6144,
-                   help="infostates per GPU (c3, c2d, impi): 6144 x 64 samples = 393,216 roots, two 64-root groups per "
-                        "resident wave (pools for 3072 waves = 196,608 roots)")
+    p.add_argument("--infostates", type=int, default=12288,
+                   help="infostates per GPU (c3, c2d, impi): 12288 x 64 samples = 786,432 roots, about four 64-root groups "
+                        "per resident wave (pools for 3072 waves = 196,608 roots)")
     p.add_argument("--samples", type=int, default=64, help="samples per infostate (c3, c2d)")
     p.add_argument("--roots", type=int, default=32768, help="roots per GPU (c2)")
     p.add_argument("--c", type=float, default=2.5)
@@ -421,7 +421,7 @@ def impi_flop_per_eval(d=256, seq=62, blocks=4, classes=33):
 def run_impi(args, dk, L, dev, stream, rank, world, local_rank, dist):
     """§8(f) row 4: the ARSampling SamplingFn (compare_impi.rs:84-105), i.e.
     forward_pred_process_with_mask (rs-doko-impi/src/forward.rs:392-661), for
-    `ar_samples` draws of each of the C3 infostates (6144 per GPU, 4 x Healthy then
+    `ar_samples` draws of each of the C3 infostates (12288 per GPU, 4 x Healthy then
     k in {0, 8, 20, 32} random plies).  One step = every card and hidden reservation
     of every sample guessed by the IMPI network (DokoImpiNet, d 256, 4 blocks, bf16),
     one batched network call per round, temperature 0.4 (all_policies.rs:30), then the

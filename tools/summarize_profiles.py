@@ -16,7 +16,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def main(tag="r01", roots=262144, iterations=1000):
+def main(tag="r01", roots=None, iterations=None):
     src = os.path.join(ROOT, "gpurun_out", "prof_" + tag)
     dst = os.path.join(ROOT, "profiles", tag)
     os.makedirs(dst, exist_ok=True)
@@ -43,6 +43,11 @@ def main(tag="r01", roots=262144, iterations=1000):
     if traced_bench is not None:
         with open(os.path.join(dst, "bench_under_trace.json"), "w") as fh:
             json.dump(traced_bench, fh, indent=1)
+    # the launch size the PMC passes ran (bench.py defaults: the traced run's config)
+    if roots is None:
+        roots = traced_bench["config"]["roots_per_gpu"] if traced_bench else None
+    if iterations is None:
+        iterations = traced_bench["config"]["iterations"] if traced_bench else None
     pmc = {}
     for f in sorted(glob.glob(os.path.join(src, "pmc*", "p_counter_collection.csv"))):
         per = {}
