@@ -639,9 +639,10 @@ struct dk_ctx {
     int hot_layout = 0;             // DK_HOT_RECORD=16|32 fixes the hot-record layout; 0 = per launch
     bool ln_in_lds = false;         // DK_LN_LDS=1: ln(N) table copied into every workgroup's LDS (8 KB at
                                     // 1000 iterations); by default it is read through the L1/L2 caches
-    int lds_path = 16;              // DK_LDS_PATH (path entries kept in LDS, <= MAX_PATH; deeper ones
-                                    // spill to global).  16 keeps a workgroup at 12 KB of LDS so that
-                                    // 12 single-wave workgroups (3 per SIMD) fit a CU's 160 KB.
+    int lds_path = 16;              // path entries kept in LDS (deeper ones spill to global): at most
+                                    // 16, shortened per launch while it costs residency (launch_search_t)
+    bool lds_path_fixed = false;    // DK_LDS_PATH (1..MAX_PATH) fixes it
+    bool verbose = false;           // DK_VERBOSE=1: one stderr line per search launch (shape, residency)
     uint64_t* prof = nullptr;       // phase timers (DK_PHASE_PROF builds only)
     // AlphaZero PUCT search (dk_az_*): per-game node / state regions, allocated on first use
     dk::az::Node* az_nodes = nullptr;
@@ -709,17 +710,36 @@ uint32_t launch_rpw(const dk_ctx* ctx, uint32_t n) {
 template <class E, bool LN, class H>
 hipError_t launch_search_t(dk_ctx* ctx, const dk_state* roots, const uint64_t* seeds, uint32_t n, uint32_t iters,
                            double c, uint32_t* visits, double* values, uint8_t* best, hipStream_t st,
-                           size_t lds_bytes, uint32_t rpw) {
+                           size_t ln_bytes, uint32_t rpw) {
     const auto kern = search_kernel<E, LN, H>;
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, WAVE, lds_bytes) != hipSuccess || per_cu < 1)
-        per_cu = 1;
+    auto occupancy = [&](int lp) {
+        int b = 0;
+        const size_t bytes = ln_bytes + (size_t)lp * rpw * 12;
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kern, WAVE, bytes) == hipSuccess ? b : 0;
+    };
+    // LDS path length: DK_LDS_PATH, or else the longest (<= 16) that keeps the residency
+    // the registers allow with one entry of headroom.  At 64 roots per wave a 16-entry
+    // path (12 KB + the card table) fits 11 workgroups per CU; the calculator admits 12
+    // at 15 entries, but 15 measured no faster than 16 (the hardware's LDS allocation
+    // granularity), while 14 is 4 % faster on C3 (tools/ab_ldspath.sh, medians of 5).
+    // Paths deeper than 14 are rare and spill to the global overflow.
+    int lp = ctx->lds_path;
+    if (!ctx->lds_path_fixed) {
+        const int best = occupancy(1);
+        while (lp > 1 && occupancy(lp + 1) < best) --lp;
+    }
+    const size_t lds_bytes = ln_bytes + (size_t)lp * rpw * 12;
+    int per_cu = occupancy(lp);
+    if (per_cu < 1) per_cu = 1;
     const uint32_t groups = grid_for(n, rpw);
     const uint32_t resident = (uint32_t)per_cu * (uint32_t)ctx->cu_count;
     const uint32_t regions = ctx->pool_roots / rpw;
     uint32_t grid = groups < resident ? groups : resident;
     grid = grid < regions ? grid : regions;
     if (grid == 0) return hipErrorInvalidValue;
+    if (ctx->verbose)
+        fprintf(stderr, "doko_amd: search n=%u rpw=%u hot=%dB lds_path=%d lds=%zuB resident/CU=%d grid=%u\n", n, rpw,
+                (int)sizeof(H), lp, lds_bytes, per_cu, grid);
     hipError_t e = hipMemsetAsync(ctx->queue, 0, sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
     // group order only matters when waves take several groups each
@@ -732,7 +752,7 @@ hipError_t launch_search_t(dk_ctx* ctx, const dk_state* roots, const uint64_t* s
     }
     hipLaunchKernelGGL(kern, dim3(grid), dim3(WAVE), lds_bytes, st, roots, seeds, n, iters, c, ctx->ln_table,
                        ctx->hot, ctx->cold, (typename E::Work*)ctx->states, ctx->ovf, ctx->ovf_st, ctx->cap_slots,
-                       rpw, ctx->lds_path, visits, values, best, ctx->err, ctx->queue, ctx->prof,
+                       rpw, lp, visits, values, best, ctx->err, ctx->queue, ctx->prof,
                        ordered ? (const uint32_t*)ctx->order : (const uint32_t*)nullptr);
     return hipGetLastError();
 }
@@ -742,16 +762,16 @@ hipError_t launch_search(dk_ctx* ctx, const dk_state* roots, const uint64_t* see
                          double c, uint32_t* visits, double* values, uint8_t* best, hipStream_t st) {
     const bool ln = iters + 1 <= LN_LDS_MAX && ctx->ln_in_lds;
     const uint32_t rpw = launch_rpw(ctx, n);
-    const size_t lds_bytes = (ln ? (size_t)((iters + 2) & ~1u) * 8 : 0) + (size_t)ctx->lds_path * rpw * 12;
+    const size_t ln_bytes = ln ? (size_t)((iters + 2) & ~1u) * 8 : 0;
     // hot-record layout (search_core.h): 16 B once the batch gives every SIMD two waves,
     // 32 B (cached means) when a single wave per SIMD leaves the pick's latency exposed
     const uint32_t simds = 4u * (uint32_t)ctx->cu_count;
     const bool h16 = ctx->hot_layout ? ctx->hot_layout == 16 : grid_for(n, rpw) >= 2u * simds;
     if (h16)
-        return ln ? launch_search_t<E, true, dk::NodeHot16>(ctx, roots, seeds, n, iters, c, visits, values, best, st, lds_bytes, rpw)
-                  : launch_search_t<E, false, dk::NodeHot16>(ctx, roots, seeds, n, iters, c, visits, values, best, st, lds_bytes, rpw);
-    return ln ? launch_search_t<E, true, dk::NodeHot32>(ctx, roots, seeds, n, iters, c, visits, values, best, st, lds_bytes, rpw)
-              : launch_search_t<E, false, dk::NodeHot32>(ctx, roots, seeds, n, iters, c, visits, values, best, st, lds_bytes, rpw);
+        return ln ? launch_search_t<E, true, dk::NodeHot16>(ctx, roots, seeds, n, iters, c, visits, values, best, st, ln_bytes, rpw)
+                  : launch_search_t<E, false, dk::NodeHot16>(ctx, roots, seeds, n, iters, c, visits, values, best, st, ln_bytes, rpw);
+    return ln ? launch_search_t<E, true, dk::NodeHot32>(ctx, roots, seeds, n, iters, c, visits, values, best, st, ln_bytes, rpw)
+              : launch_search_t<E, false, dk::NodeHot32>(ctx, roots, seeds, n, iters, c, visits, values, best, st, ln_bytes, rpw);
 }
 
 }  // namespace
@@ -801,10 +821,11 @@ dk_ctx* dk_create(const dk_config* cfg) {
         const int v = atoi(e);
         if (v == 16 || v == 32) ctx->hot_layout = v;
     }
+    if (const char* e = getenv("DK_VERBOSE")) ctx->verbose = atoi(e) != 0;
     if (const char* e = getenv("DK_LN_LDS")) ctx->ln_in_lds = atoi(e) != 0;
     if (const char* e = getenv("DK_LDS_PATH")) {
         const int v = atoi(e);
-        if (v >= 1 && v <= MAX_PATH) ctx->lds_path = v;
+        if (v >= 1 && v <= MAX_PATH) { ctx->lds_path = v; ctx->lds_path_fixed = true; }
     }
     // The search grid is persistent (search_kernel): the pools hold the resident waves'
     // roots, and a larger batch streams through them.

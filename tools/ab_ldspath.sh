@@ -1,10 +1,17 @@
 #!/bin/bash
-# C3: LDS path entries per lane (DK_LDS_PATH; 14 lets 12 workgroups fit a CU's LDS) and batch size.
+# C3 at the bench default batch: LDS path entries per lane (interleaved reps; box clocks
+# drift, so compare medians).  "auto" = the per-launch choice (launch_search_t);
+# DK_VERBOSE prints the residency each launch gets.
 set -u
-for r in 1 2 3; do
-  for cfg in "16 6144" "14 6144" "16 5632"; do
-    set -- $cfg
-    out=$(DK_LDS_PATH=$1 timeout -k 10 200 python bench.py --infostates $2 --steps 2 --warmup 1 --no-cpu-baseline) || exit $?
-    echo "lds_path=$1 inf=$2 $(echo "$out" | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print("%.3f G/s kernel %.2f ms" % (d["value"]/1e9, d["search_kernel_ms"]))')"
+REPS=${REPS:-5}
+for lp in auto 16 15 14; do
+  if [ "$lp" = auto ]; then env_lp=""; else env_lp="DK_LDS_PATH=$lp"; fi
+  env $env_lp DK_VERBOSE=1 timeout -k 10 300 python bench.py --steps 1 --warmup 0 --no-cpu-baseline 2>&1 >/dev/null | grep "search n=" | sort | uniq -c || exit $?
+done
+for r in $(seq $REPS); do
+  for lp in ${LPS:-16 15 14}; do
+    if [ "$lp" = auto ]; then env_lp=""; else env_lp="DK_LDS_PATH=$lp"; fi
+    out=$(env $env_lp timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline) || exit $?
+    echo "lds_path=$lp $(echo "$out" | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print("%.3f G/s kernel %.2f ms" % (d["value"]/1e9, d["search_kernel_ms"]))')"
   done
 done
