@@ -2,11 +2,11 @@
 
 One step = one determinized decision batch of BASELINE.json config 3 on every
 GPU, entirely on the device:
-    CAP determinization (card_matching_full)  -> 12288 infostates x 64 samples = 786,432 roots
+    CAP determinization (card_matching_full)  -> 18432 infostates x 64 samples = 1,179,648 roots
     UCT search, 1000 simulations per root (select/expand/random rollout/backup)
     policy fusion (MaxN) of the per-sample visit counts per infostate
-With N GPUs (config 4) the global batch holds 12288*N infostates; the 64 samples
-of every infostate are split evenly over the ranks (786,432 roots per GPU, weak
+With N GPUs (config 4) the global batch holds 18432*N infostates; the 64 samples
+of every infostate are split evenly over the ranks (1,179,648 roots per GPU, weak
 scaling) and the per-infostate fusion accumulators are summed with one RCCL
 all-reduce over xGMI before the fused action is selected.
 
@@ -47,9 +47,9 @@ def parse():
     p.add_argument("--ar-samples", type=int, default=4, help="AR samples per infostate (impi)")
     p.add_argument("--ar-temperature", type=float, default=0.4, help="AR sampling temperature (impi; all_policies.rs:30)")
     p.add_argument("--iterations", type=int, default=1000)
-    p.add_argument("--infostates", type=int, default=12288,
-                   help="infostates per GPU (c3, c2d, impi): 12288 x 64 samples = 786,432 roots, about four 64-root groups "
-                        "per resident wave (pools for 3072 waves = 196,608 roots)")
+    p.add_argument("--infostates", type=int, default=None,
+                   help="infostates per GPU (c3: default 18432 x 64 samples = 1,179,648 roots, six 64-root groups per "
+                        "resident wave (3072 waves); c2d, impi, impid: default 12288)")
     p.add_argument("--samples", type=int, default=64, help="samples per infostate (c3, c2d)")
     p.add_argument("--roots", type=int, default=32768, help="roots per GPU (c2)")
     p.add_argument("--c", type=float, default=2.5)
@@ -58,7 +58,10 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=0)
     p.add_argument("--cpu-roots-per-thread", type=int, default=96)
     p.add_argument("--dump-actions", default="", help="rank 0 writes the fused actions (.npy) of the last step")
-    return p.parse_args()
+    a = p.parse_args()
+    if a.infostates is None:
+        a.infostates = 18432 if a.workload == "c3" else 12288   # c2d: 2.18 G/s at 18432 against 2.24 at 12288
+    return a
 
 
 def make_workload(args, dk, L, dev, sp, rank, world, local_rank, dist=None):
