@@ -58,13 +58,17 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=0)
     p.add_argument("--cpu-roots-per-thread", type=int, default=96)
     p.add_argument("--dump-actions", default="", help="rank 0 writes the fused actions (.npy) of the last step")
+    p.add_argument("--dump-acc", default="", help="rank 0 writes the all-reduced fusion accumulators (.npy) of the last step")
+    p.add_argument("--small-infostates", type=int, default=512,
+                   help="c3: also time the survey's small decision batch (512 infostates x 64 = 32,768 roots); 0 = skip")
+    p.add_argument("--small-steps", type=int, default=5)
     a = p.parse_args()
     if a.infostates is None:
         a.infostates = 18432 if a.workload == "c3" else 12288   # c2d: 2.18 G/s at 18432 against 2.24 at 12288
     return a
 
 
-def make_workload(args, dk, L, dev, sp, rank, world, local_rank, dist=None):
+def make_workload(args, dk, L, dev, sp, rank, world, local_rank, dist=None, eng=None):
     """Build the synthetic inputs on the GPU (untimed) and return (engine, step,
     n_roots, buffers).  `step()` runs one pass of the hot path on stream `sp`."""
     import torch
@@ -89,7 +93,8 @@ def make_workload(args, dk, L, dev, sp, rank, world, local_rank, dist=None):
     else:
         I, S_r = 0, 0
         n_roots = args.roots
-    eng = dk.Engine(device=local_rank, max_roots=n_roots, max_iterations=iters)
+    if eng is None:
+        eng = dk.Engine(device=local_rank, max_roots=n_roots, max_iterations=iters)
 
     # ------------------------------------------------------------ inputs (untimed, on the GPU)
     def healthy_round(states_t, n):
@@ -143,30 +148,79 @@ def make_workload(args, dk, L, dev, sp, rank, world, local_rank, dist=None):
                                        ptr(visits), ptr(values), ptr(best), sp))
 
     return eng, step, n_roots, {"visits": visits, "values": values, "best": best, "roots": roots, "I": I, "S_r": S_r,
-                                "actions": actions if determinized else None}
+                                "actions": actions if determinized else None,
+                                "acc": (acc_u if fuse_mode == dk.FUSE_MAXN else acc_f) if determinized else None}
+
+
+def launch_ranks(args):
+    """`--gpus N` outside a torchrun environment: start the N ranks (one process per GPU)
+    as children under torch.distributed.run and return their exit status.  Called before
+    this process touches the GPU (no HIP call, no torch.cuda query)."""
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def timed_steps(step, steps, warmup, eng, L, dev, world, dist, ck, sp):
+    """W untimed steps, then exactly K steps bracketed by barrier + synchronize; returns
+    (max-over-ranks wall seconds, per-step search-kernel ms)."""
+    import torch
+    search_ms = []
+    for _ in range(warmup):
+        step()
+    ck(L.dk_sync(eng.ctx, sp))
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+        search_ms.append(eng.last_search_ms())  # waits for this step's search kernel (HIP events on its stream)
+    torch.cuda.synchronize(dev)
+    ck(L.dk_sync(eng.ctx, sp))
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item()), search_ms
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d (launch one rank per GPU)" % (args.gpus, world))
     import torch
     import torch.distributed as dist
 
     import master_doko_reinforcement_learning_amd as dk
     from master_doko_reinforcement_learning_amd import _native
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     # one GPU per rank; DK_DIST_BACKEND=gloo + more ranks than GPUs is the
     # rehearsal mode for the multi-GPU path on a one-GPU box (ranks share a device)
     backend = os.environ.get("DK_DIST_BACKEND", "nccl")
-    device = local_rank % max(1, torch.cuda.device_count()) if backend != "nccl" else local_rank
+    ndev = torch.cuda.device_count()
+    if backend == "nccl" and world > ndev:
+        raise SystemExit("bench.py: --gpus %d needs %d GPUs, %d visible (DK_DIST_BACKEND=gloo shares devices)"
+                         % (world, world, ndev))
+    device = local_rank % max(1, ndev) if backend != "nccl" else local_rank
     torch.cuda.set_device(device)
     if world > 1:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", device))   # RCCL over xGMI
         else:
             dist.init_process_group(backend)
+        assert dist.get_world_size() == args.gpus
     dev = torch.device("cuda", device)
     local_rank = device
     L = _native.lib()
@@ -187,38 +241,35 @@ def main():
         return run_impi(args, dk, L, dev, stream, rank, world, local_rank, dist)
     eng, step, n_roots, bufs = make_workload(args, dk, L, dev, sp, rank, world, local_rank, dist)
     determinized = args.workload in ("c3", "c2d")
-    search_ms = []
     iters = args.iterations
     visits = bufs["visits"]
     I = bufs["I"]
 
-    for _ in range(args.warmup):
-        step()
-    ck(L.dk_sync(eng.ctx, sp))
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-        ms = eng.last_search_ms()  # waits for this step's search kernel (HIP events on its stream)
-        search_ms.append(ms)
-    torch.cuda.synchronize(dev)
-    ck(L.dk_sync(eng.ctx, sp))
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
-
+    elapsed, search_ms = timed_steps(step, args.steps, args.warmup, eng, L, dev, world, dist, ck, sp)
     if rank == 0 and args.dump_actions and bufs["actions"] is not None:
         np.save(args.dump_actions, bufs["actions"].cpu().numpy())
+    if rank == 0 and args.dump_acc and bufs["acc"] is not None:
+        np.save(args.dump_acc, bufs["acc"].cpu().numpy())
     v = visits.cpu().numpy()
     assert np.all(v.sum(axis=1) == iters), "every root must have exactly `iterations` simulations"
     sims_total = n_roots * iters * args.steps * world
     kernel_ms = float(np.mean(search_ms))
+    del v, bufs, visits
+
+    # the survey's C3 decision batch (512 infostates x 64 samples = 32,768 roots): the regime a
+    # DefaultImpiPolicy caller with one decision batch per game step sees (same engine, own buffers)
+    small = None
+    if args.workload == "c3" and args.small_infostates:
+        import copy
+        sa = copy.copy(args)
+        sa.infostates = args.small_infostates
+        _, sstep, s_roots, sbufs = make_workload(sa, dk, L, dev, sp, rank, world, local_rank, dist, eng=eng)
+        s_el, s_ms = timed_steps(sstep, args.small_steps, 1, eng, L, dev, world, dist, ck, sp)
+        assert np.all(sbufs["visits"].cpu().numpy().sum(axis=1) == iters)
+        small = {"infostates_per_gpu": args.small_infostates, "roots_per_gpu": s_roots, "steps": args.small_steps,
+                 "value": s_roots * iters * args.small_steps * world / s_el, "unit": "rollouts/s",
+                 "ms_per_step": s_el / args.small_steps * 1e3, "search_kernel_ms": float(np.mean(s_ms))}
+        del sbufs
 
     result = None
     if rank == 0:
@@ -228,7 +279,7 @@ def main():
         b_sim = alg_bytes_per_sim(args.workload)
         achieved = n_roots * iters * b_sim / (kernel_ms / 1e3) / 1e9 if b_sim else None
         traffic = pmc_traffic(n_roots, iters) if args.workload == "c3" else None
-        valu_busy, mem_wait = pmc_valu_busy() if args.workload == "c3" else (None, None)
+        valu = pmc_valu() if args.workload == "c3" else None
         workload_desc = {
             "c3": "C3 rs-full-doko determinized UCT: %d infostates x %d CAP samples/GPU-share, %d roots x %d sims per GPU"
                   % (I, args.samples, n_roots, iters),
@@ -266,22 +317,28 @@ def main():
             "kernel_only_rollouts_per_s": n_roots * iters * world / (kernel_ms / 1e3),
             "search_kernel_ms": kernel_ms,
             "roofline": {
-                "bound": "hbm",
+                # the binding resource is VALU issue (PMC below); achieved/peak/frac are the
+                # north-star's HBM figures: algorithmic bytes / event-timed kernel vs 8 TB/s
+                "bound": "valu",
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS if achieved else None,
+                "hbm_target_0p40_met": (achieved / HBM_PEAK_GBS >= 0.40) if achieved else None,
                 "traffic": traffic,
                 "alg_bytes_per_sim": b_sim,
                 "stream_copy_peak_measured_gbs": stream_peak,
-                "valu_busy_pmc": valu_busy,
-                "note": "the search is bound by VALU issue and dependent-load latency (64-root waves, three per SIMD; "
-                        "PMC: VALU busy %s of the launch, %s of wave cycles waiting on memory); achieved = the "
-                        "SURVEY 8(d) algorithmic bytes from the oracle's counters / event-timed kernel; "
-                        % ("%.0f%%" % (100 * valu_busy) if valu_busy else "n/a",
-                           "%.0f%%" % (100 * mem_wait) if mem_wait else "n/a") +
-                        "traffic = 2*FETCH_SIZE+WRITE_SIZE from profiles/pmc_search.json scaled per launch",
+                "valu": valu,
+                "note": "bound by VALU issue and divergence, not HBM bandwidth: PMC VALU busy %s of the launch, %s of "
+                        "wave cycles waiting on memory; achieved = the SURVEY 8(d) algorithmic bytes from the oracle's "
+                        "counters / event-timed kernel; traffic = 2*FETCH_SIZE+WRITE_SIZE from profiles/pmc_search.json "
+                        "scaled per launch"
+                        % ("%.0f%%" % (100 * valu["busy"]) if valu else "n/a",
+                           "%.0f%%" % (100 * valu["mem_wait_frac"]) if valu else "n/a"),
             },
+            "small_batch": small,
+            "ranks": world,
+            "dist_backend": backend if world > 1 else None,
             "cpu_baseline": cpu,
         }
         print(json.dumps(result))
@@ -547,71 +604,93 @@ def run_impi(args, dk, L, dev, stream, rank, world, local_rank, dist):
     return result
 
 
-def cpu_baseline(args, dk):
-    """The ORACLE (C++ restatement of the reference hot path) timed on this box's
-    host cores on a bounded sample of the same workload."""
+def cpu_quota_cores():
+    """CPU cores this process may use: the affinity set, capped by a cgroup v2 cpu.max quota."""
+    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()
+        if q != "max":
+            quota = float(q) / float(per)
+    except Exception:
+        pass
+    return cores, quota
+
+
+def cpu_baseline(args, dk, target_s=5.0):
+    """The ORACLE (C++ restatement of the reference hot path) timed on this box's host
+    cores on a bounded sample of the same workload: one worker thread per usable core,
+    root-parallel with a shared work queue like MCTSWorkers (mcts_policy.rs:55-126,
+    run.rs:508-520), sized to about `target_s` seconds of wall time; plus a 1-thread figure."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import ctypes
 
     import oracle_lib as ol
-    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-    n = threads * args.cpu_roots_per_thread
+    cores, quota = cpu_quota_cores()
+    threads = args.cpu_threads or cores
+    eff = min(threads, quota) if quota else threads
     iters = args.iterations
-    roots = []
-    seeds = []
-    if args.workload in ("c3", "c2d"):
-        do = args.workload == "c2d"
+    do = args.workload in ("c2", "c2d")
+
+    def make_roots(n):
+        roots, seeds = [], []
         for k in range(n):
-            j, s = k % args.infostates, k // args.infostates
-            st = (ol.DoState if do else ol.FdoState).new_game(0xC3000000 + j)
-            for _ in range(4):
-                st.play(24)
-            rng = ol.arr(ctypes.c_uint64, 4, [int(x) for x in dk.splitmix_rng_states(np.array([0xC3100000 + j], dtype=np.uint64))[0]])
-            if do:
-                st.random_plies(rng, [0, 8, 20, 32][j % 4])
-                smp = st.sample_assignment_full(ol.rng_seed(0xC3200000 + j * args.samples + s))
+            if args.workload in ("c3", "c2d"):
+                j, s = k % args.infostates, (k // args.infostates) % args.samples
+                st = (ol.DoState if do else ol.FdoState).new_game(0xC3000000 + j)
+                for _ in range(4):
+                    st.play(24)
+                rng = ol.arr(ctypes.c_uint64, 4, [int(x) for x in dk.splitmix_rng_states(np.array([0xC3100000 + j], dtype=np.uint64))[0]])
+                if do:
+                    st.random_plies(rng, [0, 8, 20, 32][j % 4])
+                    smp = st.sample_assignment_full(ol.rng_seed(0xC3200000 + j * args.samples + s))
+                else:
+                    st.random_plies(rng, [0, 8, 20, 32][j % 4], True)
+                    smp = st.card_matching(ol.rng_seed(0xC3200000 + j * args.samples + s))
+                roots.append(smp)
+                seeds.append(0xC3300000 + j * args.samples + s)
             else:
-                st.random_plies(rng, [0, 8, 20, 32][j % 4], True)
-                smp = st.card_matching(ol.rng_seed(0xC3200000 + j * args.samples + s))
-            roots.append(smp)
-            seeds.append(0xC3300000 + j * args.samples + s)
+                st = ol.DoState.new_game(0xD0C00000 + k)
+                for _ in range(4):
+                    st.play(24)
+                roots.append(st)
+                seeds.append((k * 0x9E3779B97F4A7C15 + 1) & 0xFFFFFFFFFFFFFFFF)
+        return roots, seeds
+
+    def run(roots, seeds, nthreads):
+        n = len(roots)
         handles = (ctypes.c_void_p * n)(*[r.h for r in roots])
         vis = (ctypes.c_uint32 * (39 * n))()
         sd = ol.arr(ctypes.c_uint64, n, seeds)
         if do:
-            secs = ol.lib().or_do_search_many(handles, sd, n, iters, args.c, vis, threads)
-        else:
-            secs = ol.lib().or_fdo_search_many(None, handles, sd, n, iters, args.c, vis, threads)
-        n1 = min(n, 64)
-        if do:
-            secs1 = ol.lib().or_do_search_many(handles, sd, n1, iters, args.c, vis, 1)
-        else:
-            secs1 = ol.lib().or_fdo_search_many(None, handles, sd, n1, iters, args.c, vis, 1)
-    else:
-        for k in range(n):
-            st = ol.DoState.new_game(0xD0C00000 + k)
-            for _ in range(4):
-                st.play(24)
-            roots.append(st)
-            seeds.append((k * 0x9E3779B97F4A7C15 + 1) & 0xFFFFFFFFFFFFFFFF)
-        handles = (ctypes.c_void_p * n)(*[r.h for r in roots])
-        vis = (ctypes.c_uint32 * (39 * n))()
-        sd = ol.arr(ctypes.c_uint64, n, seeds)
-        secs = ol.lib().or_do_search_many(handles, sd, n, iters, args.c, vis, threads)
-        n1 = min(n, 64)
-        secs1 = ol.lib().or_do_search_many(handles, sd, n1, iters, args.c, vis, 1)
+            return ol.lib().or_do_search_many(handles, sd, n, iters, args.c, vis, nthreads)
+        return ol.lib().or_fdo_search_many(None, handles, sd, n, iters, args.c, vis, nthreads)
+
+    n1 = 64
+    r1, s1 = make_roots(n1)
+    secs1 = run(r1, s1, 1)
+    rate1 = n1 * iters / secs1
+    n = int(np.ceil(target_s * rate1 * eff / iters / threads)) * threads
+    n = max(n, threads)
+    roots, seeds = make_roots(min(n, 8192))          # distinct roots, tiled beyond 8192 (Python setup time)
+    roots = [roots[k % len(roots)] for k in range(n)]
+    seeds = [seeds[k % len(seeds)] for k in range(n)]
+    secs = run(roots, seeds, threads)
     model = ""
     try:
         model = subprocess.run(["lscpu"], capture_output=True, text=True).stdout
         model = [l.split(":", 1)[1].strip() for l in model.splitlines() if l.startswith("Model name")][0]
     except Exception:
         model = platform.processor()
-    cpu = {"value": n * iters / secs, "unit": "rollouts/s", "cores": threads, "kind": "port",
-           "sample": "%d roots x %d sims of the same workload (oracle C++ restatement, root-parallel like MCTSWorkers), "
-                     "%.1f s wall on %d threads of %s; 1-thread figure on the first %d roots"
-                     % (n, iters, secs, threads, model, n1),
-           "value_1_thread": n1 * iters / secs1}
-    return cpu
+    return {"value": n * iters / secs, "unit": "rollouts/s", "cores": threads, "kind": "port",
+            "host_cpus": os.cpu_count(), "cpu_quota_cores": quota,
+            "sample": "%d roots x %d sims of the same workload (oracle C++ restatement, one worker per usable core, "
+                      "shared root queue like MCTSWorkers), %.1f s wall on %d threads of %s (%d CPUs visible, "
+                      "cgroup quota %s cores); 1-thread figure on %d roots"
+                      % (n, iters, secs, threads, model, os.cpu_count() or 0,
+                         "%.1f" % quota if quota else "none", n1),
+            "value_1_thread": rate1}
 
 
 def alg_bytes_per_sim(workload):
@@ -641,16 +720,22 @@ def stream_copy_gbs(torch, dev, nbytes=1 << 31, reps=10):
     return gbs
 
 
-def pmc_valu_busy():
-    """VALU busy fraction of the search launch from the committed PMC summary:
-    SQ_INSTS_VALU x 4 cycles per wave64 instruction / SIMDs over GRBM_GUI_ACTIVE per XCD."""
+def pmc_valu():
+    """VALU figures of the search launch from the committed PMC summary: busy = SQ_INSTS_VALU x 4
+    cycles per wave64 instruction / 1024 SIMDs over GRBM_GUI_ACTIVE per XCD; VALU instructions per
+    simulation per 64-root wave; share of wave cycles waiting on memory."""
     path = os.path.join(ROOT, "profiles", "pmc_search.json")
     try:
         with open(path) as fh:
-            c = json.load(fh)["pmc_per_launch"]
-        return c["SQ_INSTS_VALU"] * 4.0 / 1024.0 / (c["GRBM_GUI_ACTIVE"] / 8.0), c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"]
+            d = json.load(fh)
+        c = d["pmc_per_launch"]
+        sims = d["roots"] * d["iterations"]
+        return {"busy": c["SQ_INSTS_VALU"] * 4.0 / 1024.0 / (c["GRBM_GUI_ACTIVE"] / 8.0),
+                "mem_wait_frac": c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"],
+                "wave_insts_per_sim": c["SQ_INSTS_VALU"] * 64.0 / sims,
+                "source": "profiles/pmc_search.json"}
     except Exception:
-        return None, None
+        return None
 
 
 def pmc_traffic(n_roots, iters):

@@ -78,6 +78,28 @@ def splitmix_rng_states(seeds):
     return out
 
 
+def _run_on_stream(dev, fn, *args):
+    """Run fn(*args, stream_handle) on torch's current stream of `dev` when it is a real
+    stream; on the legacy default stream (handle 0, which would select the library's own
+    unordered stream) run it on a side stream ordered after the caller's work, make the
+    caller wait for it, and record the caller's stream on every returned tensor so the
+    caching allocator does not hand their blocks to new side-stream work while
+    caller-stream kernels that read them are still queued."""
+    import torch
+    caller = torch.cuda.current_stream(dev)
+    if caller.cuda_stream != 0:
+        return fn(*args, caller.cuda_stream)
+    side = torch.cuda.Stream(dev)
+    side.wait_stream(caller)
+    with torch.cuda.stream(side):
+        out = fn(*args, side.cuda_stream)
+    caller.wait_stream(side)
+    for t in out:
+        if isinstance(t, torch.Tensor):
+            t.record_stream(caller)
+    return out
+
+
 class Engine:
     """A device context: node pools for `max_roots` searches of up to
     `max_iterations` iterations (the reference's CachedMCTS arenas, one per root)."""
@@ -274,17 +296,7 @@ class ArImpiPolicy:
         """infostates: uint8 [n, 160] dk_az_state records (GPU); seeds: uint64, n*S sampling seeds,
         then n*S search seeds, then n fallback seeds.  Returns (actions uint8 [n], successes int32 [n],
         visits int32 [n*S, 39]) as GPU tensors."""
-        import torch
-        dev = infostates.device
-        caller = torch.cuda.current_stream(dev)
-        if caller.cuda_stream != 0:
-            return self._execute(infostates, seeds, caller.cuda_stream)
-        side = torch.cuda.Stream(dev)   # a real handle: 0 would select the library's own stream
-        side.wait_stream(caller)
-        with torch.cuda.stream(side):
-            out = self._execute(infostates, seeds, side.cuda_stream)
-        caller.wait_stream(side)
-        return out
+        return _run_on_stream(infostates.device, self._execute, infostates, seeds)
 
     def _execute(self, infostates, seeds, st):
         import torch
@@ -343,19 +355,9 @@ class AlphaZeroSearch:
     def mcts_search(self, roots, network, noise, iterations, seeds):
         """roots: uint8 [n, 160] dk_az_state records (GPU); noise: float32 [n, 39] Dirichlet samples (GPU);
         seeds: uint64 [n] (SmallRng per game).  Returns (actions uint8 [n], visits int32 [n, 39])."""
-        import torch
-        dev = roots.device
         # the launches need a real stream handle shared with torch (handle 0 would
         # select the library's own stream, unordered with the network's kernels)
-        caller = torch.cuda.current_stream(dev)
-        if caller.cuda_stream != 0:
-            return self._search(roots, network, noise, iterations, seeds, caller.cuda_stream)
-        side = torch.cuda.Stream(dev)
-        side.wait_stream(caller)
-        with torch.cuda.stream(side):
-            out = self._search(roots, network, noise, iterations, seeds, side.cuda_stream)
-        caller.wait_stream(side)
-        return out
+        return _run_on_stream(roots.device, self._search, roots, network, noise, iterations, seeds)
 
     def _search(self, roots, network, noise, iterations, seeds, st):
         import torch
@@ -411,17 +413,7 @@ class ARSampling:
         Returns (states uint8 [n, 128], status uint8 [n], reason uint8 [n]) with n = n_info * samples,
         lane = info * samples + sample; status AR_CONSISTENT rows hold the sample, the others the
         infostate (AR_NOT_CONSISTENT: reason = index into NOT_CONSISTENT_REASONS)."""
-        import torch
-        dev = infostates.device
-        caller = torch.cuda.current_stream(dev)
-        if caller.cuda_stream != 0:
-            return self._sample(infostates, samples, seeds, caller.cuda_stream)
-        side = torch.cuda.Stream(dev)
-        side.wait_stream(caller)
-        with torch.cuda.stream(side):
-            out = self._sample(infostates, samples, seeds, side.cuda_stream)
-        caller.wait_stream(side)
-        return out
+        return _run_on_stream(infostates.device, self._sample, infostates, samples, seeds)
 
     def _sample(self, infostates, samples, seeds, st):
         import torch

@@ -721,7 +721,8 @@ hipError_t launch_search_t(dk_ctx* ctx, const dk_state* roots, const uint64_t* s
     // the registers allow with one entry of headroom.  At 64 roots per wave a 16-entry
     // path (12 KB + the card table) fits 11 workgroups per CU; the calculator admits 12
     // at 15 entries, but 15 measured no faster than 16 (the hardware's LDS allocation
-    // granularity), while 14 is 4 % faster on C3 (tools/ab_ldspath.sh, medians of 5).
+    // granularity), while 14 (12 workgroups per CU) is 12 % faster on C3 than 16: medians of 5
+    // interleaved runs, 1,885 against 1,685 M rollouts/s (tools/ab_ldspath.sh).
     // Paths deeper than 14 are rare and spill to the global overflow.
     int lp = ctx->lds_path;
     if (!ctx->lds_path_fixed) {

@@ -8,6 +8,8 @@
 #include <cstdio>
 #include <cstring>
 #include <thread>
+#include <atomic>
+#include <memory>
 #include <vector>
 
 #include "../include/doko_amd.h"
@@ -156,10 +158,11 @@ double or_fdo_search_many(const uint8_t* packed_unused, void** roots, const uint
     (void)packed_unused;
     auto t0 = std::chrono::steady_clock::now();
     std::vector<std::thread> pool;
+    auto next = std::make_shared<std::atomic<uint32_t>>(0);   // shared root queue (MCTSWorkers' MPMC channel)
     for (int t = 0; t < threads; ++t) {
         pool.emplace_back([=]() {
             Mcts<fdo::Env> m;
-            for (uint32_t i = (uint32_t)t; i < n; i += (uint32_t)threads) {
+            for (uint32_t i; (i = next->fetch_add(1)) < n;) {
                 fdo::Env e; e.doko = *(fdo::State*)roots[i];
                 SmallRng r = SmallRng::seed_from_u64(seeds[i]);
                 auto moves = m.search(e, c, iters, r, nullptr);
@@ -236,10 +239,11 @@ int or_do_search(void* sp, uint64_t* rng_state, uint32_t iters, double c, uint32
 double or_do_search_many(void** roots, const uint64_t* seeds, uint32_t n, uint32_t iters, double c, uint32_t* visits, int threads) {
     auto t0 = std::chrono::steady_clock::now();
     std::vector<std::thread> pool;
+    auto next = std::make_shared<std::atomic<uint32_t>>(0);   // shared root queue (MCTSWorkers' MPMC channel)
     for (int t = 0; t < threads; ++t) {
         pool.emplace_back([=]() {
             Mcts<dko::Env> m;
-            for (uint32_t i = (uint32_t)t; i < n; i += (uint32_t)threads) {
+            for (uint32_t i; (i = next->fetch_add(1)) < n;) {
                 dko::Env e; e.doko = *(dko::State*)roots[i];
                 SmallRng r = SmallRng::seed_from_u64(seeds[i]);
                 auto moves = m.search(e, c, iters, r, nullptr);

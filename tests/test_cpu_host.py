@@ -158,3 +158,13 @@ def test_ar_engine_vs_oracle(native_bins):
     assert out.startswith("OK"), out
     lanes, ok, bad, panic = map(int, out.split()[1:5])
     assert lanes == 1800 and ok > 1000 and bad > 20
+
+
+def test_bench_refuses_world_size_mismatch():
+    """bench.py --gpus N inside a launcher that started a different number of ranks
+    fails before any GPU call (it would otherwise report an N-GPU metric for fewer)."""
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run(["python", os.path.join(ROOT, "bench.py"), "--gpus", "2"], env=env, capture_output=True,
+                         text=True, timeout=60)
+    assert out.returncode != 0
+    assert "--gpus 2 but WORLD_SIZE=1" in out.stderr

@@ -1,0 +1,67 @@
+"""The bench's N>1 path with the real HIP kernels (config C4 rehearsed on one GPU).
+
+`bench.py --gpus 2` starts two ranks itself (torch.distributed.run, before touching
+the GPU); with DK_DIST_BACKEND=gloo both ranks share cuda:0.  Each rank determinizes
+and searches its half of every infostate's samples, runs dk_fuse_accumulate_async on
+them, the accumulators are all-reduced (gloo here, RCCL on an 8-GPU node) and every
+rank runs dk_fuse_select_async.  Reference: the sample fan-out of DefaultImpiPolicy
+(rs-doko-py-bridge/src/compare_impi/compare_impi.rs:217-291) and the fusions
+(policy_fusion.rs:23-123).
+
+MaxN fuses integer rank sums, so the 2-rank decision must equal the 1-rank run over
+the same global workload bit for bit.  Average-strategy fusion sums f32
+probabilities: the two ranks' partial sums added by the all-reduce are a different
+f32 summation order than one rank's sequential sum (the reference's own order is
+JoinSet completion order, compare_impi.rs:276-288), so the accumulators agree within
+f32 rounding (rtol 1e-6 on sums of <= 64 terms <= 1) and the action agrees wherever
+the top two sums are further apart than that.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+pytestmark = pytest.mark.gpu
+
+INFO_PER_RANK, ITERS = 48, 200
+
+
+def _bench(tmp_path, gpus, infostates, fusion, tag):
+    env = dict(os.environ)
+    env["DK_DIST_BACKEND"] = "gloo"
+    env.pop("WORLD_SIZE", None)
+    act = str(tmp_path / ("act_%s.npy" % tag))
+    acc = str(tmp_path / ("acc_%s.npy" % tag))
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--steps", "1", "--warmup", "0",
+           "--no-cpu-baseline", "--small-infostates", "0", "--infostates", str(infostates),
+           "--iterations", str(ITERS), "--fusion", fusion, "--dump-actions", act, "--dump-acc", acc]
+    out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=110)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
+    line = [l for l in out.stdout.splitlines() if l.startswith("{")][-1]
+    return json.loads(line), np.load(act), np.load(acc)
+
+
+def test_bench_two_ranks_maxn_exact(tmp_path):
+    r2, a2, acc2 = _bench(tmp_path, 2, INFO_PER_RANK, "maxn", "2")
+    assert r2["n_gpus"] == 2 and r2["ranks"] == 2
+    assert r2["config"]["roots_per_gpu"] == 2 * INFO_PER_RANK * 32
+    r1, a1, acc1 = _bench(tmp_path, 1, 2 * INFO_PER_RANK, "maxn", "1")
+    assert r1["n_gpus"] == 1
+    assert a2.shape == (2 * INFO_PER_RANK,)
+    assert np.array_equal(acc2, acc1)
+    assert np.array_equal(a2, a1)
+
+
+def test_bench_two_ranks_avg_tolerance(tmp_path):
+    _, a2, acc2 = _bench(tmp_path, 2, INFO_PER_RANK, "avg", "2a")
+    _, a1, acc1 = _bench(tmp_path, 1, 2 * INFO_PER_RANK, "avg", "1a")
+    np.testing.assert_allclose(acc2, acc1, rtol=1e-6, atol=1e-6)
+    for i in range(a1.shape[0]):
+        if a1[i] != a2[i]:
+            top = np.sort(acc1[i])[-2:]
+            assert top[1] - top[0] <= 1e-5, (i, a1[i], a2[i], top)
