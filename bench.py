@@ -628,7 +628,9 @@ def cpu_baseline(args, dk, target_s=5.0):
 
     import oracle_lib as ol
     cores, quota = cpu_quota_cores()
-    threads = args.cpu_threads or cores
+    # one worker per core this process may actually use: on a box whose cgroup quota is
+    # smaller than the visible CPUs, more threads only time-slice the same quota
+    threads = args.cpu_threads or (min(cores, int(np.ceil(quota))) if quota else cores)
     eff = min(threads, quota) if quota else threads
     iters = args.iterations
     do = args.workload in ("c2", "c2d")
@@ -677,14 +679,19 @@ def cpu_baseline(args, dk, target_s=5.0):
     roots = [roots[k % len(roots)] for k in range(n)]
     seeds = [seeds[k % len(seeds)] for k in range(n)]
     secs = run(roots, seeds, threads)
-    model = ""
+    model, phys = "", None
     try:
-        model = subprocess.run(["lscpu"], capture_output=True, text=True).stdout
-        model = [l.split(":", 1)[1].strip() for l in model.splitlines() if l.startswith("Model name")][0]
+        ls = subprocess.run(["lscpu"], capture_output=True, text=True).stdout
+        kv = {l.split(":", 1)[0].strip(): l.split(":", 1)[1].strip() for l in ls.splitlines() if ":" in l}
+        model = kv.get("Model name", "")
+        phys = int(kv["Core(s) per socket"]) * int(kv["Socket(s)"])
     except Exception:
-        model = platform.processor()
+        model = model or platform.processor()
     return {"value": n * iters / secs, "unit": "rollouts/s", "cores": threads, "kind": "port",
-            "host_cpus": os.cpu_count(), "cpu_quota_cores": quota,
+            "host_cpus": os.cpu_count(), "host_physical_cores": phys, "cpu_quota_cores": quota,
+            # NOT measured: the 1-thread rate times the host's physical cores (linear scaling,
+            # no SMT gain), for comparison with a whole-machine MCTSWorkers pool
+            "value_all_physical_cores_extrapolated": rate1 * phys if phys else None,
             "sample": "%d roots x %d sims of the same workload (oracle C++ restatement, one worker per usable core, "
                       "shared root queue like MCTSWorkers), %.1f s wall on %d threads of %s (%d CPUs visible, "
                       "cgroup quota %s cores); 1-thread figure on %d roots"

@@ -26,6 +26,9 @@ struct SearchCounters {
     uint64_t nodes = 0;              // nodes allocated (incl. root)
     uint64_t child_slots = 0;        // sum of popcount(allowed) over nodes that got >=1 child (+1 root)
     uint64_t rollout_plies = 0;
+    // deepest selection path of the device kernel's path stack (search_core.h): a forced
+    // chain (single-action nodes) below its head costs one entry, like the skip pointer
+    uint64_t max_path_entries = 0;
 };
 
 struct MoveOut { int action; uint64_t visits; double value; };
@@ -40,6 +43,7 @@ struct Mcts {
         uint64_t visits = 0;
         double win_score = 0.0;
         uint64_t unexpanded;
+        int n_actions;             // popcount of the allowed actions at creation (for the counters)
         std::vector<int> children;
         int parent;
     };
@@ -89,6 +93,7 @@ struct Mcts {
         n.state = (int)states.size();
         states.push_back(st);
         n.unexpanded = states.back().allowed_actions(first);
+        n.n_actions = __builtin_popcountll(n.unexpanded);
         n.parent = parent;
         nodes.push_back(n);
         return (int)nodes.size() - 1;
@@ -110,9 +115,13 @@ struct Mcts {
         if (ctr) { ctr->nodes = 1; ctr->child_slots = 1; }
         for (uint64_t it = 0; it < iterations; ++it) {
             // select_promising_node (mcts.rs:45-61)
-            int node = root; uint64_t depth = 0;
+            int node = root; uint64_t depth = 0, entries = 0;
             while (!nodes[node].children.empty()) {
                 if (nodes[node].unexpanded != 0) break;
+                const Node& nd = nodes[node];
+                const bool forced = nd.n_actions == 1;
+                const bool head = nd.parent == root || (nd.parent >= 0 && nodes[nd.parent].n_actions >= 2);
+                if (!(node != root && forced && !head)) entries++;
                 node = find_best_child(node, c, ctr);
                 depth++;
             }
@@ -127,6 +136,7 @@ struct Mcts {
                 nodes[node].children.push_back(child);
                 explore = child;
                 depth++;
+                entries++;
                 if (ctr) ctr->nodes++;
             }
             double result[4];
@@ -141,7 +151,8 @@ struct Mcts {
                 nodes[t].win_score += result[nodes[p].current_player];
                 t = p;
             }
-            if (ctr) { ctr->iterations++; ctr->path_nodes += path; if (depth > ctr->max_depth) ctr->max_depth = depth; }
+            if (ctr) { ctr->iterations++; ctr->path_nodes += path; if (depth > ctr->max_depth) ctr->max_depth = depth;
+                       if (entries > ctr->max_path_entries) ctr->max_path_entries = entries; }
             if (it == iterations - 1) (void)rng.random_bool((double)(1.0f / 1000.0f));
         }
         std::vector<MoveOut> moves;

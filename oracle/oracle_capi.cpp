@@ -132,6 +132,7 @@ int or_fdo_search(void* sp, uint64_t* rng_state, uint32_t iters, double c, uint3
     if (counters) {
         counters[0] = ctr.iterations; counters[1] = ctr.children_scanned; counters[2] = ctr.path_nodes;
         counters[3] = ctr.max_depth; counters[4] = ctr.nodes; counters[5] = ctr.child_slots;
+        counters[6] = ctr.max_path_entries;
     }
     return moves_to_arrays(moves, visits, values, DK_NUM_ACTIONS);
 }
@@ -233,7 +234,8 @@ int or_do_search(void* sp, uint64_t* rng_state, uint32_t iters, double c, uint32
     dko::Env e; e.doko = *(dko::State*)sp; SmallRng r = rng_from(rng_state);
     Mcts<dko::Env> m; SearchCounters ctr; auto moves = m.search(e, c, iters, r, &ctr); rng_to(r, rng_state);
     if (counters) { counters[0] = ctr.iterations; counters[1] = ctr.children_scanned; counters[2] = ctr.path_nodes;
-                    counters[3] = ctr.max_depth; counters[4] = ctr.nodes; counters[5] = ctr.child_slots; }
+                    counters[3] = ctr.max_depth; counters[4] = ctr.nodes; counters[5] = ctr.child_slots;
+        counters[6] = ctr.max_path_entries; }
     return moves_to_arrays(moves, visits, values, DK_NUM_ACTIONS);
 }
 double or_do_search_many(void** roots, const uint64_t* seeds, uint32_t n, uint32_t iters, double c, uint32_t* visits, int threads) {
