@@ -149,6 +149,93 @@ typedef struct dk_az_state {
     uint8_t reserved[7];     /* 153                                                          */
 } dk_az_state;
 
+/* ---- state wire format from the reference's fields (host only, no device) -------
+ * dk_fdo_fields mirrors FdoState (rs-full-doko/src/state/state.rs:24-75) field by field,
+ * so a caller holding an FdoState fills it without knowing the 128-B layout:
+ *   reservations_round  (reservation/reservation_round.rs:9-77)  res_start, res_len, reservations[]
+ *                        FdoReservation: 0 Healthy 1 Wedding 2 DiamondsSolo 3 HeartsSolo 4 SpadesSolo
+ *                        5 ClubsSolo 6 TrumplessSolo 7 QueensSolo 8 JacksSolo
+ *   tricks              (trick/trick.rs:10-17)  n_tricks, trick_start[], trick_cards[][] (FdoCard or -1)
+ *   hands               (hand/hand.rs:17-20)     reference bit layout
+ *   announcements       (announcement/announcement.rs:47-59)  the occurrence list (card_index,
+ *                        player, FdoAnnouncement bit), lowest Re / Kontra (bit, 0 = None),
+ *                        number_of_turns_without_announcement, starting_player,
+ *                        current_player_allowed_announcements (FdoAnnouncementSet bits)
+ *   card_index, current_player (-1 = None), current_phase (0 Reservation 1 Announcement
+ *   2 PlayCard 3 Finished), reservation_result (rr_kind -1 None, 0 NoReservation, 1 Solo,
+ *   2 Wedding; rr_player; rr_reservation), game_type (FdoGameType, -1 = None), player_eyes,
+ *   player_num_tricks, team_state (team/team_logic.rs:11-28: team_kind 0 InReservations
+ *   1 WeddingUnsolved 2 WeddingSolved 3 NoWedding; wedding_player; solved_trick_index;
+ *   re_players as a player bit mask).
+ * end_of_game_stats is derived (recomputed by dk_env_rewards_batch) and trick winners are
+ * recomputed from the cards and the game type.  dk_fdo_to_fields is the inverse except for
+ * the announcement occurrence list, which the wire format keeps only as a count and a
+ * player mask (ann_card_index / ann_player / ann_announcement come back as -1 / -1 / 0).
+ * Returns DK_OK, DK_E_INVALID (NULL) or DK_E_STATE (fields that contradict each other:
+ * card counts, card_index against the tricks, players or enums out of range). */
+typedef struct dk_fdo_fields {
+    uint64_t hands[4];
+    uint32_t player_eyes[4];
+    uint32_t player_num_tricks[4];
+    int8_t res_start;
+    int8_t res_len;
+    int8_t reservations[4];
+    int8_t n_tricks;
+    int8_t trick_start[12];
+    int8_t trick_cards[12][4];
+    int8_t ann_n;
+    int8_t ann_card_index[12];
+    int8_t ann_player[12];
+    uint8_t ann_announcement[12];
+    uint8_t re_lowest;
+    uint8_t contra_lowest;
+    int8_t ann_turns_without;
+    int8_t ann_start;
+    uint8_t ann_allowed;
+    int8_t card_index;
+    int8_t current_player;
+    int8_t phase;
+    int8_t rr_kind;
+    int8_t rr_player;
+    int8_t rr_reservation;
+    int8_t game_type;
+    int8_t team_kind;
+    int8_t wedding_player;
+    int8_t solved_trick;
+    uint8_t re_players;
+} dk_fdo_fields;
+
+/* dk_do_fields mirrors DoState (rs-doko/src/state/state.rs:28-76): reservations (DoReservation
+ * 0 Wedding 1 Healthy, -1 = not yet played, in round order from res_start), tricks (12 slots,
+ * present ones with trick_start >= 0; cards -1 when not yet played), hands (bit layout of
+ * rs-doko/src/hand/hand.rs:13), current_player (-1 = None), phase (0 Reservation 1 PlayCard
+ * 2 Finished), current_trick_index, reservation result (rr_kind -1 None, 0 NoReservation,
+ * 2 Wedding; rr_player), player_eyes, player_num_tricks, team_state (teams/team_logic.rs:
+ * team_kind, wedding_player, solved_trick, re_players mask). */
+typedef struct dk_do_fields {
+    uint64_t hands[4];
+    uint32_t player_eyes[4];
+    uint32_t player_num_tricks[4];
+    int8_t res_start;
+    int8_t reservations[4];
+    int8_t trick_start[12];
+    int8_t trick_cards[12][4];
+    int8_t current_player;
+    int8_t phase;
+    int8_t trick_index;
+    int8_t rr_kind;
+    int8_t rr_player;
+    int8_t team_kind;
+    int8_t wedding_player;
+    int8_t solved_trick;
+    uint8_t re_players;
+} dk_do_fields;
+
+int dk_fdo_from_fields(const dk_fdo_fields* fields, dk_state* out);
+int dk_fdo_to_fields(const dk_state* state, dk_fdo_fields* fields);
+int dk_do_from_fields(const dk_do_fields* fields, dk_state* out);
+int dk_do_to_fields(const dk_state* state, dk_do_fields* fields);
+
 /* ---- context ---------------------------------------------------------------- */
 typedef struct dk_config {
     int32_t device;          /* HIP device ordinal                                          */

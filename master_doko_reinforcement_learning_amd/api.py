@@ -506,3 +506,58 @@ def az_encode(engine, records, out=None):
     if st == 0:
         _check(_native.lib().dk_sync(engine.ctx, None))
     return out
+
+
+# ---- state wire format from the reference's fields (host only; include/doko_amd.h) ----
+class FdoFields(ctypes.Structure):
+    """dk_fdo_fields: FdoState (rs-full-doko/src/state/state.rs:24-75) field by field."""
+    _fields_ = [("hands", ctypes.c_uint64 * 4), ("player_eyes", ctypes.c_uint32 * 4),
+                ("player_num_tricks", ctypes.c_uint32 * 4), ("res_start", ctypes.c_int8), ("res_len", ctypes.c_int8),
+                ("reservations", ctypes.c_int8 * 4), ("n_tricks", ctypes.c_int8), ("trick_start", ctypes.c_int8 * 12),
+                ("trick_cards", (ctypes.c_int8 * 4) * 12), ("ann_n", ctypes.c_int8),
+                ("ann_card_index", ctypes.c_int8 * 12), ("ann_player", ctypes.c_int8 * 12),
+                ("ann_announcement", ctypes.c_uint8 * 12), ("re_lowest", ctypes.c_uint8),
+                ("contra_lowest", ctypes.c_uint8), ("ann_turns_without", ctypes.c_int8), ("ann_start", ctypes.c_int8),
+                ("ann_allowed", ctypes.c_uint8), ("card_index", ctypes.c_int8), ("current_player", ctypes.c_int8),
+                ("phase", ctypes.c_int8), ("rr_kind", ctypes.c_int8), ("rr_player", ctypes.c_int8),
+                ("rr_reservation", ctypes.c_int8), ("game_type", ctypes.c_int8), ("team_kind", ctypes.c_int8),
+                ("wedding_player", ctypes.c_int8), ("solved_trick", ctypes.c_int8), ("re_players", ctypes.c_uint8)]
+
+
+class DoFields(ctypes.Structure):
+    """dk_do_fields: DoState (rs-doko/src/state/state.rs:28-76) field by field."""
+    _fields_ = [("hands", ctypes.c_uint64 * 4), ("player_eyes", ctypes.c_uint32 * 4),
+                ("player_num_tricks", ctypes.c_uint32 * 4), ("res_start", ctypes.c_int8),
+                ("reservations", ctypes.c_int8 * 4), ("trick_start", ctypes.c_int8 * 12),
+                ("trick_cards", (ctypes.c_int8 * 4) * 12), ("current_player", ctypes.c_int8), ("phase", ctypes.c_int8),
+                ("trick_index", ctypes.c_int8), ("rr_kind", ctypes.c_int8), ("rr_player", ctypes.c_int8),
+                ("team_kind", ctypes.c_int8), ("wedding_player", ctypes.c_int8), ("solved_trick", ctypes.c_int8),
+                ("re_players", ctypes.c_uint8)]
+
+
+def fdo_from_fields(fields):
+    """dk_fdo_from_fields: the 128-B packed state (bytes) of an FdoFields; DokoError on inconsistent fields."""
+    out = (ctypes.c_uint8 * STATE_BYTES)()
+    _check(_native.lib().dk_fdo_from_fields(ctypes.byref(fields), out))
+    return bytes(out)
+
+
+def fdo_to_fields(packed):
+    f = FdoFields()
+    buf = (ctypes.c_uint8 * STATE_BYTES).from_buffer_copy(bytes(packed))
+    _check(_native.lib().dk_fdo_to_fields(buf, ctypes.byref(f)))
+    return f
+
+
+def do_from_fields(fields):
+    """dk_do_from_fields: the 128-B packed rs-doko state (bytes) of a DoFields."""
+    out = (ctypes.c_uint8 * STATE_BYTES)()
+    _check(_native.lib().dk_do_from_fields(ctypes.byref(fields), out))
+    return bytes(out)
+
+
+def do_to_fields(packed):
+    f = DoFields()
+    buf = (ctypes.c_uint8 * STATE_BYTES).from_buffer_copy(bytes(packed))
+    _check(_native.lib().dk_do_to_fields(buf, ctypes.byref(f)))
+    return f

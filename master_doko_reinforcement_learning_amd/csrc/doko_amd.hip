@@ -24,6 +24,7 @@
 #include "az_net_kernels.h"
 #include "engine/cap_engine.h"
 #include "engine/search_core.h"
+#include "state_fields.h"
 
 namespace {
 
@@ -31,7 +32,10 @@ constexpr int WAVE = 64;
 // register budget of the search kernel: per hot-record layout (NodeHot16::MIN_WAVES = 3 waves
 // per SIMD, 167 VGPRs with a 24-B spill; NodeHot32: the compiler's choice, two waves).
 // Resident single-wave workgroups per CU at that budget (sizes the node pools):
-constexpr uint32_t RESIDENT_WG_PER_CU = 12;
+#ifndef DK_RESIDENT_WG
+#define DK_RESIDENT_WG 12
+#endif
+constexpr uint32_t RESIDENT_WG_PER_CU = DK_RESIDENT_WG;
 constexpr int MAX_PATH = 64;   // LDS path entries per lane (deeper paths spill to a global overflow)
 
 #define DK_HIP(call)                                              \

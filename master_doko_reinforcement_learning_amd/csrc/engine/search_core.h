@@ -64,12 +64,15 @@ namespace dk {
 //  NodeHot32 (32 B): also the exact mean and an f32 1/sqrt(visits) written by the
 //    backup.  Faster at one wave per SIMD (C2's 32,768 roots: 7 %), where the pick's
 //    dependent chain is exposed and a cached mean shortens it.
+#ifndef DK_HOT16_WAVES
+#define DK_HOT16_WAVES 3
+#endif
 struct alignas(16) NodeHot16 {
     uint64_t stats;       // visits (low 32) | win_score (high 32, two's complement)
     uint32_t child_base;  // first slot of the child block (valid when nchild > 0)
     uint32_t info;        // nchild:6 | player:2 | has_unexpanded:1 | chain_head:1 | state_idx:22
     static constexpr bool CACHED_MEAN = false;
-    static constexpr int MIN_WAVES = 3;   // search-kernel register budget: 3 waves per SIMD (<= 168 VGPRs)
+    static constexpr int MIN_WAVES = DK_HOT16_WAVES;   // search-kernel register budget (3 waves per SIMD: <= 168 VGPRs)
 };
 struct alignas(32) NodeHot32 {
     uint64_t stats;

@@ -29,6 +29,9 @@ struct SearchCounters {
     // deepest selection path of the device kernel's path stack (search_core.h): a forced
     // chain (single-action nodes) below its head costs one entry, like the skip pointer
     uint64_t max_path_entries = 0;
+    // optional: per iteration, the child count of every branching pick (>= 2 children),
+    // then a 0 (design data for the device kernel's pick width; tools/pick_width.py)
+    std::vector<uint8_t>* pick_trace = nullptr;
 };
 
 struct MoveOut { int action; uint64_t visits; double value; };
@@ -122,6 +125,7 @@ struct Mcts {
                 const bool forced = nd.n_actions == 1;
                 const bool head = nd.parent == root || (nd.parent >= 0 && nodes[nd.parent].n_actions >= 2);
                 if (!(node != root && forced && !head)) entries++;
+                if (ctr && ctr->pick_trace && nd.children.size() >= 2) ctr->pick_trace->push_back((uint8_t)nd.children.size());
                 node = find_best_child(node, c, ctr);
                 depth++;
             }
@@ -151,6 +155,7 @@ struct Mcts {
                 nodes[t].win_score += result[nodes[p].current_player];
                 t = p;
             }
+            if (ctr && ctr->pick_trace) ctr->pick_trace->push_back(0);
             if (ctr) { ctr->iterations++; ctr->path_nodes += path; if (depth > ctr->max_depth) ctr->max_depth = depth;
                        if (entries > ctr->max_path_entries) ctr->max_path_entries = entries; }
             if (it == iterations - 1) (void)rng.random_bool((double)(1.0f / 1000.0f));

@@ -105,6 +105,37 @@ void or_fdo_pack(void* sp, uint8_t* out) {
     memcpy(out, &d, sizeof(d));
 }
 
+// The reference's FdoState fields as the C-ABI's dk_fdo_fields (the input of dk_fdo_from_fields).
+void or_fdo_fields(void* sp, dk_fdo_fields* f) {
+    const fdo::State& s = *(fdo::State*)sp;
+    memset(f, 0, sizeof(*f));
+    for (int p = 0; p < 4; ++p) { f->hands[p] = s.hands[p].bits; f->player_eyes[p] = s.player_eyes[p]; f->player_num_tricks[p] = s.player_num_tricks[p]; }
+    f->res_start = (int8_t)s.res_start; f->res_len = (int8_t)s.res_len;
+    for (int i = 0; i < 4; ++i) f->reservations[i] = i < s.res_len ? (int8_t)s.res[i] : (int8_t)-1;
+    f->n_tricks = (int8_t)s.n_tricks;
+    memset(f->trick_start, -1, sizeof(f->trick_start)); memset(f->trick_cards, -1, sizeof(f->trick_cards));
+    for (int t = 0; t < s.n_tricks; ++t) {
+        f->trick_start[t] = (int8_t)s.tricks[t].start;
+        for (int i = 0; i < s.tricks[t].len; ++i) f->trick_cards[t][i] = (int8_t)s.tricks[t].cards[i];
+    }
+    f->ann_n = (int8_t)s.announcements.n;
+    memset(f->ann_card_index, -1, sizeof(f->ann_card_index)); memset(f->ann_player, -1, sizeof(f->ann_player));
+    for (int k = 0; k < s.announcements.n; ++k) {
+        f->ann_card_index[k] = (int8_t)s.announcements.list[k].card_index; f->ann_player[k] = (int8_t)s.announcements.list[k].player;
+        f->ann_announcement[k] = (uint8_t)s.announcements.list[k].announcement;
+    }
+    f->re_lowest = s.announcements.re_lowest < 0 ? 0 : (uint8_t)s.announcements.re_lowest;
+    f->contra_lowest = s.announcements.contra_lowest < 0 ? 0 : (uint8_t)s.announcements.contra_lowest;
+    f->ann_turns_without = (int8_t)s.announcements.turns_without; f->ann_start = (int8_t)s.announcements.starting_player;
+    f->ann_allowed = (uint8_t)s.announcements.allowed; f->card_index = (int8_t)s.card_index;
+    f->current_player = (int8_t)s.current_player; f->phase = (int8_t)s.phase;
+    f->rr_kind = s.has_reservation_result ? (int8_t)s.reservation_result.kind : (int8_t)-1;
+    f->rr_player = (int8_t)s.reservation_result.player; f->rr_reservation = (int8_t)s.reservation_result.reservation;
+    f->game_type = (int8_t)s.game_type;
+    f->team_kind = (int8_t)s.team_state.kind; f->wedding_player = (int8_t)s.team_state.wedding_player;
+    f->solved_trick = (int8_t)s.team_state.solved_trick_index; f->re_players = s.team_state.re_players;
+}
+
 int or_fdo_random_plies(void* sp, uint64_t* rng_state, int k, int no_announcement) {
     fdo::State& s = *(fdo::State*)sp; SmallRng r = rng_from(rng_state);
     int done = 0;
@@ -124,6 +155,15 @@ void or_fdo_rollout(void* sp, uint64_t* rng_state, double* out) {
 }
 int or_fdo_rewards(void* sp, double* out) { fdo::Env e; e.doko = *(fdo::State*)sp; return e.rewards_or_none(out); }
 
+// design data: the branching-pick child counts of one search (see SearchCounters::pick_trace)
+int or_fdo_search_trace(void* sp, uint64_t* rng_state, uint32_t iters, double c, uint8_t* out, int cap) {
+    fdo::Env e; e.doko = *(fdo::State*)sp; SmallRng r = rng_from(rng_state);
+    Mcts<fdo::Env> m; SearchCounters ctr; std::vector<uint8_t> tr; ctr.pick_trace = &tr;
+    m.search(e, c, iters, r, &ctr);
+    const int n = (int)tr.size() < cap ? (int)tr.size() : cap;
+    for (int i = 0; i < n; ++i) out[i] = tr[i];
+    return (int)tr.size();
+}
 int or_fdo_search(void* sp, uint64_t* rng_state, uint32_t iters, double c, uint32_t* visits, double* values, uint64_t* counters) {
     fdo::Env e; e.doko = *(fdo::State*)sp; SmallRng r = rng_from(rng_state);
     Mcts<fdo::Env> m; SearchCounters ctr;
@@ -221,6 +261,23 @@ void or_do_pack(void* sp, uint8_t* out) {
     d.team_kind = (uint8_t)s.team.kind; d.wedding_player = (uint8_t)s.team.wedding_player; d.solved_trick = (uint8_t)s.team.solved;
     d.re_players = s.team.re; d.trick_index = (uint8_t)s.trick_index; d.game = DK_GAME_DOKO;
     memcpy(out, &d, sizeof(d));
+}
+// The reference's DoState fields as the C-ABI's dk_do_fields (the input of dk_do_from_fields).
+void or_do_fields(void* sp, dk_do_fields* f) {
+    const dko::State& s = *(dko::State*)sp;
+    memset(f, 0, sizeof(*f));
+    for (int p = 0; p < 4; ++p) { f->hands[p] = s.hands[p]; f->player_eyes[p] = s.eyes[p]; f->player_num_tricks[p] = s.ntricks[p]; }
+    f->res_start = (int8_t)s.res_start;
+    for (int i = 0; i < 4; ++i) f->reservations[i] = (int8_t)s.res[i];
+    for (int t = 0; t < 12; ++t) {
+        f->trick_start[t] = s.tricks[t].present ? (int8_t)s.tricks[t].start : (int8_t)-1;
+        for (int i = 0; i < 4; ++i) f->trick_cards[t][i] = s.tricks[t].present ? (int8_t)s.tricks[t].cards[i] : (int8_t)-1;
+    }
+    f->current_player = (int8_t)s.current_player; f->phase = (int8_t)s.phase; f->trick_index = (int8_t)s.trick_index;
+    f->rr_kind = !s.has_rr ? (int8_t)-1 : (s.rr_wedding < 0 ? (int8_t)0 : (int8_t)2);
+    f->rr_player = (int8_t)(s.rr_wedding < 0 ? 0 : s.rr_wedding);
+    f->team_kind = (int8_t)s.team.kind; f->wedding_player = (int8_t)s.team.wedding_player;
+    f->solved_trick = (int8_t)s.team.solved; f->re_players = s.team.re;
 }
 int or_do_random_plies(void* sp, uint64_t* rng_state, int k) {
     dko::State& s = *(dko::State*)sp; SmallRng r = rng_from(rng_state); int done = 0;

@@ -48,6 +48,8 @@ def lib():
             "or_fdo_hands": (None, [vp, u64p]),
             "or_fdo_info": (None, [vp, i32p]),
             "or_fdo_pack": (None, [vp, u8p]),
+            "or_fdo_fields": (None, [vp, vp]),
+            "or_do_fields": (None, [vp, vp]),
             "or_fdo_random_plies": (ctypes.c_int, [vp, u64p, ctypes.c_int, ctypes.c_int]),
             "or_fdo_rollout": (None, [vp, u64p, f64p]),
             "or_fdo_rewards": (ctypes.c_int, [vp, f64p]),
