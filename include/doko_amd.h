@@ -153,8 +153,9 @@ typedef struct dk_az_state {
  * dk_fdo_fields mirrors FdoState (rs-full-doko/src/state/state.rs:24-75) field by field,
  * so a caller holding an FdoState fills it without knowing the 128-B layout:
  *   reservations_round  (reservation/reservation_round.rs:9-77)  res_start, res_len, reservations[]
- *                        FdoReservation: 0 Healthy 1 Wedding 2 DiamondsSolo 3 HeartsSolo 4 SpadesSolo
- *                        5 ClubsSolo 6 TrumplessSolo 7 QueensSolo 8 JacksSolo
+ *                        FdoReservation (reservation/reservation.rs:11-24): 0 Healthy 1 Wedding
+ *                        2 DiamondsSolo 3 HeartsSolo 4 SpadesSolo 5 ClubsSolo 6 QueensSolo
+ *                        7 JacksSolo 8 TrumplessSolo
  *   tricks              (trick/trick.rs:10-17)  n_tricks, trick_start[], trick_cards[][] (FdoCard or -1)
  *   hands               (hand/hand.rs:17-20)     reference bit layout
  *   announcements       (announcement/announcement.rs:47-59)  the occurrence list (card_index,

@@ -101,7 +101,7 @@ State new_game(SmallRng& rng) {
 }
 
 // teams/team_logic.rs:69-143
-static TeamState resolve(const State& s) {
+TeamState resolve_team(const State& s) {
     TeamState t;
     if (s.rr_wedding < 0) {
         t.kind = NoWedding;
@@ -162,7 +162,7 @@ void play_action(State& s, int a) {
             const int w = winning_player_in_trick(t);
             s.eyes[w] += trick_eyes(t);
             s.ntricks[w] += 1;
-            if (!team_final(s.team)) s.team = resolve(s);
+            if (!team_final(s.team)) s.team = resolve_team(s);
             if (s.trick_index == 12) {
                 s.phase = Finished; s.current_player = -1;
                 if (!team_final(s.team)) panic("teams unknown");
@@ -187,7 +187,7 @@ void play_action(State& s, int a) {
             s.has_rr = true; s.rr_wedding = wi < 0 ? -1 : (wi + s.res_start) % 4;
             s.trick_index = 0;
             s.tricks[0] = Trick(); s.tricks[0].start = np; s.tricks[0].present = true;
-            if (!team_final(s.team)) s.team = resolve(s);
+            if (!team_final(s.team)) s.team = resolve_team(s);
         }
     }
 }

@@ -53,6 +53,7 @@ void play_action(State& s, int action_idx);
 bool random_action_for_current_player(State& s, SmallRng& rng);
 uint64_t observation_allowed(const State& s);
 Stats calculate_stats(uint8_t re, const uint32_t eyes[4], const uint32_t ntricks[4]);
+TeamState resolve_team(const State& s);   // teams/team_logic.rs:69-143
 
 struct Env {
     State doko;

@@ -369,7 +369,7 @@ static AnnFlags ann_flags(uint32_t prev) {
     f.only_u30 = f.u30 && !f.black; f.only_black = f.black;
     return f;
 }
-static bool re_won(uint32_t re_eyes, uint32_t re_prev, uint32_t ko_prev, bool re_all, bool ko_all) {
+bool re_won(uint32_t re_eyes, uint32_t re_prev, uint32_t ko_prev, bool re_all, bool ko_all) {
     const AnnFlags r = ann_flags(re_prev), k = ann_flags(ko_prev);
     if (re_eyes >= 121 && r.none && k.none) return true;
     if (re_eyes >= 121 && r.only_ann && !k.ann) return true;
@@ -385,7 +385,7 @@ static bool re_won(uint32_t re_eyes, uint32_t re_prev, uint32_t ko_prev, bool re
     if (!ko_all && k.only_black && !r.u90) return true;
     return false;
 }
-static bool kontra_won(uint32_t ko_eyes, uint32_t re_prev, uint32_t ko_prev, bool re_all, bool ko_all) {
+bool kontra_won(uint32_t ko_eyes, uint32_t re_prev, uint32_t ko_prev, bool re_all, bool ko_all) {
     const AnnFlags r = ann_flags(re_prev), k = ann_flags(ko_prev);
     if (ko_eyes >= 120 && r.none && k.none) return true;
     if (ko_eyes >= 120 && r.only_ann && !k.ann) return true;
@@ -403,58 +403,45 @@ static bool kontra_won(uint32_t ko_eyes, uint32_t re_prev, uint32_t ko_prev, boo
 }
 
 // stats/basic_points/basic_winning_points.rs:48-285
-static void basic_winning_points(uint32_t loser_eyes, bool winner_all, uint32_t re_prev, uint32_t ko_prev,
-                                 uint32_t re_eyes, uint32_t ko_eyes, int* win, int* lose) {
+// details[23] in the field order of FdoBasicWinningPointsDetails (basic_winning_points.rs:8-46)
+void basic_winning_points(uint32_t loser_eyes, bool winner_all, uint32_t re_prev, uint32_t ko_prev,
+                          uint32_t re_eyes, uint32_t ko_eyes, int* win, int* lose, int* details) {
     const AnnFlags r = ann_flags(re_prev), k = ann_flags(ko_prev);
+    int d[23] = {0};
+    d[0] = 1;                                        // (a) won
+    d[1] = loser_eyes < 90; d[2] = loser_eyes < 60; d[3] = loser_eyes < 30; d[4] = winner_all;
+    d[5] = r.ann ? 2 : 0;                            // (b)
+    d[6] = k.ann ? 2 : 0;
+    d[7] = r.u90; d[8] = r.u60; d[9] = r.u30; d[10] = r.black;       // (c)
+    d[11] = k.u90; d[12] = k.u60; d[13] = k.u30; d[14] = k.black;    // (d)
+    d[15] = re_eyes >= 120 && k.u90; d[16] = re_eyes >= 90 && k.u60; // (e)
+    d[17] = re_eyes >= 60 && k.u30; d[18] = re_eyes >= 30 && k.black;
+    d[19] = ko_eyes >= 120 && r.u90; d[20] = ko_eyes >= 90 && r.u60; // (f)
+    d[21] = ko_eyes >= 60 && r.u30; d[22] = ko_eyes >= 30 && r.black;
     int w = 0;
-    w += 1;                              // (a) won
-    if (loser_eyes < 90) w += 1;
-    if (loser_eyes < 60) w += 1;
-    if (loser_eyes < 30) w += 1;
-    if (winner_all) w += 1;
-    if (r.ann) w += 2;                   // (b)
-    if (k.ann) w += 2;
-    if (r.u90) w += 1;                   // (c)
-    if (r.u60) w += 1;
-    if (r.u30) w += 1;
-    if (r.black) w += 1;
-    if (k.u90) w += 1;                   // (d)
-    if (k.u60) w += 1;
-    if (k.u30) w += 1;
-    if (k.black) w += 1;
-    if (re_eyes >= 120 && k.u90) w += 1; // (e)
-    if (re_eyes >= 90 && k.u60) w += 1;
-    if (re_eyes >= 60 && k.u30) w += 1;
-    if (re_eyes >= 30 && k.black) w += 1;
-    if (ko_eyes >= 120 && r.u90) w += 1; // (f)
-    if (ko_eyes >= 90 && r.u60) w += 1;
-    if (ko_eyes >= 60 && r.u30) w += 1;
-    if (ko_eyes >= 30 && r.black) w += 1;
+    for (int i = 0; i < 23; ++i) w += d[i];
+    if (details) for (int i = 0; i < 23; ++i) details[i] = d[i];
     *win = w; *lose = -w;
 }
 // stats/basic_points/basic_draw_points.rs:27-175
-static void basic_draw_points(uint32_t re_prev, uint32_t ko_prev, uint32_t re_eyes, uint32_t ko_eyes, int* re, int* ko) {
+// details[14] in the field order of FdoBasicDrawPointsDetails (basic_draw_points.rs:8-25):
+// winning_under_{90,60,30}_re, winning_under_{90,60,30}_kontra, re_reached_*, kontra_reached_*
+void basic_draw_points(uint32_t re_prev, uint32_t ko_prev, uint32_t re_eyes, uint32_t ko_eyes, int* re, int* ko,
+                       int* details) {
     const AnnFlags r = ann_flags(re_prev), k = ann_flags(ko_prev);
-    int rp = 0, kp = 0;
-    if (re_eyes < 90) { kp += 1; rp -= 1; }
-    if (ko_eyes < 90) { rp += 1; kp -= 1; }
-    if (re_eyes < 60) { kp += 1; rp -= 1; }
-    if (ko_eyes < 60) { rp += 1; kp -= 1; }
-    if (re_eyes < 30) { kp += 1; rp -= 1; }
-    if (ko_eyes < 30) { rp += 1; kp -= 1; }
-    if (re_eyes >= 120 && k.u90) { rp += 1; kp -= 1; }
-    if (re_eyes >= 90 && k.u60) { rp += 1; kp -= 1; }
-    if (re_eyes >= 60 && k.u30) { rp += 1; kp -= 1; }
-    if (re_eyes >= 30 && k.black) { rp += 1; kp -= 1; }
-    if (ko_eyes >= 120 && r.u90) { kp += 1; rp -= 1; }
-    if (ko_eyes >= 90 && r.u60) { kp += 1; rp -= 1; }
-    if (ko_eyes >= 60 && r.u30) { kp += 1; rp -= 1; }
-    if (ko_eyes >= 30 && r.black) { kp += 1; rp -= 1; }
-    *re = rp; *ko = kp;
+    int d[14] = {0};
+    d[0] = ko_eyes < 90; d[1] = ko_eyes < 60; d[2] = ko_eyes < 30;      // Re's gains
+    d[3] = re_eyes < 90; d[4] = re_eyes < 60; d[5] = re_eyes < 30;      // Kontra's gains
+    d[6] = re_eyes >= 120 && k.u90; d[7] = re_eyes >= 90 && k.u60; d[8] = re_eyes >= 60 && k.u30; d[9] = re_eyes >= 30 && k.black;
+    d[10] = ko_eyes >= 120 && r.u90; d[11] = ko_eyes >= 90 && r.u60; d[12] = ko_eyes >= 60 && r.u30; d[13] = ko_eyes >= 30 && r.black;
+    const int rp = d[0] + d[1] + d[2] + d[6] + d[7] + d[8] + d[9];
+    const int kp = d[3] + d[4] + d[5] + d[10] + d[11] + d[12] + d[13];
+    if (details) for (int i = 0; i < 14; ++i) details[i] = d[i];
+    *re = rp - kp; *ko = kp - rp;
 }
 
 // stats/additional_points/*.rs
-static AdditionalDetails additional_points(uint8_t re_players, int winning_team /*0 re,1 ko,-1 none*/,
+AdditionalDetails additional_points(uint8_t re_players, int winning_team /*0 re,1 ko,-1 none*/,
                                            const Trick* tricks, int n_tricks, int* re_add, int* ko_add) {
     AdditionalDetails d{};
     for (int i = 0; i < n_tricks; ++i) {                       // doppelkopf.rs:8-28
@@ -502,7 +489,7 @@ EndOfGameStats calculate_stats(const uint32_t eyes[4], const uint32_t ntricks[4]
     const int winning_team = rw ? 0 : (kw ? 1 : -1);
     int re_pts, ko_pts;
     if (!rw && !kw) {
-        int rb, kb; basic_draw_points(re_prev, ko_prev, re_eyes, ko_eyes, &rb, &kb);
+        int rb, kb; basic_draw_points(re_prev, ko_prev, re_eyes, ko_eyes, &rb, &kb, s.draw_details);
         int ra = 0, ka = 0;
         if (!is_solo) { s.additional = additional_points(re_players, winning_team, tricks, n_tricks, &ra, &ka); s.has_additional = true; }
         re_pts = rb + ra; ko_pts = kb + ka;
@@ -510,7 +497,7 @@ EndOfGameStats calculate_stats(const uint32_t eyes[4], const uint32_t ntricks[4]
     } else {
         const uint32_t loser_eyes = rw ? ko_eyes : re_eyes;
         const bool winner_all = rw ? re_all : (kw ? ko_all : false);
-        int wp, lp; basic_winning_points(loser_eyes, winner_all, re_prev, ko_prev, re_eyes, ko_eyes, &wp, &lp);
+        int wp, lp; basic_winning_points(loser_eyes, winner_all, re_prev, ko_prev, re_eyes, ko_eyes, &wp, &lp, s.win_details);
         int ra = 0, ka = 0;
         if (!is_solo) { s.additional = additional_points(re_players, winning_team, tricks, n_tricks, &ra, &ka); s.has_additional = true; }
         re_pts = rw ? wp + ra : lp + ra;
@@ -691,5 +678,28 @@ void Env::random_rollout(SmallRng& rng, double out[4]) const {
     for (int p = 0; p < 4; ++p) out[p] = (double)r.stats.player_points[p];
 }
 
+}  // namespace fdo
+}  // namespace oracle
+
+// ---- public entry points for the reference's rule KATs (tests/test_rule_kats.py) ----
+namespace oracle {
+namespace fdo {
+int announcements_start_round(Announcements& a, int card_index, int start, const int hand_lens[4], const TeamState& ts,
+                              int* next) {
+    a.turns_without = 0;                                   // start_round (announcement.rs:83-101)
+    a.starting_player = start;
+    return internal_progress(a, start, card_index, hand_lens, ts, next);
+}
+int announcements_play(Announcements& a, int player, uint32_t ann, int card_index, const int hand_lens[4],
+                       const TeamState& ts, int* next) {
+    internal_play_announcement(a, player, ann, card_index, ts);   // play_announcement (announcement.rs:103-124)
+    return internal_progress(a, (player + 1) % 4, card_index, hand_lens, ts, next);
+}
+int calc_cards_last_announcement_pub(uint32_t set, int wedding_solved, bool* some) {
+    return calc_cards_last_announcement(set, wedding_solved, some);
+}
+uint32_t internal_calc_allowed_pub(int n_cards, uint32_t prev, int wedding_solved, bool enemy_some, int enemy_cards) {
+    return internal_calc_allowed(n_cards, prev, wedding_solved, enemy_some, enemy_cards);
+}
 }  // namespace fdo
 }  // namespace oracle

@@ -112,6 +112,8 @@ struct EndOfGameStats {
     int32_t re_points, kontra_points, player_points[4];
     bool has_winning_details; bool has_draw_details; bool has_additional;
     AdditionalDetails additional;
+    int win_details[23];     // FdoBasicWinningPointsDetails fields in declaration order
+    int draw_details[14];    // FdoBasicDrawPointsDetails fields in declaration order
 };
 
 struct State {
@@ -153,6 +155,23 @@ ReservationResult winning_player_in_reservation_round(const State& s);
 int reservation_to_game_type(const ReservationResult& rr);
 EndOfGameStats calculate_stats(const uint32_t eyes[4], const uint32_t ntricks[4], uint8_t re_players,
                                int re_lowest, int contra_lowest, const Trick* tricks, int n_tricks);
+
+// stats building blocks (stats/win_conditions, stats/basic_points, stats/additional_points)
+bool re_won(uint32_t re_eyes, uint32_t re_prev, uint32_t ko_prev, bool re_all, bool ko_all);
+bool kontra_won(uint32_t ko_eyes, uint32_t re_prev, uint32_t ko_prev, bool re_all, bool ko_all);
+void basic_winning_points(uint32_t loser_eyes, bool winner_all, uint32_t re_prev, uint32_t ko_prev,
+                          uint32_t re_eyes, uint32_t ko_eyes, int* win, int* lose, int* details);
+void basic_draw_points(uint32_t re_prev, uint32_t ko_prev, uint32_t re_eyes, uint32_t ko_eyes, int* re, int* ko,
+                       int* details);
+AdditionalDetails additional_points(uint8_t re_players, int winning_team, const Trick* tricks, int n_tricks,
+                                    int* re_add, int* ko_add);
+// announcement rounds (announcement/announcement.rs:83-215); returns 0 NextPlayerIs / 1 RoundIsOver
+int announcements_start_round(Announcements& a, int card_index, int start, const int hand_lens[4], const TeamState& ts,
+                              int* next);
+int announcements_play(Announcements& a, int player, uint32_t ann, int card_index, const int hand_lens[4],
+                       const TeamState& ts, int* next);
+int calc_cards_last_announcement_pub(uint32_t set, int wedding_solved, bool* some);
+uint32_t internal_calc_allowed_pub(int n_cards, uint32_t prev, int wedding_solved, bool enemy_some, int enemy_cards);
 
 State new_game_from_hand_and_start_player(const Hand hands[4], int start_player);
 State new_game(SmallRng& rng);
