@@ -424,6 +424,17 @@ int dk_ar_output_async(dk_ctx* ctx, dk_state* d_out, uint8_t* d_status, uint8_t*
 int dk_ar_fallback_async(dk_ctx* ctx, uint32_t n_info, uint32_t samples, const uint8_t* d_status, const uint64_t* d_allowed,
                          const uint64_t* d_seeds, uint8_t* d_action, uint32_t* d_successes, void* stream);
 
+/* is_consistent (rs-full-doko/src/matching/is_consistent.rs:38-305): whether assumed hands
+ * hands[4*i..] (reference bit layout) and assumed reservations reservations[4*i..] (FdoReservation,
+ * DK_NONE = None; by player) are consistent with infostate record i, as the observer (its
+ * current player) sees it.  reasons[i] = DK_NONE when consistent, else the NotConsistentReason
+ * (is_consistent.rs:26-36: 0 HandSizeMismatch 1 NotInRemainingCards 2 RemainingCardsLeft
+ * 3 AlreadyDiscardedColor 4 HasClubQueenButSomeoneElseAnnouncedWedding 5 HasNoClubQueenButAnnouncedRe
+ * 6 HasClubQueenButAnnouncedKontra 7 WrongReservation 8 WrongReservationClubQ); 0xFE for a finished
+ * infostate (the reference unwraps its current player). */
+int dk_is_consistent_batch(dk_ctx* ctx, const dk_az_state* infostates, const uint64_t* hands, const uint8_t* reservations,
+                           uint32_t n, uint8_t* reasons);
+
 /* Game records for self-play.  dk_az_records_async: records of packed rs-full-doko states
  * without announcements (new games, DK_E_STATE otherwise).  dk_az_step_async:
  * take_action_by_action_index(action, skip_single = true) (full_doko.rs:121-157) on every

@@ -98,6 +98,7 @@ def lib():
         "dk_ar_fallback_async": (ctypes.c_int, [vp, u32, u32, vp, vp, vp, vp, vp, vp]),
         "dk_fuse_accumulate_masked_async": (ctypes.c_int, [vp, vp, u32, u32, vp, vp, ctypes.c_int, vp, vp, vp]),
         "dk_fdo_from_fields": (ctypes.c_int, [vp, vp]),
+        "dk_is_consistent_batch": (ctypes.c_int, [vp, vp, vp, vp, u32, vp]),
         "dk_fdo_to_fields": (ctypes.c_int, [vp, vp]),
         "dk_do_from_fields": (ctypes.c_int, [vp, vp]),
         "dk_do_to_fields": (ctypes.c_int, [vp, vp]),
@@ -126,5 +127,5 @@ EXPORTED = [
     "dk_az_records_async", "dk_az_step_async", "dk_az_encode_async", "dk_net_embed_ln_bf16_async",
     "dk_net_add_ln_bf16_async", "dk_net_attn62_bf16_async", "dk_net_fc_gelu_bf16_async", "dk_ar_begin_async", "dk_ar_guesses_async", "dk_ar_prepare_async",
     "dk_ar_choose_async", "dk_ar_output_async", "dk_ar_fallback_async", "dk_fuse_accumulate_masked_async",
-    "dk_fdo_from_fields", "dk_fdo_to_fields", "dk_do_from_fields", "dk_do_to_fields",
+    "dk_fdo_from_fields", "dk_fdo_to_fields", "dk_do_from_fields", "dk_do_to_fields", "dk_is_consistent_batch",
 ]

@@ -186,6 +186,20 @@ __global__ void __launch_bounds__(WAVE, H::MIN_WAVES) search_kernel(const dk_sta
     }
 }
 
+// is_consistent (rs-full-doko/src/matching/is_consistent.rs:38-305) of assumed hands and
+// reservations for an infostate record, one lane per check: the IMPI lanes' facts (init)
+// with the given assumption, then the same consistency pass the sampler ends with.
+__global__ void is_consistent_kernel(const dk_az_state* info, const uint64_t* hands, const uint8_t* res, uint32_t n,
+                                     uint8_t* reasons) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const dk_az_state r = info[i];
+    dk::ar::Lane L;
+    (void)dk::ar::init(r, 0, L);
+    for (int p = 0; p < 4; ++p) { L.hands[p] = hands[4 * (size_t)i + p]; L.res[p] = res[4 * (size_t)i + p]; }
+    reasons[i] = L.status == dk::ar::PANIC ? (uint8_t)0xFE : dk::ar::consistency(r, L);
+}
+
 __device__ void new_game_packed(int game, uint64_t seed, dk_state& out) {
     dk::Rng rng = dk::Rng::seed_from_u64(seed);
     const uint32_t start = rng.range_u32(4);  // FdoPlayer::from_rng / gen_range(0..4)
@@ -1157,6 +1171,25 @@ int dk_fuse(dk_ctx* ctx, const uint32_t* visits, uint32_t n_info, uint32_t sampl
     rc = dk_fuse_select_async(ctx, n_info, mode, d_a, d_u, d_f, d_out, ctx->stream);
     if (rc) return rc;
     DK_HIP(hipMemcpyAsync(action, d_out, n_info, hipMemcpyDeviceToHost, ctx->stream));
+    return finish(ctx, ctx->stream);
+}
+
+int dk_is_consistent_batch(dk_ctx* ctx, const dk_az_state* infostates, const uint64_t* hands, const uint8_t* reservations,
+                           uint32_t n, uint8_t* reasons) {
+    if (!ctx || !infostates || !hands || !reservations || !reasons) return DK_E_INVALID;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    if (n == 0) return DK_OK;
+    dk_az_state* d_i = (dk_az_state*)scratch(ctx, 0, n * sizeof(dk_az_state));
+    uint64_t* d_h = (uint64_t*)scratch(ctx, 1, 4 * (size_t)n * sizeof(uint64_t));
+    uint8_t* d_r = (uint8_t*)scratch(ctx, 2, 4 * (size_t)n);
+    uint8_t* d_o = (uint8_t*)scratch(ctx, 3, n);
+    if (!d_i || !d_h || !d_r || !d_o) return DK_E_CAPACITY;
+    DK_HIP(hipMemcpyAsync(d_i, infostates, n * sizeof(dk_az_state), hipMemcpyHostToDevice, ctx->stream));
+    DK_HIP(hipMemcpyAsync(d_h, hands, 4 * (size_t)n * sizeof(uint64_t), hipMemcpyHostToDevice, ctx->stream));
+    DK_HIP(hipMemcpyAsync(d_r, reservations, 4 * (size_t)n, hipMemcpyHostToDevice, ctx->stream));
+    hipLaunchKernelGGL(is_consistent_kernel, dim3(grid_for(n, 64)), dim3(64), 0, ctx->stream, d_i, d_h, d_r, n, d_o);
+    DK_HIP(hipGetLastError());
+    DK_HIP(hipMemcpyAsync(reasons, d_o, n, hipMemcpyDeviceToHost, ctx->stream));
     return finish(ctx, ctx->stream);
 }
 
