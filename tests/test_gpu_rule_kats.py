@@ -256,7 +256,7 @@ def test_announcement_rounds_on_device(eng):
         start = k["ops"][0]["op"][0]
         re = k["team"]["re"]
         hands = [0, 0, 0, 0]
-        pool = [c for c in range(24) if c != 15]
+        pool = [c for c in range(24) if c != 15] * 2
         for p in range(4):
             n = k["hand_lens"][p]
             cards = ([15] if re >> p & 1 else []) + [pool.pop() for _ in range(n - (1 if re >> p & 1 else 0))]
@@ -293,36 +293,57 @@ def test_announcement_rounds_on_device(eng):
 
 
 def _finished_fdo(k):
-    """The stats KAT as a finished state; the stats API takes no game type, so the first
-    FdoGameType under which the recorded trick starts follow the winners is used (extra
-    points, the only part that reads the tricks, count in non-solo games only)."""
+    """The stats KAT as a finished state.  The stats API takes no game type; the recorded
+    tricks are used under the first FdoGameType whose trick order makes each trick start with
+    the previous winner.  A solo's score reads no trick (extra points count in non-solo games
+    only), and the solo KATs list tricks no game can reach (a third copy of a card), so a solo
+    KAT's eyes / tricks won / teams / announcements sit on the tricks of a finished seeded game."""
     import master_doko_reinforcement_learning_amd as dk
-    for gt in range(9):
+
+    def fields(tricks, gt):
         f = dk.FdoFields()
         for p in range(4):
             f.player_eyes[p], f.player_num_tricks[p] = k["eyes"][p], k["ntricks"][p]
-        f.res_start = k["tricks"][0][0]
+        f.res_start = tricks[0][0]
         f.res_len = 4
         f.n_tricks = 12
-        for t, tr in enumerate(k["tricks"]):
+        for t, tr in enumerate(tricks):
             f.trick_start[t] = tr[0]
             for i in range(4):
                 f.trick_cards[t][i] = tr[1 + i]
         f.re_lowest, f.contra_lowest = k["re_lowest"], k["contra_lowest"]
         f.card_index, f.current_player, f.phase, f.rr_kind, f.game_type = 48, -1, 3, 0, gt
         f.team_kind, f.re_players = 3, k["re_players"]
+        return f
+
+    for gt in range(9):
         try:
-            return dk.fdo_from_fields(f), gt
+            return dk.fdo_from_fields(fields(k["tricks"], gt)), gt
         except dk.DokoError:
             continue
-    raise AssertionError("no game type fits the trick sequence of " + k["test"])
+    if not k["expect"]["is_solo"]:
+        return None, None     # extra points read these tricks, and no game reaches them
+    g = ol.FdoState.new_game(11)
+    for _ in range(4):
+        g.play(24)
+    g.random_plies(ol.rng_seed(11), 200, True)
+    real = dk.fdo_to_fields(g.pack())
+    tricks = [[real.trick_start[t]] + [real.trick_cards[t][i] for i in range(4)] for t in range(12)]
+    return dk.fdo_from_fields(fields(tricks, real.game_type)), -1
 
 
 def test_stats_on_device(eng):
     import master_doko_reinforcement_learning_amd as dk
     rows, exp = [], []
+    unreachable = []
     for k in FDO["stats"]:
         row, gt = _finished_fdo(k)
+        if row is None:
+            # e.g. test_end_of_game_stats_normalspiel_kontra_verloren: trick 8 starts with LEFT
+            # although RIGHT took trick 7, and every player_num_tricks is 0 -- checked on the
+            # oracle only (tests/test_rule_kats.py::test_end_of_game_stats)
+            unreachable.append(k["test"])
+            continue
         if not k["expect"]["is_solo"]:
             assert gt in (0, 1), k["test"]        # extra points need the normal-game trick winners
         rows.append(row)
@@ -330,6 +351,7 @@ def test_stats_on_device(eng):
     has, r = dk.McEnv(eng).rewards_or_none(packed(rows))
     assert has.all()
     assert r.astype(int).tolist() == exp
+    assert len(rows) >= 2 and len(unreachable) <= 2, unreachable
 
 
 def test_is_consistent_on_device(eng):
