@@ -293,6 +293,9 @@ def main():
                        "on the GPU by the rs-doko-assignment sampler",
                 "c2": "synthetic: seeded rs-doko deals (SmallRng::seed_from_u64(0xD0C00000+i)), 4x Healthy"}[args.workload]
         stream_peak = stream_copy_gbs(torch, dev)
+        hw, cap, overflowed = eng.pool_high_water(sp)
+        pools = {"bytes": eng.pool_bytes(), "slot_capacity": cap, "proven_slot_bound": 40 + 12 * iters,
+                 "slot_high_water": hw, "overflowed_roots": overflowed}
         result = {
             "metric": METRIC,
             "value": sims_total / elapsed,
@@ -336,6 +339,7 @@ def main():
                         % ("%.0f%%" % (100 * valu["busy"]) if valu else "n/a",
                            "%.0f%%" % (100 * valu["mem_wait_frac"]) if valu else "n/a"),
             },
+            "node_pools": pools,
             "small_batch": small,
             "ranks": world,
             "dist_backend": backend if world > 1 else None,

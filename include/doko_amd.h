@@ -242,15 +242,22 @@ typedef struct dk_config {
     int32_t device;          /* HIP device ordinal                                          */
     uint32_t max_roots;      /* largest batch of roots one search call may carry            */
     uint32_t max_iterations; /* largest `iterations` one search call may use                */
-    uint32_t slot_capacity;  /* child slots per root (0 = derive the proven bound)          */
+    uint32_t slot_capacity;  /* child slots per root in the main pools (0 = 64 + 4 x        */
+                             /* max_iterations); see dk_pool_high_water                     */
 } dk_config;
 
 typedef struct dk_ctx dk_ctx;
 
 /* The node / state pools hold min(max_roots, resident roots) trees at once (resident
- * roots = CUs x 8 waves x 64 lanes; env DK_POOL_ROOTS overrides).  The search grid is
+ * roots = CUs x 12 waves x 64 lanes; env DK_POOL_ROOTS overrides).  The search grid is
  * persistent: a batch larger than the pools streams through them, one wave-sized group of
- * roots at a time, so max_roots bounds the batch, not the memory. */
+ * roots at a time, so max_roots bounds the batch, not the memory.
+ * Child slots: a search needs at most 40 + 12 x iterations of them (proven bound) but
+ * measured far fewer, so the main pools hold slot_capacity per root (default
+ * 64 + 4 x max_iterations, rounded up to a multiple of 256; env DK_SLOT_CAPACITY overrides).  A root that runs out is
+ * searched again, from its seed, by a second launch over a small pool with the proven
+ * bound (4,096 roots at once): results are identical whatever the capacity.  With
+ * slot_capacity at or above the proven bound there is no second pool. */
 dk_ctx* dk_create(const dk_config* cfg);
 void dk_destroy(dk_ctx* ctx);
 int dk_last_error(const dk_ctx* ctx);
@@ -478,6 +485,10 @@ int dk_sync(dk_ctx* ctx, void* stream);
 int dk_last_search_ms(dk_ctx* ctx, float* ms);
 /* memory footprint of the node / state pools reserved by dk_create (bytes) */
 uint64_t dk_pool_bytes(const dk_ctx* ctx);
+/* Pool demand since dk_create (waits for `stream`): the most child slots one search used
+ * (in either pool), the main pools' capacity per root, and how many roots overflowed it
+ * and were searched again in the fallback pool. */
+int dk_pool_high_water(dk_ctx* ctx, void* stream, uint32_t* slots, uint32_t* capacity, uint32_t* overflowed);
 
 #ifdef __cplusplus
 }

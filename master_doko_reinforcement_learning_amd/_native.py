@@ -61,6 +61,7 @@ def lib():
         "dk_destroy": (None, [vp]),
         "dk_last_error": (ctypes.c_int, [vp]),
         "dk_pool_bytes": (u64, [vp]),
+        "dk_pool_high_water": (ctypes.c_int, [vp, vp, ctypes.POINTER(u32), ctypes.POINTER(u32), ctypes.POINTER(u32)]),
         "dk_sync": (ctypes.c_int, [vp, vp]),
         "dk_last_search_ms": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_float)]),
         "dk_new_game_batch": (ctypes.c_int, [vp, ctypes.c_int, vp, u32, vp]),
@@ -128,4 +129,5 @@ EXPORTED = [
     "dk_net_add_ln_bf16_async", "dk_net_attn62_bf16_async", "dk_net_fc_gelu_bf16_async", "dk_ar_begin_async", "dk_ar_guesses_async", "dk_ar_prepare_async",
     "dk_ar_choose_async", "dk_ar_output_async", "dk_ar_fallback_async", "dk_fuse_accumulate_masked_async",
     "dk_fdo_from_fields", "dk_fdo_to_fields", "dk_do_from_fields", "dk_do_to_fields", "dk_is_consistent_batch",
+    "dk_pool_high_water",
 ]

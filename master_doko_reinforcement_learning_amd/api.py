@@ -131,6 +131,13 @@ class Engine:
     def pool_bytes(self):
         return int(_native.lib().dk_pool_bytes(self._ctx))
 
+    def pool_high_water(self, stream=None):
+        """(most child slots one search used, main-pool slots per root, roots that
+        overflowed the main pools and were searched again in the fallback pool), since creation."""
+        h, cap, ovf = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+        _check(_native.lib().dk_pool_high_water(self._ctx, stream, ctypes.byref(h), ctypes.byref(cap), ctypes.byref(ovf)))
+        return int(h.value), int(cap.value), int(ovf.value)
+
     def last_search_ms(self):
         ms = ctypes.c_float()
         _check(_native.lib().dk_last_search_ms(self._ctx, ctypes.byref(ms)))

@@ -138,7 +138,8 @@ __global__ void __launch_bounds__(WAVE, H::MIN_WAVES) search_kernel(const dk_sta
                                                       uint32_t cap_slots, uint32_t rpw, int lds_n,
                                                       uint32_t* visits, double* values,
                                                       uint8_t* best, int* err, uint32_t* queue, uint64_t* prof,
-                                                      const uint32_t* __restrict__ order) {
+                                                      const uint32_t* __restrict__ order, uint32_t* retry,
+                                                      const uint32_t* __restrict__ list, uint32_t* high_water) {
     const uint32_t lane = threadIdx.x;
     const uint32_t T = iters + 1;
     const uint32_t n_ln = LN_LDS ? T : 0u;
@@ -148,16 +149,21 @@ __global__ void __launch_bounds__(WAVE, H::MIN_WAVES) search_kernel(const dk_sta
     const uint32_t n_ln16 = (n_ln + 1u) & ~1u;                           // keep the next region 16-B aligned
     const uint32_t path_st_base = n_ln16;
     const uint32_t path_base32 = 2u * (path_st_base + (uint32_t)lds_n * rpw);   // in u32 units
+    // fallback pass (list != nullptr): the roots the main pass could not fit, list[0] of them
+    // at list[1..], searched again in a pool with the proven capacity
+    if (list) n = list[0];
     const uint32_t groups = (n + rpw - 1) / rpw;
     const size_t pr = (size_t)blockIdx.x * rpw + lane;                  // this lane's pool region
+    uint32_t hw = 0;                                                    // slot high-water of this lane's roots
     for (;;) {
         uint32_t g = 0;
         if (lane == 0) g = atomicAdd(queue, 1u);
         g = __shfl(g, 0);
         if (g >= groups) break;                                         // every wave reaches this
         if (order) g = order[g];                                        // longest groups first
-        const uint32_t root = g * rpw + lane;
-        if (lane >= rpw || root >= n) continue;
+        const uint32_t idx = g * rpw + lane;
+        if (lane >= rpw || idx >= n) continue;
+        const uint32_t root = list ? list[1 + idx] : idx;
         typename E::Work w;
         E::load(roots[root], w);
         dk::Rng rng = dk::Rng::seed_from_u64(seeds[root]);
@@ -179,11 +185,22 @@ __global__ void __launch_bounds__(WAVE, H::MIN_WAVES) search_kernel(const dk_sta
         (void)prof;
 #endif
         uint8_t b;
+        uint32_t used[2];
         const int st = dk::search_root<E>(w, rng, iters, c, mem, visits + (size_t)root * 39,
-                                          values + (size_t)root * 39, &b, nullptr);
-        if (st != dk::SR_OK) atomicOr(err, 1);
+                                          values + (size_t)root * 39, &b, nullptr, used);
+        if (st != dk::SR_OK) {
+            if (retry) {                                                // searched again by the fallback pass
+                retry[1 + atomicAdd(retry, 1u)] = root;
+                atomicAdd(high_water + 1, 1u);
+            } else {
+                atomicOr(err, 1);
+            }
+        } else {
+            hw = used[0] > hw ? used[0] : hw;
+        }
         best[root] = b;
     }
+    if (hw) atomicMax(high_water, hw);
 }
 
 // is_consistent (rs-full-doko/src/matching/is_consistent.rs:38-305) of assumed hands and
@@ -639,6 +656,22 @@ struct dk_ctx {
                                     // the resident capacity: CUs x 12 single-wave workgroups x 64 lanes))
     int cu_count = 0;
     uint32_t* queue = nullptr;      // root-group counter of the persistent search grid
+    // Slot-capacity fallback: pools are sized from the measured demand (default 64 + 4 x
+    // iterations slots per root, against the proven 40 + 12 x iterations); a root that runs out
+    // is appended to `retry` ([0] = count) and searched again, from its seed, by a second
+    // launch over a small pool with the proven capacity (fb_*).  Results do not change.
+    uint32_t* retry = nullptr;
+    uint32_t* queue_fb = nullptr;
+    uint32_t* high_water = nullptr; // [0] largest slot demand of a root completed in the main pools, [1] roots
+                                    // that overflowed them, [2] largest demand of a root the fallback pass
+                                    // completed (cumulative since dk_create; dk_pool_high_water)
+    void* fb_hot = nullptr;
+    dk::NodeCold* fb_cold = nullptr;
+    uint32_t* fb_ovf = nullptr;
+    uint64_t* fb_ovf_st = nullptr;
+    void* fb_states = nullptr;
+    uint32_t fb_slots = 0, fb_roots = 0;
+    uint64_t fb_bytes = 0;
     uint32_t* order = nullptr;      // queue order of the root groups (group_order_kernel)
     int group_order = -1;           // DK_GROUP_ORDER=0 / 1 forces index order / longest-first; -1: per engine
     void* hot = nullptr;            // hot records, 32 B per slot (NodeHot16 launches use half)
@@ -681,6 +714,8 @@ struct dk_ctx {
 };
 
 namespace {
+
+constexpr size_t FALLBACK_ROOTS = 64 * 64;   // roots the fallback pool holds at once
 
 constexpr size_t STATE_SLOT_BYTES =
     sizeof(dk::fdo::Work) > sizeof(dk::dko::Work) ? sizeof(dk::fdo::Work) : sizeof(dk::dko::Work);
@@ -769,10 +804,27 @@ hipError_t launch_search_t(dk_ctx* ctx, const dk_state* roots, const uint64_t* s
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
+    const bool fallback = ctx->fb_hot != nullptr;
+    if (fallback) {
+        e = hipMemsetAsync(ctx->retry, 0, sizeof(uint32_t), st);
+        if (e == hipSuccess) e = hipMemsetAsync(ctx->queue_fb, 0, sizeof(uint32_t), st);
+        if (e != hipSuccess) return e;
+    }
     hipLaunchKernelGGL(kern, dim3(grid), dim3(WAVE), lds_bytes, st, roots, seeds, n, iters, c, ctx->ln_table,
                        ctx->hot, ctx->cold, (typename E::Work*)ctx->states, ctx->ovf, ctx->ovf_st, ctx->cap_slots,
                        rpw, lp, visits, values, best, ctx->err, ctx->queue, ctx->prof,
-                       ordered ? (const uint32_t*)ctx->order : (const uint32_t*)nullptr);
+                       ordered ? (const uint32_t*)ctx->order : (const uint32_t*)nullptr,
+                       fallback ? ctx->retry : (uint32_t*)nullptr, (const uint32_t*)nullptr, ctx->high_water);
+    e = hipGetLastError();
+    if (e != hipSuccess || !fallback) return e;
+    // Second pass over the roots the main pool could not hold (retry[0] of them; the grid
+    // drains at once when there are none): same kernel, proven-capacity pool, no retry list,
+    // so running out there is DK_E_CAPACITY.
+    const uint32_t fb_grid = ctx->fb_roots / rpw;
+    hipLaunchKernelGGL(kern, dim3(fb_grid), dim3(WAVE), lds_bytes, st, roots, seeds, n, iters, c, ctx->ln_table,
+                       ctx->fb_hot, ctx->fb_cold, (typename E::Work*)ctx->fb_states, ctx->fb_ovf, ctx->fb_ovf_st,
+                       ctx->fb_slots, rpw, lp, visits, values, best, ctx->err, ctx->queue_fb, ctx->prof,
+                       (const uint32_t*)nullptr, (uint32_t*)nullptr, (const uint32_t*)ctx->retry, ctx->high_water + 2);
     return hipGetLastError();
 }
 
@@ -785,7 +837,9 @@ hipError_t launch_search(dk_ctx* ctx, const dk_state* roots, const uint64_t* see
     // hot-record layout (search_core.h): 16 B once the batch gives every SIMD two waves,
     // 32 B (cached means) when a single wave per SIMD leaves the pick's latency exposed
     const uint32_t simds = 4u * (uint32_t)ctx->cu_count;
-    const bool h16 = ctx->hot_layout ? ctx->hot_layout == 16 : grid_for(n, rpw) >= 2u * simds;
+    // (16-B records compare means by 24-bit cross products: exact up to P24_MAX_ITERS iterations)
+    const bool h16 = iters <= dk::P24_MAX_ITERS &&
+                     (ctx->hot_layout ? ctx->hot_layout == 16 : grid_for(n, rpw) >= 2u * simds);
     if (h16)
         return ln ? launch_search_t<E, true, dk::NodeHot16>(ctx, roots, seeds, n, iters, c, visits, values, best, st, ln_bytes, rpw)
                   : launch_search_t<E, false, dk::NodeHot16>(ctx, roots, seeds, n, iters, c, visits, values, best, st, ln_bytes, rpw);
@@ -829,7 +883,24 @@ dk_ctx* dk_create(const dk_config* cfg) {
     ctx->max_iters = cfg->max_iterations;
     // Proven bound: the root block (<= 39) plus one block of <= 12 children per
     // iteration (non-root nodes offer at most 12 cards / 9 reservations / 1 pass).
-    ctx->cap_slots = cfg->slot_capacity ? cfg->slot_capacity : 40u + 12u * cfg->max_iterations;
+    // The measured demand is far lower (largest over the C3 bench roots: ~2,400 slots at
+    // 1,000 iterations), so by default the main pools hold 64 + 4 x iterations
+    // slots per root and the rare root that needs more is searched again in the fallback
+    // pool, which has the proven bound.  cfg->slot_capacity (or env DK_SLOT_CAPACITY) sets
+    // the main pools' capacity; at or above the proven bound there is no fallback pool.
+    // The capacity is also the stride between the lanes' pool regions, and it is rounded up
+    // to a multiple of 256 slots (4 KB of 16-B records): strides 512 B off a multiple of
+    // 64 KB (4,064 or 4,128 slots) ran the C3 search 1.6x slower than 4,096 or 12,040
+    // (tools/cap_sweep.py; the lanes' accesses fall into the same memory channels).
+    const uint32_t proven = 40u + 12u * cfg->max_iterations;
+    uint32_t cap = cfg->slot_capacity ? cfg->slot_capacity : 64u + 4u * cfg->max_iterations;
+    if (const char* e = getenv("DK_SLOT_CAPACITY")) {
+        const long v = atol(e);
+        if (v >= 1) cap = (uint32_t)v;
+    }
+    cap = cap < proven ? (cap + 255u) & ~255u : proven;
+    ctx->cap_slots = cap < proven ? cap : proven;
+    const bool with_fallback = ctx->cap_slots < proven;
     ctx->cu_count = prop.multiProcessorCount;
     if (const char* e = getenv("DK_ROOTS_PER_WAVE")) {
         const int v = atoi(e);
@@ -866,6 +937,23 @@ dk_ctx* dk_create(const dk_config* cfg) {
     ok = ok && hipMalloc(&ctx->ln_table, (T + 1) * sizeof(double)) == hipSuccess;
     ok = ok && hipMalloc(&ctx->err, sizeof(int)) == hipSuccess;
     ok = ok && hipMalloc(&ctx->queue, sizeof(uint32_t)) == hipSuccess;
+    ok = ok && hipMalloc(&ctx->high_water, 4 * sizeof(uint32_t)) == hipSuccess;
+    ok = ok && hipMemset(ctx->high_water, 0, 4 * sizeof(uint32_t)) == hipSuccess;
+    if (ok && with_fallback) {
+        // 64 waves of 64 roots (fewer when the context is smaller): overflow is rare, and the
+        // pass only has to finish the few roots that need it
+        const size_t FR = R < FALLBACK_ROOTS ? R : FALLBACK_ROOTS, FS = proven;
+        ctx->fb_roots = (uint32_t)FR;
+        ctx->fb_slots = proven;
+        ok = hipMalloc(&ctx->retry, ((size_t)cfg->max_roots + 1) * sizeof(uint32_t)) == hipSuccess;
+        ok = ok && hipMalloc(&ctx->queue_fb, sizeof(uint32_t)) == hipSuccess;
+        ok = ok && hipMalloc(&ctx->fb_hot, FR * FS * sizeof(dk::NodeHot32)) == hipSuccess;
+        ok = ok && hipMalloc(&ctx->fb_cold, FR * FS * sizeof(dk::NodeCold)) == hipSuccess;
+        ok = ok && hipMalloc(&ctx->fb_ovf, FR * dk::MAX_DEPTH * sizeof(uint32_t)) == hipSuccess;
+        ok = ok && hipMalloc(&ctx->fb_ovf_st, FR * dk::MAX_DEPTH * sizeof(uint64_t)) == hipSuccess;
+        ok = ok && hipMalloc(&ctx->fb_states, FR * T * STATE_SLOT_BYTES) == hipSuccess;
+        ctx->fb_bytes = FR * FS * (sizeof(dk::NodeHot32) + sizeof(dk::NodeCold)) + FR * T * STATE_SLOT_BYTES;
+    }
     ok = ok && hipMalloc(&ctx->order, ((size_t)cfg->max_roots + 1) * sizeof(uint32_t)) == hipSuccess;
     ok = ok && hipEventCreate(&ctx->ev0) == hipSuccess && hipEventCreate(&ctx->ev1) == hipSuccess;
 #ifdef DK_PHASE_PROF
@@ -879,7 +967,7 @@ dk_ctx* dk_create(const dk_config* cfg) {
         ok = hipMemcpy(ctx->ln_table, ln.data(), ln.size() * sizeof(double), hipMemcpyHostToDevice) == hipSuccess;
         ok = ok && hipMemset(ctx->err, 0, sizeof(int)) == hipSuccess;
     }
-    ctx->pool_bytes = R * S * (sizeof(dk::NodeHot32) + sizeof(dk::NodeCold)) + R * T * STATE_SLOT_BYTES;
+    ctx->pool_bytes = R * S * (sizeof(dk::NodeHot32) + sizeof(dk::NodeCold)) + R * T * STATE_SLOT_BYTES + ctx->fb_bytes;
     if (!ok) { dk_destroy(ctx); return nullptr; }
     return ctx;
 }
@@ -897,6 +985,9 @@ void dk_destroy(dk_ctx* ctx) {
     if (ctx->ln_table) (void)hipFree(ctx->ln_table);
     if (ctx->err) (void)hipFree(ctx->err);
     if (ctx->queue) (void)hipFree(ctx->queue);
+    for (void* p : {(void*)ctx->high_water, (void*)ctx->retry, (void*)ctx->queue_fb, ctx->fb_hot, (void*)ctx->fb_cold,
+                    (void*)ctx->fb_ovf, (void*)ctx->fb_ovf_st, ctx->fb_states})
+        if (p) (void)hipFree(p);
     if (ctx->order) (void)hipFree(ctx->order);
     if (ctx->prof) (void)hipFree(ctx->prof);
     if (ctx->az_nodes) (void)hipFree(ctx->az_nodes);
@@ -922,6 +1013,17 @@ int dk_phase_profile(dk_ctx* ctx, uint64_t* out, uint32_t n) {
 }
 #endif
 uint64_t dk_pool_bytes(const dk_ctx* ctx) { return ctx ? ctx->pool_bytes : 0; }
+
+int dk_pool_high_water(dk_ctx* ctx, void* stream, uint32_t* slots, uint32_t* capacity, uint32_t* overflowed) {
+    if (!ctx || !slots || !capacity || !overflowed) return DK_E_INVALID;
+    uint32_t h[4];
+    DK_HIP(hipStreamSynchronize(pick(ctx, stream)));
+    DK_HIP(hipMemcpy(h, ctx->high_water, sizeof(h), hipMemcpyDeviceToHost));
+    *slots = h[0] > h[2] ? h[0] : h[2];
+    *capacity = ctx->cap_slots;
+    *overflowed = h[1];
+    return DK_OK;
+}
 
 int dk_sync(dk_ctx* ctx, void* stream) {
     if (!ctx) return DK_E_INVALID;

@@ -269,8 +269,25 @@ DK_HD uint32_t pick_child_reg(const Block& b, uint32_t n, double lnN, double c, 
     return pick;
 }
 
+// Exact comparison of two means w_a/v_a < w_b/v_b (v > 0) by cross products in 24-bit
+// multiplies (v_mul_i32_i24, full rate): exact while |w| < 2^23, v < 2^23 and |w| v < 2^31.
+// A simulation's reward is a player_points value, |r| <= 123 for every engine (DKV scoring:
+// 25 basic + 10 extra points, x3 for a solo, stats/**), so |w| <= 123 v and v <= iterations;
+// the launch takes 16-B records only for iterations <= P24_MAX_ITERS (doko_amd.hip).
+static constexpr uint32_t P24_MAX_ITERS = 4095;
+static_assert((uint64_t)P24_MAX_ITERS * P24_MAX_ITERS * 123u < (1ull << 31), "cross products exceed 31 bits");
+static_assert((uint64_t)P24_MAX_ITERS * 123u < (1ull << 23), "win scores exceed 24-bit operands");
+DK_HD int mul24(int a, int b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __mul24(a, b);
+#else
+    return a * b;
+#endif
+}
+DK_HD bool mean_lt(int32_t wa, uint32_t va, int32_t wb, uint32_t vb) { return mul24(wa, (int)vb) < mul24(wb, (int)va); }
+
 // The pick for 16-B hot records (no stored mean): the sibling min / max are found
-// EXACTLY by comparing the means w/v as 64-bit cross products w_a v_b < w_b v_a
+// EXACTLY by comparing the means w/v as cross products w_a v_b < w_b v_a (mean_lt)
 // (division-free; rounding to f64 is monotone, so the winner's f64 mean is the
 // reference's f64 min / max), and only min, max and the candidates' means are
 // divided in f64.  The f32 estimate of every child's normalised mean is
@@ -290,11 +307,12 @@ DK_HD uint32_t pick_child_reg(const Block& b, uint32_t n, double lnN, double c, 
     }
     int32_t wmin = w[0], wmax = w[0];
     uint32_t vmin = v[0], vmax = v[0];
+    // (a branch per child, not a select: a wave whose blocks are all narrower than j skips it)
 #pragma unroll
     for (int j = 1; j < SCAN_REG; ++j) {
         if ((uint32_t)j < n) {
-            const bool lt = (int64_t)w[j] * (int64_t)vmin < (int64_t)wmin * (int64_t)v[j];
-            const bool gt = (int64_t)w[j] * (int64_t)vmax > (int64_t)wmax * (int64_t)v[j];
+            const bool lt = mean_lt(w[j], v[j], wmin, vmin);
+            const bool gt = mean_lt(wmax, vmax, w[j], v[j]);
             wmin = lt ? w[j] : wmin; vmin = lt ? v[j] : vmin;
             wmax = gt ? w[j] : wmax; vmax = gt ? v[j] : vmax;
         }
@@ -365,7 +383,8 @@ DK_HD uint32_t pick_child_reg(const Block& b, uint32_t n, double lnN, double c, 
 
 template <class E, class Mem>
 DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, double c,
-                      Mem& mem, uint32_t* visits39, double* values39, uint8_t* best_out, uint64_t* ctr_scanned) {
+                      Mem& mem, uint32_t* visits39, double* values39, uint8_t* best_out, uint64_t* ctr_scanned,
+                      uint32_t* used = nullptr) {
     using Work = typename E::Work;
     using NodeHot = typename Mem::Hot;
     // the root's structure (child_base, info) lives in registers: it changes only
@@ -560,6 +579,7 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
         DK_PROF(mem, 3, t4 - t3);
     }
     if (ctr_scanned) *ctr_scanned = scanned;
+    if (used) { used[0] = next_slot; used[1] = next_state; }   // pool high-water of this root
     DK_PROF_FLUSH(mem);
 
     // ---------------- result: root children in expansion order

@@ -51,8 +51,10 @@ int main(int argc, char** argv) {
         dk::NodeHot rec[dk::SCAN_REG];
         memset(rec, 0, sizeof(rec));
         const uint32_t n = 2 + (uint32_t)(r() % 11);
-        const int mode = (int)(r() % 7);
-        const uint32_t vmax = mode == 5 ? 100000u : 1000u;
+        const int mode = (int)(r() % 8);
+        // 16-B builds compare means by 24-bit cross products, exact for v <= P24_MAX_ITERS
+        // and |mean| <= 123 (search_core.h); mode 5 probes large visit counts within that
+        const uint32_t vmax = mode == 5 ? (DK_HOT16 ? dk::P24_MAX_ITERS : 100000u) : 1000u;
         uint32_t total = 0;
         // mode 6: Farey neighbours a/b and c/d (|ad - bc| = 1, b, d in [500, 1000]) around a
         // common integer part k differ by 1/(bd) ~ 1e-6, ~3e-8 relative at |mean| ~ 40:
@@ -77,6 +79,10 @@ int main(int argc, char** argv) {
                 const bool first = (j % 2) == 0;
                 v = (uint32_t)(first ? fb : fd);
                 s = (int32_t)(first ? fa + fk * fb : fc + fk * fd);
+            }
+            else if (mode == 7) {   // the bound itself: |w| up to 123 v at v up to P24_MAX_ITERS
+                v = dk::P24_MAX_ITERS - (uint32_t)(r() % 64);
+                s = (int32_t)(r() % (2 * 123 * v + 1)) - (int32_t)(123 * v);
             }
             else s = (int32_t)(r() % (2 * 20 * v + 1)) - (int32_t)(20 * v);
             rec[j].stats = (uint64_t)v | ((uint64_t)(uint32_t)s << 32);

@@ -224,6 +224,62 @@ def test_search_parity_fdo_launch_variants(env, monkeypatch):
         e.close()
 
 
+@pytest.mark.parametrize("cap,env", [(120, {}), (600, {}), (600, {"DK_HOT_RECORD": "16"}),
+                                     (300, {"DK_POOL_ROOTS": "1", "DK_ROOTS_PER_WAVE": "4"}),
+                                     (500, {"DK_POOL_ROOTS": "16", "DK_ROOTS_PER_WAVE": "5", "DK_GROUP_ORDER": "1"})])
+def test_search_capacity_fallback(cap, env, monkeypatch):
+    """Main pools smaller than a search needs: roots that run out of child slots are
+    searched again by the fallback launch (proven-capacity pool) and the results are the
+    oracle's.  120 (256 after rounding) slots overflow most roots (400 iterations take
+    ~2.4 slots each), 600 (768) a part of them; with DK_POOL_ROOTS=1 the fallback pool has one 4-root region, so one wave
+    streams all retried roots through it.  dk_pool_high_water counts the overflowed roots
+    and reports the demand of the largest search, which then exceeds the capacity."""
+    import master_doko_reinforcement_learning_amd as dk
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    e = dk.Engine(device=0, max_roots=64, max_iterations=400, slot_capacity=cap)
+    try:
+        pool = [s for s in fdo_states(12, 29) if s.info()["phase"] != 3]
+        rng = np.random.default_rng(cap)
+        pick = [pool[i] for i in rng.choice(len(pool), size=24, replace=False)]
+        seeds = rng.integers(0, 2**63, size=len(pick), dtype=np.uint64)
+        visits, values, best = dk.CachedMCTS(e, dk.GAME_FULL_DOKO).monte_carlo_tree_search(pack_all(pick), 2.5, 400, seeds)
+        hw, got_cap, overflowed = e.pool_high_water()
+        assert got_cap == (cap + 255) // 256 * 256          # region stride rounded to 256 slots
+        assert overflowed > 0 and hw > cap      # an overflowed root needed more than the main pools hold
+        for i, (b, v, val) in enumerate(_oracle_search(pick, seeds, 400, 2.5, "fdo")):
+            assert list(visits[i]) == v, i
+            assert values[i].tobytes() == np.array(val, dtype=np.float64).tobytes(), i
+            assert int(best[i]) == (b if b >= 0 else 255), i
+    finally:
+        e.close()
+
+
+def test_search_capacity_fallback_doko(monkeypatch):
+    """The same fallback for rs-doko roots (longest-first queue order by default)."""
+    import master_doko_reinforcement_learning_amd as dk
+    monkeypatch.setenv("DK_POOL_ROOTS", "16")
+    monkeypatch.setenv("DK_ROOTS_PER_WAVE", "5")
+    e = dk.Engine(device=0, max_roots=64, max_iterations=500, slot_capacity=500)
+    try:
+        states = []
+        for g in range(32):
+            s = ol.DoState.new_game(0xD0C10000 + g)
+            for _ in range(4):
+                s.play(24)
+            s.random_plies(ol.rng_seed(g), g % 30)
+            states.append(s)
+        seeds = np.arange(32, dtype=np.uint64) * 7 + 3
+        visits, values, best = dk.CachedMCTS(e, dk.GAME_DOKO).monte_carlo_tree_search(pack_all(states), 2.5, 500, seeds)
+        assert e.pool_high_water()[2] > 0
+    finally:
+        e.close()
+    for i, (b, v, val) in enumerate(_oracle_search(states, seeds, 500, 2.5, "do")):
+        assert list(visits[i]) == v
+        assert values[i].tobytes() == np.array(val, dtype=np.float64).tobytes()
+        assert int(best[i]) == b
+
+
 @pytest.mark.parametrize("layout", [None, "16", "ordered"])
 def test_search_parity_doko(eng, layout, monkeypatch):
     """rs-doko search parity; "16" forces the 16-B records, "ordered" streams 7 groups of 5
@@ -399,6 +455,9 @@ def test_full_size_properties(eng, monkeypatch):
     finally:
         e16.close()
     assert np.array_equal(v1, v3) and np.array_equal(val1.view(np.uint64), val3.view(np.uint64)) and np.array_equal(b1, b3)
+    # the default main-pool capacity (64 + 4 x iterations) holds every one of these searches
+    hw, cap, overflowed = eng.pool_high_water()
+    assert cap == 4096 and 0 < hw <= cap and overflowed == 0, (hw, cap, overflowed)
 
 
 # ---------------------------------------------------------------- rs-doko rule-based sampler
