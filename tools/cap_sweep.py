@@ -27,25 +27,7 @@ def main(caps, infostates=18432, reps=3):
     sp = stream.cuda_stream
     I, S, iters = infostates, 64, 1000
     n = I * S
-    gen = dk.Engine(device=0, max_roots=n, max_iterations=1, slot_capacity=64)
-    c0 = gen.ctx
-    seeds = torch.tensor((np.arange(I, dtype=np.uint64) + np.uint64(0xC3000000)).view(np.int64), device=dev)
-    info = torch.zeros((I, 128), dtype=torch.uint8, device=dev)
-    assert L.dk_new_game_batch_async(c0, 0, seeds.data_ptr(), I, info.data_ptr(), sp) == 0
-    h = torch.full((I,), 1 << 24, dtype=torch.int64, device=dev)
-    for _ in range(4):
-        assert L.dk_env_step_batch_async(c0, info.data_ptr(), h.data_ptr(), I, sp) == 0
-    plies = torch.tensor(np.array([[0, 8, 20, 32][j % 4] for j in range(I)], dtype=np.uint32).view(np.int32), device=dev)
-    rng = torch.tensor(dk.splitmix_rng_states(np.arange(I, dtype=np.uint64) + np.uint64(0xC3100000)).view(np.int64), device=dev)
-    assert L.dk_env_random_plies_batch_async(c0, info.data_ptr(), rng.data_ptr(), plies.data_ptr(), I, sp) == 0
-    j = np.arange(I, dtype=np.uint64)[:, None]
-    s = np.arange(S, dtype=np.uint64)[None, :]
-    d_samp = torch.tensor((np.uint64(0xC3200000) + j * np.uint64(S) + s).reshape(-1).view(np.int64), device=dev)
-    d_srch = torch.tensor((np.uint64(0xC3300000) + j * np.uint64(S) + s).reshape(-1).view(np.int64), device=dev)
-    roots = torch.zeros((n, 128), dtype=torch.uint8, device=dev)
-    assert L.dk_determinize_batch_async(c0, info.data_ptr(), I, S, d_samp.data_ptr(), roots.data_ptr(), sp) == 0
-    assert L.dk_sync(c0, sp) == 0
-    gen.close()
+    roots, d_srch = c3_roots(dk, L, dev, sp, I, S)
     v = torch.zeros((n, 39), dtype=torch.int32, device=dev)
     q = torch.zeros((n, 39), dtype=torch.float64, device=dev)
     bst = torch.zeros(n, dtype=torch.uint8, device=dev)
@@ -69,6 +51,32 @@ def main(caps, infostates=18432, reps=3):
                                                               hw, e_bytes(cap, n, iters)), flush=True)
     for cap in caps:
         print("cap %6d median %.1f ms" % (cap, float(np.median(times[cap]))))
+
+
+def c3_roots(dk, L, dev, sp, I, S=64):
+    """The bench's C3 roots (determinized on the device) and search seeds."""
+    import torch
+    n = I * S
+    gen = dk.Engine(device=0, max_roots=n, max_iterations=1, slot_capacity=64)
+    c0 = gen.ctx
+    seeds = torch.tensor((np.arange(I, dtype=np.uint64) + np.uint64(0xC3000000)).view(np.int64), device=dev)
+    info = torch.zeros((I, 128), dtype=torch.uint8, device=dev)
+    assert L.dk_new_game_batch_async(c0, 0, seeds.data_ptr(), I, info.data_ptr(), sp) == 0
+    h = torch.full((I,), 1 << 24, dtype=torch.int64, device=dev)
+    for _ in range(4):
+        assert L.dk_env_step_batch_async(c0, info.data_ptr(), h.data_ptr(), I, sp) == 0
+    plies = torch.tensor(np.array([[0, 8, 20, 32][j % 4] for j in range(I)], dtype=np.uint32).view(np.int32), device=dev)
+    rng = torch.tensor(dk.splitmix_rng_states(np.arange(I, dtype=np.uint64) + np.uint64(0xC3100000)).view(np.int64), device=dev)
+    assert L.dk_env_random_plies_batch_async(c0, info.data_ptr(), rng.data_ptr(), plies.data_ptr(), I, sp) == 0
+    j = np.arange(I, dtype=np.uint64)[:, None]
+    s = np.arange(S, dtype=np.uint64)[None, :]
+    d_samp = torch.tensor((np.uint64(0xC3200000) + j * np.uint64(S) + s).reshape(-1).view(np.int64), device=dev)
+    d_srch = torch.tensor((np.uint64(0xC3300000) + j * np.uint64(S) + s).reshape(-1).view(np.int64), device=dev)
+    roots = torch.zeros((n, 128), dtype=torch.uint8, device=dev)
+    assert L.dk_determinize_batch_async(c0, info.data_ptr(), I, S, d_samp.data_ptr(), roots.data_ptr(), sp) == 0
+    assert L.dk_sync(c0, sp) == 0
+    gen.close()
+    return roots, d_srch
 
 
 def e_bytes(cap, n, iters):

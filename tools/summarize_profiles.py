@@ -23,8 +23,17 @@ def main(tag="r01", roots=None, iterations=None):
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
     with open(os.path.join(src, "trace", "run_kernel_trace.csv")) as fh:
         rows = [r for r in csv.DictReader(fh) if "search_kernel" in r["Kernel_Name"]]
+    # the dominant launch shape only: (kernel, grid) with the largest total time -- a step's
+    # fallback pass (small grid, drains at once) and the small-batch leg are other shapes
+    tot = {}
+    for r in rows:
+        key = (r["Kernel_Name"], r.get("Grid_Size_X", r.get("Grid_Size")))
+        tot[key] = tot.get(key, 0) + int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    if tot:
+        dom = max(tot, key=tot.get)
+        rows = [r for r in rows if (r["Kernel_Name"], r.get("Grid_Size_X", r.get("Grid_Size"))) == dom]
     with open(os.path.join(dst, "kernel_trace_search.csv"), "w", newline="") as fh:
-        keep = ["Kernel_Name", "Grid_Size", "Workgroup_Size", "LDS_Block_Size", "Scratch_Size", "VGPR_Count",
+        keep = ["Kernel_Name", "Grid_Size_X", "Workgroup_Size", "LDS_Block_Size", "Scratch_Size", "VGPR_Count",
                 "SGPR_Count", "Start_Timestamp", "End_Timestamp"]
         w = csv.DictWriter(fh, fieldnames=keep + ["Duration_ns"])
         w.writeheader()
@@ -57,8 +66,14 @@ def main(tag="r01", roots=None, iterations=None):
                     continue
                 key = (r["Dispatch_Id"], r["Counter_Name"])
                 per[key] = per.get(key, 0.0) + float(r["Counter_Value"])
+        # main launches only (the fallback pass of a step drains at once: tiny counter totals)
+        wt = {}
         for (disp, name), v in per.items():
-            pmc.setdefault(name, []).append(v)
+            wt[disp] = wt.get(disp, 0.0) + v
+        top = max(wt.values()) if wt else 0.0
+        for (disp, name), v in per.items():
+            if wt[disp] >= 0.05 * top:
+                pmc.setdefault(name, []).append(v)
     vals = {k: sum(v) / len(v) for k, v in pmc.items()}
     fetch_kb = vals.get("FETCH_SIZE")
     write_kb = vals.get("WRITE_SIZE")
