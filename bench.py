@@ -294,7 +294,7 @@ def main():
                 "c2": "synthetic: seeded rs-doko deals (SmallRng::seed_from_u64(0xD0C00000+i)), 4x Healthy"}[args.workload]
         stream_peak = stream_copy_gbs(torch, dev)
         hw, cap, overflowed = eng.pool_high_water(sp)
-        pools = {"bytes": eng.pool_bytes(), "slot_capacity": cap, "proven_slot_bound": 40 + 12 * iters,
+        pools = {"bytes": eng.pool_bytes(), "slot_capacity": cap, "proven_slot_bound": 42 + 12 * iters,
                  "slot_high_water": hw, "overflowed_roots": overflowed}
         result = {
             "metric": METRIC,

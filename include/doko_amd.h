@@ -252,7 +252,7 @@ typedef struct dk_ctx dk_ctx;
  * roots = CUs x 12 waves x 64 lanes; env DK_POOL_ROOTS overrides).  The search grid is
  * persistent: a batch larger than the pools streams through them, one wave-sized group of
  * roots at a time, so max_roots bounds the batch, not the memory.
- * Child slots: a search needs at most 40 + 12 x iterations of them (proven bound) but
+ * Child slots: a search needs at most 42 + 12 x iterations of them (proven bound) but
  * measured far fewer, so the main pools hold slot_capacity per root (default
  * 64 + 4 x max_iterations, rounded up to a multiple of 256; env DK_SLOT_CAPACITY overrides).  A root that runs out is
  * searched again, from its seed, by a second launch over a small pool with the proven

@@ -58,7 +58,9 @@ constexpr uint32_t LN_LDS_MAX = 2048;   // ln(N) entries staged in LDS (16 KB)
 // (L1-cacheable, program-ordered within the lane) are sufficient.
 template <class W, bool LN_LDS, class H>
 struct GpuMem {
-    using Hot = H;
+    static constexpr bool P8 = dk::is_p8<H>::value;
+    using Rec = H;                                                  // the stored layout
+    using Hot = typename std::conditional<P8, dk::NodeHot16, H>::type;   // the in-register form
     H* hot;
     dk::NodeCold* cold;
     W* states;
@@ -82,16 +84,47 @@ struct GpuMem {
         if constexpr (LN_LDS) return __longlong_as_double((long long)dk_lds[v]);
         else return ln_glob[v];
     }
-    __device__ H load_hot(uint32_t s) const { return hot[s]; }
-    __device__ void store_hot(uint32_t s, const H& h) const { hot[s] = h; }
-    __device__ void store_stats(uint32_t s, uint64_t v) const { hot[s].stats = v; }
-    __device__ void store_backup(uint32_t s, uint64_t v, double q, float isv) const {
-        dk::hot_backup(hot[s], v, q, isv);
+    __device__ Hot load_hot(uint32_t s) const {
+        if constexpr (P8) {
+            const dk::NodeHot8 r = hot[s];
+            Hot h;
+            h.stats = dk::p8_stats(r.w0); h.child_base = dk::p8_cb(r.w1); h.info = dk::p8_info(r.w1);
+            return h;
+        } else {
+            return hot[s];
+        }
     }
-    __device__ void store_child_base(uint32_t s, uint32_t child_base) const { hot[s].child_base = child_base; }
+    // two 8-B records (the pair starting at slot 2i)
+    __device__ dk::U4 load_pair(uint32_t i) const { return reinterpret_cast<const dk::U4*>(hot)[i]; }
+    __device__ void store_hot(uint32_t s, const Hot& h) const {
+        if constexpr (P8) {
+            dk::NodeHot8 r;
+            r.w0 = dk::p8_w0(h.stats); r.w1 = dk::p8_w1(h.child_base, h.info);
+            hot[s] = r;
+        } else {
+            hot[s] = h;
+        }
+    }
+    __device__ void store_stats(uint32_t s, uint64_t v) const {
+        if constexpr (P8) hot[s].w0 = dk::p8_w0(v);
+        else hot[s].stats = v;
+    }
+    __device__ void store_backup(uint32_t s, uint64_t v, double q, float isv) const {
+        if constexpr (P8) hot[s].w0 = dk::p8_w0(v);
+        else dk::hot_backup(hot[s], v, q, isv);
+    }
+    // the chain head's skip pointer (8-B records rewrite the structure word: `info` is the head's)
+    __device__ void store_child_base(uint32_t s, uint32_t child_base, uint32_t info) const {
+        if constexpr (P8) hot[s].w1 = dk::p8_w1(child_base, info);
+        else hot[s].child_base = child_base;
+    }
     __device__ void store_node_tail(uint32_t s, uint32_t child_base, uint32_t info) const {
-        hot[s].child_base = child_base;
-        hot[s].info = info;
+        if constexpr (P8) {
+            hot[s].w1 = dk::p8_w1(child_base, info);
+        } else {
+            hot[s].child_base = child_base;
+            hot[s].info = info;
+        }
     }
     __device__ dk::NodeCold load_cold(uint32_t s) const { return cold[s]; }
     __device__ void store_cold(uint32_t s, const dk::NodeCold& c) const { cold[s] = c; }
@@ -657,7 +690,7 @@ struct dk_ctx {
     int cu_count = 0;
     uint32_t* queue = nullptr;      // root-group counter of the persistent search grid
     // Slot-capacity fallback: pools are sized from the measured demand (default 64 + 4 x
-    // iterations slots per root, against the proven 40 + 12 x iterations); a root that runs out
+    // iterations slots per root, against the proven 42 + 12 x iterations); a root that runs out
     // is appended to `retry` ([0] = count) and searched again, from its seed, by a second
     // launch over a small pool with the proven capacity (fb_*).  Results do not change.
     uint32_t* retry = nullptr;
@@ -687,7 +720,8 @@ struct dk_ctx {
     uint64_t pool_bytes = 0;
     uint32_t roots_per_wave = 64;   // pool region width; DK_ROOTS_PER_WAVE fixes the launch width too
     bool rpw_fixed = false;
-    int hot_layout = 0;             // DK_HOT_RECORD=16|32 fixes the hot-record layout; 0 = per launch
+    int hot_layout = 0;             // DK_HOT_RECORD=8|16|32 fixes the hot-record layout; 0 = per launch
+    bool p8_ok = false;             // the pools' slot capacities fit the 8-B records' child_base field
     bool ln_in_lds = false;         // DK_LN_LDS=1: ln(N) table copied into every workgroup's LDS (8 KB at
                                     // 1000 iterations); by default it is read through the L1/L2 caches
     int lds_path = 16;              // path entries kept in LDS (deeper ones spill to global): at most
@@ -839,7 +873,12 @@ hipError_t launch_search(dk_ctx* ctx, const dk_state* roots, const uint64_t* see
     const uint32_t simds = 4u * (uint32_t)ctx->cu_count;
     // (16-B records compare means by 24-bit cross products: exact up to P24_MAX_ITERS iterations)
     const bool h16 = iters <= dk::P24_MAX_ITERS &&
-                     (ctx->hot_layout ? ctx->hot_layout == 16 : grid_for(n, rpw) >= 2u * simds);
+                     (ctx->hot_layout ? ctx->hot_layout <= 16 : grid_for(n, rpw) >= 2u * simds);
+    // 8-B records where their fields hold the search (visits, state index, slots: P8_MAX_ITERS)
+    const bool h8 = h16 && iters <= dk::P8_MAX_ITERS && ctx->hot_layout != 16 && ctx->p8_ok;
+    if (h8)
+        return ln ? launch_search_t<E, true, dk::NodeHot8>(ctx, roots, seeds, n, iters, c, visits, values, best, st, ln_bytes, rpw)
+                  : launch_search_t<E, false, dk::NodeHot8>(ctx, roots, seeds, n, iters, c, visits, values, best, st, ln_bytes, rpw);
     if (h16)
         return ln ? launch_search_t<E, true, dk::NodeHot16>(ctx, roots, seeds, n, iters, c, visits, values, best, st, ln_bytes, rpw)
                   : launch_search_t<E, false, dk::NodeHot16>(ctx, roots, seeds, n, iters, c, visits, values, best, st, ln_bytes, rpw);
@@ -892,7 +931,8 @@ dk_ctx* dk_create(const dk_config* cfg) {
     // to a multiple of 256 slots (4 KB of 16-B records): strides 512 B off a multiple of
     // 64 KB (4,064 or 4,128 slots) ran the C3 search 1.6x slower than 4,096 or 12,040
     // (tools/cap_sweep.py; the lanes' accesses fall into the same memory channels).
-    const uint32_t proven = 40u + 12u * cfg->max_iterations;
+    // (+2 for the 8-B records' even-aligned blocks: search_core.h P8_SLOT_BOUND)
+    const uint32_t proven = dk::P8_SLOT_BOUND(cfg->max_iterations);
     uint32_t cap = cfg->slot_capacity ? cfg->slot_capacity : 64u + 4u * cfg->max_iterations;
     if (const char* e = getenv("DK_SLOT_CAPACITY")) {
         const long v = atol(e);
@@ -909,7 +949,7 @@ dk_ctx* dk_create(const dk_config* cfg) {
     if (const char* e = getenv("DK_GROUP_ORDER")) ctx->group_order = atoi(e) != 0 ? 1 : 0;
     if (const char* e = getenv("DK_HOT_RECORD")) {
         const int v = atoi(e);
-        if (v == 16 || v == 32) ctx->hot_layout = v;
+        if (v == 8 || v == 16 || v == 32) ctx->hot_layout = v;
     }
     if (const char* e = getenv("DK_VERBOSE")) ctx->verbose = atoi(e) != 0;
     if (const char* e = getenv("DK_LN_LDS")) ctx->ln_in_lds = atoi(e) != 0;
@@ -967,6 +1007,8 @@ dk_ctx* dk_create(const dk_config* cfg) {
         ok = hipMemcpy(ctx->ln_table, ln.data(), ln.size() * sizeof(double), hipMemcpyHostToDevice) == hipSuccess;
         ok = ok && hipMemset(ctx->err, 0, sizeof(int)) == hipSuccess;
     }
+    ctx->p8_ok = ctx->cap_slots <= (1u << 14) && (ctx->fb_slots == 0 || ctx->fb_slots <= (1u << 14)) &&
+                 ctx->cap_slots % 2 == 0 && ctx->fb_slots % 2 == 0;
     ctx->pool_bytes = R * S * (sizeof(dk::NodeHot32) + sizeof(dk::NodeCold)) + R * T * STATE_SLOT_BYTES + ctx->fb_bytes;
     if (!ok) { dk_destroy(ctx); return nullptr; }
     return ctx;

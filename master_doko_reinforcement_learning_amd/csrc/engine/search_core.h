@@ -84,6 +84,37 @@ struct alignas(32) NodeHot32 {
     static constexpr bool CACHED_MEAN = true;
     static constexpr int MIN_WAVES = 1;   // no budget (its launches have one wave per SIMD)
 };
+// 8-B records (launches of <= P8_MAX_ITERS iterations): everything packed into two words
+//   w0 = win_score << 11 | visits                         (the stats: the backup stores w0 only)
+//   w1 = child_base/2 : 13 | nchild : 4 | player : 2 | open : 1 | head : 1 | state : 11
+// Child blocks start at even slots, so one 16-B load fetches two children and a block of
+// twelve is 96 B.  The root's record is never stored (nchild <= 39 does not fit 4 bits):
+// the root lives in registers, its stats are the iteration count.  In registers a node is
+// carried in the 16-B logical form (NodeHot16 fields); GpuMem / HostMem decode on load.
+struct alignas(16) U4 { uint32_t x, y, z, w; };   // one 16-B load: two 8-B records
+struct alignas(8) NodeHot8 {
+    uint32_t w0, w1;
+    static constexpr bool CACHED_MEAN = false;
+    static constexpr int MIN_WAVES = DK_HOT16_WAVES;
+};
+static constexpr uint32_t P8_MAX_ITERS = 1200;   // visits / state index < 2^11, slots < 2^14
+// proven slot bound with even-aligned blocks: the root and its padding slot, the root block
+// (<= 39 children, padded to 40) and one block of <= 12 children per iteration
+static constexpr uint32_t P8_SLOT_BOUND(uint32_t iters) { return 42u + 12u * iters; }
+static_assert(P8_SLOT_BOUND(P8_MAX_ITERS) <= (1u << 14), "8-B child_base field");
+DK_HD uint32_t p8_w0(uint64_t stats) { return ((uint32_t)(stats >> 32) << 11) | ((uint32_t)stats & 2047u); }
+DK_HD uint32_t p8_w1(uint32_t child_base, uint32_t info) {
+    return (child_base >> 1) | (info & 15u) << 13 | ((info >> 6) & 15u) << 17 | (info >> 10) << 21;
+}
+DK_HD uint32_t p8_visits(uint32_t w0) { return w0 & 2047u; }
+DK_HD int32_t p8_win(uint32_t w0) { return (int32_t)w0 >> 11; }
+DK_HD uint64_t p8_stats(uint32_t w0) { return (uint64_t)(uint32_t)p8_win(w0) << 32 | p8_visits(w0); }
+DK_HD uint32_t p8_cb(uint32_t w1) { return (w1 & 0x1FFFu) << 1; }
+DK_HD uint32_t p8_info(uint32_t w1) { return ((w1 >> 13) & 15u) | ((w1 >> 17) & 15u) << 6 | (w1 >> 21) << 10; }
+DK_HD bool p8_forced(uint32_t w1) { return (w1 & (15u << 13 | 1u << 19)) == 1u << 13; }   // nchild == 1 && !open
+template <class H> struct is_p8 { static constexpr bool value = false; };
+template <> struct is_p8<NodeHot8> { static constexpr bool value = true; };
+
 // the layout of host builds (test harnesses); -DDK_HOT16=0 selects the 32-B one
 #ifndef DK_HOT16
 #define DK_HOT16 1
@@ -381,12 +412,103 @@ DK_HD uint32_t pick_child_reg(const Block& b, uint32_t n, double lnN, double c, 
     return pick;
 }
 
+// The 16-B pick (above) on a block of 8-B records held as raw words: visits and win_score
+// are extracted per child, structure fields only for the candidates and the picked child.
+struct Block8 {
+    uint32_t w0[SCAN_REG], w1[SCAN_REG];
+};
+template <class Mem>
+DK_HD uint32_t pick_child_p8(const Block8& b, uint32_t n, double lnN, double c, Mem& mem, uint64_t* p_st, uint32_t* p_cb,
+                             uint32_t* p_inf, NodeHot16* end, bool* end_ok) {
+    int32_t w[SCAN_REG];
+    uint32_t v[SCAN_REG], vis[SCAN_REG];
+#pragma unroll
+    for (int j = 0; j < SCAN_REG; ++j) {
+        vis[j] = p8_visits(b.w0[j]);
+        w[j] = vis[j] ? p8_win(b.w0[j]) : 0;
+        v[j] = vis[j] ? vis[j] : 1u;   // an unvisited child's mean is 0 = 0/1
+    }
+    int32_t wmin = w[0], wmax = w[0];
+    uint32_t vmin = v[0], vmax = v[0];
+#pragma unroll
+    for (int j = 1; j < SCAN_REG; ++j) {
+        if ((uint32_t)j < n) {
+            const bool lt = mean_lt(w[j], v[j], wmin, vmin);
+            const bool gt = mean_lt(wmax, vmax, w[j], v[j]);
+            wmin = lt ? w[j] : wmin; vmin = lt ? v[j] : vmin;
+            wmax = gt ? w[j] : wmax; vmax = gt ? v[j] : vmax;
+        }
+    }
+    const double min_q = (double)wmin / (double)vmin, max_q = (double)wmax / (double)vmax;
+    const double range = max_q - min_q;
+    const bool flat = fabs(range) < DK_F64_EPSILON;
+    const float inv_r = flat ? 0.0f : 2.0f * rcp_approx((float)range);
+    const float minf = (float)min_q;
+    const float qabs = fmaxf(fabsf(minf), fabsf((float)max_q));
+    const float ex = (float)c * sqrt_approx((float)lnN);
+    float ue[SCAN_REG];
+    float umax = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < SCAN_REG; ++j) {
+        const float qf = (float)w[j] * rcp_approx((float)v[j]);
+        const float nq = flat ? 1.0f : (qf - minf) * inv_r - 1.0f;
+        const float u = vis[j] == 0 ? INFINITY : nq + ex * rsqrt_approx((float)vis[j]);
+        ue[j] = (uint32_t)j < n ? u : -INFINITY;
+        umax = ue[j] > umax ? ue[j] : umax;
+    }
+    const float cut = umax - (3e-6f * (3.0f + fabsf(ex)) + 4e-6f * qabs * inv_r);
+    uint32_t a1 = b.w0[0], a2 = b.w0[0], m1 = b.w1[0], m2 = b.w1[0];
+    uint32_t j1 = 0, j2 = 0, nc = 0;
+#pragma unroll
+    for (int j = 0; j < SCAN_REG; ++j) {
+        const bool cj = ue[j] >= cut;   // implies j < n
+        const bool first = cj && nc == 0, second = cj && nc == 1;
+        a1 = first ? b.w0[j] : a1; m1 = first ? b.w1[j] : m1; j1 = first ? (uint32_t)j : j1;
+        a2 = second ? b.w0[j] : a2; m2 = second ? b.w1[j] : m2; j2 = second ? (uint32_t)j : j2;
+        nc += cj ? 1u : 0u;
+    }
+    const bool f1 = p8_forced(m1);
+    const bool f2 = nc >= 2 && p8_forced(m2);
+    NodeHot16 e1, e2;
+    if (f1) e1 = mem.load_hot(p8_cb(m1));
+    if (f2) e2 = mem.load_hot(p8_cb(m2));
+    uint32_t pick = j1;
+    if (nc == 2) {
+        const uint64_t s1 = p8_stats(a1), s2 = p8_stats(a2);
+        const double u1 = uct_exact(s1, mean_of(s1), flat, min_q, max_q, lnN, c);
+        const double u2 = uct_exact(s2, mean_of(s2), flat, min_q, max_q, lnN, c);
+        if (u2 > u1) pick = j2;
+    } else if (nc > 2) {
+        double best = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < SCAN_REG; ++j) {
+            if (ue[j] >= cut) {
+                const uint64_t sj = p8_stats(b.w0[j]);
+                const double u = uct_exact(sj, mean_of(sj), flat, min_q, max_q, lnN, c);
+                if (u > best) { best = u; pick = (uint32_t)j; }
+            }
+        }
+    }
+    uint32_t pa = b.w0[0], pm = b.w1[0];
+#pragma unroll
+    for (int j = 1; j < SCAN_REG; ++j) {
+        pa = (uint32_t)j == pick ? b.w0[j] : pa;
+        pm = (uint32_t)j == pick ? b.w1[j] : pm;
+    }
+    *p_st = p8_stats(pa); *p_cb = p8_cb(pm); *p_inf = p8_info(pm);
+    *end_ok = (pick == j1 && f1) || (nc >= 2 && pick == j2 && f2);
+    if (pick == j1 && f1) *end = e1;
+    else if (nc >= 2 && pick == j2 && f2) *end = e2;
+    return pick;
+}
+
 template <class E, class Mem>
 DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, double c,
                       Mem& mem, uint32_t* visits39, double* values39, uint8_t* best_out, uint64_t* ctr_scanned,
                       uint32_t* used = nullptr) {
     using Work = typename E::Work;
-    using NodeHot = typename Mem::Hot;
+    using NodeHot = typename Mem::Hot;   // the in-register form of a node (8-B records: NodeHot16)
+    constexpr bool P8 = is_p8<typename Mem::Rec>::value;
     // the root's structure (child_base, info) lives in registers: it changes only
     // when the root itself is expanded, and its visits are the iteration count
     uint32_t root_cb = 0, root_info;
@@ -396,11 +518,12 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
         root_info = h.info;
         NodeCold cd;
         cd.unexpanded = ra; cd.parent = 0xFFFFFFFFu; cd.action = 0xFFu;
-        mem.store_hot(0, h);
+        if constexpr (!P8) mem.store_hot(0, h);   // 8-B records: the root is never stored
         mem.store_cold(0, cd);
         mem.store_state(0, root);
     }
-    uint32_t next_slot = 1, next_state = 1;
+    // 8-B records: child blocks start at even slots (slot 1 is padding)
+    uint32_t next_slot = P8 ? 2 : 1, next_state = 1;
     int status = SR_OK;
     uint64_t scanned = 0;
     DK_PROF_DECL;
@@ -414,6 +537,7 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
         uint32_t x_visits = it;   // root visits == completed iterations
         int depth = 0;
         uint32_t chain_head = 0xFFFFFFFFu;   // head whose skip pointer led to x
+        uint32_t chain_info = 0;             // its info (8-B records rewrite both fields)
         mem.path_set(0, 0u, x.stats);
         // One trip per BRANCHING level: a lane first hops through single-child nodes
         // (a chain head jumps to its chain end), then picks among its children.  A wave
@@ -422,6 +546,7 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
         for (;;) {
             while (ni_nchild(x.info) == 1 && !ni_open(x.info)) {
                 chain_head = ni_head(x.info) ? slot : 0xFFFFFFFFu;
+                chain_info = x.info;
                 const NodeHot y = mem.load_hot(x.child_base);
                 scanned += 1;
                 DK_PROF(mem, 5, 1);
@@ -438,23 +563,44 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
             NodeHot y, end;
             bool end_ok = false;
             if (n <= (uint32_t)SCAN_REG) {
-                DK_STAMP_DRAINED(tl0);
-                const double lnN = mem.ln(x_visits);
-                Block blk;
+                if constexpr (P8) {
+                    // blocks start at even slots: one 16-B load per pair of children
+                    DK_STAMP_DRAINED(tl0);
+                    const double lnN = mem.ln(x_visits);
+                    Block8 blk;
 #pragma unroll
-                for (int j = 0; j < SCAN_REG; ++j) {
-                    if ((uint32_t)j < n) {
-                        const NodeHot h = mem.load_hot(x.child_base + (uint32_t)j);
-                        blk.st[j] = h.stats; blk.cb[j] = h.child_base; blk.inf[j] = h.info; blk.q[j] = hot_q(h); blk.isv[j] = hot_isv(h);
-                    } else {
-                        blk.st[j] = 0; blk.cb[j] = 0; blk.inf[j] = 0; blk.q[j] = 0.0; blk.isv[j] = 0.0f;
+                    for (int j = 0; j < SCAN_REG / 2; ++j) {
+                        if ((uint32_t)(2 * j) < n) {
+                            const U4 q = mem.load_pair((x.child_base >> 1) + (uint32_t)j);
+                            blk.w0[2 * j] = q.x; blk.w1[2 * j] = q.y; blk.w0[2 * j + 1] = q.z; blk.w1[2 * j + 1] = q.w;
+                        } else {
+                            blk.w0[2 * j] = 0; blk.w1[2 * j] = 0; blk.w0[2 * j + 1] = 0; blk.w1[2 * j + 1] = 0;
+                        }
                     }
+                    DK_STAMP_DRAINED(tl1);
+                    DK_PROF(mem, 8, tl1 - tl0);
+                    pick = pick_child_p8(blk, n, lnN, c, mem, &y.stats, &y.child_base, &y.info, &end, &end_ok);
+                    DK_STAMP_DRAINED(tl2);
+                    DK_PROF(mem, 9, tl2 - tl1);
+                } else {
+                    DK_STAMP_DRAINED(tl0);
+                    const double lnN = mem.ln(x_visits);
+                    Block blk;
+#pragma unroll
+                    for (int j = 0; j < SCAN_REG; ++j) {
+                        if ((uint32_t)j < n) {
+                            const NodeHot h = mem.load_hot(x.child_base + (uint32_t)j);
+                            blk.st[j] = h.stats; blk.cb[j] = h.child_base; blk.inf[j] = h.info; blk.q[j] = hot_q(h); blk.isv[j] = hot_isv(h);
+                        } else {
+                            blk.st[j] = 0; blk.cb[j] = 0; blk.inf[j] = 0; blk.q[j] = 0.0; blk.isv[j] = 0.0f;
+                        }
+                    }
+                    DK_STAMP_DRAINED(tl1);
+                    DK_PROF(mem, 8, tl1 - tl0);
+                    pick = pick_child_reg(blk, n, lnN, c, mem, &y.stats, &y.child_base, &y.info, &end, &end_ok);
+                    DK_STAMP_DRAINED(tl2);
+                    DK_PROF(mem, 9, tl2 - tl1);
                 }
-                DK_STAMP_DRAINED(tl1);
-                DK_PROF(mem, 8, tl1 - tl0);
-                pick = pick_child_reg(blk, n, lnN, c, mem, &y.stats, &y.child_base, &y.info, &end, &end_ok);
-                DK_STAMP_DRAINED(tl2);
-                DK_PROF(mem, 9, tl2 - tl1);
             } else {
                 // generic block (never produced by the doko engines, whose nodes offer <= 12 actions)
                 const double lnN = mem.ln(x_visits);
@@ -487,6 +633,7 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
             if (end_ok) {
                 // the picked child is a forced chain head: its prefetched chain end
                 chain_head = ni_head(x.info) ? slot : 0xFFFFFFFFu;
+                chain_info = x.info;
                 scanned += 1;
                 DK_PROF(mem, 5, 1);
                 depth += 1;
@@ -518,17 +665,17 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
                     break;
                 }
                 x.child_base = next_slot;
-                next_slot += block;
+                next_slot += P8 ? (block + 1u) & ~1u : block;
             }
             cd.unexpanded &= ~bit;
             const uint32_t child = x.child_base + nch;
             nch += 1;
             const uint32_t new_info = ni_make(nch, ni_player(x.info), cd.unexpanded != 0, ni_head(x.info), ni_state(x.info));
-            mem.store_node_tail(slot, x.child_base, new_info);
             if (slot == 0) { root_cb = x.child_base; root_info = new_info; }
+            if (!P8 || slot != 0) mem.store_node_tail(slot, x.child_base, new_info);
             mem.store_unexpanded(slot, cd.unexpanded);
             // a forced chain grew: its head now points at the new end
-            if (block == 1 && chain_head != 0xFFFFFFFFu) mem.store_child_base(chain_head, child);
+            if (block == 1 && chain_head != 0xFFFFFFFFu) mem.store_child_base(chain_head, child, chain_info);
             DK_STAMP_DRAINED(te0);
             E::step(w, a);
             DK_STAMP_DRAINED(te1);
@@ -573,7 +720,7 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
             const uint64_t ns = st + (((uint64_t)(uint32_t)sel4i(r, (int)(e >> 30)) << 32) | 1ULL);
             mem.store_backup(e & 0x3FFFFFFFu, ns, mean_of(ns), rsqrt_approx((float)(uint32_t)ns));
         }
-        mem.store_stats(0, (uint64_t)(it + 1));
+        if constexpr (!P8) mem.store_stats(0, (uint64_t)(it + 1));
         if (it + 1 == iters) (void)rng.next_u64();  // random_bool((1f32/1000f32) as f64)
         DK_STAMP(t4);
         DK_PROF(mem, 3, t4 - t3);
@@ -584,11 +731,10 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
 
     // ---------------- result: root children in expansion order
     for (int a = 0; a < 39; ++a) { visits39[a] = 0; values39[a] = 0.0; }
-    const NodeHot r0 = mem.load_hot(0);
     int best = -1; uint32_t bv = 0;
-    for (uint32_t j = 0; j < ni_nchild(r0.info); ++j) {
-        const uint64_t st = mem.load_hot(r0.child_base + j).stats;
-        const uint32_t act = mem.load_cold(r0.child_base + j).action;
+    for (uint32_t j = 0; j < ni_nchild(root_info); ++j) {
+        const uint64_t st = mem.load_hot(root_cb + j).stats;
+        const uint32_t act = mem.load_cold(root_cb + j).action;
         const uint32_t v = (uint32_t)st;
         visits39[act] = v;
         values39[act] = (double)(int32_t)(st >> 32) / (double)v;

@@ -61,6 +61,13 @@ def test_hot32_variant_exact(native_bins):
     assert _run("search_check32", 6, 400, 5) > 10
 
 
+def test_hot8_variant_exact(native_bins):
+    """The 8-B packed hot records (DK_HOT8: even-aligned child blocks, pair loads, the root
+    in registers) give the oracle's searches exactly."""
+    assert _run("search_check8", 8, 400, 9) > 10
+    assert _run("search_check8", 4, 1000, 11, 2) > 4
+
+
 def test_engine_cap_vs_oracle(native_bins):
     """cap_engine.h (host build) = oracle card_matching_full; samples always consistent."""
     assert _run("cap_check", 120, 3) > 5000

@@ -1,7 +1,7 @@
 """Parity of the configuration bench.py actually measures.
 
 The bench's launch differs from the small parity tests' launches: with >= 2 groups
-per resident wave the search kernel takes the 16-B hot records, the LDS path length
+per resident wave the search kernel takes the 8-B hot records, the LDS path length
 the occupancy calculator picks (14 entries at 64 roots per wave), a persistent grid
 whose waves each stream several 64-root groups through one reused pool region, and
 for rs-doko the longest-first group queue (group_order_kernel).  These tests build the
@@ -96,7 +96,7 @@ def test_c3_bench_launch_parity(monkeypatch, capfd):
     I, S = 6144, 64
     args, n_roots, out = _bench_workload(["--infostates", str(I), "--iterations", str(ITERS)], monkeypatch)
     ln = _launch_line(capfd)
-    assert ln["hot"] == "16B", ln
+    assert ln["hot"] == "8B", ln
     grid, rpw = int(ln["grid"]), int(ln["rpw"])
     assert rpw == 64 and n_roots == I * S
     assert n_roots // rpw >= 2 * grid, ln           # waves stream >= 2 groups through their pool region
@@ -132,13 +132,13 @@ def test_c3_bench_launch_parity(monkeypatch, capfd):
 
 
 def test_c2d_bench_launch_parity(monkeypatch, capfd):
-    """Determinized rs-doko (c2d) at 6144 infostates x 64 rule-based samples: 16-B records,
+    """Determinized rs-doko (c2d) at 6144 infostates x 64 rule-based samples: 8-B records,
     longest-first group queue, pool reuse."""
     I, S = 6144, 64
     args, n_roots, out = _bench_workload(["--workload", "c2d", "--infostates", str(I), "--iterations", str(ITERS)],
                                          monkeypatch)
     ln = _launch_line(capfd)
-    assert ln["hot"] == "16B", ln
+    assert ln["hot"] == "8B", ln
     grid = int(ln["grid"])
     assert n_roots // int(ln["rpw"]) >= 2 * grid
     rng = np.random.default_rng(77)

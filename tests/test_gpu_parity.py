@@ -198,13 +198,16 @@ def test_search_parity_fdo(eng, iters):
                                  {"DK_HOT_RECORD": "16"}, {"DK_HOT_RECORD": "32"},
                                  {"DK_HOT_RECORD": "16", "DK_LDS_PATH": "2"},
                                  {"DK_HOT_RECORD": "16", "DK_POOL_ROOTS": "1", "DK_ROOTS_PER_WAVE": "4"},
+                                 {"DK_HOT_RECORD": "8"}, {"DK_HOT_RECORD": "8", "DK_LDS_PATH": "2"},
+                                 {"DK_HOT_RECORD": "8", "DK_POOL_ROOTS": "1", "DK_ROOTS_PER_WAVE": "4"},
+                                 {"DK_HOT_RECORD": "8", "DK_ROOTS_PER_WAVE": "7"},
                                  {"DK_GROUP_ORDER": "1", "DK_POOL_ROOTS": "16", "DK_ROOTS_PER_WAVE": "5"}])
 def test_search_parity_fdo_launch_variants(env, monkeypatch):
     """Path overflow into global memory (2 LDS entries), partial / narrow waves, the LDS
     ln table, and batches larger than the node pools: with DK_POOL_ROOTS=1 one wave
     streams all six 4-root groups through a single pool region (stale trees of the
     previous group stay in it), with 16 four waves share five groups.  DK_HOT_RECORD
-    forces either hot-record layout (small batches pick the 32-B one by themselves);
+    forces a hot-record layout (8, 16 or 32 B; small batches pick the 32-B one by themselves);
     DK_GROUP_ORDER=1 queues the root groups longest-first (group_order_kernel)."""
     import master_doko_reinforcement_learning_amd as dk
     for k, v in env.items():
@@ -225,6 +228,7 @@ def test_search_parity_fdo_launch_variants(env, monkeypatch):
 
 
 @pytest.mark.parametrize("cap,env", [(120, {}), (600, {}), (600, {"DK_HOT_RECORD": "16"}),
+                                     (120, {"DK_HOT_RECORD": "8"}), (600, {"DK_HOT_RECORD": "8"}),
                                      (300, {"DK_POOL_ROOTS": "1", "DK_ROOTS_PER_WAVE": "4"}),
                                      (500, {"DK_POOL_ROOTS": "16", "DK_ROOTS_PER_WAVE": "5", "DK_GROUP_ORDER": "1"})])
 def test_search_capacity_fallback(cap, env, monkeypatch):
@@ -280,12 +284,12 @@ def test_search_capacity_fallback_doko(monkeypatch):
         assert int(best[i]) == b
 
 
-@pytest.mark.parametrize("layout", [None, "16", "ordered"])
+@pytest.mark.parametrize("layout", [None, "16", "8", "ordered"])
 def test_search_parity_doko(eng, layout, monkeypatch):
-    """rs-doko search parity; "16" forces the 16-B records, "ordered" streams 7 groups of 5
+    """rs-doko search parity; "16" / "8" force those hot records, "ordered" streams 7 groups of 5
     roots through 3 pool regions so the rs-doko default longest-first queue order applies."""
     import master_doko_reinforcement_learning_amd as dk
-    if layout == "16":
+    if layout in ("16", "8"):
         monkeypatch.setenv("DK_HOT_RECORD", layout)
     if layout == "ordered":
         monkeypatch.setenv("DK_POOL_ROOTS", "16")
