@@ -18,6 +18,7 @@ namespace dk {
 
 DK_HD int popc64(uint64_t x) { return __builtin_popcountll(x); }
 DK_HD int popc32(uint32_t x) { return __builtin_popcount(x); }
+DK_HD int ctz32(uint32_t x) { return x ? __builtin_ctz(x) : 32; }
 DK_HD int ctz64(uint64_t x) { return __builtin_ctzll(x); }
 DK_HD int clz32(uint32_t x) { return x == 0 ? 32 : __builtin_clz(x); }
 DK_HD int clz64(uint64_t x) { return x == 0 ? 64 : __builtin_clzll(x); }

@@ -317,185 +317,154 @@ DK_HD int mul24(int a, int b) {
 }
 DK_HD bool mean_lt(int32_t wa, uint32_t va, int32_t wb, uint32_t vb) { return mul24(wa, (int)vb) < mul24(wb, (int)va); }
 
-// The pick for 16-B hot records (no stored mean): the sibling min / max are found
-// EXACTLY by comparing the means w/v as cross products w_a v_b < w_b v_a (mean_lt)
-// (division-free; rounding to f64 is monotone, so the winner's f64 mean is the
-// reference's f64 min / max), and only min, max and the candidates' means are
-// divided in f64.  The f32 estimate of every child's normalised mean is
-// (w * rcp(v) - min) * 2 / range - 1; its error now also scales with
-// |q|max / range (the f32 means carry a relative error), so the candidate margin
-// grows with that ratio and a nearly flat block falls back to the full exact pass.
-template <class Mem>
-DK_HD uint32_t pick_child_reg(const Block& b, uint32_t n, double lnN, double c, Mem& mem, uint64_t* p_st, uint32_t* p_cb,
-                              uint32_t* p_inf, NodeHot16* end, bool* end_ok) {
-    int32_t w[SCAN_REG];
-    uint32_t v[SCAN_REG];
-#pragma unroll
-    for (int j = 0; j < SCAN_REG; ++j) {
-        const uint32_t vv = (uint32_t)b.st[j];
-        w[j] = vv ? (int32_t)(b.st[j] >> 32) : 0;
-        v[j] = vv ? vv : 1u;   // an unvisited child's mean is 0 = 0/1
-    }
-    int32_t wmin = w[0], wmax = w[0];
-    uint32_t vmin = v[0], vmax = v[0];
+// Blocks of 8-B records held as raw words.
+struct Block8 {
+    uint32_t w0[SCAN_REG], w1[SCAN_REG];
+};
+
+// Record accessors of the shared pick (pick_child_x): a child's raw fields as the block
+// holds them, its visits / win_score, and the in-register decode of the picked child.
+struct Raw16 {
+    uint64_t st; uint32_t cb, inf;
+    DK_HD static Raw16 at(const Block& b, int j) { return Raw16{b.st[j], b.cb[j], b.inf[j]}; }
+    DK_HD uint32_t vis() const { return (uint32_t)st; }
+    DK_HD int32_t win() const { return (int32_t)(st >> 32); }
+    DK_HD uint64_t stats() const { return st; }
+    DK_HD uint32_t child_base() const { return cb; }
+    DK_HD uint32_t info() const { return inf; }
+    DK_HD bool forced() const { return ni_nchild(inf) == 1 && !ni_open(inf); }
+};
+struct Raw8 {
+    uint32_t w0, w1;
+    DK_HD static Raw8 at(const Block8& b, int j) { return Raw8{b.w0[j], b.w1[j]}; }
+    DK_HD uint32_t vis() const { return p8_visits(w0); }
+    DK_HD int32_t win() const { return p8_win(w0); }
+    DK_HD uint64_t stats() const { return p8_stats(w0); }
+    DK_HD uint32_t child_base() const { return p8_cb(w1); }
+    DK_HD uint32_t info() const { return p8_info(w1); }
+    DK_HD bool forced() const { return p8_forced(w1); }
+};
+template <class R>
+DK_HD R sel_raw(bool p, const R& a, const R& b);
+template <>
+DK_HD Raw16 sel_raw(bool p, const Raw16& a, const Raw16& b) { return Raw16{p ? a.st : b.st, p ? a.cb : b.cb, p ? a.inf : b.inf}; }
+template <>
+DK_HD Raw8 sel_raw(bool p, const Raw8& a, const Raw8& b) { return Raw8{p ? a.w0 : b.w0, p ? a.w1 : b.w1}; }
+
+// true if any active lane of the wave has p (host builds: p itself)
+DK_HD bool wave_any(bool p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_ballot_w64(p) != 0;
+#else
+    return p;
+#endif
+}
+
+// The pick for 8-B and 16-B records (no stored mean), bit-exact with the reference's first
+// strict maximum of the f64 UCT values (node.rs:238-277):
+//  1. the sibling min / max EXACTLY, by comparing means w/v as 24-bit cross products
+//     (mean_lt; an unvisited child's mean is 0/1).  The spread is D / (vmin vmax) with the
+//     integer D = wmax vmin - wmin vmax, so the reference's `range < f64::EPSILON` is D == 0:
+//     two distinct fractions of denominators <= 4095 differ by >= 6e-8 (the f64 quotients
+//     keep that gap), equal ones give range 0.
+//  2. every child's UCT value estimated in f32: with r = rsq(v), the mean is w r^2 and the
+//     exploration term c sqrt(ln N) r, so one transcendental per child; the normalisation
+//     2 (q - min) / range - 1 is one fma with A = 2 vmin vmax / D, B = -(A min + 1).  The
+//     estimate's error stays under the cut's margin: the f32 mean carries
+//     a relative error of a few ulp (<= 1e-6 with rsq perturbed by 4 ulp), covered by the
+//     4e-6 |q|max / range term.
+//  3. the exact f64 formula only for the children within the margin of the best estimate
+//     (a 12-bit candidate mask): none with one candidate; the f64 min / max quotients are
+//     computed only then.
+// A child index j that no lane's block reaches is skipped wave-uniformly (wave_any), so a
+// wave whose blocks are all narrow pays for its widest block, not for twelve children.
+// Chain-end prefetch as in pick_child_reg.
+template <class R, class B, class Mem>
+DK_HD uint32_t pick_child_x(const B& b, uint32_t n, double lnN, double c, Mem& mem, uint64_t* p_st, uint32_t* p_cb,
+                            uint32_t* p_inf, NodeHot16* end, bool* end_ok) {
+    int32_t wmin = R::at(b, 0).win(), wmax = wmin;
+    uint32_t vmin = R::at(b, 0).vis(), vmax;
+    vmin = vmin ? vmin : 1u;
+    vmax = vmin;
     // (a branch per child, not a select: a wave whose blocks are all narrower than j skips it)
 #pragma unroll
     for (int j = 1; j < SCAN_REG; ++j) {
         if ((uint32_t)j < n) {
-            const bool lt = mean_lt(w[j], v[j], wmin, vmin);
-            const bool gt = mean_lt(wmax, vmax, w[j], v[j]);
-            wmin = lt ? w[j] : wmin; vmin = lt ? v[j] : vmin;
-            wmax = gt ? w[j] : wmax; vmax = gt ? v[j] : vmax;
+            const R r = R::at(b, j);
+            const int32_t w = r.win();
+            const uint32_t v = r.vis() ? r.vis() : 1u;
+            const bool lt = mean_lt(w, v, wmin, vmin);
+            const bool gt = mean_lt(wmax, vmax, w, v);
+            wmin = lt ? w : wmin; vmin = lt ? v : vmin;
+            wmax = gt ? w : wmax; vmax = gt ? v : vmax;
         }
     }
-    const double min_q = (double)wmin / (double)vmin, max_q = (double)wmax / (double)vmax;
-    const double range = max_q - min_q;
-    const bool flat = fabs(range) < DK_F64_EPSILON;
-    const float inv_r = flat ? 0.0f : 2.0f * rcp_approx((float)range);
-    const float minf = (float)min_q;
-    const float qabs = fmaxf(fabsf(minf), fabsf((float)max_q));
+    // >= 0 and < 2^32: exact in u32 arithmetic (each product is < 2^31 in magnitude, mean_lt)
+    const uint32_t D = (uint32_t)mul24(wmax, (int)vmin) - (uint32_t)mul24(wmin, (int)vmax);
+    const bool flat = D == 0;
+    const float vv = (float)vmin * (float)vmax;                           // exact: < 2^24
+    const float A = flat ? 0.0f : 2.0f * vv * rcp_approx((float)D);
+    const float minf = (float)wmin * rcp_approx((float)vmin);
+    const float maxf = (float)wmax * rcp_approx((float)vmax);
+    const float Bc = flat ? 1.0f : -(minf * A + 1.0f);
+    const float qabs = fmaxf(fabsf(minf), fabsf(maxf));
     const float ex = (float)c * sqrt_approx((float)lnN);
     float ue[SCAN_REG];
     float umax = -INFINITY;
 #pragma unroll
     for (int j = 0; j < SCAN_REG; ++j) {
-        const float qf = (float)w[j] * rcp_approx((float)v[j]);
-        const float nq = flat ? 1.0f : (qf - minf) * inv_r - 1.0f;
-        const uint32_t vis = (uint32_t)b.st[j];
-        const float u = vis == 0 ? INFINITY : nq + ex * rsqrt_approx((float)vis);
-        ue[j] = (uint32_t)j < n ? u : -INFINITY;
-        umax = ue[j] > umax ? ue[j] : umax;
+        ue[j] = -INFINITY;
+        if (wave_any((uint32_t)j < n)) {
+            const R r = R::at(b, j);
+            const uint32_t vis = r.vis();
+            const float rs = rsqrt_approx((float)vis);
+            const float nq = fmaf((float)r.win() * (rs * rs), A, Bc);
+            const float u = vis == 0 ? INFINITY : fmaf(ex, rs, nq);
+            ue[j] = (uint32_t)j < n ? u : -INFINITY;
+            umax = ue[j] > umax ? ue[j] : umax;
+        }
     }
-    const float cut = umax - (3e-6f * (3.0f + fabsf(ex)) + 4e-6f * qabs * inv_r);
-    uint64_t s1 = b.st[0], s2 = b.st[0];
-    uint32_t j1 = 0, j2 = 0, nc = 0, cb1 = b.cb[0], cb2 = b.cb[0], in1 = b.inf[0], in2 = b.inf[0];
+    const float cut = umax - (3e-6f * (3.0f + fabsf(ex)) + 4e-6f * qabs * A);
+    uint32_t cmask = 0;
 #pragma unroll
-    for (int j = 0; j < SCAN_REG; ++j) {
-        const bool cj = ue[j] >= cut;   // implies j < n
-        const bool first = cj && nc == 0, second = cj && nc == 1;
-        s1 = first ? b.st[j] : s1; j1 = first ? (uint32_t)j : j1; cb1 = first ? b.cb[j] : cb1; in1 = first ? b.inf[j] : in1;
-        s2 = second ? b.st[j] : s2; j2 = second ? (uint32_t)j : j2; cb2 = second ? b.cb[j] : cb2; in2 = second ? b.inf[j] : in2;
-        nc += cj ? 1u : 0u;
+    for (int j = 0; j < SCAN_REG; ++j) cmask |= (ue[j] >= cut ? 1u : 0u) << j;   // implies j < n
+    const uint32_t nc = (uint32_t)popc32(cmask);
+    const uint32_t j1 = (uint32_t)ctz32(cmask), j2 = (uint32_t)ctz32(cmask & (cmask - 1u));   // (j2 valid if nc >= 2)
+    R r1 = R::at(b, 0), r2 = R::at(b, 0);
+#pragma unroll
+    for (int j = 1; j < SCAN_REG; ++j) {
+        r1 = sel_raw((uint32_t)j == j1, R::at(b, j), r1);
+        r2 = sel_raw((uint32_t)j == j2, R::at(b, j), r2);
     }
-    const bool f1 = ni_nchild(in1) == 1 && !ni_open(in1);
-    const bool f2 = nc >= 2 && ni_nchild(in2) == 1 && !ni_open(in2);
+    // prefetch the chain ends of forced candidates (their child_base is the chain end)
+    const bool f1 = r1.forced();
+    const bool f2 = nc >= 2 && r2.forced();
     NodeHot16 e1, e2;
-    if (f1) e1 = mem.load_hot(cb1);
-    if (f2) e2 = mem.load_hot(cb2);
+    if (f1) e1 = mem.load_hot(r1.child_base());
+    if (f2) e2 = mem.load_hot(r2.child_base());
     uint32_t pick = j1;
-    if (nc == 2) {
-        const double u1 = uct_exact(s1, mean_of(s1), flat, min_q, max_q, lnN, c);
-        const double u2 = uct_exact(s2, mean_of(s2), flat, min_q, max_q, lnN, c);
-        if (u2 > u1) pick = j2;
-    } else if (nc > 2) {
-        double best = -INFINITY;
+    R rp = r1;
+    if (nc >= 2) {
+        const double min_q = (double)wmin / (double)vmin, max_q = (double)wmax / (double)vmax;
+        if (nc == 2) {
+            const uint64_t s1 = r1.stats(), s2 = r2.stats();
+            const double u1 = uct_exact(s1, mean_of(s1), flat, min_q, max_q, lnN, c);
+            const double u2 = uct_exact(s2, mean_of(s2), flat, min_q, max_q, lnN, c);
+            if (u2 > u1) { pick = j2; rp = r2; }
+        } else {
+            double best = -INFINITY;
 #pragma unroll
-        for (int j = 0; j < SCAN_REG; ++j) {
-            if (ue[j] >= cut) {
-                const double u = uct_exact(b.st[j], mean_of(b.st[j]), flat, min_q, max_q, lnN, c);
-                if (u > best) { best = u; pick = (uint32_t)j; }
+            for (int j = 0; j < SCAN_REG; ++j) {
+                if ((cmask >> j) & 1u) {
+                    const R r = R::at(b, j);
+                    const uint64_t sj = r.stats();
+                    const double u = uct_exact(sj, mean_of(sj), flat, min_q, max_q, lnN, c);
+                    if (u > best) { best = u; pick = (uint32_t)j; rp = r; }
+                }
             }
         }
     }
-    uint64_t ps = b.st[0];
-    uint32_t pc = b.cb[0], pi = b.inf[0];
-#pragma unroll
-    for (int j = 1; j < SCAN_REG; ++j) {
-        ps = (uint32_t)j == pick ? b.st[j] : ps;
-        pc = (uint32_t)j == pick ? b.cb[j] : pc;
-        pi = (uint32_t)j == pick ? b.inf[j] : pi;
-    }
-    *p_st = ps; *p_cb = pc; *p_inf = pi;
-    *end_ok = (pick == j1 && f1) || (nc >= 2 && pick == j2 && f2);
-    if (pick == j1 && f1) *end = e1;
-    else if (nc >= 2 && pick == j2 && f2) *end = e2;
-    return pick;
-}
-
-// The 16-B pick (above) on a block of 8-B records held as raw words: visits and win_score
-// are extracted per child, structure fields only for the candidates and the picked child.
-struct Block8 {
-    uint32_t w0[SCAN_REG], w1[SCAN_REG];
-};
-template <class Mem>
-DK_HD uint32_t pick_child_p8(const Block8& b, uint32_t n, double lnN, double c, Mem& mem, uint64_t* p_st, uint32_t* p_cb,
-                             uint32_t* p_inf, NodeHot16* end, bool* end_ok) {
-    int32_t w[SCAN_REG];
-    uint32_t v[SCAN_REG], vis[SCAN_REG];
-#pragma unroll
-    for (int j = 0; j < SCAN_REG; ++j) {
-        vis[j] = p8_visits(b.w0[j]);
-        w[j] = vis[j] ? p8_win(b.w0[j]) : 0;
-        v[j] = vis[j] ? vis[j] : 1u;   // an unvisited child's mean is 0 = 0/1
-    }
-    int32_t wmin = w[0], wmax = w[0];
-    uint32_t vmin = v[0], vmax = v[0];
-#pragma unroll
-    for (int j = 1; j < SCAN_REG; ++j) {
-        if ((uint32_t)j < n) {
-            const bool lt = mean_lt(w[j], v[j], wmin, vmin);
-            const bool gt = mean_lt(wmax, vmax, w[j], v[j]);
-            wmin = lt ? w[j] : wmin; vmin = lt ? v[j] : vmin;
-            wmax = gt ? w[j] : wmax; vmax = gt ? v[j] : vmax;
-        }
-    }
-    const double min_q = (double)wmin / (double)vmin, max_q = (double)wmax / (double)vmax;
-    const double range = max_q - min_q;
-    const bool flat = fabs(range) < DK_F64_EPSILON;
-    const float inv_r = flat ? 0.0f : 2.0f * rcp_approx((float)range);
-    const float minf = (float)min_q;
-    const float qabs = fmaxf(fabsf(minf), fabsf((float)max_q));
-    const float ex = (float)c * sqrt_approx((float)lnN);
-    float ue[SCAN_REG];
-    float umax = -INFINITY;
-#pragma unroll
-    for (int j = 0; j < SCAN_REG; ++j) {
-        const float qf = (float)w[j] * rcp_approx((float)v[j]);
-        const float nq = flat ? 1.0f : (qf - minf) * inv_r - 1.0f;
-        const float u = vis[j] == 0 ? INFINITY : nq + ex * rsqrt_approx((float)vis[j]);
-        ue[j] = (uint32_t)j < n ? u : -INFINITY;
-        umax = ue[j] > umax ? ue[j] : umax;
-    }
-    const float cut = umax - (3e-6f * (3.0f + fabsf(ex)) + 4e-6f * qabs * inv_r);
-    uint32_t a1 = b.w0[0], a2 = b.w0[0], m1 = b.w1[0], m2 = b.w1[0];
-    uint32_t j1 = 0, j2 = 0, nc = 0;
-#pragma unroll
-    for (int j = 0; j < SCAN_REG; ++j) {
-        const bool cj = ue[j] >= cut;   // implies j < n
-        const bool first = cj && nc == 0, second = cj && nc == 1;
-        a1 = first ? b.w0[j] : a1; m1 = first ? b.w1[j] : m1; j1 = first ? (uint32_t)j : j1;
-        a2 = second ? b.w0[j] : a2; m2 = second ? b.w1[j] : m2; j2 = second ? (uint32_t)j : j2;
-        nc += cj ? 1u : 0u;
-    }
-    const bool f1 = p8_forced(m1);
-    const bool f2 = nc >= 2 && p8_forced(m2);
-    NodeHot16 e1, e2;
-    if (f1) e1 = mem.load_hot(p8_cb(m1));
-    if (f2) e2 = mem.load_hot(p8_cb(m2));
-    uint32_t pick = j1;
-    if (nc == 2) {
-        const uint64_t s1 = p8_stats(a1), s2 = p8_stats(a2);
-        const double u1 = uct_exact(s1, mean_of(s1), flat, min_q, max_q, lnN, c);
-        const double u2 = uct_exact(s2, mean_of(s2), flat, min_q, max_q, lnN, c);
-        if (u2 > u1) pick = j2;
-    } else if (nc > 2) {
-        double best = -INFINITY;
-#pragma unroll
-        for (int j = 0; j < SCAN_REG; ++j) {
-            if (ue[j] >= cut) {
-                const uint64_t sj = p8_stats(b.w0[j]);
-                const double u = uct_exact(sj, mean_of(sj), flat, min_q, max_q, lnN, c);
-                if (u > best) { best = u; pick = (uint32_t)j; }
-            }
-        }
-    }
-    uint32_t pa = b.w0[0], pm = b.w1[0];
-#pragma unroll
-    for (int j = 1; j < SCAN_REG; ++j) {
-        pa = (uint32_t)j == pick ? b.w0[j] : pa;
-        pm = (uint32_t)j == pick ? b.w1[j] : pm;
-    }
-    *p_st = p8_stats(pa); *p_cb = p8_cb(pm); *p_inf = p8_info(pm);
+    *p_st = rp.stats(); *p_cb = rp.child_base(); *p_inf = rp.info();
     *end_ok = (pick == j1 && f1) || (nc >= 2 && pick == j2 && f2);
     if (pick == j1 && f1) *end = e1;
     else if (nc >= 2 && pick == j2 && f2) *end = e2;
@@ -579,7 +548,7 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
                     }
                     DK_STAMP_DRAINED(tl1);
                     DK_PROF(mem, 8, tl1 - tl0);
-                    pick = pick_child_p8(blk, n, lnN, c, mem, &y.stats, &y.child_base, &y.info, &end, &end_ok);
+                    pick = pick_child_x<Raw8>(blk, n, lnN, c, mem, &y.stats, &y.child_base, &y.info, &end, &end_ok);
                     DK_STAMP_DRAINED(tl2);
                     DK_PROF(mem, 9, tl2 - tl1);
                 } else {
@@ -597,7 +566,10 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
                     }
                     DK_STAMP_DRAINED(tl1);
                     DK_PROF(mem, 8, tl1 - tl0);
-                    pick = pick_child_reg(blk, n, lnN, c, mem, &y.stats, &y.child_base, &y.info, &end, &end_ok);
+                    if constexpr (NodeHot::CACHED_MEAN)
+                        pick = pick_child_reg(blk, n, lnN, c, mem, &y.stats, &y.child_base, &y.info, &end, &end_ok);
+                    else
+                        pick = pick_child_x<Raw16>(blk, n, lnN, c, mem, &y.stats, &y.child_base, &y.info, &end, &end_ok);
                     DK_STAMP_DRAINED(tl2);
                     DK_PROF(mem, 9, tl2 - tl1);
                 }

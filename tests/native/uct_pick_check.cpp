@@ -1,4 +1,5 @@
-// TEST INFRASTRUCTURE: pick_child_reg (filtered exact UCT) against the plain
+// TEST INFRASTRUCTURE: the search's UCT picks (pick_child_x over 16-B or, with
+// -DDK_PICK8, 8-B records; pick_child_reg over 32-B records in DK_HOT16=0 builds) against the plain
 // two-pass f64 UCT of the reference (node.rs:202-277) on random and near-tied
 // child blocks, with the f32 reciprocal / sqrt perturbed by up to 4 ulp (the
 // GPU's v_rcp_f32 / v_sqrt_f32 are within 1 ulp).  Prints "OK <n>".
@@ -22,7 +23,7 @@ float dk::rcp_approx(float x) { return perturb(1.0f / x); }
 float dk::sqrt_approx(float x) { return perturb(sqrtf(x)); }
 float dk::rsqrt_approx(float x) { return perturb(1.0f / sqrtf(x)); }
 
-struct NullMem {   // chain-end prefetch target (never a forced node here: info = j*13 has nchild 13*j & 63)
+struct NullMem {   // chain-end prefetch target (never a forced node here: info = j*13 << 6 has nchild 0)
     dk::NodeHot load_hot(uint32_t) const { dk::NodeHot h; memset(&h, 0, sizeof(h)); return h; }
 };
 
@@ -54,7 +55,12 @@ int main(int argc, char** argv) {
         const int mode = (int)(r() % 8);
         // 16-B builds compare means by 24-bit cross products, exact for v <= P24_MAX_ITERS
         // and |mean| <= 123 (search_core.h); mode 5 probes large visit counts within that
-        const uint32_t vmax = mode == 5 ? (DK_HOT16 ? dk::P24_MAX_ITERS : 100000u) : 1000u;
+#if DK_PICK8
+        const uint32_t VBOUND = dk::P8_MAX_ITERS;
+#else
+        const uint32_t VBOUND = dk::P24_MAX_ITERS;
+#endif
+        const uint32_t vmax = mode == 5 ? (DK_HOT16 ? VBOUND : 100000u) : 1000u;
         uint32_t total = 0;
         // mode 6: Farey neighbours a/b and c/d (|ad - bc| = 1, b, d in [500, 1000]) around a
         // common integer part k differ by 1/(bd) ~ 1e-6, ~3e-8 relative at |mean| ~ 40:
@@ -81,7 +87,7 @@ int main(int argc, char** argv) {
                 s = (int32_t)(first ? fa + fk * fb : fc + fk * fd);
             }
             else if (mode == 7) {   // the bound itself: |w| up to 123 v at v up to P24_MAX_ITERS
-                v = dk::P24_MAX_ITERS - (uint32_t)(r() % 64);
+                v = VBOUND - (uint32_t)(r() % 64);
                 s = (int32_t)(r() % (2 * 123 * v + 1)) - (int32_t)(123 * v);
             }
             else s = (int32_t)(r() % (2 * 20 * v + 1)) - (int32_t)(20 * v);
@@ -92,17 +98,34 @@ int main(int argc, char** argv) {
         for (uint32_t j = 0; j < n; ++j) rec[j] = dk::make_hot<dk::NodeHot>(rec[j].stats, 0, 0);   // as the backup leaves it
         const double lnN = std::log((double)(total + (uint32_t)(r() % 5)));
         const double c = (r() % 4 == 0) ? 0.7 + (double)(r() % 100) / 10.0 : 2.5;
-        dk::Block blk;
-        for (int j = 0; j < dk::SCAN_REG; ++j) {
-            blk.st[j] = rec[j].stats; blk.cb[j] = (uint32_t)j * 7; blk.inf[j] = (uint32_t)j * 13;
-            blk.q[j] = dk::hot_q(rec[j]); blk.isv[j] = dk::hot_isv(rec[j]);
-        }
         uint64_t gs; uint32_t gc, gi;
         dk::NodeHot end; bool end_ok;
         NullMem nm;
-        const uint32_t a = dk::pick_child_reg(blk, n, lnN, c, nm, &gs, &gc, &gi, &end, &end_ok);
         const uint32_t b = naive(rec, n, lnN, c);
-        if (a != b || gs != rec[b].stats || gc != b * 7 || gi != b * 13) {
+        auto cb_of = [](uint32_t j) { return j * 14u; };
+        auto info_of = [](uint32_t j) { return (j * 13u) << 6; };   // player / flags / state bits, nchild 0
+#if DK_PICK8
+        dk::Block8 blk;
+        for (int j = 0; j < dk::SCAN_REG; ++j) {
+            blk.w0[j] = dk::p8_w0(rec[j].stats);
+            blk.w1[j] = dk::p8_w1(cb_of((uint32_t)j), info_of((uint32_t)j));
+        }
+        const uint32_t a = dk::pick_child_x<dk::Raw8>(blk, n, lnN, c, nm, &gs, &gc, &gi, &end, &end_ok);
+        const uint32_t want_info = dk::p8_info(dk::p8_w1(cb_of(b), info_of(b)));
+#else
+        dk::Block blk;
+        for (int j = 0; j < dk::SCAN_REG; ++j) {
+            blk.st[j] = rec[j].stats; blk.cb[j] = cb_of((uint32_t)j); blk.inf[j] = info_of((uint32_t)j);
+            blk.q[j] = dk::hot_q(rec[j]); blk.isv[j] = dk::hot_isv(rec[j]);
+        }
+#if DK_HOT16
+        const uint32_t a = dk::pick_child_x<dk::Raw16>(blk, n, lnN, c, nm, &gs, &gc, &gi, &end, &end_ok);
+#else
+        const uint32_t a = dk::pick_child_reg(blk, n, lnN, c, nm, &gs, &gc, &gi, &end, &end_ok);
+#endif
+        const uint32_t want_info = info_of(b);
+#endif
+        if (a != b || gs != rec[b].stats || gc != cb_of(b) || gi != want_info) {
             printf("MISMATCH case %ld n %u mode %d: got %u want %u\n", t, n, mode, a, b);
             return 1;
         }

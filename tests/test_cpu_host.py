@@ -53,6 +53,7 @@ def test_uct_pick_filter_exact(native_bins):
     """Filtered UCT pick (f32 estimate + exact f64 on candidates) == plain f64 UCT,
     with the f32 reciprocal / sqrt adversarially perturbed by up to 4 ulp."""
     assert _run("uct_pick_check", 1000000, 3) == 1000000
+    assert _run("uct_pick_check8", 1000000, 4) == 1000000   # the same pick over 8-B records
 
 
 def test_hot32_variant_exact(native_bins):
