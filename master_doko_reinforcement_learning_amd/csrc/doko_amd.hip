@@ -166,7 +166,7 @@ template <class E, bool LN_LDS, class H>
 __global__ void __launch_bounds__(WAVE, H::MIN_WAVES) search_kernel(const dk_state* __restrict__ roots,
                                                       const uint64_t* __restrict__ seeds, uint32_t n,
                                                       uint32_t iters, double c, const double* __restrict__ ln_table,
-                                                      void* hot_pool, dk::NodeCold* cold, typename E::Work* states,
+                                                      void* hot_pool, dk::NodeCold* cold, typename E::Node* states,
                                                       uint32_t* ovf, uint64_t* ovf_st,
                                                       uint32_t cap_slots, uint32_t rpw, int lds_n,
                                                       uint32_t* visits, double* values,
@@ -200,7 +200,7 @@ __global__ void __launch_bounds__(WAVE, H::MIN_WAVES) search_kernel(const dk_sta
         typename E::Work w;
         E::load(roots[root], w);
         dk::Rng rng = dk::Rng::seed_from_u64(seeds[root]);
-        GpuMem<typename E::Work, LN_LDS, H> mem;
+        GpuMem<typename E::Node, LN_LDS, H> mem;
         mem.hot = reinterpret_cast<H*>(hot_pool) + pr * cap_slots;
         mem.cold = cold + pr * cap_slots;
         mem.states = states + pr * T;
@@ -221,7 +221,9 @@ __global__ void __launch_bounds__(WAVE, H::MIN_WAVES) search_kernel(const dk_sta
         uint32_t used[2];
         const int st = dk::search_root<E>(w, rng, iters, c, mem, visits + (size_t)root * 39,
                                           values + (size_t)root * 39, &b, nullptr, used);
-        if (st != dk::SR_OK) {
+        if (st == dk::SR_STATE) {
+            atomicOr(err, 2);                                           // malformed root (DK_E_STATE)
+        } else if (st != dk::SR_OK) {
             if (retry) {                                                // searched again by the fallback pass
                 retry[1 + atomicAdd(retry, 1u)] = root;
                 atomicAdd(high_water + 1, 1u);
@@ -751,8 +753,10 @@ namespace {
 
 constexpr size_t FALLBACK_ROOTS = 64 * 64;   // roots the fallback pool holds at once
 
+// node-state records (adapters.h Node: 64 B for both card games)
 constexpr size_t STATE_SLOT_BYTES =
-    sizeof(dk::fdo::Work) > sizeof(dk::dko::Work) ? sizeof(dk::fdo::Work) : sizeof(dk::dko::Work);
+    sizeof(dk::fdo::Node) > sizeof(dk::dko::Node) ? sizeof(dk::fdo::Node) : sizeof(dk::dko::Node);
+static_assert(STATE_SLOT_BYTES == 64 && sizeof(dk::ttt::Work) <= STATE_SLOT_BYTES, "node-state records");
 
 unsigned grid_for(size_t n, unsigned block) { return (unsigned)((n + block - 1) / block); }
 
@@ -845,7 +849,7 @@ hipError_t launch_search_t(dk_ctx* ctx, const dk_state* roots, const uint64_t* s
         if (e != hipSuccess) return e;
     }
     hipLaunchKernelGGL(kern, dim3(grid), dim3(WAVE), lds_bytes, st, roots, seeds, n, iters, c, ctx->ln_table,
-                       ctx->hot, ctx->cold, (typename E::Work*)ctx->states, ctx->ovf, ctx->ovf_st, ctx->cap_slots,
+                       ctx->hot, ctx->cold, (typename E::Node*)ctx->states, ctx->ovf, ctx->ovf_st, ctx->cap_slots,
                        rpw, lp, visits, values, best, ctx->err, ctx->queue, ctx->prof,
                        ordered ? (const uint32_t*)ctx->order : (const uint32_t*)nullptr,
                        fallback ? ctx->retry : (uint32_t*)nullptr, (const uint32_t*)nullptr, ctx->high_water);
@@ -856,7 +860,7 @@ hipError_t launch_search_t(dk_ctx* ctx, const dk_state* roots, const uint64_t* s
     // so running out there is DK_E_CAPACITY.
     const uint32_t fb_grid = ctx->fb_roots / rpw;
     hipLaunchKernelGGL(kern, dim3(fb_grid), dim3(WAVE), lds_bytes, st, roots, seeds, n, iters, c, ctx->ln_table,
-                       ctx->fb_hot, ctx->fb_cold, (typename E::Work*)ctx->fb_states, ctx->fb_ovf, ctx->fb_ovf_st,
+                       ctx->fb_hot, ctx->fb_cold, (typename E::Node*)ctx->fb_states, ctx->fb_ovf, ctx->fb_ovf_st,
                        ctx->fb_slots, rpw, lp, visits, values, best, ctx->err, ctx->queue_fb, ctx->prof,
                        (const uint32_t*)nullptr, (uint32_t*)nullptr, (const uint32_t*)ctx->retry, ctx->high_water + 2);
     return hipGetLastError();

@@ -8,6 +8,7 @@ namespace dk {
 
 struct FdoE {
     using Work = fdo::Work;
+    using Node = fdo::Node;   // a node's state in the search pools (64 B)
     using Packed = dk_fdo_state;
     static constexpr int GAME = DK_GAME_FULL_DOKO;
     // search queue in root-index order: longest-first ordering measured 5 % slower on C3
@@ -25,10 +26,14 @@ struct FdoE {
     DK_HD static int rollout(const Work& w, Rng& rng, int r[4]) { return fdo::rollout(w, rng, r); }
     DK_HD static void rewards(const Work& w, int r[4]) { fdo::score(w, r); }
     DK_HD static void step_packed(dk_state& s, int a) { fdo::step_packed(s.fdo, a); }
+    DK_HD static Node pack_node(const Work& w) { return fdo::pack_node(w); }
+    DK_HD static Work unpack_node(const Node& n) { return fdo::unpack_node(n); }
+    DK_HD static bool node_ok(const Work& w) { return fdo::node_ok(w); }
 };
 
 struct DoE {
     using Work = dko::Work;
+    using Node = dko::Node;
     using Packed = dk_do_state;
     static constexpr int GAME = DK_GAME_DOKO;
     // search queue longest-first (group_order_kernel): 4 % faster on C2d
@@ -41,10 +46,14 @@ struct DoE {
     DK_HD static int rollout(const Work& w, Rng& rng, int r[4]) { return dko::rollout(w, rng, r); }
     DK_HD static void rewards(const Work& w, int r[4]) { dko::score(w, r); }
     DK_HD static void step_packed(dk_state& s, int a) { dko::step_packed(s.dk, a); }
+    DK_HD static Node pack_node(const Work& w) { return dko::pack_node(w); }
+    DK_HD static Work unpack_node(const Node& n) { return dko::unpack_node(n); }
+    DK_HD static bool node_ok(const Work&) { return true; }
 };
 
 struct TttE {
     using Work = ttt::Work;
+    using Node = ttt::Work;
     using Packed = dk_ttt_state;
     static constexpr int GAME = DK_GAME_TTT;
     static constexpr bool ORDER_GROUPS = false;
@@ -56,6 +65,9 @@ struct TttE {
     DK_HD static int rollout(const Work& w, Rng& rng, int r[4]) { return ttt::rollout(w, rng, r); }
     DK_HD static void rewards(const Work& w, int r[4]) { ttt::score(w, r); }
     DK_HD static void step_packed(dk_state& s, int a) { ttt::step_packed(s.ttt, a); }
+    DK_HD static Node pack_node(const Work& w) { return w; }
+    DK_HD static Work unpack_node(const Node& n) { return n; }
+    DK_HD static bool node_ok(const Work&) { return true; }
 };
 
 }  // namespace dk

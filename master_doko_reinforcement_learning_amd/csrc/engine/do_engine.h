@@ -233,6 +233,41 @@ DK_HD int rollout(Work w, Rng& rng, int pts[4]) {
     return plies + rollout_cards(w, rng, pts);
 }
 
+// node-state record of the search pools: 64 B (hands as 48-bit masks), lossless
+struct alignas(16) Node { uint32_t w[16]; };
+DK_HD Node pack_node(const Work& x) {
+    Node n;
+    n.w[0] = (uint32_t)x.h[0];
+    n.w[1] = (uint32_t)(x.h[0] >> 32) | (uint32_t)x.h[1] << 16;
+    n.w[2] = (uint32_t)(x.h[1] >> 16);
+    n.w[3] = (uint32_t)x.h[2];
+    n.w[4] = (uint32_t)(x.h[2] >> 32) | (uint32_t)x.h[3] << 16;
+    n.w[5] = (uint32_t)(x.h[3] >> 16);
+    n.w[6] = x.trick_cards; n.w[7] = x.trick_winners; n.w[8] = x.eyes; n.w[9] = x.ntricks; n.w[10] = x.res;
+    n.w[11] = (uint32_t)x.trick_len | (uint32_t)x.trick_start << 8 | (uint32_t)x.trick_index << 16 | (uint32_t)x.card_index << 24;
+    n.w[12] = (uint32_t)x.phase | (uint32_t)x.cur << 8 | (uint32_t)x.res_len << 16 | (uint32_t)x.res_start << 24;
+    n.w[13] = (uint32_t)x.rr_wedding | (uint32_t)x.team_kind << 8 | (uint32_t)x.wedding_player << 16 | (uint32_t)x.solved_trick << 24;
+    n.w[14] = (uint32_t)x.re_players;
+    n.w[15] = 0;
+    return n;
+}
+DK_HD Work unpack_node(const Node& n) {
+    Work x;
+    const uint64_t M48 = 0xFFFFFFFFFFFFULL;
+    x.h[0] = ((uint64_t)n.w[0] | (uint64_t)n.w[1] << 32) & M48;
+    x.h[1] = (uint64_t)(n.w[1] >> 16) | (uint64_t)n.w[2] << 16;
+    x.h[2] = ((uint64_t)n.w[3] | (uint64_t)n.w[4] << 32) & M48;
+    x.h[3] = (uint64_t)(n.w[4] >> 16) | (uint64_t)n.w[5] << 16;
+    x.trick_cards = n.w[6]; x.trick_winners = n.w[7]; x.eyes = n.w[8]; x.ntricks = n.w[9]; x.res = n.w[10];
+    x.trick_len = (uint8_t)n.w[11]; x.trick_start = (uint8_t)(n.w[11] >> 8); x.trick_index = (uint8_t)(n.w[11] >> 16);
+    x.card_index = (uint8_t)(n.w[11] >> 24);
+    x.phase = (uint8_t)n.w[12]; x.cur = (uint8_t)(n.w[12] >> 8); x.res_len = (uint8_t)(n.w[12] >> 16); x.res_start = (uint8_t)(n.w[12] >> 24);
+    x.rr_wedding = (uint8_t)n.w[13]; x.team_kind = (uint8_t)(n.w[13] >> 8); x.wedding_player = (uint8_t)(n.w[13] >> 16);
+    x.solved_trick = (uint8_t)(n.w[13] >> 24);
+    x.re_players = (uint8_t)n.w[14]; x.pad0 = 0; x.pad1 = 0; x.pad2 = 0;
+    return x;
+}
+
 DK_HD void unpack(const dk_do_state& s, Work& w) {
     for (int p = 0; p < 4; ++p) w.h[p] = s.hands[p];
     w.eyes = (uint32_t)s.eyes[0] | (uint32_t)s.eyes[1] << 8 | (uint32_t)s.eyes[2] << 16 | (uint32_t)s.eyes[3] << 24;

@@ -722,6 +722,81 @@ DK_HD int rollout_stepwise(Work w, Rng& rng, int pts[4]) {
     return plies;
 }
 
+// ---- node-state record of the search pools (64 B) --------------------------------
+// The search stores one state per expanded tree node; 64 B aligned to 64 is one memory
+// sector and four 16-B accesses, against 88 B (eleven 8-B accesses, up to two lines) for
+// Work itself.  Hands are 48-bit masks; per-player trick and >= 40-eye trick counts are
+// <= 12 (nibbles); twelve small fields are nibbles (trick_len <= 4, trick_start /
+// ann_start / res_start < 4, phase / team_kind < 4, ann_turns / res_len / karl <= 4,
+// fox events < 16, n_tricks <= 12).  States the engine reaches keep these ranges; a
+// search root is checked (node_ok) before it is stored.
+struct alignas(16) Node { uint32_t w[16]; };
+DK_HD uint32_t nib4(uint32_t x) { return (x & 0xFu) | ((x >> 4) & 0xF0u) | ((x >> 8) & 0xF00u) | ((x >> 12) & 0xF000u); }
+DK_HD uint32_t unnib4(uint32_t y) { return (y & 0xFu) | ((y & 0xF0u) << 4) | ((y & 0xF00u) << 8) | ((y & 0xF000u) << 12); }
+DK_HD Node pack_node(const Work& x) {
+    Node n;
+    n.w[0] = (uint32_t)x.h[0];
+    n.w[1] = (uint32_t)(x.h[0] >> 32) | (uint32_t)x.h[1] << 16;
+    n.w[2] = (uint32_t)(x.h[1] >> 16);
+    n.w[3] = (uint32_t)x.h[2];
+    n.w[4] = (uint32_t)(x.h[2] >> 32) | (uint32_t)x.h[3] << 16;
+    n.w[5] = (uint32_t)(x.h[3] >> 16);
+    n.w[6] = x.trick_cards;
+    n.w[7] = x.trick_winners | (uint32_t)x.fox_n << 24;
+    n.w[8] = x.eyes;
+    n.w[9] = nib4(x.ntricks) | nib4(x.doko) << 16;
+    n.w[10] = x.res;
+    n.w[11] = (uint32_t)x.trick_len | (uint32_t)x.trick_start << 4 | (uint32_t)x.phase << 8 | (uint32_t)x.team_kind << 12 |
+              (uint32_t)x.ann_turns << 16 | (uint32_t)x.ann_start << 20 | (uint32_t)x.res_start << 24 | (uint32_t)x.res_len << 28;
+    n.w[12] = (uint32_t)x.karl | (uint32_t)x.fox0 << 4 | (uint32_t)x.fox1 << 8 | (uint32_t)x.n_tricks << 12 |
+              (uint32_t)x.card_index << 16 | (uint32_t)x.game_type << 24;
+    n.w[13] = (uint32_t)x.rr_kind | (uint32_t)x.rr_player << 8 | (uint32_t)x.rr_res << 16 | (uint32_t)x.wedding_player << 24;
+    n.w[14] = (uint32_t)x.solved_trick | (uint32_t)x.re_players << 8 | (uint32_t)x.re_lowest << 16 | (uint32_t)x.contra_lowest << 24;
+    n.w[15] = (uint32_t)x.ann_allowed | (uint32_t)x.ann_count << 8 | (uint32_t)x.ann_players << 16 | (uint32_t)x.cur << 24;
+    return n;
+}
+DK_HD Work unpack_node(const Node& n) {
+    Work x;
+    const uint64_t M48 = 0xFFFFFFFFFFFFULL;
+    x.h[0] = ((uint64_t)n.w[0] | (uint64_t)n.w[1] << 32) & M48;
+    x.h[1] = (uint64_t)(n.w[1] >> 16) | (uint64_t)n.w[2] << 16;
+    x.h[2] = ((uint64_t)n.w[3] | (uint64_t)n.w[4] << 32) & M48;
+    x.h[3] = (uint64_t)(n.w[4] >> 16) | (uint64_t)n.w[5] << 16;
+    x.trick_cards = n.w[6];
+    x.trick_winners = n.w[7] & 0xFFFFFFu; x.fox_n = (uint8_t)(n.w[7] >> 24);
+    x.eyes = n.w[8];
+    x.ntricks = unnib4(n.w[9] & 0xFFFFu); x.doko = unnib4(n.w[9] >> 16);
+    x.res = n.w[10];
+    const uint32_t a = n.w[11], b = n.w[12], c = n.w[13], d = n.w[14], e = n.w[15];
+    x.trick_len = (uint8_t)(a & 15u); x.trick_start = (uint8_t)((a >> 4) & 15u); x.phase = (uint8_t)((a >> 8) & 15u);
+    x.team_kind = (uint8_t)((a >> 12) & 15u); x.ann_turns = (uint8_t)((a >> 16) & 15u); x.ann_start = (uint8_t)((a >> 20) & 15u);
+    x.res_start = (uint8_t)((a >> 24) & 15u); x.res_len = (uint8_t)(a >> 28);
+    x.karl = (uint8_t)(b & 15u); x.fox0 = (uint8_t)((b >> 4) & 15u); x.fox1 = (uint8_t)((b >> 8) & 15u);
+    x.n_tricks = (uint8_t)((b >> 12) & 15u); x.card_index = (uint8_t)(b >> 16); x.game_type = (uint8_t)(b >> 24);
+    x.rr_kind = (uint8_t)c; x.rr_player = (uint8_t)(c >> 8); x.rr_res = (uint8_t)(c >> 16); x.wedding_player = (uint8_t)(c >> 24);
+    x.solved_trick = (uint8_t)d; x.re_players = (uint8_t)(d >> 8); x.re_lowest = (uint8_t)(d >> 16); x.contra_lowest = (uint8_t)(d >> 24);
+    x.ann_allowed = (uint8_t)e; x.ann_count = (uint8_t)(e >> 8); x.ann_players = (uint8_t)(e >> 16); x.cur = (uint8_t)(e >> 24);
+    x.pad0 = 0; x.pad1 = 0;
+    return x;
+}
+// the record holds this state exactly (the search checks every root)
+DK_HD bool node_ok(const Work& x) {
+    const Work y = unpack_node(pack_node(x));
+    bool ok = x.h[0] == y.h[0] && x.h[1] == y.h[1] && x.h[2] == y.h[2] && x.h[3] == y.h[3];
+    ok = ok && x.trick_cards == y.trick_cards && x.trick_winners == y.trick_winners && x.eyes == y.eyes;
+    ok = ok && x.ntricks == y.ntricks && x.doko == y.doko && x.res == y.res;
+    ok = ok && x.fox_n == y.fox_n && x.fox0 == y.fox0 && x.fox1 == y.fox1 && x.karl == y.karl;
+    ok = ok && x.trick_len == y.trick_len && x.trick_start == y.trick_start && x.n_tricks == y.n_tricks && x.card_index == y.card_index;
+    ok = ok && x.phase == y.phase && x.cur == y.cur && x.game_type == y.game_type && x.rr_kind == y.rr_kind;
+    ok = ok && x.rr_player == y.rr_player && x.rr_res == y.rr_res && x.team_kind == y.team_kind && x.wedding_player == y.wedding_player;
+    ok = ok && x.solved_trick == y.solved_trick && x.re_players == y.re_players && x.re_lowest == y.re_lowest &&
+         x.contra_lowest == y.contra_lowest;
+    ok = ok && x.ann_turns == y.ann_turns && x.ann_start == y.ann_start && x.ann_allowed == y.ann_allowed &&
+         x.ann_count == y.ann_count;
+    ok = ok && x.ann_players == y.ann_players && x.res_start == y.res_start && x.res_len == y.res_len;
+    return ok;
+}
+
 // ---- wire format ----------------------------------------------------------------
 DK_HD void unpack(const dk_fdo_state& s, Work& w) {
     for (int p = 0; p < 4; ++p) w.h[p] = s.hands[p];

@@ -147,7 +147,7 @@ static constexpr double DK_F64_EPSILON = 2.220446049250313e-16;
 static constexpr int SCAN_REG = 12;  // child blocks up to this size are scanned from registers
 
 // Outcome codes of search_root
-enum { SR_OK = 0, SR_CAPACITY = 1 };
+enum { SR_OK = 0, SR_CAPACITY = 1, SR_STATE = 2 };
 
 DK_HD double mean_of(uint64_t st) {
     const uint32_t v = (uint32_t)st;
@@ -481,6 +481,11 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
     // the root's structure (child_base, info) lives in registers: it changes only
     // when the root itself is expanded, and its visits are the iteration count
     uint32_t root_cb = 0, root_info;
+    if (!E::node_ok(root)) {   // a root whose fields the 64-B node record cannot hold (malformed)
+        for (int a = 0; a < 39; ++a) { visits39[a] = 0; values39[a] = 0.0; }
+        *best_out = 0xFF;
+        return SR_STATE;
+    }
     {
         const uint64_t ra = E::allowed(root, true);
         const NodeHot h = make_hot<NodeHot>(0, 0, ni_make(0, (uint32_t)E::current_player(root), ra != 0, false, 0));
@@ -489,7 +494,7 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
         cd.unexpanded = ra; cd.parent = 0xFFFFFFFFu; cd.action = 0xFFu;
         if constexpr (!P8) mem.store_hot(0, h);   // 8-B records: the root is never stored
         mem.store_cold(0, cd);
-        mem.store_state(0, root);
+        mem.store_state(0, E::pack_node(root));
     }
     // 8-B records: child blocks start at even slots (slot 1 is padding)
     uint32_t next_slot = P8 ? 2 : 1, next_state = 1;
@@ -626,7 +631,7 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
         if (ni_open(x.info)) {
             // both loads in flight together (the state index is already known)
             NodeCold cd = mem.load_cold(slot);
-            w = mem.load_state(ni_state(x.info));
+            w = E::unpack_node(mem.load_state(ni_state(x.info)));
             const uint64_t bit = random_single(cd.unexpanded, rng);
             const int a = ctz64(bit);
             uint32_t nch = ni_nchild(x.info);
@@ -660,13 +665,13 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
             mem.store_cold(child, cc);
             DK_STAMP_DRAINED(te2);
             DK_PROF(mem, 13, te2 - te1);
-            mem.store_state(next_state, w);
+            mem.store_state(next_state, E::pack_node(w));
             next_state += 1;
             depth += 1;
             mem.path_set(depth, child | (ni_player(x.info) << 30), 0ULL);
             slot = child;
         } else {
-            w = mem.load_state(ni_state(x.info));
+            w = E::unpack_node(mem.load_state(ni_state(x.info)));
         }
         DK_STAMP(t2);
         DK_PROF(mem, 1, t2 - t1);

@@ -47,7 +47,7 @@ int main(int argc, char** argv) {
     auto t1 = std::chrono::steady_clock::now();
     uint64_t scanned = 0;
     for (int j = 0; j < nroots; ++j) {
-        HostMem<dk::fdo::Work> mem(40 + 12 * iters, iters + 1, 128);
+        HostMem<dk::fdo::Node> mem(40 + 12 * iters, iters + 1, 128);
         mem.ln_table = ln.data();
         dk::Rng r2 = dk::Rng::seed_from_u64(0xC3300000ULL + j);
         uint32_t v[39]; double val[39]; uint8_t b; uint64_t sc = 0;

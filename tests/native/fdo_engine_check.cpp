@@ -40,6 +40,12 @@ static void check_state(const fdo::State& s, int game, int step, uint64_t seed) 
     dk_fdo_state rt = pk;
     dk::fdo::pack_fields(w, rt);
     if (!same_state(rt, pk)) fail("pack/unpack roundtrip", game, step);
+    if (!dk::fdo::node_ok(w)) fail("64-B node record roundtrip", game, step);
+    {   // states the search reaches by stepping (incremental trick fields) round-trip as well
+        const uint64_t la = dk::fdo::legal_actions(w);
+        for (int a = 0; a < 39; ++a)
+            if (la >> a & 1) { dk::fdo::Work x = w; dk::fdo::play_action(x, a); if (!dk::fdo::node_ok(x)) fail("64-B node record after step", game, step); }
+    }
     if (s.phase != fdo::Finished) {
         if (dk::fdo::legal_actions(w) != fdo::observation_allowed_actions(s)) fail("legal_actions", game, step);
         fdo::Env e; e.doko = s;

@@ -27,9 +27,9 @@ static void compare(const dk_state& packed, const OEnv& oenv, uint64_t seed, uin
                     const double* ln, uint32_t max_path, int idx, const char* name) {
     typename E::Work w; E::load(packed, w);
 #if DK_HOT8
-    HostMem8<typename E::Work> mem(dk::P8_SLOT_BOUND(iters), iters + 1, max_path);
+    HostMem8<typename E::Node> mem(dk::P8_SLOT_BOUND(iters), iters + 1, max_path);
 #else
-    HostMem<typename E::Work> mem(40 + 12 * iters, iters + 1, max_path);
+    HostMem<typename E::Node> mem(40 + 12 * iters, iters + 1, max_path);
 #endif
     mem.ln_table = ln;
     dk::Rng rng = dk::Rng::seed_from_u64(seed);
