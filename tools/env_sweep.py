@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--contexts", type=int, default=4)
     ap.add_argument("--infostates", type=int, default=18432)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--no-check", action="store_true", help="speed-of-light variants: results may differ")
     a = ap.parse_args()
     import torch
     import master_doko_reinforcement_learning_amd as dk
@@ -80,7 +81,7 @@ def main():
             Lk.dk_destroy(ctx)
             if ref is None:
                 ref = v.clone()
-            assert torch.equal(ref, v), "variant changed the results"
+            assert a.no_check or torch.equal(ref, v), "variant changed the results"
             times[name].extend(got)
             print("ctx %d %-10s %s ms" % (c, name, " ".join("%.1f" % t for t in got)), flush=True)
         order = order[::-1]
