@@ -27,6 +27,10 @@
 // and a node's visits only as ln(N) of a branching node or as a root child, so
 // the interior of a chain needs no bookkeeping; which nodes exist, and every
 // value that is read, stay identical to the reference's.
+// Chain ends keep no statistics: a chain end is passed on every visit of its chain head
+// since the end was created, so its visit count is the head's minus the head's count at
+// that time, which the end's record holds instead (its win_score is never read: its
+// parent has a single child).  The backup therefore writes no chain end.
 // Sibling min/max is computed once per level (identical values to the
 // reference's per-child recomputation).  ln(N) comes from a host-built table
 // of glibc `log` values, which is what Rust's f64::ln calls, so UCT values are
@@ -512,6 +516,8 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
         int depth = 0;
         uint32_t chain_head = 0xFFFFFFFFu;   // head whose skip pointer led to x
         uint32_t chain_info = 0;             // its info (8-B records rewrite both fields)
+        uint32_t chain_visits = 0;           // visits of the last chain head passed
+        bool x_end = false;                  // x is a chain end (no stats of its own)
         mem.path_set(0, 0u, x.stats);
         // One trip per BRANCHING level: a lane first hops through single-child nodes
         // (a chain head jumps to its chain end), then picks among its children.  A wave
@@ -524,11 +530,20 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
                 const NodeHot y = mem.load_hot(x.child_base);
                 scanned += 1;
                 DK_PROF(mem, 5, 1);
-                depth += 1;
-                if (depth >= MAX_DEPTH - 1) { status = SR_CAPACITY; break; }
-                mem.path_set(depth, x.child_base | (ni_player(x.info) << 30), y.stats);
+                if (slot == 0) {
+                    // the root's only child: a root child, whose stats are the result
+                    depth += 1;
+                    if (depth >= MAX_DEPTH - 1) { status = SR_CAPACITY; break; }
+                    mem.path_set(depth, x.child_base | (ni_player(x.info) << 30), y.stats);
+                    x_visits = (uint32_t)y.stats;
+                    x_end = false;
+                } else {
+                    // a chain head's skip to its chain end (derived visits, no path entry)
+                    chain_visits = x_visits;
+                    x_visits -= (uint32_t)y.stats;
+                    x_end = true;
+                }
                 slot = x.child_base;
-                x_visits = (uint32_t)y.stats;
                 x = y;
             }
             if (status != SR_OK || ni_nchild(x.info) == 0 || ni_open(x.info)) break;
@@ -607,17 +622,17 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
             slot = child;
             x_visits = (uint32_t)y.stats;
             x = y;
+            x_end = false;
             if (end_ok) {
                 // the picked child is a forced chain head: its prefetched chain end
                 chain_head = ni_head(x.info) ? slot : 0xFFFFFFFFu;
                 chain_info = x.info;
                 scanned += 1;
                 DK_PROF(mem, 5, 1);
-                depth += 1;
-                if (depth >= MAX_DEPTH - 1) { status = SR_CAPACITY; break; }
-                mem.path_set(depth, x.child_base | (ni_player(x.info) << 30), end.stats);
+                chain_visits = x_visits;
+                x_visits -= (uint32_t)end.stats;
+                x_end = true;
                 slot = x.child_base;
-                x_visits = (uint32_t)end.stats;
                 x = end;
             }
         }
@@ -658,7 +673,11 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
             DK_STAMP_DRAINED(te1);
             DK_PROF(mem, 12, te1 - te0);
             const uint64_t ca = E::allowed(w, false);
-            const NodeHot ch = make_hot<NodeHot>(0, 0, ni_make(0, (uint32_t)E::current_player(w), ca != 0, slot == 0 || block >= 2, next_state));
+            // a single child of a non-root node is a chain end: its record holds the chain
+            // head's visits before this simulation's backup (x itself, or the head x is the end of)
+            const bool child_end = block == 1 && slot != 0;
+            const uint64_t child_stats = child_end ? (uint64_t)(x_end ? chain_visits : x_visits) : 0ULL;
+            const NodeHot ch = make_hot<NodeHot>(child_stats, 0, ni_make(0, (uint32_t)E::current_player(w), ca != 0, slot == 0 || block >= 2, next_state));
             NodeCold cc;
             cc.unexpanded = ca; cc.parent = slot; cc.action = (uint32_t)a;
             mem.store_hot(child, ch);
@@ -667,8 +686,10 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
             DK_PROF(mem, 13, te2 - te1);
             mem.store_state(next_state, E::pack_node(w));
             next_state += 1;
-            depth += 1;
-            mem.path_set(depth, child | (ni_player(x.info) << 30), 0ULL);
+            if (!child_end) {
+                depth += 1;
+                mem.path_set(depth, child | (ni_player(x.info) << 30), 0ULL);
+            }
             slot = child;
         } else {
             w = E::unpack_node(mem.load_state(ni_state(x.info)));
