@@ -644,12 +644,18 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
         // ---------------- expansion
         Work w;
         if (ni_open(x.info)) {
-            // both loads in flight together (the state index is already known)
-            NodeCold cd = mem.load_cold(slot);
+            // A node's action set is computed at its first expansion, from its state (a
+            // node is created with its open flag only: allowed != 0 <=> not terminal), and
+            // kept in its cold record from then on; the root's comes from dk_create's
+            // first-expansion mask.  Both loads in flight together.
+            uint32_t nch = ni_nchild(x.info);
+            const bool first = nch == 0 && slot != 0;
+            NodeCold cd;
+            if (!first) cd = mem.load_cold(slot);
             w = E::unpack_node(mem.load_state(ni_state(x.info)));
+            if (first) cd.unexpanded = E::allowed(w, false);
             const uint64_t bit = random_single(cd.unexpanded, rng);
             const int a = ctz64(bit);
-            uint32_t nch = ni_nchild(x.info);
             const uint32_t block = nch + (uint32_t)popc64(cd.unexpanded);
             if (nch == 0) {
                 if (next_slot + block > mem.cap_slots || next_state >= mem.cap_states || next_state >= NI_MAX_STATES) {
@@ -672,16 +678,19 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
             E::step(w, a);
             DK_STAMP_DRAINED(te1);
             DK_PROF(mem, 12, te1 - te0);
-            const uint64_t ca = E::allowed(w, false);
+            const bool child_open = !E::terminal(w);   // == (E::allowed(w, false) != 0)
             // a single child of a non-root node is a chain end: its record holds the chain
             // head's visits before this simulation's backup (x itself, or the head x is the end of)
             const bool child_end = block == 1 && slot != 0;
             const uint64_t child_stats = child_end ? (uint64_t)(x_end ? chain_visits : x_visits) : 0ULL;
-            const NodeHot ch = make_hot<NodeHot>(child_stats, 0, ni_make(0, (uint32_t)E::current_player(w), ca != 0, slot == 0 || block >= 2, next_state));
-            NodeCold cc;
-            cc.unexpanded = ca; cc.parent = slot; cc.action = (uint32_t)a;
+            const NodeHot ch = make_hot<NodeHot>(child_stats, 0, ni_make(0, (uint32_t)E::current_player(w), child_open, slot == 0 || block >= 2, next_state));
             mem.store_hot(child, ch);
-            mem.store_cold(child, cc);
+            if (slot == 0) {
+                // a root child: its action is part of the result
+                NodeCold cc;
+                cc.unexpanded = 0; cc.parent = slot; cc.action = (uint32_t)a;
+                mem.store_cold(child, cc);
+            }
             DK_STAMP_DRAINED(te2);
             DK_PROF(mem, 13, te2 - te1);
             mem.store_state(next_state, E::pack_node(w));

@@ -28,6 +28,7 @@ int main(int argc, char** argv) {
         for (;;) {
             dk_do_state pk; or_do_pack(&s, (uint8_t*)&pk);
             dk::dko::Work w; dk::dko::unpack(pk, w);
+            if ((dk::dko::env_allowed(w, false) != 0) != !dk::dko::is_terminal(w)) { printf("MISMATCH allowed != 0 <=> not terminal game %d\n", g); return 1; }
             if (dk::dko::legal_actions(w) != dko::observation_allowed(s)) { printf("MISMATCH legal game %d\n", g); return 1; }
             for (int rep = 0; rep < 3; ++rep) {
                 const uint64_t sd = pol();

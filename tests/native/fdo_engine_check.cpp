@@ -41,6 +41,7 @@ static void check_state(const fdo::State& s, int game, int step, uint64_t seed) 
     dk::fdo::pack_fields(w, rt);
     if (!same_state(rt, pk)) fail("pack/unpack roundtrip", game, step);
     if (!dk::fdo::node_ok(w)) fail("64-B node record roundtrip", game, step);
+    if ((dk::fdo::env_allowed(w, false) != 0) != !dk::fdo::is_terminal(w)) fail("allowed != 0 <=> not terminal", game, step);
     {   // states the search reaches by stepping (incremental trick fields) round-trip as well
         const uint64_t la = dk::fdo::legal_actions(w);
         for (int a = 0; a < 39; ++a)
