@@ -642,6 +642,8 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
         DK_PROF(mem, 4, (uint64_t)depth);
         DK_PROF_WAVEMAX(7, depth);
         // ---------------- expansion
+        int kx = -1, kc = -1;                // path entries whose whole record the backup writes
+        uint32_t x_cb = 0, x_info = 0, c_info = 0;
         Work w;
         if (ni_open(x.info)) {
             // A node's action set is computed at its first expansion, from its state (a
@@ -670,7 +672,12 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
             nch += 1;
             const uint32_t new_info = ni_make(nch, ni_player(x.info), cd.unexpanded != 0, ni_head(x.info), ni_state(x.info));
             if (slot == 0) { root_cb = x.child_base; root_info = new_info; }
-            if (!P8 || slot != 0) mem.store_node_tail(slot, x.child_base, new_info);
+            if (slot != 0 && !x_end) {
+                // x is on the path: its new structure is stored with its backup (one store)
+                kx = depth; x_cb = x.child_base; x_info = new_info;
+            } else if (!P8 || slot != 0) {
+                mem.store_node_tail(slot, x.child_base, new_info);
+            }
             mem.store_unexpanded(slot, cd.unexpanded);
             // a forced chain grew: its head now points at the new end
             if (block == 1 && chain_head != 0xFFFFFFFFu) mem.store_child_base(chain_head, child, chain_info);
@@ -683,8 +690,10 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
             // head's visits before this simulation's backup (x itself, or the head x is the end of)
             const bool child_end = block == 1 && slot != 0;
             const uint64_t child_stats = child_end ? (uint64_t)(x_end ? chain_visits : x_visits) : 0ULL;
-            const NodeHot ch = make_hot<NodeHot>(child_stats, 0, ni_make(0, (uint32_t)E::current_player(w), child_open, slot == 0 || block >= 2, next_state));
-            mem.store_hot(child, ch);
+            const uint32_t child_info = ni_make(0, (uint32_t)E::current_player(w), child_open, slot == 0 || block >= 2, next_state);
+            // the new leaf's record is written by the backup, with its first statistics
+            if (child_end) mem.store_hot(child, make_hot<NodeHot>(child_stats, 0, child_info));
+            else c_info = child_info;
             if (slot == 0) {
                 // a root child: its action is part of the result
                 NodeCold cc;
@@ -698,6 +707,7 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
             if (!child_end) {
                 depth += 1;
                 mem.path_set(depth, child | (ni_player(x.info) << 30), 0ULL);
+                kc = depth;
             }
             slot = child;
         } else {
@@ -714,18 +724,24 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
         DK_PROF(mem, 2, t3 - t2);
         // ---------------- backup (leaf -> root): stores of the stats read on the way down
         // (two loops: the global overflow part and the LDS part keep distinct address spaces)
+        // The expanded node and the new leaf get their whole record in this one store
+        // (structure from the expansion, statistics from the backup).
+        auto put = [&](int k, uint32_t e, uint64_t ns) {
+            const uint32_t s = e & 0x3FFFFFFFu;
+            if (k == kc) mem.store_hot(s, make_hot<NodeHot>(ns, 0, c_info));
+            else if (k == kx) mem.store_hot(s, make_hot<NodeHot>(ns, x_cb, x_info));
+            else mem.store_backup(s, ns, mean_of(ns), rsqrt_approx((float)(uint32_t)ns));
+        };
         const int k_lds = depth < mem.lds_entries() - 1 ? depth : mem.lds_entries() - 1;
         for (int k = depth; k > k_lds; --k) {
             uint64_t st;
             const uint32_t e = mem.path_get_ovf(k, &st);
-            const uint64_t ns = st + (((uint64_t)(uint32_t)sel4i(r, (int)(e >> 30)) << 32) | 1ULL);
-            mem.store_backup(e & 0x3FFFFFFFu, ns, mean_of(ns), rsqrt_approx((float)(uint32_t)ns));
+            put(k, e, st + (((uint64_t)(uint32_t)sel4i(r, (int)(e >> 30)) << 32) | 1ULL));
         }
         for (int k = k_lds; k >= 1; --k) {
             uint64_t st;
             const uint32_t e = mem.path_get_lds(k, &st);
-            const uint64_t ns = st + (((uint64_t)(uint32_t)sel4i(r, (int)(e >> 30)) << 32) | 1ULL);
-            mem.store_backup(e & 0x3FFFFFFFu, ns, mean_of(ns), rsqrt_approx((float)(uint32_t)ns));
+            put(k, e, st + (((uint64_t)(uint32_t)sel4i(r, (int)(e >> 30)) << 32) | 1ULL));
         }
         if constexpr (!P8) mem.store_stats(0, (uint64_t)(it + 1));
         if (it + 1 == iters) (void)rng.next_u64();  // random_bool((1f32/1000f32) as f64)
