@@ -61,9 +61,19 @@ struct GpuMem {
     static constexpr bool P8 = dk::is_p8<H>::value;
     using Rec = H;                                                  // the stored layout
     using Hot = typename std::conditional<P8, dk::NodeHot16, H>::type;   // the in-register form
+    // Wave-uniform region bases (SGPRs) and this lane's 32-bit element offsets: every
+    // access is base + 32-bit byte offset (saddr + voffset), no per-lane 64-bit pointers.
+    // A lane's region is lane * capacity elements past the wave's base (root-major).
     H* hot;
     dk::NodeCold* cold;
     W* states;
+    uint32_t lslot, lstate, lovf;   // lane * cap_slots, lane * cap_states, lane * MAX_DEPTH
+    template <class T> __device__ static T& at(T* base, uint32_t idx) {
+        return *reinterpret_cast<T*>(reinterpret_cast<char*>(base) + (uint32_t)(idx * (uint32_t)sizeof(T)));
+    }
+    __device__ H& hr(uint32_t s) const { return at(hot, lslot + s); }
+    __device__ dk::NodeCold& cr(uint32_t s) const { return at(cold, lslot + s); }
+    __device__ W& sr(uint32_t i) const { return at(states, lstate + i); }
     // LDS regions are addressed as offsets into dk_lds (u64 words) so that the
     // compiler keeps the LDS address space (ds_* instructions, not flat_*)
     uint32_t path_st_off; // path stats: dk_lds[path_st_off + k*stride]
@@ -86,67 +96,71 @@ struct GpuMem {
     }
     __device__ Hot load_hot(uint32_t s) const {
         if constexpr (P8) {
-            const dk::NodeHot8 r = hot[s];
+            const dk::NodeHot8 r = hr(s);
             Hot h;
             h.stats = dk::p8_stats(r.w0); h.child_base = dk::p8_cb(r.w1); h.info = dk::p8_info(r.w1);
             return h;
         } else {
-            return hot[s];
+            return hr(s);
         }
     }
+    // a whole 8-B record from its two words
+    __device__ void store_rec8(uint32_t s, uint32_t w0, uint32_t w1) const {
+        if constexpr (P8) { dk::NodeHot8 r; r.w0 = w0; r.w1 = w1; hr(s) = r; }
+    }
     // two 8-B records (the pair starting at slot 2i)
-    __device__ dk::U4 load_pair(uint32_t i) const { return reinterpret_cast<const dk::U4*>(hot)[i]; }
+    __device__ dk::U4 load_pair(uint32_t i) const { return at(reinterpret_cast<dk::U4*>(hot), (lslot >> 1) + i); }
     __device__ void store_hot(uint32_t s, const Hot& h) const {
         if constexpr (P8) {
             dk::NodeHot8 r;
             r.w0 = dk::p8_w0(h.stats); r.w1 = dk::p8_w1(h.child_base, h.info);
-            hot[s] = r;
+            hr(s) = r;
         } else {
-            hot[s] = h;
+            hr(s) = h;
         }
     }
     __device__ void store_stats(uint32_t s, uint64_t v) const {
-        if constexpr (P8) hot[s].w0 = dk::p8_w0(v);
-        else hot[s].stats = v;
+        if constexpr (P8) hr(s).w0 = dk::p8_w0(v);
+        else hr(s).stats = v;
     }
     __device__ void store_backup(uint32_t s, uint64_t v, double q, float isv) const {
-        if constexpr (P8) hot[s].w0 = dk::p8_w0(v);
-        else dk::hot_backup(hot[s], v, q, isv);
+        if constexpr (P8) hr(s).w0 = dk::p8_w0(v);
+        else dk::hot_backup(hr(s), v, q, isv);
     }
     // the chain head's skip pointer (8-B records rewrite the structure word: `info` is the head's)
     __device__ void store_child_base(uint32_t s, uint32_t child_base, uint32_t info) const {
-        if constexpr (P8) hot[s].w1 = dk::p8_w1(child_base, info);
-        else hot[s].child_base = child_base;
+        if constexpr (P8) hr(s).w1 = dk::p8_w1(child_base, info);
+        else hr(s).child_base = child_base;
     }
     __device__ void store_node_tail(uint32_t s, uint32_t child_base, uint32_t info) const {
         if constexpr (P8) {
-            hot[s].w1 = dk::p8_w1(child_base, info);
+            hr(s).w1 = dk::p8_w1(child_base, info);
         } else {
-            hot[s].child_base = child_base;
-            hot[s].info = info;
+            hr(s).child_base = child_base;
+            hr(s).info = info;
         }
     }
-    __device__ dk::NodeCold load_cold(uint32_t s) const { return cold[s]; }
-    __device__ void store_cold(uint32_t s, const dk::NodeCold& c) const { cold[s] = c; }
-    __device__ void store_unexpanded(uint32_t s, uint64_t u) const { cold[s].unexpanded = u; }
-    __device__ W load_state(uint32_t i) const { return states[i]; }
-    __device__ void store_state(uint32_t i, const W& w) const { states[i] = w; }
+    __device__ dk::NodeCold load_cold(uint32_t s) const { return cr(s); }
+    __device__ void store_cold(uint32_t s, const dk::NodeCold& c) const { cr(s) = c; }
+    __device__ void store_unexpanded(uint32_t s, uint64_t u) const { cr(s).unexpanded = u; }
+    __device__ W load_state(uint32_t i) const { return sr(i); }
+    __device__ void store_state(uint32_t i, const W& w) const { sr(i) = w; }
     __device__ int lds_entries() const { return lds_n; }
     __device__ uint32_t path_get_lds(int k, uint64_t* st) const {
         *st = dk_lds[path_st_off + k * path_stride];
         return reinterpret_cast<const uint32_t*>(dk_lds)[path_off + k * path_stride];
     }
     __device__ uint32_t path_get_ovf(int k, uint64_t* st) const {
-        *st = ovf_st[k - lds_n];
-        return ovf[k - lds_n];
+        *st = at(ovf_st, lovf + (uint32_t)(k - lds_n));
+        return at(ovf, lovf + (uint32_t)(k - lds_n));
     }
     __device__ void path_set(int k, uint32_t v, uint64_t st) const {
         if (k < lds_n) {
             reinterpret_cast<uint32_t*>(dk_lds)[path_off + k * path_stride] = v;
             dk_lds[path_st_off + k * path_stride] = st;
         } else {
-            ovf[k - lds_n] = v;
-            ovf_st[k - lds_n] = st;
+            at(ovf, lovf + (uint32_t)(k - lds_n)) = v;
+            at(ovf_st, lovf + (uint32_t)(k - lds_n)) = st;
         }
     }
 #ifdef DK_PHASE_PROF
@@ -186,7 +200,6 @@ __global__ void __launch_bounds__(WAVE, H::MIN_WAVES) search_kernel(const dk_sta
     // at list[1..], searched again in a pool with the proven capacity
     if (list) n = list[0];
     const uint32_t groups = (n + rpw - 1) / rpw;
-    const size_t pr = (size_t)blockIdx.x * rpw + lane;                  // this lane's pool region
     uint32_t hw = 0;                                                    // slot high-water of this lane's roots
     for (;;) {
         uint32_t g = 0;
@@ -201,16 +214,19 @@ __global__ void __launch_bounds__(WAVE, H::MIN_WAVES) search_kernel(const dk_sta
         E::load(roots[root], w);
         dk::Rng rng = dk::Rng::seed_from_u64(seeds[root]);
         GpuMem<typename E::Node, LN_LDS, H> mem;
-        mem.hot = reinterpret_cast<H*>(hot_pool) + pr * cap_slots;
-        mem.cold = cold + pr * cap_slots;
-        mem.states = states + pr * T;
+        // wave bases (uniform) + lane offsets: pool region pr = blockIdx.x * rpw + lane
+        const size_t wr = (size_t)blockIdx.x * rpw;
+        mem.hot = reinterpret_cast<H*>(hot_pool) + wr * cap_slots;
+        mem.cold = cold + wr * cap_slots;
+        mem.states = states + wr * T;
+        mem.lslot = lane * cap_slots; mem.lstate = lane * T; mem.lovf = lane * (uint32_t)dk::MAX_DEPTH;
         mem.path_st_off = path_st_base + lane;
         mem.path_off = path_base32 + lane;
         mem.ln_glob = ln_table;
         mem.lds_n = lds_n;
         mem.path_stride = rpw;
-        mem.ovf = ovf + pr * dk::MAX_DEPTH;
-        mem.ovf_st = ovf_st + pr * dk::MAX_DEPTH;
+        mem.ovf = ovf + wr * dk::MAX_DEPTH;
+        mem.ovf_st = ovf_st + wr * dk::MAX_DEPTH;
         mem.cap_slots = cap_slots; mem.cap_states = T;
 #ifdef DK_PHASE_PROF
         mem.prof = prof + (size_t)root * 16;

@@ -642,7 +642,9 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
         DK_PROF(mem, 4, (uint64_t)depth);
         DK_PROF_WAVEMAX(7, depth);
         // ---------------- expansion
-        int kx = -1, kc = -1;                // path entries whose whole record the backup writes
+        // path entries whose whole record the backup writes: the new leaf (kc = depth) and the
+        // expanded node (kx); 8-B records carry their structure words pre-encoded
+        int kx = -1, kc = -1;
         uint32_t x_cb = 0, x_info = 0, c_info = 0;
         Work w;
         if (ni_open(x.info)) {
@@ -674,7 +676,9 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
             if (slot == 0) { root_cb = x.child_base; root_info = new_info; }
             if (slot != 0 && !x_end) {
                 // x is on the path: its new structure is stored with its backup (one store)
-                kx = depth; x_cb = x.child_base; x_info = new_info;
+                kx = depth;
+                if constexpr (P8) x_info = p8_w1(x.child_base, new_info);
+                else { x_cb = x.child_base; x_info = new_info; }
             } else if (!P8 || slot != 0) {
                 mem.store_node_tail(slot, x.child_base, new_info);
             }
@@ -693,7 +697,7 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
             const uint32_t child_info = ni_make(0, (uint32_t)E::current_player(w), child_open, slot == 0 || block >= 2, next_state);
             // the new leaf's record is written by the backup, with its first statistics
             if (child_end) mem.store_hot(child, make_hot<NodeHot>(child_stats, 0, child_info));
-            else c_info = child_info;
+            else c_info = P8 ? p8_w1(0, child_info) : child_info;
             if (slot == 0) {
                 // a root child: its action is part of the result
                 NodeCold cc;
@@ -728,9 +732,14 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
         // (structure from the expansion, statistics from the backup).
         auto put = [&](int k, uint32_t e, uint64_t ns) {
             const uint32_t s = e & 0x3FFFFFFFu;
-            if (k == kc) mem.store_hot(s, make_hot<NodeHot>(ns, 0, c_info));
-            else if (k == kx) mem.store_hot(s, make_hot<NodeHot>(ns, x_cb, x_info));
-            else mem.store_backup(s, ns, mean_of(ns), rsqrt_approx((float)(uint32_t)ns));
+            if constexpr (P8) {
+                if (k == kc || k == kx) mem.store_rec8(s, p8_w0(ns), k == kc ? c_info : x_info);
+                else mem.store_backup(s, ns, 0.0, 0.0f);
+            } else {
+                if (k == kc) mem.store_hot(s, make_hot<NodeHot>(ns, 0, c_info));
+                else if (k == kx) mem.store_hot(s, make_hot<NodeHot>(ns, x_cb, x_info));
+                else mem.store_backup(s, ns, mean_of(ns), rsqrt_approx((float)(uint32_t)ns));
+            }
         };
         const int k_lds = depth < mem.lds_entries() - 1 ? depth : mem.lds_entries() - 1;
         for (int k = depth; k > k_lds; --k) {

@@ -44,6 +44,7 @@ struct HostMem : HostMemBase<W, dk::NodeHot> {
     void store_backup(uint32_t s, uint64_t v, double q, float isv) { dk::hot_backup(this->hot[s], v, q, isv); }
     void store_child_base(uint32_t s, uint32_t cb, uint32_t) { this->hot[s].child_base = cb; }
     void store_node_tail(uint32_t s, uint32_t cb, uint32_t info) { this->hot[s].child_base = cb; this->hot[s].info = info; }
+    void store_rec8(uint32_t, uint32_t, uint32_t) {}
 };
 
 // 8-B records (search_core.h NodeHot8): encoded on store, decoded on load
@@ -63,6 +64,7 @@ struct HostMem8 : HostMemBase<W, dk::NodeHot8> {
         return q;
     }
     void store_hot(uint32_t s, const dk::NodeHot16& h) { this->hot[s].w0 = dk::p8_w0(h.stats); this->hot[s].w1 = dk::p8_w1(h.child_base, h.info); }
+    void store_rec8(uint32_t s, uint32_t w0, uint32_t w1) { this->hot[s].w0 = w0; this->hot[s].w1 = w1; }
     void store_stats(uint32_t s, uint64_t v) { this->hot[s].w0 = dk::p8_w0(v); }
     void store_backup(uint32_t s, uint64_t v, double, float) { this->hot[s].w0 = dk::p8_w0(v); }
     void store_child_base(uint32_t s, uint32_t cb, uint32_t info) { this->hot[s].w1 = dk::p8_w1(cb, info); }
