@@ -76,7 +76,8 @@ struct GpuMem {
     __device__ W& sr(uint32_t i) const { return at(states, lstate + i); }
     // LDS regions are addressed as offsets into dk_lds (u64 words) so that the
     // compiler keeps the LDS address space (ds_* instructions, not flat_*)
-    uint32_t path_st_off; // path stats: dk_lds[path_st_off + k*stride]
+    uint32_t path_st_off; // path stats: dk_lds[path_st_off + k*stride] (8-B records: their stats
+                          // word, ((uint32_t*)dk_lds)[path_st_off + k*stride])
     uint32_t path_off;    // path slots: ((uint32_t*)dk_lds)[path_off + k*stride]
     uint32_t* ovf;        // global overflow of the path (entries >= lds_n)
     uint64_t* ovf_st;
@@ -147,7 +148,8 @@ struct GpuMem {
     __device__ void store_state(uint32_t i, const W& w) const { sr(i) = w; }
     __device__ int lds_entries() const { return lds_n; }
     __device__ uint32_t path_get_lds(int k, uint64_t* st) const {
-        *st = dk_lds[path_st_off + k * path_stride];
+        if constexpr (P8) *st = dk::p8_stats(reinterpret_cast<const uint32_t*>(dk_lds)[path_st_off + k * path_stride]);
+        else *st = dk_lds[path_st_off + k * path_stride];
         return reinterpret_cast<const uint32_t*>(dk_lds)[path_off + k * path_stride];
     }
     __device__ uint32_t path_get_ovf(int k, uint64_t* st) const {
@@ -157,7 +159,8 @@ struct GpuMem {
     __device__ void path_set(int k, uint32_t v, uint64_t st) const {
         if (k < lds_n) {
             reinterpret_cast<uint32_t*>(dk_lds)[path_off + k * path_stride] = v;
-            dk_lds[path_st_off + k * path_stride] = st;
+            if constexpr (P8) reinterpret_cast<uint32_t*>(dk_lds)[path_st_off + k * path_stride] = dk::p8_w0(st);
+            else dk_lds[path_st_off + k * path_stride] = st;
         } else {
             at(ovf, lovf + (uint32_t)(k - lds_n)) = v;
             at(ovf_st, lovf + (uint32_t)(k - lds_n)) = st;
@@ -194,8 +197,10 @@ __global__ void __launch_bounds__(WAVE, H::MIN_WAVES) search_kernel(const dk_sta
     if (E::GAME != DK_GAME_TTT) dk::fdo::card_table_init();   // ends with a barrier
     __syncthreads();
     const uint32_t n_ln16 = (n_ln + 1u) & ~1u;                           // keep the next region 16-B aligned
-    const uint32_t path_st_base = n_ln16;
-    const uint32_t path_base32 = 2u * (path_st_base + (uint32_t)lds_n * rpw);   // in u32 units
+    // path stats: u64 words (8-B records: u32 words), then the u32 slots
+    constexpr bool P8 = dk::is_p8<H>::value;
+    const uint32_t path_st_base = P8 ? 2u * n_ln16 : n_ln16;
+    const uint32_t path_base32 = P8 ? path_st_base + (uint32_t)lds_n * rpw : 2u * (path_st_base + (uint32_t)lds_n * rpw);
     // fallback pass (list != nullptr): the roots the main pass could not fit, list[0] of them
     // at list[1..], searched again in a pool with the proven capacity
     if (list) n = list[0];
@@ -819,9 +824,11 @@ hipError_t launch_search_t(dk_ctx* ctx, const dk_state* roots, const uint64_t* s
                            double c, uint32_t* visits, double* values, uint8_t* best, hipStream_t st,
                            size_t ln_bytes, uint32_t rpw) {
     const auto kern = search_kernel<E, LN, H>;
+    // LDS per path entry and lane: slot word + stats (8-B records: their 32-bit stats word)
+    constexpr size_t PATH_ENTRY_BYTES = dk::is_p8<H>::value ? 8 : 12;
     auto occupancy = [&](int lp) {
         int b = 0;
-        const size_t bytes = ln_bytes + (size_t)lp * rpw * 12;
+        const size_t bytes = ln_bytes + (size_t)lp * rpw * PATH_ENTRY_BYTES;
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kern, WAVE, bytes) == hipSuccess ? b : 0;
     };
     // LDS path length: DK_LDS_PATH, or else the longest (<= 16) that keeps the residency
@@ -836,7 +843,7 @@ hipError_t launch_search_t(dk_ctx* ctx, const dk_state* roots, const uint64_t* s
         const int best = occupancy(1);
         while (lp > 1 && occupancy(lp + 1) < best) --lp;
     }
-    const size_t lds_bytes = ln_bytes + (size_t)lp * rpw * 12;
+    const size_t lds_bytes = ln_bytes + (size_t)lp * rpw * PATH_ENTRY_BYTES;
     int per_cu = occupancy(lp);
     if (per_cu < 1) per_cu = 1;
     const uint32_t groups = grid_for(n, rpw);

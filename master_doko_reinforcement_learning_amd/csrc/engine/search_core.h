@@ -682,7 +682,8 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
             } else if (!P8 || slot != 0) {
                 mem.store_node_tail(slot, x.child_base, new_info);
             }
-            mem.store_unexpanded(slot, cd.unexpanded);
+            // (a node left without unexpanded actions is never expanded again: no store)
+            if (cd.unexpanded != 0) mem.store_unexpanded(slot, cd.unexpanded);
             // a forced chain grew: its head now points at the new end
             if (block == 1 && chain_head != 0xFFFFFFFFu) mem.store_child_base(chain_head, child, chain_info);
             DK_STAMP_DRAINED(te0);
