@@ -29,6 +29,7 @@ def main(tag="r01", roots=None, iterations=None):
     for r in rows:
         key = (r["Kernel_Name"], r.get("Grid_Size_X", r.get("Grid_Size")))
         tot[key] = tot.get(key, 0) + int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    dom = None
     if tot:
         dom = max(tot, key=tot.get)
         rows = [r for r in rows if (r["Kernel_Name"], r.get("Grid_Size_X", r.get("Grid_Size"))) == dom]
@@ -63,6 +64,10 @@ def main(tag="r01", roots=None, iterations=None):
         with open(f) as fh:
             for r in csv.DictReader(fh):
                 if "search_kernel" not in r["Kernel_Name"]:
+                    continue
+                # the trace's dominant launch shape only (the small-batch leg and the fallback
+                # pass are other kernels / grids)
+                if dom is not None and (r["Kernel_Name"], r.get("Grid_Size")) != dom:
                     continue
                 key = (r["Dispatch_Id"], r["Counter_Name"])
                 per[key] = per.get(key, 0.0) + float(r["Counter_Value"])
