@@ -213,15 +213,24 @@ DK_HD CardInfo card_info_calc(uint32_t gt, uint32_t c) {
     ci.y = tr ? 32u + rank_fast(c) : eyes_fast(c);
     return ci;
 }
+// Position of the set bit of rank k (from the LSB) in a byte: bit_rank_calc(v, k).
+DK_HD uint32_t bit_rank_calc(uint32_t v, uint32_t k) {
+    for (uint32_t b = 0; b < 8u; ++b)
+        if ((v >> b) & 1u) { if (k == 0) return b; --k; }
+    return 0;
+}
 #if defined(__HIP_DEVICE_COMPILE__)
 __shared__ uint2 dk_card_tab[9 * 24];
+__shared__ uint8_t dk_bit_rank_tab[256 * 8];   // [byte][rank] -> bit position (2 KB)
 __device__ inline void card_table_init() {
     for (uint32_t i = threadIdx.x; i < 9u * 24u; i += blockDim.x) {
         const CardInfo ci = card_info_calc(i / 24u, i % 24u);
         dk_card_tab[i] = make_uint2(ci.x, ci.y);
     }
+    for (uint32_t i = threadIdx.x; i < 256u * 8u; i += blockDim.x) dk_bit_rank_tab[i] = (uint8_t)bit_rank_calc(i >> 3, i & 7u);
     __syncthreads();
 }
+__device__ inline uint32_t bit_rank(uint32_t v, uint32_t k) { return dk_bit_rank_tab[v * 8u + k]; }
 __device__ inline CardInfo card_info(uint32_t gt, uint32_t c) {
     const uint2 v = dk_card_tab[gt * 24u + c];
     CardInfo ci;
@@ -231,7 +240,19 @@ __device__ inline CardInfo card_info(uint32_t gt, uint32_t c) {
 #else
 inline void card_table_init() {}
 inline CardInfo card_info(uint32_t gt, uint32_t c) { return card_info_calc(gt, c); }
+inline uint32_t bit_rank(uint32_t v, uint32_t k) { return bit_rank_calc(v, k); }
 #endif
+// Position of the set bit of rank k (from the LSB) in a 24-bit mask with more than k set
+// bits: the byte holding it from two byte popcounts, the bit from the [byte][rank] table.
+DK_HD uint32_t nth_set_bit24(uint32_t m, uint32_t k) {
+    const uint32_t c0 = (uint32_t)popc32(m & 0xFFu), c1 = (uint32_t)popc32(m & 0xFF00u);
+    const bool ge0 = k >= c0;
+    const uint32_t k1 = k - c0;
+    const bool ge1 = ge0 && k1 >= c1;
+    const uint32_t sh = ge1 ? 16u : (ge0 ? 8u : 0u);
+    const uint32_t kk = ge1 ? k1 - c1 : (ge0 ? k1 : k);
+    return sh + bit_rank((m >> sh) & 0xFFu, kk);
+}
 
 
 // announcement.rs:182-215 (the announcing player's team decides which lowest moves)
@@ -595,15 +616,7 @@ DK_HD int rollout_cards(const Work& w0, Rng& rng, int pts[4]) {
         const uint32_t legal = f ? f : a;
         const uint32_t r = rng.range_u32((uint32_t)popc32(legal));
         // bit of rank r from the MSB = bit of rank popc-1-r from the LSB
-        uint32_t k = (uint32_t)popc32(legal) - 1u - r, pos = 0;
-#pragma unroll
-        for (int wdt = 16; wdt >= 1; wdt >>= 1) {
-            const uint32_t cnt = (uint32_t)popc32((legal >> pos) & ((1u << wdt) - 1u));
-            const bool hi = k >= cnt;
-            k = hi ? k - cnt : k;
-            pos = hi ? pos + (uint32_t)wdt : pos;
-        }
-        const uint32_t card = pos, bit = 1u << card;
+        const uint32_t card = nth_set_bit24(legal, (uint32_t)popc32(legal) - 1u - r), bit = 1u << card;
         const bool dup = (t2 & bit) != 0u;
         const uint32_t na = dup ? a : (a ^ bit), nt = dup ? (t2 ^ bit) : t2;
         any0 = cur == 0u ? na : any0; any1 = cur == 1u ? na : any1; any2 = cur == 2u ? na : any2; any3 = cur == 3u ? na : any3;

@@ -11,7 +11,17 @@ namespace dk {
 struct Rng {
     uint64_t s0, s1, s2, s3;
 
-    DK_HD static uint64_t rotl(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+    DK_HD static uint64_t rotl(uint64_t x, int k) {
+#if defined(__HIP_DEVICE_COMPILE__)
+        // two funnel shifts (v_alignbit_b32) instead of 64-bit shifts and an or
+        uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+        if (k >= 32) { const uint32_t t = lo; lo = hi; hi = t; k -= 32; }
+        const uint32_t nh = __builtin_amdgcn_alignbit(hi, lo, 32 - k), nl = __builtin_amdgcn_alignbit(lo, hi, 32 - k);
+        return (uint64_t)nh << 32 | nl;
+#else
+        return (x << k) | (x >> (64 - k));
+#endif
+    }
 
     DK_HD static Rng seed_from_u64(uint64_t state) {
         // rand_core 0.9 SeedableRng::seed_from_u64 (SplitMix64); Xoshiro256++ maps an
