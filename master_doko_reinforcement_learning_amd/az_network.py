@@ -95,8 +95,13 @@ class ClassHead(nn.Module):
         w = torch.softmax(torch.einsum("cd,bsd->bcs", self.queries, x) * self.scale, dim=-1)
         a = torch.einsum("bcs,bsd->bcd", w, x)                  # [B, C, d]
         a = F.layer_norm(a, a.shape[-1:]) * self.ln_w + self.ln_b
-        h = F.gelu(torch.einsum("bci,coi->bco", a, self.w1) + self.b1)
-        return torch.einsum("bco,co->bc", h, self.w2) + self.b2
+        # per-class MLP as one batched GEMM over the classes on a contiguous [C, B, d]
+        # operand: einsum("bci,coi->bco") hands the GEMM a class-batched view whose batch
+        # stride (d) is smaller than its row stride (C d), and a PyTorch TunableOp candidate
+        # faulted on that layout
+        ac = a.transpose(0, 1).contiguous()                      # [C, B, d]
+        h = F.gelu(torch.bmm(ac, self.w1.transpose(1, 2)) + self.b1[:, None, :])   # [C, B, d]
+        return ((h * self.w2[:, None, :]).sum(-1) + self.b2[:, None]).transpose(0, 1)   # [B, C]
 
 
 class FusedTrunk:
