@@ -101,7 +101,9 @@ struct alignas(8) NodeHot8 {
     static constexpr bool CACHED_MEAN = false;
     static constexpr int MIN_WAVES = DK_HOT16_WAVES;
 };
-static constexpr uint32_t P8_MAX_ITERS = 1200;   // visits / state index < 2^11, slots < 2^14
+// visits < 2^11, slots < 2^14, state indices < 2^10 (bit 10 of the state field marks a
+// resolved chain head, below)
+static constexpr uint32_t P8_MAX_ITERS = 1023;
 // proven slot bound with even-aligned blocks: the root and its padding slot, the root block
 // (<= 39 children, padded to 40) and one block of <= 12 children per iteration
 static constexpr uint32_t P8_SLOT_BOUND(uint32_t iters) { return 42u + 12u * iters; }
@@ -116,6 +118,14 @@ DK_HD uint64_t p8_stats(uint32_t w0) { return (uint64_t)(uint32_t)p8_win(w0) << 
 DK_HD uint32_t p8_cb(uint32_t w1) { return (w1 & 0x1FFFu) << 1; }
 DK_HD uint32_t p8_info(uint32_t w1) { return ((w1 >> 13) & 15u) | ((w1 >> 17) & 15u) << 6 | (w1 >> 21) << 10; }
 DK_HD bool p8_forced(uint32_t w1) { return (w1 & (15u << 13 | 1u << 19)) == 1u << 13; }   // nchild == 1 && !open
+// A resolved chain head: a forced chain head whose chain end is fully expanded stores the
+// end's child block, child count and player in place of its own (never used again) state,
+// marked by bit 10 of the state field, so that the selection descends from the head to the
+// end's children without loading the end's record.  The end's visit count, the ln(N) of its
+// pick, is 1 + the sum of its children's visits (every simulation through a non-terminal
+// node after the one that created it goes on to one of its children).
+static constexpr uint32_t P8_RESOLVED = 0x400u;
+DK_HD bool ni_resolved(uint32_t info) { return ((info >> 10) & P8_RESOLVED) != 0; }   // (state field: info >> 10)
 template <class H> struct is_p8 { static constexpr bool value = false; };
 template <> struct is_p8<NodeHot8> { static constexpr bool value = true; };
 
@@ -346,7 +356,7 @@ struct Raw8 {
     DK_HD uint64_t stats() const { return p8_stats(w0); }
     DK_HD uint32_t child_base() const { return p8_cb(w1); }
     DK_HD uint32_t info() const { return p8_info(w1); }
-    DK_HD bool forced() const { return p8_forced(w1); }
+    DK_HD bool forced() const { return p8_forced(w1) && !(w1 >> 31); }   // (resolved heads need no prefetch)
 };
 template <class R>
 DK_HD R sel_raw(bool p, const R& a, const R& b);
@@ -517,6 +527,7 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
         uint32_t chain_head = 0xFFFFFFFFu;   // head whose skip pointer led to x
         uint32_t chain_info = 0;             // its info (8-B records rewrite both fields)
         uint32_t chain_visits = 0;           // visits of the last chain head passed
+        constexpr uint32_t N_FROM_BLOCK = 0xFFFFFFFFu;   // x_visits of a resolved chain end
         bool x_end = false;                  // x is a chain end (no stats of its own)
         mem.path_set(0, 0u, x.stats);
         // One trip per BRANCHING level: a lane first hops through single-child nodes
@@ -527,6 +538,17 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
             while (ni_nchild(x.info) == 1 && !ni_open(x.info)) {
                 chain_head = ni_head(x.info) ? slot : 0xFFFFFFFFu;
                 chain_info = x.info;
+                if (P8 && slot != 0 && ni_resolved(x.info)) {
+                    // resolved chain head: its chain end's children directly (no load)
+                    scanned += 1;
+                    DK_PROF(mem, 5, 1);
+                    chain_visits = x_visits;
+                    x_visits = N_FROM_BLOCK;
+                    x_end = true;
+                    x.info = ni_make(ni_state(x.info) & 15u, ni_player(x.info), false, false, 0);
+                    slot = 0xFFFFFFFFu;
+                    break;
+                }
                 const NodeHot y = mem.load_hot(x.child_base);
                 scanned += 1;
                 DK_PROF(mem, 5, 1);
@@ -555,7 +577,7 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
                 if constexpr (P8) {
                     // blocks start at even slots: one 16-B load per pair of children
                     DK_STAMP_DRAINED(tl0);
-                    const double lnN = mem.ln(x_visits);
+                    const double lnN = x_visits == N_FROM_BLOCK ? 0.0 : mem.ln(x_visits);
                     Block8 blk;
 #pragma unroll
                     for (int j = 0; j < SCAN_REG / 2; ++j) {
@@ -568,7 +590,15 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
                     }
                     DK_STAMP_DRAINED(tl1);
                     DK_PROF(mem, 8, tl1 - tl0);
-                    pick = pick_child_x<Raw8>(blk, n, lnN, c, mem, &y.stats, &y.child_base, &y.info, &end, &end_ok);
+                    double lnN_x = lnN;
+                    if (x_visits == N_FROM_BLOCK) {
+                        uint32_t N = 1;
+#pragma unroll
+                        for (int j = 0; j < SCAN_REG; ++j) N += (uint32_t)j < n ? p8_visits(blk.w0[j]) : 0u;
+                        x_visits = N;
+                        lnN_x = mem.ln(N);
+                    }
+                    pick = pick_child_x<Raw8>(blk, n, lnN_x, c, mem, &y.stats, &y.child_base, &y.info, &end, &end_ok);
                     DK_STAMP_DRAINED(tl2);
                     DK_PROF(mem, 9, tl2 - tl1);
                 } else {
@@ -623,7 +653,18 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
             x_visits = (uint32_t)y.stats;
             x = y;
             x_end = false;
-            if (end_ok) {
+            if (P8 && ni_nchild(x.info) == 1 && !ni_open(x.info) && ni_resolved(x.info)) {
+                // the picked child is a resolved chain head: on to its chain end's children
+                chain_head = slot;
+                chain_info = x.info;
+                scanned += 1;
+                DK_PROF(mem, 5, 1);
+                chain_visits = x_visits;
+                x_visits = N_FROM_BLOCK;
+                x_end = true;
+                x.info = ni_make(ni_state(x.info) & 15u, ni_player(x.info), false, false, 0);
+                slot = 0xFFFFFFFFu;
+            } else if (end_ok) {
                 // the picked child is a forced chain head: its prefetched chain end
                 chain_head = ni_head(x.info) ? slot : 0xFFFFFFFFu;
                 chain_info = x.info;
@@ -672,6 +713,9 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
             cd.unexpanded &= ~bit;
             const uint32_t child = x.child_base + nch;
             nch += 1;
+            // a chain end that is now fully expanded with >= 2 children: resolve its head
+            if (P8 && x_end && chain_head != 0xFFFFFFFFu && cd.unexpanded == 0 && nch >= 2)
+                mem.store_node_tail(chain_head, x.child_base, ni_make(1, ni_player(x.info), false, true, P8_RESOLVED | nch));
             const uint32_t new_info = ni_make(nch, ni_player(x.info), cd.unexpanded != 0, ni_head(x.info), ni_state(x.info));
             if (slot == 0) { root_cb = x.child_base; root_info = new_info; }
             if (slot != 0 && !x_end) {
