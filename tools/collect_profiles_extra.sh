@@ -5,7 +5,7 @@
 # Output: gpurun_out/prof_extra/<workload>/ (rocprofv3 --kernel-trace --stats) + the traced bench line.
 set -u
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-OUT=gpurun_out/prof_extra
+OUT=gpurun_out/prof_extra${TAG:+_$TAG}
 mkdir -p $OUT
 for w in ${WORKLOADS:-c2d c2 c5 impi}; do
   case $w in
