@@ -344,6 +344,7 @@ struct Raw16 {
     DK_HD uint32_t vis() const { return (uint32_t)st; }
     DK_HD int32_t win() const { return (int32_t)(st >> 32); }
     DK_HD uint64_t stats() const { return st; }
+    DK_HD uint64_t key() const { return st; }        // equal keys <=> equal statistics
     DK_HD uint32_t child_base() const { return cb; }
     DK_HD uint32_t info() const { return inf; }
     DK_HD bool forced() const { return ni_nchild(inf) == 1 && !ni_open(inf); }
@@ -354,6 +355,7 @@ struct Raw8 {
     DK_HD uint32_t vis() const { return p8_visits(w0); }
     DK_HD int32_t win() const { return p8_win(w0); }
     DK_HD uint64_t stats() const { return p8_stats(w0); }
+    DK_HD uint32_t key() const { return w0; }        // equal keys <=> equal statistics
     DK_HD uint32_t child_base() const { return p8_cb(w1); }
     DK_HD uint32_t info() const { return p8_info(w1); }
     DK_HD bool forced() const { return p8_forced(w1) && !(w1 >> 31); }   // (resolved heads need no prefetch)
@@ -443,6 +445,12 @@ DK_HD uint32_t pick_child_x(const B& b, uint32_t n, double lnN, double c, Mem& m
 #pragma unroll
     for (int j = 0; j < SCAN_REG; ++j) cmask |= (ue[j] >= cut ? 1u : 0u) << j;   // implies j < n
     const uint32_t nc = (uint32_t)popc32(cmask);
+#ifdef DK_PICK_CENSUS
+    dk_pick_census(n, nc);
+    { uint32_t c1 = (uint32_t)ctz32(cmask), dif = 0;
+      for (int j = 0; j < SCAN_REG; ++j) dif |= ((cmask >> j) & 1u) && R::at(b, j).key() != R::at(b, (int)c1).key();
+      dk_pick_tie(dif == 0); }
+#endif
     const uint32_t j1 = (uint32_t)ctz32(cmask), j2 = (uint32_t)ctz32(cmask & (cmask - 1u));   // (j2 valid if nc >= 2)
     R r1 = R::at(b, 0), r2 = R::at(b, 0);
 #pragma unroll
@@ -458,8 +466,18 @@ DK_HD uint32_t pick_child_x(const B& b, uint32_t n, double lnN, double c, Mem& m
     if (f2) e2 = mem.load_hot(r2.child_base());
     uint32_t pick = j1;
     R rp = r1;
+    // Candidates with the first candidate's statistics have its f64 value exactly and come
+    // later, so they cannot be the first strict maximum: only candidates whose statistics
+    // differ need the f64 formula (ties of identical statistics are ~98 % of the two-
+    // candidate picks at C3).
+    uint32_t emask = 0;
     if (nc >= 2) {
+#pragma unroll
+        for (int j = 0; j < SCAN_REG; ++j) emask |= (((cmask >> j) & 1u) && R::at(b, j).key() != r1.key() ? 1u : 0u) << j;
+    }
+    if (emask) {
         const double min_q = (double)wmin / (double)vmin, max_q = (double)wmax / (double)vmax;
+        emask |= 1u << j1;
         if (nc == 2) {
             const uint64_t s1 = r1.stats(), s2 = r2.stats();
             const double u1 = uct_exact(s1, mean_of(s1), flat, min_q, max_q, lnN, c);
@@ -469,7 +487,7 @@ DK_HD uint32_t pick_child_x(const B& b, uint32_t n, double lnN, double c, Mem& m
             double best = -INFINITY;
 #pragma unroll
             for (int j = 0; j < SCAN_REG; ++j) {
-                if ((cmask >> j) & 1u) {
+                if ((emask >> j) & 1u) {
                     const R r = R::at(b, j);
                     const uint64_t sj = r.stats();
                     const double u = uct_exact(sj, mean_of(sj), flat, min_q, max_q, lnN, c);
