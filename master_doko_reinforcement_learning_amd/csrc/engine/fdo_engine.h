@@ -606,8 +606,35 @@ DK_HD int rollout_cards(const Work& w0, Rng& rng, int pts[4]) {
         t_eyes += eyes_fast(c);
         if (c == (uint32_t)DIAMOND_ACE) { const uint32_t pl = (trick_start + i) & 3u; if (da_n == 0) da0 = pl; else da1 = pl; da_n += 1; }
     }
+    // a completed trick goes to its winner (complete_trick): eyes, trick count, Doppelkopf,
+    // Diamond-Ace events in play order (fox0 / fox1), Karlchen, wedding resolution
+    auto complete = [&](uint32_t winner) {
+        const uint32_t sh = 8u * winner;
+        eyes += t_eyes << sh;
+        ntr += 1u << sh;
+        doko += (t_eyes >= 40u ? 1u : 0u) << sh;
+        if (da_n != 0u) {
+            const uint32_t e0 = (da0 << 2) | winner, e1 = (da1 << 2) | winner;
+            fox0 = fox_n == 0u ? e0 : fox0;
+            fox1 = fox_n == 1u ? e0 : fox1;
+            fox_n += 1u;
+            if (da_n == 2u) { fox1 = fox_n == 1u ? e1 : fox1; fox_n += 1u; }
+        }
+        const uint32_t t = n_tricks - 1u;
+        karl = (t == 11u && win_card == (uint32_t)CLUB_JACK) ? 1u + winner : karl;
+        if (team_kind == TK_WED_UNSOLVED && t < 3u && (winner != wedding_player || t == 2u)) {
+            team_kind = TK_WED_SOLVED;
+            solved = winner != wedding_player ? t : 2u;
+            re_players = (1u << wedding_player) | (winner != wedding_player ? 1u << winner : 0u);
+            theta = ann_thetas(team_kind, solved, re_players, w0.re_lowest, w0.contra_lowest);
+        }
+    };
     int plies = 0;
-    for (;;) {
+    // The loop stops at the start of the last trick, whose four plays are forced (one card
+    // per hand) and leave no announcement offer (thresholds are >= 4 cards, ann_theta), so the
+    // wave plays it once below in straight-line code instead of four more loop iterations.
+    const bool tail_only = n_tricks == 12u && trick_len == 0u;
+    if (!tail_only) for (;;) {
         // ---- one card for `cur`
         const uint32_t a = sel4u(any0, any1, any2, any3, cur);
         const uint32_t t2 = sel4u(two0, two1, two2, two3, cur);
@@ -642,33 +669,45 @@ DK_HD int rollout_cards(const Work& w0, Rng& rng, int pts[4]) {
         plies += 1;
         if (trick_len == 4u) {
             const uint32_t winner = (trick_start + best_pos) & 3u;
-            const uint32_t sh = 8u * winner;
-            eyes += t_eyes << sh;
-            ntr += 1u << sh;
-            doko += (t_eyes >= 40u ? 1u : 0u) << sh;
-            // Diamond-Ace events in play order (fox0 / fox1)
-            if (da_n != 0u) {
-                const uint32_t e0 = (da0 << 2) | winner, e1 = (da1 << 2) | winner;
-                fox0 = fox_n == 0u ? e0 : fox0;
-                fox1 = fox_n == 1u ? e0 : fox1;
-                fox_n += 1u;
-                if (da_n == 2u) { fox1 = fox_n == 1u ? e1 : fox1; fox_n += 1u; }
-            }
-            const uint32_t t = n_tricks - 1u;
-            karl = (t == 11u && win_card == (uint32_t)CLUB_JACK) ? 1u + winner : karl;
-            if (team_kind == TK_WED_UNSOLVED && t < 3u && (winner != wedding_player || t == 2u)) {
-                team_kind = TK_WED_SOLVED;
-                solved = winner != wedding_player ? t : 2u;
-                re_players = (1u << wedding_player) | (winner != wedding_player ? 1u << winner : 0u);
-                theta = ann_thetas(team_kind, solved, re_players, w0.re_lowest, w0.contra_lowest);
-            }
-            if (n_tricks == 12u) break;
+            complete(winner);
+            if (n_tricks == 12u) break;   // the rollout started within the last trick
             cur = winner; trick_start = winner; trick_len = 0; n_tricks += 1u;
+            if (n_tricks == 12u) break;   // every hand holds one card: no offer, forced tail below
         }
         // ---- collapsed announcement round: one forced NoAnnouncement draw per offered player
         const uint32_t d = (uint32_t)popc32(((nb | 0x80808080u) - theta) & 0x80808080u);
         for (uint32_t i = 0; i < d; ++i) rng.advance();
         plies += (int)d;
+    }
+    if (n_tricks == 12u && trick_len == 0u) {
+        // ---- the last trick: four forced plays from `trick_start`, one range(0..1) draw each
+        const uint32_t s = trick_start;
+        uint32_t best = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < 4u; ++i) {
+            const uint32_t p = (s + i) & 3u;
+            const uint32_t card = (uint32_t)ctz32(sel4u(any0, any1, any2, any3, p));
+            rng.advance();
+            const CardInfo ci = card_info(gt, card);
+            if (i == 0u) {
+                lead = ci.x & 0xFFFFFFu;
+                best_key = (int)ci.y; best = 0; win_card = card;
+                t_eyes = (ci.x >> 24) & 15u; da_n = 0;
+            } else {
+                const int key = (((ci.x >> 28) & 1u) || ((lead >> card) & 1u)) ? (int)ci.y : -1;
+                const bool better = key > best_key;
+                best_key = better ? key : best_key;
+                best = better ? i : best;
+                win_card = better ? card : win_card;
+                t_eyes += (ci.x >> 24) & 15u;
+            }
+            const bool is_da = card == (uint32_t)DIAMOND_ACE;
+            da0 = (is_da && da_n == 0u) ? p : da0;
+            da1 = (is_da && da_n == 1u) ? p : da1;
+            da_n += is_da ? 1u : 0u;
+        }
+        plies += 4;
+        complete((s + best) & 3u);
     }
     Work fin = w0;
     fin.eyes = eyes; fin.ntricks = ntr; fin.doko = doko;
