@@ -638,8 +638,8 @@ DK_HD int rollout_cards(const Work& w0, Rng& rng, int pts[4]) {
         // ---- one card for `cur`
         const uint32_t a = sel4u(any0, any1, any2, any3, cur);
         const uint32_t t2 = sel4u(two0, two1, two2, two3, cur);
-        const uint32_t follow_mask = (trick_len == 0u || n_tricks >= 12u) ? 0xFFFFFFu : lead;
-        const uint32_t f = a & follow_mask;
+        // (`lead` is all cards between tricks; in the last trick every hand holds one card)
+        const uint32_t f = a & lead;
         const uint32_t legal = f ? f : a;
         const uint32_t r = rng.range_u32((uint32_t)popc32(legal));
         // bit of rank r from the MSB = bit of rank popc-1-r from the LSB
@@ -671,7 +671,7 @@ DK_HD int rollout_cards(const Work& w0, Rng& rng, int pts[4]) {
             const uint32_t winner = (trick_start + best_pos) & 3u;
             complete(winner);
             if (n_tricks == 12u) break;   // the rollout started within the last trick
-            cur = winner; trick_start = winner; trick_len = 0; n_tricks += 1u;
+            cur = winner; trick_start = winner; trick_len = 0; n_tricks += 1u; lead = 0xFFFFFFu;
             if (n_tricks == 12u) break;   // every hand holds one card: no offer, forced tail below
         }
         // ---- collapsed announcement round: one forced NoAnnouncement draw per offered player
