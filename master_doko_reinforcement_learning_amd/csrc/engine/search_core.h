@@ -37,6 +37,8 @@
 // bit-exact.
 #pragma once
 #include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include "common.h"
 #include "rng.h"
 
@@ -395,12 +397,18 @@ DK_HD bool wave_any(bool p) {
 // A child index j that no lane's block reaches is skipped wave-uniformly (wave_any), so a
 // wave whose blocks are all narrow pays for its widest block, not for twelve children.
 // Chain-end prefetch as in pick_child_reg.
+// Every child it scans has been visited: the selection descends only into fully expanded
+// nodes, and each child was backed up by the simulation that created it (the reference's
+// +inf for an unvisited child never arises; host builds check this).
 template <class R, class B, class Mem>
 DK_HD uint32_t pick_child_x(const B& b, uint32_t n, double lnN, double c, Mem& mem, uint64_t* p_st, uint32_t* p_cb,
                             uint32_t* p_inf, NodeHot16* end, bool* end_ok) {
+#if !defined(__HIP_DEVICE_COMPILE__)
+    for (uint32_t j = 0; j < n; ++j)
+        if (R::at(b, (int)j).vis() == 0) { fprintf(stderr, "pick_child_x: unvisited child\n"); abort(); }
+#endif
     int32_t wmin = R::at(b, 0).win(), wmax = wmin;
     uint32_t vmin = R::at(b, 0).vis(), vmax;
-    vmin = vmin ? vmin : 1u;
     vmax = vmin;
     // (a branch per child, not a select: a wave whose blocks are all narrower than j skips it)
 #pragma unroll
@@ -408,7 +416,7 @@ DK_HD uint32_t pick_child_x(const B& b, uint32_t n, double lnN, double c, Mem& m
         if ((uint32_t)j < n) {
             const R r = R::at(b, j);
             const int32_t w = r.win();
-            const uint32_t v = r.vis() ? r.vis() : 1u;
+            const uint32_t v = r.vis();
             const bool lt = mean_lt(w, v, wmin, vmin);
             const bool gt = mean_lt(wmax, vmax, w, v);
             wmin = lt ? w : wmin; vmin = lt ? v : vmin;
@@ -425,8 +433,12 @@ DK_HD uint32_t pick_child_x(const B& b, uint32_t n, double lnN, double c, Mem& m
     const float Bc = flat ? 1.0f : -(minf * A + 1.0f);
     const float qabs = fmaxf(fabsf(minf), fabsf(maxf));
     const float ex = (float)c * sqrt_approx((float)lnN);
+    // The first maximum of the estimates is tracked with its record, so no per-index
+    // selection is needed afterwards.
     float ue[SCAN_REG];
     float umax = -INFINITY;
+    uint32_t jm = 0;
+    R rm = R::at(b, 0);
 #pragma unroll
     for (int j = 0; j < SCAN_REG; ++j) {
         ue[j] = -INFINITY;
@@ -435,9 +447,11 @@ DK_HD uint32_t pick_child_x(const B& b, uint32_t n, double lnN, double c, Mem& m
             const uint32_t vis = r.vis();
             const float rs = rsqrt_approx((float)vis);
             const float nq = fmaf((float)r.win() * (rs * rs), A, Bc);
-            const float u = vis == 0 ? INFINITY : fmaf(ex, rs, nq);
-            ue[j] = (uint32_t)j < n ? u : -INFINITY;
-            umax = ue[j] > umax ? ue[j] : umax;
+            ue[j] = (uint32_t)j < n ? fmaf(ex, rs, nq) : -INFINITY;
+            const bool gt = ue[j] > umax;
+            umax = gt ? ue[j] : umax;
+            jm = gt ? (uint32_t)j : jm;
+            rm = sel_raw(gt, r, rm);
         }
     }
     const float cut = umax - (3e-6f * (3.0f + fabsf(ex)) + 4e-6f * qabs * A);
@@ -451,55 +465,38 @@ DK_HD uint32_t pick_child_x(const B& b, uint32_t n, double lnN, double c, Mem& m
       for (int j = 0; j < SCAN_REG; ++j) dif |= ((cmask >> j) & 1u) && R::at(b, j).key() != R::at(b, (int)c1).key();
       dk_pick_tie(dif == 0); }
 #endif
-    const uint32_t j1 = (uint32_t)ctz32(cmask), j2 = (uint32_t)ctz32(cmask & (cmask - 1u));   // (j2 valid if nc >= 2)
-    R r1 = R::at(b, 0), r2 = R::at(b, 0);
-#pragma unroll
-    for (int j = 1; j < SCAN_REG; ++j) {
-        r1 = sel_raw((uint32_t)j == j1, R::at(b, j), r1);
-        r2 = sel_raw((uint32_t)j == j2, R::at(b, j), r2);
-    }
-    // prefetch the chain ends of forced candidates (their child_base is the chain end)
-    const bool f1 = r1.forced();
-    const bool f2 = nc >= 2 && r2.forced();
-    NodeHot16 e1, e2;
-    if (f1) e1 = mem.load_hot(r1.child_base());
-    if (f2) e2 = mem.load_hot(r2.child_base());
-    uint32_t pick = j1;
-    R rp = r1;
-    // Candidates with the first candidate's statistics have its f64 value exactly and come
-    // later, so they cannot be the first strict maximum: only candidates whose statistics
-    // differ need the f64 formula (ties of identical statistics are ~98 % of the two-
-    // candidate picks at C3).
-    uint32_t emask = 0;
+    // prefetch the chain end of the leading candidate if it is a forced chain head
+    const bool f1 = rm.forced();
+    NodeHot16 e1;
+    if (f1) e1 = mem.load_hot(rm.child_base());
+    uint32_t pick = jm;
+    R rp = rm;
+    // When every candidate has the leading one's statistics, their f64 values are equal and
+    // the first candidate wins, which is jm (equal statistics give equal estimates; the test
+    // jm == first candidate keeps this exact even where they would not).  Otherwise (0.09 %
+    // of the picks at C3) the reference's f64 formula decides among all candidates, first
+    // strict maximum.
+    uint32_t emask = jm != (uint32_t)ctz32(cmask) ? 1u : 0u;
     if (nc >= 2) {
 #pragma unroll
-        for (int j = 0; j < SCAN_REG; ++j) emask |= (((cmask >> j) & 1u) && R::at(b, j).key() != r1.key() ? 1u : 0u) << j;
+        for (int j = 0; j < SCAN_REG; ++j) emask |= (((cmask >> j) & 1u) && R::at(b, j).key() != rm.key() ? 1u : 0u) << j;
     }
     if (emask) {
         const double min_q = (double)wmin / (double)vmin, max_q = (double)wmax / (double)vmax;
-        emask |= 1u << j1;
-        if (nc == 2) {
-            const uint64_t s1 = r1.stats(), s2 = r2.stats();
-            const double u1 = uct_exact(s1, mean_of(s1), flat, min_q, max_q, lnN, c);
-            const double u2 = uct_exact(s2, mean_of(s2), flat, min_q, max_q, lnN, c);
-            if (u2 > u1) { pick = j2; rp = r2; }
-        } else {
-            double best = -INFINITY;
+        double best = -INFINITY;
 #pragma unroll
-            for (int j = 0; j < SCAN_REG; ++j) {
-                if ((emask >> j) & 1u) {
-                    const R r = R::at(b, j);
-                    const uint64_t sj = r.stats();
-                    const double u = uct_exact(sj, mean_of(sj), flat, min_q, max_q, lnN, c);
-                    if (u > best) { best = u; pick = (uint32_t)j; rp = r; }
-                }
+        for (int j = 0; j < SCAN_REG; ++j) {
+            if ((cmask >> j) & 1u) {
+                const R r = R::at(b, j);
+                const uint64_t sj = r.stats();
+                const double u = uct_exact(sj, mean_of(sj), flat, min_q, max_q, lnN, c);
+                if (u > best) { best = u; pick = (uint32_t)j; rp = r; }
             }
         }
     }
     *p_st = rp.stats(); *p_cb = rp.child_base(); *p_inf = rp.info();
-    *end_ok = (pick == j1 && f1) || (nc >= 2 && pick == j2 && f2);
-    if (pick == j1 && f1) *end = e1;
-    else if (nc >= 2 && pick == j2 && f2) *end = e2;
+    *end_ok = pick == jm && f1;
+    if (*end_ok) *end = e1;
     return pick;
 }
 
