@@ -224,6 +224,15 @@ struct Block {
     float isv[SCAN_REG];
 };
 
+// true if any active lane of the wave has p (host builds: p itself)
+DK_HD bool wave_any(bool p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_ballot_w64(p) != 0;
+#else
+    return p;
+#endif
+}
+
 // UCT pick over a register block (32-B records); returns the index and the picked node's
 // stats / child_base / info.  Bit-exact with the reference's first-strict-
 // maximum over f64 UCT values:
@@ -233,17 +242,20 @@ struct Block {
 //     B ~ 4e-7 * (2 + c*sqrt(ln N)) + 5e-7 (derivation in DESIGN.md);
 //  3. exact f64 UCT only for children whose estimate is within 2B (taken
 //     with a x3.7 safety factor) of the best estimate -- all others are
-//     strictly below the maximum -- first strict maximum among them.  The
-//     first two candidates are gathered with selects; more is rare and takes
-//     a full exact pass.
+//     strictly below the maximum -- first strict maximum among them, and only
+//     when their statistics differ (equal statistics: the first one wins).
+// Every scanned child has been visited (see pick_child_x).
 //
-// Chain-end prefetch: once the (usually one or two) candidates are known, the
-// chain ends of candidates that are expanded single-action nodes (forced chain
-// heads) are loaded while the exact evaluation runs; *end_ok tells whether
-// *end holds the picked child's chain end.
+// Chain-end prefetch: the chain end of the leading candidate, if it is an expanded
+// single-action node (a forced chain head), is loaded while the exact evaluation
+// runs; *end_ok tells whether *end holds the picked child's chain end.
 template <class Mem>
 DK_HD uint32_t pick_child_reg(const Block& b, uint32_t n, double lnN, double c, Mem& mem, uint64_t* p_st, uint32_t* p_cb,
                               uint32_t* p_inf, NodeHot32* end, bool* end_ok) {
+#if !defined(__HIP_DEVICE_COMPILE__)
+    for (uint32_t j = 0; j < n; ++j)
+        if ((uint32_t)b.st[j] == 0) { fprintf(stderr, "pick_child_reg: unvisited child\n"); abort(); }
+#endif
     double min_q = INFINITY, max_q = -INFINITY;
 #pragma unroll
     for (int j = 0; j < SCAN_REG; ++j) {
@@ -256,63 +268,55 @@ DK_HD uint32_t pick_child_reg(const Block& b, uint32_t n, double lnN, double c, 
     const bool flat = fabs(range) < DK_F64_EPSILON;
     const float inv_r = flat ? 0.0f : 2.0f * rcp_approx((float)range);
     const float ex = (float)c * sqrt_approx((float)lnN);
+    // the first maximum of the estimates, tracked with its record
     float ue[SCAN_REG];
     float umax = -INFINITY;
+    uint32_t jm = 0, cbm = b.cb[0], inm = b.inf[0];
+    uint64_t sm = b.st[0];
 #pragma unroll
     for (int j = 0; j < SCAN_REG; ++j) {
-        const float nq = flat ? 1.0f : (float)(b.q[j] - min_q) * inv_r - 1.0f;
-        const float u = (uint32_t)b.st[j] == 0 ? INFINITY : nq + ex * b.isv[j];
-        ue[j] = (uint32_t)j < n ? u : -INFINITY;
-        umax = ue[j] > umax ? ue[j] : umax;
+        ue[j] = -INFINITY;
+        if (wave_any((uint32_t)j < n)) {
+            const float nq = flat ? 1.0f : (float)(b.q[j] - min_q) * inv_r - 1.0f;
+            ue[j] = (uint32_t)j < n ? nq + ex * b.isv[j] : -INFINITY;
+            const bool gt = ue[j] > umax;
+            umax = gt ? ue[j] : umax;
+            jm = gt ? (uint32_t)j : jm;
+            sm = gt ? b.st[j] : sm; cbm = gt ? b.cb[j] : cbm; inm = gt ? b.inf[j] : inm;
+        }
     }
     const float cut = umax - 3e-6f * (3.0f + fabsf(ex));
-    uint64_t s1 = b.st[0], s2 = b.st[0];
-    double q1 = b.q[0], q2 = b.q[0];
-    uint32_t j1 = 0, j2 = 0, nc = 0, cb1 = b.cb[0], cb2 = b.cb[0], in1 = b.inf[0], in2 = b.inf[0];
+    uint32_t cmask = 0;
 #pragma unroll
-    for (int j = 0; j < SCAN_REG; ++j) {
-        const bool cj = ue[j] >= cut;   // implies j < n
-        const bool first = cj && nc == 0, second = cj && nc == 1;
-        s1 = first ? b.st[j] : s1; q1 = first ? b.q[j] : q1; j1 = first ? (uint32_t)j : j1;
-        cb1 = first ? b.cb[j] : cb1; in1 = first ? b.inf[j] : in1;
-        s2 = second ? b.st[j] : s2; q2 = second ? b.q[j] : q2; j2 = second ? (uint32_t)j : j2;
-        cb2 = second ? b.cb[j] : cb2; in2 = second ? b.inf[j] : in2;
-        nc += cj ? 1u : 0u;
+    for (int j = 0; j < SCAN_REG; ++j) cmask |= (ue[j] >= cut ? 1u : 0u) << j;   // implies j < n
+    const uint32_t nc = (uint32_t)popc32(cmask);
+    // prefetch the chain end of the leading candidate if it is a forced chain head
+    const bool f1 = ni_nchild(inm) == 1 && !ni_open(inm);
+    NodeHot32 e1;
+    if (f1) e1 = mem.load_hot(cbm);
+    // As in pick_child_x: candidates sharing the leader's statistics (equal f64 values, the
+    // first of them wins) need no exact evaluation; otherwise the f64 formula decides among
+    // all candidates, first strict maximum.
+    uint32_t pick = jm, pc = cbm, pi = inm;
+    uint64_t ps = sm;
+    uint32_t emask = jm != (uint32_t)ctz32(cmask) ? 1u : 0u;
+    if (nc >= 2) {
+#pragma unroll
+        for (int j = 0; j < SCAN_REG; ++j) emask |= (((cmask >> j) & 1u) && b.st[j] != sm ? 1u : 0u) << j;
     }
-    // prefetch the chain ends of forced candidates (their child_base is the chain end)
-    const bool f1 = ni_nchild(in1) == 1 && !ni_open(in1);
-    const bool f2 = nc >= 2 && ni_nchild(in2) == 1 && !ni_open(in2);
-    NodeHot32 e1, e2;
-    if (f1) e1 = mem.load_hot(cb1);
-    if (f2) e2 = mem.load_hot(cb2);
-    // a single candidate is the unique maximum: no exact evaluation needed
-    uint32_t pick = j1;
-    if (nc == 2) {
-        const double u1 = uct_exact(s1, q1, flat, min_q, max_q, lnN, c);
-        const double u2 = uct_exact(s2, q2, flat, min_q, max_q, lnN, c);
-        if (u2 > u1) pick = j2;
-    } else if (nc > 2) {
+    if (emask) {
         double best = -INFINITY;
 #pragma unroll
         for (int j = 0; j < SCAN_REG; ++j) {
-            if (ue[j] >= cut) {
+            if ((cmask >> j) & 1u) {
                 const double u = uct_exact(b.st[j], b.q[j], flat, min_q, max_q, lnN, c);
-                if (u > best) { best = u; pick = (uint32_t)j; }
+                if (u > best) { best = u; pick = (uint32_t)j; ps = b.st[j]; pc = b.cb[j]; pi = b.inf[j]; }
             }
         }
     }
-    uint64_t ps = b.st[0];
-    uint32_t pc = b.cb[0], pi = b.inf[0];
-#pragma unroll
-    for (int j = 1; j < SCAN_REG; ++j) {
-        ps = (uint32_t)j == pick ? b.st[j] : ps;
-        pc = (uint32_t)j == pick ? b.cb[j] : pc;
-        pi = (uint32_t)j == pick ? b.inf[j] : pi;
-    }
     *p_st = ps; *p_cb = pc; *p_inf = pi;
-    *end_ok = (pick == j1 && f1) || (nc >= 2 && pick == j2 && f2);
-    if (pick == j1 && f1) *end = e1;
-    else if (nc >= 2 && pick == j2 && f2) *end = e2;
+    *end_ok = pick == jm && f1;
+    if (*end_ok) *end = e1;
     return pick;
 }
 
@@ -369,14 +373,6 @@ DK_HD Raw16 sel_raw(bool p, const Raw16& a, const Raw16& b) { return Raw16{p ? a
 template <>
 DK_HD Raw8 sel_raw(bool p, const Raw8& a, const Raw8& b) { return Raw8{p ? a.w0 : b.w0, p ? a.w1 : b.w1}; }
 
-// true if any active lane of the wave has p (host builds: p itself)
-DK_HD bool wave_any(bool p) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    return __builtin_amdgcn_ballot_w64(p) != 0;
-#else
-    return p;
-#endif
-}
 
 // The pick for 8-B and 16-B records (no stored mean), bit-exact with the reference's first
 // strict maximum of the f64 UCT values (node.rs:238-277):

@@ -94,9 +94,7 @@ int main(int argc, char** argv) {
             rec[j].stats = (uint64_t)v | ((uint64_t)(uint32_t)s << 32);
             total += v;
         }
-#if !DK_HOT16
-        if (r() % 50 == 0) rec[r() % n].stats = 0;   // an unvisited child (pick_child_x never sees one)
-#endif
+        // (no unvisited child: the search's picks only scan visited children, checked there)
         for (uint32_t j = 0; j < n; ++j) rec[j] = dk::make_hot<dk::NodeHot>(rec[j].stats, 0, 0);   // as the backup leaves it
         const double lnN = std::log((double)(total + (uint32_t)(r() % 5)));
         const double c = (r() % 4 == 0) ? 0.7 + (double)(r() % 100) / 10.0 : 2.5;
