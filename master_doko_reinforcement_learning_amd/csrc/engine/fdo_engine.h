@@ -596,7 +596,9 @@ DK_HD int rollout_cards(const Work& w0, Rng& rng, int pts[4]) {
     uint32_t eyes = w0.eyes, ntr = w0.ntricks, doko = w0.doko;
     uint32_t fox_n = w0.fox_n, fox0 = w0.fox0, fox1 = w0.fox1, karl = w0.karl;
     // running evaluation of the current trick (cards already on the table replayed)
-    uint32_t lead = 0xFFFFFFu, best_pos = 0, win_card = 0, t_eyes = 0, da_n = 0, da0 = 0, da1 = 0;
+    // da_bits: players who played a Diamond Ace in the current trick (fox events are counted
+    // by the scoring, their order within a trick does not matter)
+    uint32_t lead = 0xFFFFFFu, best_pos = 0, win_card = 0, t_eyes = 0, da_bits = 0;
     int best_key = -2;
     for (uint32_t i = 0; i < trick_len; ++i) {
         const uint32_t c = (w0.trick_cards >> (8u * i)) & 0xFFu;
@@ -604,7 +606,7 @@ DK_HD int rollout_cards(const Work& w0, Rng& rng, int pts[4]) {
         const int k = key_fast(c, tm, lead);
         if (k > best_key) { best_key = k; best_pos = i; win_card = c; }
         t_eyes += eyes_fast(c);
-        if (c == (uint32_t)DIAMOND_ACE) { const uint32_t pl = (trick_start + i) & 3u; if (da_n == 0) da0 = pl; else da1 = pl; da_n += 1; }
+        if (c == (uint32_t)DIAMOND_ACE) da_bits |= 1u << ((trick_start + i) & 3u);
     }
     // a completed trick goes to its winner (complete_trick): eyes, trick count, Doppelkopf,
     // Diamond-Ace events in play order (fox0 / fox1), Karlchen, wedding resolution
@@ -613,12 +615,13 @@ DK_HD int rollout_cards(const Work& w0, Rng& rng, int pts[4]) {
         eyes += t_eyes << sh;
         ntr += 1u << sh;
         doko += (t_eyes >= 40u ? 1u : 0u) << sh;
-        if (da_n != 0u) {
-            const uint32_t e0 = (da0 << 2) | winner, e1 = (da1 << 2) | winner;
+        if (da_bits != 0u) {
+            const uint32_t rest = da_bits & (da_bits - 1u);
+            const uint32_t e0 = ((uint32_t)ctz32(da_bits) << 2) | winner;
             fox0 = fox_n == 0u ? e0 : fox0;
             fox1 = fox_n == 1u ? e0 : fox1;
             fox_n += 1u;
-            if (da_n == 2u) { fox1 = fox_n == 1u ? e1 : fox1; fox_n += 1u; }
+            if (rest != 0u) { fox1 = fox_n == 1u ? (((uint32_t)ctz32(rest) << 2) | winner) : fox1; fox_n += 1u; }
         }
         const uint32_t t = n_tricks - 1u;
         karl = (t == 11u && win_card == (uint32_t)CLUB_JACK) ? 1u + winner : karl;
@@ -659,11 +662,7 @@ DK_HD int rollout_cards(const Work& w0, Rng& rng, int pts[4]) {
         best_pos = better ? trick_len : best_pos;
         win_card = better ? card : win_card;
         t_eyes = (first ? 0u : t_eyes) + ((ci.x >> 24) & 15u);
-        da_n = first ? 0u : da_n;
-        const bool is_da = card == (uint32_t)DIAMOND_ACE;
-        da0 = (is_da && da_n == 0u) ? cur : da0;
-        da1 = (is_da && da_n == 1u) ? cur : da1;
-        da_n += is_da ? 1u : 0u;
+        da_bits = (first ? 0u : da_bits) | (card == (uint32_t)DIAMOND_ACE ? 1u << cur : 0u);
         trick_len += 1u;
         cur = (cur + 1u) & 3u;
         plies += 1;
@@ -692,7 +691,7 @@ DK_HD int rollout_cards(const Work& w0, Rng& rng, int pts[4]) {
             if (i == 0u) {
                 lead = ci.x & 0xFFFFFFu;
                 best_key = (int)ci.y; best = 0; win_card = card;
-                t_eyes = (ci.x >> 24) & 15u; da_n = 0;
+                t_eyes = (ci.x >> 24) & 15u; da_bits = 0;
             } else {
                 const int key = (((ci.x >> 28) & 1u) || ((lead >> card) & 1u)) ? (int)ci.y : -1;
                 const bool better = key > best_key;
@@ -701,10 +700,7 @@ DK_HD int rollout_cards(const Work& w0, Rng& rng, int pts[4]) {
                 win_card = better ? card : win_card;
                 t_eyes += (ci.x >> 24) & 15u;
             }
-            const bool is_da = card == (uint32_t)DIAMOND_ACE;
-            da0 = (is_da && da_n == 0u) ? p : da0;
-            da1 = (is_da && da_n == 1u) ? p : da1;
-            da_n += is_da ? 1u : 0u;
+            da_bits |= card == (uint32_t)DIAMOND_ACE ? 1u << p : 0u;
         }
         plies += 4;
         complete((s + best) & 3u);

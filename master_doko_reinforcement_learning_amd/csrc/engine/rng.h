@@ -46,25 +46,18 @@ struct Rng {
 
     DK_HD uint64_t next_u64() {
         const uint64_t res = rotl(s0 + s3, 23) + s0;
-        const uint64_t t = s1 << 17;
-        s2 ^= s0;
-        s3 ^= s1;
-        s1 ^= s2;
-        s0 ^= s3;
-        s2 ^= t;
-        s3 = rotl(s3, 45);
+        advance();
         return res;
     }
     DK_HD uint32_t next_u32() { return (uint32_t)(next_u64() >> 32); }
-    // state transition only (a draw whose value is discarded)
+    // state transition only (a draw whose value is discarded).  The reference's sequence
+    // s2 ^= s0; s3 ^= s1; s1 ^= s2; s0 ^= s3; s2 ^= t; s3 = rotl(s3, 45) written as
+    // three-input XORs of the old words (v_xor3_b32 per half)
     DK_HD void advance() {
         const uint64_t t = s1 << 17;
-        s2 ^= s0;
-        s3 ^= s1;
-        s1 ^= s2;
-        s0 ^= s3;
-        s2 ^= t;
-        s3 = rotl(s3, 45);
+        const uint64_t n0 = s0 ^ s3 ^ s1, n1 = s1 ^ s2 ^ s0, n2 = s2 ^ s0 ^ t, n3 = s3 ^ s1;
+        s0 = n0; s1 = n1; s2 = n2;
+        s3 = rotl(n3, 45);
     }
 
     // random_range(0..n) on u32 (n >= 1).
