@@ -165,6 +165,16 @@ def launch_ranks(args):
     return subprocess.call(cmd)
 
 
+def check_visits(v, iters, bufs, leg):
+    """Every root must have exactly `iterations` simulations; on failure name the roots."""
+    s = v.sum(axis=1)
+    bad = np.nonzero(s != iters)[0]
+    if len(bad):
+        best = bufs["best"].cpu().numpy()
+        detail = [(int(i), int(s[i]), int(best[i]), v[i].tolist()) for i in bad[:8]]
+        raise AssertionError("%s: %d roots without exactly %d simulations, first: %s" % (leg, len(bad), iters, detail))
+
+
 def timed_steps(step, steps, warmup, eng, L, dev, world, dist, ck, sp):
     """W untimed steps, then exactly K steps bracketed by barrier + synchronize; returns
     (max-over-ranks wall seconds, per-step search-kernel ms)."""
@@ -251,7 +261,7 @@ def main():
     if rank == 0 and args.dump_acc and bufs["acc"] is not None:
         np.save(args.dump_acc, bufs["acc"].cpu().numpy())
     v = visits.cpu().numpy()
-    assert np.all(v.sum(axis=1) == iters), "every root must have exactly `iterations` simulations"
+    check_visits(v, iters, bufs, "batch")
     sims_total = n_roots * iters * args.steps * world
     kernel_ms = float(np.mean(search_ms))
     del v, bufs, visits
@@ -265,7 +275,7 @@ def main():
         sa.infostates = args.small_infostates
         _, sstep, s_roots, sbufs = make_workload(sa, dk, L, dev, sp, rank, world, local_rank, dist, eng=eng)
         s_el, s_ms = timed_steps(sstep, args.small_steps, 1, eng, L, dev, world, dist, ck, sp)
-        assert np.all(sbufs["visits"].cpu().numpy().sum(axis=1) == iters)
+        check_visits(sbufs["visits"].cpu().numpy(), iters, sbufs, "small batch")
         small = {"infostates_per_gpu": args.small_infostates, "roots_per_gpu": s_roots, "steps": args.small_steps,
                  "value": s_roots * iters * args.small_steps * world / s_el, "unit": "rollouts/s",
                  "ms_per_step": s_el / args.small_steps * 1e3, "search_kernel_ms": float(np.mean(s_ms))}
