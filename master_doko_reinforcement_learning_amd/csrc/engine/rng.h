@@ -50,12 +50,23 @@ struct Rng {
         return res;
     }
     DK_HD uint32_t next_u32() { return (uint32_t)(next_u64() >> 32); }
+    // a ^ b ^ c (gfx950: one v_bitop3_b32 per half, truth table 0x96; the compiler splits a
+    // written three-way XOR into two-input XORs)
+    DK_HD static uint64_t xor3(uint64_t a, uint64_t b, uint64_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+        const uint32_t lo = __builtin_amdgcn_bitop3_b32((uint32_t)a, (uint32_t)b, (uint32_t)c, 0x96);
+        const uint32_t hi = __builtin_amdgcn_bitop3_b32((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32), 0x96);
+        return (uint64_t)hi << 32 | lo;
+#else
+        return a ^ b ^ c;
+#endif
+    }
     // state transition only (a draw whose value is discarded).  The reference's sequence
     // s2 ^= s0; s3 ^= s1; s1 ^= s2; s0 ^= s3; s2 ^= t; s3 = rotl(s3, 45) written as
-    // three-input XORs of the old words (v_xor3_b32 per half)
+    // three-input XORs of the old words
     DK_HD void advance() {
         const uint64_t t = s1 << 17;
-        const uint64_t n0 = s0 ^ s3 ^ s1, n1 = s1 ^ s2 ^ s0, n2 = s2 ^ s0 ^ t, n3 = s3 ^ s1;
+        const uint64_t n0 = xor3(s0, s3, s1), n1 = xor3(s1, s2, s0), n2 = xor3(s2, s0, t), n3 = s3 ^ s1;
         s0 = n0; s1 = n1; s2 = n2;
         s3 = rotl(n3, 45);
     }
