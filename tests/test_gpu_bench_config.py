@@ -171,3 +171,29 @@ def test_c2_bench_parity_1000(monkeypatch, capfd):
         seed = (i * 0x9E3779B97F4A7C15 + 1) & 0xFFFFFFFFFFFFFFFF
         best, v, val, _ = st.search(ol.rng_seed(seed), ITERS, args.c)
         _check_root(out["visits"][i], out["values"][i], out["best"][i], best, v, val, (i, ln))
+
+
+def test_c3_small_batch_parity(monkeypatch, capfd):
+    """C3's small-batch leg (bench.py --small-infostates: 512 infostates x 64 CAP samples =
+    32,768 roots): one group per wave, 32-root waves and the 32-B hot records the launch
+    picks when the grid gives a SIMD fewer than two waves.  Every root's visits sum to the
+    iterations, and roots spread over the batch match oracle searches bitwise."""
+    I, S = 512, 64
+    args, n_roots, out = _bench_workload(["--infostates", str(I), "--iterations", str(ITERS)], monkeypatch)
+    ln = _launch_line(capfd)
+    assert n_roots == I * S
+    assert ln["hot"] == "32B" and int(ln["rpw"]) == 32, ln
+    sums = out["visits"].astype(np.int64).sum(axis=1)
+    bad = np.nonzero(sums != ITERS)[0]
+    assert bad.size == 0, (bad[:16].tolist(), sums[bad[:16]].tolist())
+    rng = np.random.default_rng(512)
+    checked = 0
+    for j in sorted(set([0, 1, 255, 256, I - 2, I - 1] + rng.choice(I, size=6, replace=False).tolist())):
+        st = _fdo_info(j)
+        for s in sorted(set([0, 31, 32, S - 1] + rng.choice(S, size=2, replace=False).tolist())):
+            r = j * S + s
+            smp = st.card_matching(ol.rng_seed(0xC3200000 + j * S + s))
+            best, v, val, _ = smp.search(ol.rng_seed(0xC3300000 + j * S + s), ITERS, args.c)
+            _check_root(out["visits"][r], out["values"][r], out["best"][r], best, v, val, (j, s))
+            checked += 1
+    assert checked >= 48
