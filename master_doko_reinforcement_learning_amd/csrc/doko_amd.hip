@@ -185,7 +185,7 @@ __global__ void __launch_bounds__(WAVE, H::MIN_WAVES) search_kernel(const dk_sta
                                                       uint32_t iters, double c, const double* __restrict__ ln_table,
                                                       void* hot_pool, dk::NodeCold* cold, typename E::Node* states,
                                                       uint32_t* ovf, uint64_t* ovf_st,
-                                                      uint32_t cap_slots, uint32_t rpw, int lds_n,
+                                                      uint32_t cap_slots, uint32_t st_stride, uint32_t rpw, int lds_n,
                                                       uint32_t* visits, double* values,
                                                       uint8_t* best, int* err, uint32_t* queue, uint64_t* prof,
                                                       const uint32_t* __restrict__ order, uint32_t* retry,
@@ -223,8 +223,8 @@ __global__ void __launch_bounds__(WAVE, H::MIN_WAVES) search_kernel(const dk_sta
         const size_t wr = (size_t)blockIdx.x * rpw;
         mem.hot = reinterpret_cast<H*>(hot_pool) + wr * cap_slots;
         mem.cold = cold + wr * cap_slots;
-        mem.states = states + wr * T;
-        mem.lslot = lane * cap_slots; mem.lstate = lane * T; mem.lovf = lane * (uint32_t)dk::MAX_DEPTH;
+        mem.states = states + wr * st_stride;
+        mem.lslot = lane * cap_slots; mem.lstate = lane * st_stride; mem.lovf = lane * (uint32_t)dk::MAX_DEPTH;
         mem.path_st_off = path_st_base + lane;
         mem.path_off = path_base32 + lane;
         mem.ln_glob = ln_table;
@@ -708,6 +708,7 @@ struct dk_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     uint32_t max_roots = 0, max_iters = 0, cap_slots = 0;
+    uint32_t state_stride = 0;      // node-state records per lane region (>= max_iters + 1)
     uint32_t pool_roots = 0;        // roots the node pools hold at once (min(max_roots, DK_POOL_ROOTS or
                                     // the resident capacity: CUs x 12 single-wave workgroups x 64 lanes))
     int cu_count = 0;
@@ -873,6 +874,7 @@ hipError_t launch_search_t(dk_ctx* ctx, const dk_state* roots, const uint64_t* s
     }
     hipLaunchKernelGGL(kern, dim3(grid), dim3(WAVE), lds_bytes, st, roots, seeds, n, iters, c, ctx->ln_table,
                        ctx->hot, ctx->cold, (typename E::Node*)ctx->states, ctx->ovf, ctx->ovf_st, ctx->cap_slots,
+                       ctx->state_stride,
                        rpw, lp, visits, values, best, ctx->err, ctx->queue, ctx->prof,
                        ordered ? (const uint32_t*)ctx->order : (const uint32_t*)nullptr,
                        fallback ? ctx->retry : (uint32_t*)nullptr, (const uint32_t*)nullptr, ctx->high_water);
@@ -884,7 +886,7 @@ hipError_t launch_search_t(dk_ctx* ctx, const dk_state* roots, const uint64_t* s
     const uint32_t fb_grid = ctx->fb_roots / rpw;
     hipLaunchKernelGGL(kern, dim3(fb_grid), dim3(WAVE), lds_bytes, st, roots, seeds, n, iters, c, ctx->ln_table,
                        ctx->fb_hot, ctx->fb_cold, (typename E::Node*)ctx->fb_states, ctx->fb_ovf, ctx->fb_ovf_st,
-                       ctx->fb_slots, rpw, lp, visits, values, best, ctx->err, ctx->queue_fb, ctx->prof,
+                       ctx->fb_slots, ctx->state_stride, rpw, lp, visits, values, best, ctx->err, ctx->queue_fb, ctx->prof,
                        (const uint32_t*)nullptr, (uint32_t*)nullptr, (const uint32_t*)ctx->retry, ctx->high_water + 2);
     return hipGetLastError();
 }
@@ -995,12 +997,19 @@ dk_ctx* dk_create(const dk_config* cfg) {
     const uint32_t rpw = ctx->roots_per_wave;
     ctx->pool_roots = (uint32_t)((pool + rpw - 1) / rpw * rpw);   // whole regions of rpw roots
     const size_t R = ctx->pool_roots, S = ctx->cap_slots, T = (size_t)cfg->max_iterations + 1;
+    // node states per lane region (>= T): DK_STATE_STRIDE, else T
+    size_t ST = T;
+    if (const char* e = getenv("DK_STATE_STRIDE")) {
+        const long long v = atoll(e);
+        if (v >= (long long)T) ST = (size_t)v;
+    }
+    ctx->state_stride = (uint32_t)ST;
     bool ok = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) == hipSuccess;
     ok = ok && hipMalloc(&ctx->hot, R * S * sizeof(dk::NodeHot32)) == hipSuccess;
     ok = ok && hipMalloc(&ctx->cold, R * S * sizeof(dk::NodeCold)) == hipSuccess;
     ok = ok && hipMalloc(&ctx->ovf, R * dk::MAX_DEPTH * sizeof(uint32_t)) == hipSuccess;
     ok = ok && hipMalloc(&ctx->ovf_st, R * dk::MAX_DEPTH * sizeof(uint64_t)) == hipSuccess;
-    ok = ok && hipMalloc(&ctx->states, R * T * STATE_SLOT_BYTES) == hipSuccess;
+    ok = ok && hipMalloc(&ctx->states, R * ST * STATE_SLOT_BYTES) == hipSuccess;
     ok = ok && hipMalloc(&ctx->ln_table, (T + 1) * sizeof(double)) == hipSuccess;
     ok = ok && hipMalloc(&ctx->err, sizeof(int)) == hipSuccess;
     ok = ok && hipMalloc(&ctx->queue, sizeof(uint32_t)) == hipSuccess;
@@ -1018,8 +1027,8 @@ dk_ctx* dk_create(const dk_config* cfg) {
         ok = ok && hipMalloc(&ctx->fb_cold, FR * FS * sizeof(dk::NodeCold)) == hipSuccess;
         ok = ok && hipMalloc(&ctx->fb_ovf, FR * dk::MAX_DEPTH * sizeof(uint32_t)) == hipSuccess;
         ok = ok && hipMalloc(&ctx->fb_ovf_st, FR * dk::MAX_DEPTH * sizeof(uint64_t)) == hipSuccess;
-        ok = ok && hipMalloc(&ctx->fb_states, FR * T * STATE_SLOT_BYTES) == hipSuccess;
-        ctx->fb_bytes = FR * FS * (sizeof(dk::NodeHot32) + sizeof(dk::NodeCold)) + FR * T * STATE_SLOT_BYTES;
+        ok = ok && hipMalloc(&ctx->fb_states, FR * ST * STATE_SLOT_BYTES) == hipSuccess;
+        ctx->fb_bytes = FR * FS * (sizeof(dk::NodeHot32) + sizeof(dk::NodeCold)) + FR * ST * STATE_SLOT_BYTES;
     }
     ok = ok && hipMalloc(&ctx->order, ((size_t)cfg->max_roots + 1) * sizeof(uint32_t)) == hipSuccess;
     ok = ok && hipEventCreate(&ctx->ev0) == hipSuccess && hipEventCreate(&ctx->ev1) == hipSuccess;
@@ -1036,7 +1045,7 @@ dk_ctx* dk_create(const dk_config* cfg) {
     }
     ctx->p8_ok = ctx->cap_slots <= (1u << 14) && (ctx->fb_slots == 0 || ctx->fb_slots <= (1u << 14)) &&
                  ctx->cap_slots % 2 == 0 && ctx->fb_slots % 2 == 0;
-    ctx->pool_bytes = R * S * (sizeof(dk::NodeHot32) + sizeof(dk::NodeCold)) + R * T * STATE_SLOT_BYTES + ctx->fb_bytes;
+    ctx->pool_bytes = R * S * (sizeof(dk::NodeHot32) + sizeof(dk::NodeCold)) + R * ST * STATE_SLOT_BYTES + ctx->fb_bytes;
     if (!ok) { dk_destroy(ctx); return nullptr; }
     return ctx;
 }
