@@ -668,3 +668,32 @@ def test_az_selfplay_with_network(eng):
         for g in range(G):
             assert visits[g, a[g]] > 0
         dk.az_step(eng, recs, actions)
+
+
+@pytest.mark.parametrize("iters,env,hot", [(1023, {"DK_HOT_RECORD": "8"}, "8B"), (1024, {"DK_HOT_RECORD": "8"}, "16B"),
+                                           (4095, {"DK_HOT_RECORD": "16"}, "16B"), (4096, {"DK_HOT_RECORD": "16"}, "32B")])
+def test_search_record_width_limits(iters, env, hot, monkeypatch, capfd):
+    """The iteration limits of the packed hot records (search_core.h): 8-B records hold
+    <= 1023 iterations (11-bit visits, 10-bit state indices), 16-B records <= 4095 (24-bit
+    cross products); one iteration more takes the next wider layout even when a narrower
+    one is forced.  Roots at the limit equal oracle searches bitwise."""
+    import master_doko_reinforcement_learning_amd as dk
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    monkeypatch.setenv("DK_VERBOSE", "1")
+    e = dk.Engine(device=0, max_roots=16, max_iterations=iters)
+    try:
+        pool = [s for s in fdo_states(6, 41) if s.info()["phase"] != 3]
+        rng = np.random.default_rng(iters)
+        pick = [pool[i] for i in rng.choice(len(pool), size=6, replace=False)]
+        seeds = rng.integers(0, 2**63, size=len(pick), dtype=np.uint64)
+        visits, values, best = dk.CachedMCTS(e, dk.GAME_FULL_DOKO).monte_carlo_tree_search(pack_all(pick), 2.5, iters, seeds)
+        err = capfd.readouterr().err
+        lines = [l for l in err.splitlines() if l.startswith("doko_amd: search")]
+        assert lines and ("hot=%s" % hot) in lines[0], err[-1000:]
+        for i, (b, v, val) in enumerate(_oracle_search(pick, seeds, iters, 2.5, "fdo")):
+            assert sum(v) == iters and list(visits[i]) == v, i
+            assert values[i].tobytes() == np.array(val, dtype=np.float64).tobytes(), i
+            assert int(best[i]) == (b if b >= 0 else 255), i
+    finally:
+        e.close()
