@@ -342,8 +342,8 @@ def main():
                 "alg_bytes_per_sim": b_sim,
                 "stream_copy_peak_measured_gbs": stream_peak,
                 "valu": valu,
-                "note": "bound by VALU issue and divergence, not HBM bandwidth: PMC VALU busy %s of the launch, %s of "
-                        "wave cycles waiting on memory; achieved = the SURVEY 8(d) algorithmic bytes from the oracle's "
+                "note": "bound by VALU issue and the dependent latency of the per-lane tree walks, not HBM bandwidth: "
+                        "PMC VALU busy %s of the launch, %s of wave cycles waiting on memory; achieved = the SURVEY 8(d) algorithmic bytes from the oracle's "
                         "counters / event-timed kernel; traffic = 2*FETCH_SIZE+WRITE_SIZE from profiles/pmc_search.json "
                         "scaled per launch"
                         % ("%.0f%%" % (100 * valu["busy"]) if valu else "n/a",

@@ -570,12 +570,16 @@ DK_HD int round_draws(const Work& w) {
 }
 
 // Card phase to the end (w.phase == PH_PLAYCARD).  Returns plies played.
-// The trick is evaluated incrementally as its cards are played (running best
-// key = first strict maximum, eyes, Diamond-Ace players), so completing a trick
-// is a handful of register updates: with the lanes of a wave at different trick
-// positions, the wave no longer pays a full trick evaluation on most plies.
+// The trick is evaluated incrementally as its cards are played (running best key = first
+// strict maximum, eyes, Diamond-Ace players).  Hands are kept relative to the leader: after
+// the partial first trick (at most three plies, played with the absolute hands), A_k / T_k
+// hold the hand of player (trick_start + k) & 3 and the loop plays one whole trick per trip
+// -- four plies unrolled, so each ply's hand is a register known at compile time, no
+// per-ply player select or masked four-way update -- and rotates the hands by the winner's
+// position once per trick.  The lanes of a wave then complete their tricks in the same trip,
+// so the wave pays one trick completion per four plies.  Draw order, rewards and plies are
+// the reference's (state.rs:401-431; host check fdo_engine_check).
 DK_HD int rollout_cards(const Work& w0, Rng& rng, int pts[4]) {
-    // hands as "kinds held" / "kinds held twice" (removal takes the second copy first)
     uint32_t any0, any1, any2, any3, two0, two1, two2, two3;
     {
         const uint64_t h0 = w0.h[0], h1 = w0.h[1], h2 = w0.h[2], h3 = w0.h[3];
@@ -595,9 +599,6 @@ DK_HD int rollout_cards(const Work& w0, Rng& rng, int pts[4]) {
     uint32_t cur = w0.cur, trick_start = w0.trick_start, trick_len = w0.trick_len, n_tricks = w0.n_tricks;
     uint32_t eyes = w0.eyes, ntr = w0.ntricks, doko = w0.doko;
     uint32_t fox_n = w0.fox_n, fox0 = w0.fox0, fox1 = w0.fox1, karl = w0.karl;
-    // running evaluation of the current trick (cards already on the table replayed)
-    // da_bits: players who played a Diamond Ace in the current trick (fox events are counted
-    // by the scoring, their order within a trick does not matter)
     uint32_t lead = 0xFFFFFFu, best_pos = 0, win_card = 0, t_eyes = 0, da_bits = 0;
     int best_key = -2;
     for (uint32_t i = 0; i < trick_len; ++i) {
@@ -608,8 +609,6 @@ DK_HD int rollout_cards(const Work& w0, Rng& rng, int pts[4]) {
         t_eyes += eyes_fast(c);
         if (c == (uint32_t)DIAMOND_ACE) da_bits |= 1u << ((trick_start + i) & 3u);
     }
-    // a completed trick goes to its winner (complete_trick): eyes, trick count, Doppelkopf,
-    // Diamond-Ace events in play order (fox0 / fox1), Karlchen, wedding resolution
     auto complete = [&](uint32_t winner) {
         const uint32_t sh = 8u * winner;
         eyes += t_eyes << sh;
@@ -633,28 +632,17 @@ DK_HD int rollout_cards(const Work& w0, Rng& rng, int pts[4]) {
         }
     };
     int plies = 0;
-    // The loop stops at the start of the last trick, whose four plays are forced (one card
-    // per hand) and leave no announcement offer (thresholds are >= 4 cards, ann_theta), so the
-    // wave plays it once below in straight-line code instead of four more loop iterations.
-    const bool tail_only = n_tricks == 12u && trick_len == 0u;
-    if (!tail_only) for (;;) {
-        // ---- one card for `cur`
-        const uint32_t a = sel4u(any0, any1, any2, any3, cur);
-        const uint32_t t2 = sel4u(two0, two1, two2, two3, cur);
-        // (`lead` is all cards between tricks; in the last trick every hand holds one card)
+    // one card of player p, whose hand is (a, t2); updates the hand and the running trick
+    auto play = [&](uint32_t& a, uint32_t& t2, uint32_t p, bool first) {
         const uint32_t f = a & lead;
         const uint32_t legal = f ? f : a;
         const uint32_t r = rng.range_u32((uint32_t)popc32(legal));
-        // bit of rank r from the MSB = bit of rank popc-1-r from the LSB
         const uint32_t card = nth_set_bit24(legal, (uint32_t)popc32(legal) - 1u - r), bit = 1u << card;
         const bool dup = (t2 & bit) != 0u;
-        const uint32_t na = dup ? a : (a ^ bit), nt = dup ? (t2 ^ bit) : t2;
-        any0 = cur == 0u ? na : any0; any1 = cur == 1u ? na : any1; any2 = cur == 2u ? na : any2; any3 = cur == 3u ? na : any3;
-        two0 = cur == 0u ? nt : two0; two1 = cur == 1u ? nt : two1; two2 = cur == 2u ? nt : two2; two3 = cur == 3u ? nt : two3;
-        nb -= 1u << (8u * cur);
-        // ---- running trick evaluation (complete_trick, spread over the four cards)
+        a = dup ? a : (a ^ bit);
+        t2 = dup ? (t2 ^ bit) : t2;
+        nb -= 1u << (8u * p);
         const CardInfo ci = card_info(gt, card);
-        const bool first = trick_len == 0u;
         lead = first ? (ci.x & 0xFFFFFFu) : lead;
         const int key = (((ci.x >> 28) & 1u) || ((lead >> card) & 1u)) ? (int)ci.y : -1;
         const bool better = first || key > best_key;
@@ -662,30 +650,70 @@ DK_HD int rollout_cards(const Work& w0, Rng& rng, int pts[4]) {
         best_pos = better ? trick_len : best_pos;
         win_card = better ? card : win_card;
         t_eyes = (first ? 0u : t_eyes) + ((ci.x >> 24) & 15u);
-        da_bits = (first ? 0u : da_bits) | (card == (uint32_t)DIAMOND_ACE ? 1u << cur : 0u);
+        da_bits = (first ? 0u : da_bits) | (card == (uint32_t)DIAMOND_ACE ? 1u << p : 0u);
         trick_len += 1u;
-        cur = (cur + 1u) & 3u;
         plies += 1;
-        if (trick_len == 4u) {
-            const uint32_t winner = (trick_start + best_pos) & 3u;
-            complete(winner);
-            if (n_tricks == 12u) break;   // the rollout started within the last trick
-            cur = winner; trick_start = winner; trick_len = 0; n_tricks += 1u; lead = 0xFFFFFFu;
-            if (n_tricks == 12u) break;   // every hand holds one card: no offer, forced tail below
-        }
-        // ---- collapsed announcement round: one forced NoAnnouncement draw per offered player
+    };
+    // collapsed announcement round after a card: one forced draw per offered player
+    auto draws = [&]() {
         const uint32_t d = (uint32_t)popc32(((nb | 0x80808080u) - theta) & 0x80808080u);
         for (uint32_t i = 0; i < d; ++i) rng.advance();
         plies += (int)d;
+    };
+    bool done = false;
+    // the partial first trick, absolute hands (a wave runs at most three of these plies)
+    while (trick_len != 0u) {
+        uint32_t a = sel4u(any0, any1, any2, any3, cur), t2 = sel4u(two0, two1, two2, two3, cur);
+        play(a, t2, cur, false);
+        any0 = cur == 0u ? a : any0; any1 = cur == 1u ? a : any1; any2 = cur == 2u ? a : any2; any3 = cur == 3u ? a : any3;
+        two0 = cur == 0u ? t2 : two0; two1 = cur == 1u ? t2 : two1; two2 = cur == 2u ? t2 : two2; two3 = cur == 3u ? t2 : two3;
+        cur = (cur + 1u) & 3u;
+        if (trick_len == 4u) {
+            const uint32_t winner = (trick_start + best_pos) & 3u;
+            complete(winner);
+            if (n_tricks == 12u) { done = true; break; }   // the rollout started within the last trick
+            cur = winner; trick_start = winner; trick_len = 0; n_tricks += 1u; lead = 0xFFFFFFu;
+            if (n_tricks == 12u) break;                   // forced tail below
+        }
+        draws();
     }
-    if (n_tricks == 12u && trick_len == 0u) {
+    if (!done) {
+        // hands relative to trick_start (== cur between tricks)
+        const uint32_t s0 = trick_start;
+        uint32_t A0 = sel4u(any0, any1, any2, any3, s0), A1 = sel4u(any0, any1, any2, any3, (s0 + 1u) & 3u);
+        uint32_t A2 = sel4u(any0, any1, any2, any3, (s0 + 2u) & 3u), A3 = sel4u(any0, any1, any2, any3, (s0 + 3u) & 3u);
+        uint32_t T0 = sel4u(two0, two1, two2, two3, s0), T1 = sel4u(two0, two1, two2, two3, (s0 + 1u) & 3u);
+        uint32_t T2 = sel4u(two0, two1, two2, two3, (s0 + 2u) & 3u), T3 = sel4u(two0, two1, two2, two3, (s0 + 3u) & 3u);
+        while (n_tricks < 12u) {
+            const uint32_t s = trick_start;
+            play(A0, T0, s, true);
+            draws();
+            play(A1, T1, (s + 1u) & 3u, false);
+            draws();
+            play(A2, T2, (s + 2u) & 3u, false);
+            draws();
+            play(A3, T3, (s + 3u) & 3u, false);
+            const uint32_t bp = best_pos;
+            const uint32_t winner = (s + bp) & 3u;
+            complete(winner);
+            trick_start = winner; trick_len = 0; n_tricks += 1u; lead = 0xFFFFFFu;
+            // the winner leads: rotate the hands left by its position in the trick
+            const bool r1 = (bp & 1u) != 0u, r2 = (bp & 2u) != 0u;
+            uint32_t b0 = r1 ? A1 : A0, b1 = r1 ? A2 : A1, b2 = r1 ? A3 : A2, b3 = r1 ? A0 : A3;
+            A0 = r2 ? b2 : b0; A1 = r2 ? b3 : b1; A2 = r2 ? b0 : b2; A3 = r2 ? b1 : b3;
+            b0 = r1 ? T1 : T0; b1 = r1 ? T2 : T1; b2 = r1 ? T3 : T2; b3 = r1 ? T0 : T3;
+            T0 = r2 ? b2 : b0; T1 = r2 ? b3 : b1; T2 = r2 ? b0 : b2; T3 = r2 ? b1 : b3;
+            if (n_tricks == 12u) break;   // every hand holds one card: no offer, forced tail below
+            draws();
+        }
         // ---- the last trick: four forced plays from `trick_start`, one range(0..1) draw each
         const uint32_t s = trick_start;
         uint32_t best = 0;
+        const uint32_t hs[4] = {A0, A1, A2, A3};
 #pragma unroll
         for (uint32_t i = 0; i < 4u; ++i) {
             const uint32_t p = (s + i) & 3u;
-            const uint32_t card = (uint32_t)ctz32(sel4u(any0, any1, any2, any3, p));
+            const uint32_t card = (uint32_t)ctz32(hs[i]);
             rng.advance();
             const CardInfo ci = card_info(gt, card);
             if (i == 0u) {

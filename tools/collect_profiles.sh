@@ -2,6 +2,9 @@
 # Profiles committed under profiles/ (run on the GPU box):
 #   1. rocprofv3 --kernel-trace --stats over the default bench workload
 #   2. separate PMC passes (FETCH_SIZE, WRITE_SIZE, EA request counts) over one bench step
+#      of the dominant launch only (--small-infostates 0: twice, a counter pass left rows of
+#      the small-batch leg's visits overwritten with u64 words of 1000, never outside rocprofv3
+#      --pmc)
 set -u
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 TAG=${TAG:-r01}
@@ -18,7 +21,7 @@ for set in "FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TC
   i=$((i+1))
   echo "== pmc $i: $set"
   timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/pmc$i -o p --pmc $set -- \
-      python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline > $OUT/pmc$i.log 2>&1
+      python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --small-infostates 0 > $OUT/pmc$i.log 2>&1
   rc=$?; echo "rc=$rc"; [ $rc -ne 0 ] && { tail -20 $OUT/pmc$i.log; exit $rc; }
 done
 exit 0
