@@ -144,10 +144,11 @@ DK_HD int rollout_stepwise(Work w, Rng& rng, int pts[4]) {
 
 // Card phase to the end (w.phase == PH_PLAYCARD), the rs-doko counterpart of
 // fdo::rollout_cards: hands as "kinds held" / "kinds held twice" 24-bit masks
-// (which copy a removal takes is invisible to the rewards), per-player values
-// selected without register-array indexing, and the trick evaluated
-// incrementally as its cards are played (first strict maximum, eyes).  One
-// range draw per card, as random_single draws one even for a single option.
+// (which copy a removal takes is invisible to the rewards), the trick evaluated
+// incrementally as its cards are played (first strict maximum, eyes), and after the
+// partial first trick one whole trick per loop trip with the hands relative to the
+// leader (four plies unrolled, one rotation by the winner per trick).  One range draw
+// per card, as random_single draws one even for a single option.
 DK_HD int rollout_cards(const Work& w0, Rng& rng, int pts[4]) {
     uint32_t any0, any1, any2, any3, two0, two1, two2, two3;
     {
@@ -173,27 +174,16 @@ DK_HD int rollout_cards(const Work& w0, Rng& rng, int pts[4]) {
         t_eyes += fdo::eyes_fast(c);
     }
     int plies = 0;
-    for (;;) {
-        const uint32_t a = fdo::sel4u(any0, any1, any2, any3, cur);
-        const uint32_t t2 = fdo::sel4u(two0, two1, two2, two3, cur);
-        const uint32_t f = a & (trick_len == 0u ? 0xFFFFFFu : lead);
+    // one card of the player whose hand is (a, t2); updates the hand and the running trick
+    auto play = [&](uint32_t& a, uint32_t& t2, bool first) {
+        const uint32_t f = a & lead;
         const uint32_t legal = f ? f : a;
         const uint32_t r = rng.range_u32((uint32_t)popc32(legal));
-        uint32_t k = (uint32_t)popc32(legal) - 1u - r, pos = 0;   // rank r from the MSB
-#pragma unroll
-        for (int wdt = 16; wdt >= 1; wdt >>= 1) {
-            const uint32_t cnt = (uint32_t)popc32((legal >> pos) & ((1u << wdt) - 1u));
-            const bool hi = k >= cnt;
-            k = hi ? k - cnt : k;
-            pos = hi ? pos + (uint32_t)wdt : pos;
-        }
-        const uint32_t card = pos, bit = 1u << card;
+        const uint32_t card = fdo::nth_set_bit24(legal, (uint32_t)popc32(legal) - 1u - r), bit = 1u << card;
         const bool dup = (t2 & bit) != 0u;
-        const uint32_t na = dup ? a : (a ^ bit), nt = dup ? (t2 ^ bit) : t2;
-        any0 = cur == 0u ? na : any0; any1 = cur == 1u ? na : any1; any2 = cur == 2u ? na : any2; any3 = cur == 3u ? na : any3;
-        two0 = cur == 0u ? nt : two0; two1 = cur == 1u ? nt : two1; two2 = cur == 2u ? nt : two2; two3 = cur == 3u ? nt : two3;
+        a = dup ? a : (a ^ bit);
+        t2 = dup ? (t2 ^ bit) : t2;
         const fdo::CardInfo ci = fdo::card_info(fdo::GT_NORMAL, card);
-        const bool first = trick_len == 0u;
         lead = first ? (ci.x & 0xFFFFFFu) : lead;
         const int key = (((ci.x >> 28) & 1u) || ((lead >> card) & 1u)) ? (int)ci.y : -1;
         const bool better = first || key > best_key;
@@ -201,19 +191,54 @@ DK_HD int rollout_cards(const Work& w0, Rng& rng, int pts[4]) {
         best_pos = better ? trick_len : best_pos;
         t_eyes = (first ? 0u : t_eyes) + ((ci.x >> 24) & 15u);
         trick_len += 1u;
-        cur = (cur + 1u) & 3u;
         plies += 1;
+    };
+    auto complete = [&](uint32_t winner) {
+        eyes += t_eyes << (8u * winner);
+        ntr += 1u << (8u * winner);
+        if (team_kind == fdo::TK_WED_UNSOLVED && t_idx < 3u && (winner != wedding_player || t_idx == 2u)) {
+            team_kind = fdo::TK_WED_SOLVED;
+            re_players = (1u << wedding_player) | (winner != wedding_player ? 1u << winner : 0u);
+        }
+        t_idx += 1u;
+    };
+    bool done = false;
+    // the partial first trick, absolute hands (a wave runs at most three of these plies)
+    while (trick_len != 0u) {
+        uint32_t a = fdo::sel4u(any0, any1, any2, any3, cur), t2 = fdo::sel4u(two0, two1, two2, two3, cur);
+        play(a, t2, false);
+        any0 = cur == 0u ? a : any0; any1 = cur == 1u ? a : any1; any2 = cur == 2u ? a : any2; any3 = cur == 3u ? a : any3;
+        two0 = cur == 0u ? t2 : two0; two1 = cur == 1u ? t2 : two1; two2 = cur == 2u ? t2 : two2; two3 = cur == 3u ? t2 : two3;
+        cur = (cur + 1u) & 3u;
         if (trick_len == 4u) {
             const uint32_t winner = (trick_start + best_pos) & 3u;
-            eyes += t_eyes << (8u * winner);
-            ntr += 1u << (8u * winner);
-            if (team_kind == fdo::TK_WED_UNSOLVED && t_idx < 3u && (winner != wedding_player || t_idx == 2u)) {
-                team_kind = fdo::TK_WED_SOLVED;
-                re_players = (1u << wedding_player) | (winner != wedding_player ? 1u << winner : 0u);
-            }
-            t_idx += 1u;
+            complete(winner);
+            if (t_idx == 12u) { done = true; break; }
+            cur = winner; trick_start = winner; trick_len = 0; lead = 0xFFFFFFu;
+        }
+    }
+    if (!done) {
+        const uint32_t s0 = trick_start;
+        uint32_t A0 = fdo::sel4u(any0, any1, any2, any3, s0), A1 = fdo::sel4u(any0, any1, any2, any3, (s0 + 1u) & 3u);
+        uint32_t A2 = fdo::sel4u(any0, any1, any2, any3, (s0 + 2u) & 3u), A3 = fdo::sel4u(any0, any1, any2, any3, (s0 + 3u) & 3u);
+        uint32_t T0 = fdo::sel4u(two0, two1, two2, two3, s0), T1 = fdo::sel4u(two0, two1, two2, two3, (s0 + 1u) & 3u);
+        uint32_t T2 = fdo::sel4u(two0, two1, two2, two3, (s0 + 2u) & 3u), T3 = fdo::sel4u(two0, two1, two2, two3, (s0 + 3u) & 3u);
+        for (;;) {
+            play(A0, T0, true);
+            play(A1, T1, false);
+            play(A2, T2, false);
+            play(A3, T3, false);
+            const uint32_t bp = best_pos;
+            const uint32_t winner = (trick_start + bp) & 3u;
+            complete(winner);
             if (t_idx == 12u) break;
-            cur = winner; trick_start = winner; trick_len = 0;
+            trick_start = winner; trick_len = 0; lead = 0xFFFFFFu;
+            // the winner leads: rotate the hands left by its position in the trick
+            const bool r1 = (bp & 1u) != 0u, r2 = (bp & 2u) != 0u;
+            uint32_t b0 = r1 ? A1 : A0, b1 = r1 ? A2 : A1, b2 = r1 ? A3 : A2, b3 = r1 ? A0 : A3;
+            A0 = r2 ? b2 : b0; A1 = r2 ? b3 : b1; A2 = r2 ? b0 : b2; A3 = r2 ? b1 : b3;
+            b0 = r1 ? T1 : T0; b1 = r1 ? T2 : T1; b2 = r1 ? T3 : T2; b3 = r1 ? T0 : T3;
+            T0 = r2 ? b2 : b0; T1 = r2 ? b3 : b1; T2 = r2 ? b0 : b2; T3 = r2 ? b1 : b3;
         }
     }
     Work fin = w0;
