@@ -62,6 +62,9 @@ def parse():
     p.add_argument("--small-infostates", type=int, default=512,
                    help="c3: also time the survey's small decision batch (512 infostates x 64 = 32,768 roots); 0 = skip")
     p.add_argument("--small-steps", type=int, default=5)
+    p.add_argument("--host-readback-check", action="store_true",
+                   help="also copy every leg's visits to pageable host memory and check them there (the round-2 "
+                        "sequence); a host-only violation is reported as host_copy_bad_roots, not raised")
     a = p.parse_args()
     if a.infostates is None:
         a.infostates = 18432 if a.workload == "c3" else 12288   # c2d: 2.18 G/s at 18432 against 2.24 at 12288
@@ -165,14 +168,40 @@ def launch_ranks(args):
     return subprocess.call(cmd)
 
 
-def check_visits(v, iters, bufs, leg):
-    """Every root must have exactly `iterations` simulations; on failure name the roots."""
-    s = v.sum(axis=1)
-    bad = np.nonzero(s != iters)[0]
-    if len(bad):
+def result_invariants(visits, best, iters):
+    """Per-root invariants of a search result, evaluated ON THE DEVICE (torch ops on the
+    current stream): the visits row sums to `iterations` (every simulation passes one root
+    child, mcts.rs:172-249), and `best` is an action of maximal visits (max_by_key over the
+    root children, mcts_policy.rs:95-111).  Returns a bool tensor, True = violated."""
+    import torch
+    s = visits.sum(dim=1, dtype=torch.int64)
+    mx = visits.max(dim=1).values
+    b = best.long()
+    vb = torch.gather(visits, 1, b.clamp(max=38)[:, None])[:, 0]
+    return (s != iters) | (b > 38) | (vb != mx)
+
+
+def check_visits(bufs, iters, leg):
+    """Check every root of a leg with `result_invariants` on the device.  On a violation the
+    device buffers are read back twice and compared, so the report says whether the DEVICE
+    data is wrong or only a host copy of it (the round-2 failure under
+    `rocprofv3 --pmc` was a stale pageable host copy, not a device write)."""
+    bad = result_invariants(bufs["visits"], bufs["best"], iters)
+    nbad = int(bad.sum().item())
+    if nbad:
+        idx = bad.nonzero()[:8, 0].cpu().numpy()
+        v1, v2 = bufs["visits"].cpu().numpy(), bufs["visits"].cpu().numpy()
         best = bufs["best"].cpu().numpy()
-        detail = [(int(i), int(s[i]), int(best[i]), v[i].tolist()) for i in bad[:8]]
-        raise AssertionError("%s: %d roots without exactly %d simulations, first: %s" % (leg, len(bad), iters, detail))
+        detail = [(int(i), int(v1[i].sum()), int(best[i]), v1[i].tolist()) for i in idx]
+        raise AssertionError("%s: %d roots violate the result invariants on the device (visit sum %d, best = an "
+                             "argmax); two host reads identical: %s; first: %s"
+                             % (leg, nbad, iters, bool(np.array_equal(v1, v2)), detail))
+
+
+def check_visits_host(v, iters, leg):
+    """The same row-sum invariant on a host copy (reported separately from the device check)."""
+    s = v.astype(np.int64).sum(axis=1)
+    return np.nonzero(s != iters)[0]
 
 
 def timed_steps(step, steps, warmup, eng, L, dev, world, dist, ck, sp):
@@ -260,11 +289,13 @@ def main():
         np.save(args.dump_actions, bufs["actions"].cpu().numpy())
     if rank == 0 and args.dump_acc and bufs["acc"] is not None:
         np.save(args.dump_acc, bufs["acc"].cpu().numpy())
-    v = visits.cpu().numpy()
-    check_visits(v, iters, bufs, "batch")
+    check_visits(bufs, iters, "batch")
+    host_bad = {}
+    if args.host_readback_check:
+        host_bad["batch"] = check_visits_host(visits.cpu().numpy(), iters, "batch").size
     sims_total = n_roots * iters * args.steps * world
     kernel_ms = float(np.mean(search_ms))
-    del v, bufs, visits
+    del bufs, visits
 
     # the survey's C3 decision batch (512 infostates x 64 samples = 32,768 roots): the regime a
     # DefaultImpiPolicy caller with one decision batch per game step sees (same engine, own buffers)
@@ -275,7 +306,9 @@ def main():
         sa.infostates = args.small_infostates
         _, sstep, s_roots, sbufs = make_workload(sa, dk, L, dev, sp, rank, world, local_rank, dist, eng=eng)
         s_el, s_ms = timed_steps(sstep, args.small_steps, 1, eng, L, dev, world, dist, ck, sp)
-        check_visits(sbufs["visits"].cpu().numpy(), iters, sbufs, "small batch")
+        check_visits(sbufs, iters, "small batch")
+        if args.host_readback_check:
+            host_bad["small"] = check_visits_host(sbufs["visits"].cpu().numpy(), iters, "small batch").size
         small = {"infostates_per_gpu": args.small_infostates, "roots_per_gpu": s_roots, "steps": args.small_steps,
                  "value": s_roots * iters * args.small_steps * world / s_el, "unit": "rollouts/s",
                  "ms_per_step": s_el / args.small_steps * 1e3, "search_kernel_ms": float(np.mean(s_ms))}
@@ -351,6 +384,7 @@ def main():
             },
             "node_pools": pools,
             "small_batch": small,
+            "host_copy_bad_roots": host_bad or None,
             "ranks": world,
             "dist_backend": backend if world > 1 else None,
             "cpu_baseline": cpu,

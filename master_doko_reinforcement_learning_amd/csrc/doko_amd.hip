@@ -189,7 +189,8 @@ __global__ void __launch_bounds__(WAVE, H::MIN_WAVES) search_kernel(const dk_sta
                                                       uint32_t* visits, double* values,
                                                       uint8_t* best, int* err, uint32_t* queue, uint64_t* prof,
                                                       const uint32_t* __restrict__ order, uint32_t* retry,
-                                                      const uint32_t* __restrict__ list, uint32_t* high_water) {
+                                                      const uint32_t* __restrict__ list, uint32_t* high_water,
+                                                      const uint32_t* __restrict__ perm) {
     const uint32_t lane = threadIdx.x;
     const uint32_t T = iters + 1;
     const uint32_t n_ln = LN_LDS ? T : 0u;
@@ -214,7 +215,7 @@ __global__ void __launch_bounds__(WAVE, H::MIN_WAVES) search_kernel(const dk_sta
         if (order) g = order[g];                                        // longest groups first
         const uint32_t idx = g * rpw + lane;
         if (lane >= rpw || idx >= n) continue;
-        const uint32_t root = list ? list[1 + idx] : idx;
+        const uint32_t root = list ? list[1 + idx] : perm ? perm[idx] : idx;   // perm: depth-sorted order
         typename E::Work w;
         E::load(roots[root], w);
         dk::Rng rng = dk::Rng::seed_from_u64(seeds[root]);
@@ -625,12 +626,12 @@ __global__ void ar_output_kernel(const dk_az_state* info, uint32_t samples, uint
 // groups (longest-processing-time-first).  Roots are independent, so the order changes no
 // result.  One workgroup: a 64-bin counting sort (order within a bin is arbitrary).
 __global__ void __launch_bounds__(1024) group_order_kernel(const dk_state* roots, uint32_t n, uint32_t rpw,
-                                                           uint32_t groups, uint32_t* order) {
+                                                           uint32_t groups, uint32_t* order, const uint32_t* perm) {
     __shared__ uint32_t hist[64];
     if (threadIdx.x < 64) hist[threadIdx.x] = 0;
     __syncthreads();
     auto key = [&](uint32_t g) {
-        const uint32_t ci = roots[(size_t)g * rpw].fdo.card_index;
+        const uint32_t ci = roots[perm ? perm[(size_t)g * rpw] : (size_t)g * rpw].fdo.card_index;
         return 63u - (ci < 48u ? 48u - ci : 0u);   // ascending key = descending cards left
     };
     for (uint32_t g = threadIdx.x; g < groups; g += blockDim.x) atomicAdd(&hist[key(g)], 1u);
@@ -642,6 +643,64 @@ __global__ void __launch_bounds__(1024) group_order_kernel(const dk_state* roots
     __syncthreads();
     for (uint32_t g = threadIdx.x; g < groups; g += blockDim.x) order[atomicAdd(&hist[key(g)], 1u)] = g;
     (void)n;
+}
+
+// Depth-homogeneous waves.  A wave pays for the union of its lanes' instruction streams:
+// roots of different depths (cards left) in one wave pay the selection of the deep ones
+// AND the rollouts of the shallow ones.  A batch whose 64-root groups mix depths (the
+// samples of several infostates per group, e.g. one rank's share of a sample-split batch)
+// is therefore searched through a permutation: within each window of W consecutive roots,
+// a STABLE counting sort by cards left (most first).  Root i of the launch order is
+// perm[i]; results stay indexed by root, so the order changes no value.  One 256-thread
+// workgroup per window; stable ranks per 64-root chunk from wave ballots.
+constexpr uint32_t ROOT_SORT_MAX_WINDOW = 4096;
+constexpr uint32_t ROOT_SORT_BINS = 49;   // card_index 0..48 (48 = finished)
+__global__ void __launch_bounds__(256) root_sort_kernel(const dk_state* roots, uint32_t n, uint32_t window,
+                                                        uint32_t* perm) {
+    __shared__ uint32_t cnt[ROOT_SORT_MAX_WINDOW / 64][ROOT_SORT_BINS];   // per-chunk counts -> chunk prefixes
+    __shared__ uint32_t base[ROOT_SORT_BINS];
+    const uint32_t start = blockIdx.x * window;
+    const uint32_t len = n - start < window ? n - start : window;
+    const uint32_t chunks = (len + 63) / 64;
+    const uint32_t wv = threadIdx.x / 64, lane = threadIdx.x % 64;
+    for (uint32_t t = threadIdx.x; t < chunks * ROOT_SORT_BINS; t += blockDim.x) cnt[t / ROOT_SORT_BINS][t % ROOT_SORT_BINS] = 0;
+    __syncthreads();
+    auto key_of = [&](uint32_t i) {
+        const uint32_t ci = roots[start + i].fdo.card_index;
+        return ci < 48u ? ci : 48u;
+    };
+    for (uint32_t c = wv; c < chunks; c += blockDim.x / 64) {
+        const uint32_t i = c * 64 + lane;
+        if (i < len) atomicAdd(&cnt[c][key_of(i)], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < ROOT_SORT_BINS) {   // exclusive prefix over the chunks, per bin
+        uint32_t s = 0;
+        for (uint32_t c = 0; c < chunks; ++c) { const uint32_t v = cnt[c][threadIdx.x]; cnt[c][threadIdx.x] = s; s += v; }
+        base[threadIdx.x] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {               // exclusive prefix over the bins (ascending card_index = most cards left first)
+        uint32_t s = 0;
+        for (uint32_t b = 0; b < ROOT_SORT_BINS; ++b) { const uint32_t v = base[b]; base[b] = s; s += v; }
+    }
+    __syncthreads();
+    for (uint32_t c = wv; c < chunks; c += blockDim.x / 64) {
+        const uint32_t i = c * 64 + lane;
+        const bool live = i < len;
+        const uint32_t k = live ? key_of(i) : 0xFFFFFFFFu;
+        const uint64_t lt = lane ? (~0ULL >> (64 - lane)) : 0ULL;
+        uint32_t rank = 0;
+        uint64_t todo = __ballot(live);
+        while (todo) {                    // one ballot per distinct key in the chunk
+            const uint32_t src = (uint32_t)__builtin_ctzll(todo);
+            const uint32_t kk = (uint32_t)__shfl((int)k, (int)src);
+            const uint64_t m = __ballot(live && k == kk);
+            if (live && k == kk) rank = (uint32_t)__builtin_popcountll(m & lt);
+            todo &= ~m;
+        }
+        if (live) perm[start + base[k] + cnt[c][k] + rank] = start + i;
+    }
 }
 
 // `valid` (nullable): per-sample flags; samples with valid == 0 (failed determinizations,
@@ -730,6 +789,10 @@ struct dk_ctx {
     uint32_t fb_slots = 0, fb_roots = 0;
     uint64_t fb_bytes = 0;
     uint32_t* order = nullptr;      // queue order of the root groups (group_order_kernel)
+    uint32_t* perm = nullptr;       // depth-sorted root order (root_sort_kernel)
+    uint32_t root_window = 1024;    // roots per depth-sort window (DK_ROOT_WINDOW; 0 = launch order = root order):
+                                    // one rank's share of C4 at N = 8 (8 samples per infostate) 410 -> 389 ms,
+                                    // C3 at N = 1 unchanged (381 / 382 ms); 4096 reorders C3's groups (+2.4 %)
     int group_order = -1;           // DK_GROUP_ORDER=0 / 1 forces index order / longest-first; -1: per engine
     void* hot = nullptr;            // hot records, 32 B per slot (NodeHot16 launches use half)
     dk::NodeCold* cold = nullptr;
@@ -854,15 +917,24 @@ hipError_t launch_search_t(dk_ctx* ctx, const dk_state* roots, const uint64_t* s
     grid = grid < regions ? grid : regions;
     if (grid == 0) return hipErrorInvalidValue;
     if (ctx->verbose)
-        fprintf(stderr, "doko_amd: search n=%u rpw=%u hot=%dB lds_path=%d lds=%zuB resident/CU=%d grid=%u\n", n, rpw,
-                (int)sizeof(H), lp, lds_bytes, per_cu, grid);
+        fprintf(stderr, "doko_amd: search n=%u rpw=%u hot=%dB lds_path=%d lds=%zuB resident/CU=%d grid=%u root_window=%u\n",
+                n, rpw, (int)sizeof(H), lp, lds_bytes, per_cu, grid, ctx->root_window);
     hipError_t e = hipMemsetAsync(ctx->queue, 0, sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
     // group order only matters when waves take several groups each
     const bool want = ctx->group_order < 0 ? E::ORDER_GROUPS : ctx->group_order == 1;
+    // depth-homogeneous waves (root_sort_kernel) when the batch has several groups
+    const uint32_t W = ctx->root_window;
+    const bool sorted = W && E::GAME != DK_GAME_TTT && groups > 1;
+    if (sorted) {
+        hipLaunchKernelGGL(root_sort_kernel, dim3(grid_for(n, W)), dim3(256), 0, st, roots, n, W, ctx->perm);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    const uint32_t* perm = sorted ? (const uint32_t*)ctx->perm : (const uint32_t*)nullptr;
     const bool ordered = want && E::GAME != DK_GAME_TTT && groups > grid;
     if (ordered) {
-        hipLaunchKernelGGL(group_order_kernel, dim3(1), dim3(1024), 0, st, roots, n, rpw, groups, ctx->order);
+        hipLaunchKernelGGL(group_order_kernel, dim3(1), dim3(1024), 0, st, roots, n, rpw, groups, ctx->order, perm);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -877,7 +949,7 @@ hipError_t launch_search_t(dk_ctx* ctx, const dk_state* roots, const uint64_t* s
                        ctx->state_stride,
                        rpw, lp, visits, values, best, ctx->err, ctx->queue, ctx->prof,
                        ordered ? (const uint32_t*)ctx->order : (const uint32_t*)nullptr,
-                       fallback ? ctx->retry : (uint32_t*)nullptr, (const uint32_t*)nullptr, ctx->high_water);
+                       fallback ? ctx->retry : (uint32_t*)nullptr, (const uint32_t*)nullptr, ctx->high_water, perm);
     e = hipGetLastError();
     if (e != hipSuccess || !fallback) return e;
     // Second pass over the roots the main pool could not hold (retry[0] of them; the grid
@@ -887,7 +959,8 @@ hipError_t launch_search_t(dk_ctx* ctx, const dk_state* roots, const uint64_t* s
     hipLaunchKernelGGL(kern, dim3(fb_grid), dim3(WAVE), lds_bytes, st, roots, seeds, n, iters, c, ctx->ln_table,
                        ctx->fb_hot, ctx->fb_cold, (typename E::Node*)ctx->fb_states, ctx->fb_ovf, ctx->fb_ovf_st,
                        ctx->fb_slots, ctx->state_stride, rpw, lp, visits, values, best, ctx->err, ctx->queue_fb, ctx->prof,
-                       (const uint32_t*)nullptr, (uint32_t*)nullptr, (const uint32_t*)ctx->retry, ctx->high_water + 2);
+                       (const uint32_t*)nullptr, (uint32_t*)nullptr, (const uint32_t*)ctx->retry, ctx->high_water + 2,
+                       (const uint32_t*)nullptr);
     return hipGetLastError();
 }
 
@@ -976,6 +1049,10 @@ dk_ctx* dk_create(const dk_config* cfg) {
         if (v >= 1 && v <= WAVE) { ctx->roots_per_wave = (uint32_t)v; ctx->rpw_fixed = true; }
     }
     if (const char* e = getenv("DK_GROUP_ORDER")) ctx->group_order = atoi(e) != 0 ? 1 : 0;
+    if (const char* e = getenv("DK_ROOT_WINDOW")) {
+        const long v = atol(e);
+        if (v >= 0 && v <= (long)ROOT_SORT_MAX_WINDOW) ctx->root_window = (uint32_t)v;
+    }
     if (const char* e = getenv("DK_HOT_RECORD")) {
         const int v = atoi(e);
         if (v == 8 || v == 16 || v == 32) ctx->hot_layout = v;
@@ -1031,6 +1108,7 @@ dk_ctx* dk_create(const dk_config* cfg) {
         ctx->fb_bytes = FR * FS * (sizeof(dk::NodeHot32) + sizeof(dk::NodeCold)) + FR * ST * STATE_SLOT_BYTES;
     }
     ok = ok && hipMalloc(&ctx->order, ((size_t)cfg->max_roots + 1) * sizeof(uint32_t)) == hipSuccess;
+    ok = ok && hipMalloc(&ctx->perm, (size_t)cfg->max_roots * sizeof(uint32_t)) == hipSuccess;
     ok = ok && hipEventCreate(&ctx->ev0) == hipSuccess && hipEventCreate(&ctx->ev1) == hipSuccess;
 #ifdef DK_PHASE_PROF
     ok = ok && hipMalloc(&ctx->prof, (size_t)cfg->max_roots * 16 * sizeof(uint64_t)) == hipSuccess;
@@ -1067,6 +1145,7 @@ void dk_destroy(dk_ctx* ctx) {
                     (void*)ctx->fb_ovf, (void*)ctx->fb_ovf_st, ctx->fb_states})
         if (p) (void)hipFree(p);
     if (ctx->order) (void)hipFree(ctx->order);
+    if (ctx->perm) (void)hipFree(ctx->perm);
     if (ctx->prof) (void)hipFree(ctx->prof);
     if (ctx->az_nodes) (void)hipFree(ctx->az_nodes);
     if (ctx->ar_lanes) (void)hipFree(ctx->ar_lanes);

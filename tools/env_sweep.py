@@ -9,7 +9,7 @@ A variant may name its own build with LIB=<file in the package dir> (libraries l
 side, as tools/ab_inproc.py does).
 
 usage: python tools/env_sweep.py "A=DK_POOL_CONTIG=0" "B=DK_POOL_CONTIG=1,LIB=libdoko_amd_x.so" [--contexts 4]
-       [--infostates 18432] [--reps 3]
+       [--infostates 18432] [--samples 64] [--reps 3]
 """
 import argparse
 import ctypes
@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--contexts", type=int, default=4)
     ap.add_argument("--infostates", type=int, default=18432)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--samples", type=int, default=64, help="samples per infostate (8 = one rank's share at N = 8)")
     ap.add_argument("--no-check", action="store_true", help="speed-of-light variants: results may differ")
     a = ap.parse_args()
     import torch
@@ -47,7 +48,7 @@ def main():
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     sp = stream.cuda_stream
-    I, S, iters = a.infostates, 64, 1000
+    I, S, iters = a.infostates, a.samples, 1000
     n = I * S
     roots, d_srch = c3_roots(dk, L, dev, sp, I, S)
     v = torch.zeros((n, 39), dtype=torch.int32, device=dev)
