@@ -321,8 +321,9 @@ def main():
             cpu = cpu_baseline(args, dk)
         b_sim = alg_bytes_per_sim(args.workload)
         achieved = n_roots * iters * b_sim / (kernel_ms / 1e3) / 1e9 if b_sim else None
-        traffic = pmc_traffic(n_roots, iters) if args.workload == "c3" else None
-        valu = pmc_valu() if args.workload == "c3" else None
+        pmc_path = pmc_summary_path(args.workload)
+        traffic = pmc_traffic(n_roots, iters, pmc_path)
+        valu = pmc_valu(pmc_path)
         workload_desc = {
             "c3": "C3 rs-full-doko determinized UCT: %d infostates x %d CAP samples/GPU-share, %d roots x %d sims per GPU"
                   % (I, args.samples, n_roots, iters),
@@ -363,9 +364,10 @@ def main():
             "kernel_only_rollouts_per_s": n_roots * iters * world / (kernel_ms / 1e3),
             "search_kernel_ms": kernel_ms,
             "roofline": {
-                # the binding resource is VALU issue (PMC below); achieved/peak/frac are the
-                # north-star's HBM figures: algorithmic bytes / event-timed kernel vs 8 TB/s
-                "bound": "valu",
+                # achieved/peak/frac: the north-star's HBM figures, algorithmic bytes / event-timed
+                # kernel vs 8 TB/s; traffic: calibrated DRAM bytes per launch (PMC); neither VALU nor
+                # DRAM is saturated (valu below): the launch is latency-bound at 3 waves per SIMD
+                "bound": "hbm",
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -375,12 +377,16 @@ def main():
                 "alg_bytes_per_sim": b_sim,
                 "stream_copy_peak_measured_gbs": stream_peak,
                 "valu": valu,
-                "note": "bound by VALU issue and the dependent latency of the per-lane tree walks, not HBM bandwidth: "
-                        "PMC VALU busy %s of the launch, %s of wave cycles waiting on memory; achieved = the SURVEY 8(d) algorithmic bytes from the oracle's "
-                        "counters / event-timed kernel; traffic = 2*FETCH_SIZE+WRITE_SIZE from profiles/pmc_search.json "
-                        "scaled per launch"
-                        % ("%.0f%%" % (100 * valu["busy"]) if valu else "n/a",
-                           "%.0f%%" % (100 * valu["mem_wait_frac"]) if valu else "n/a"),
+                "limiter": "latency of the per-lane tree walks: VALU %s busy (measured), DRAM %s of the measured "
+                           "random-line read peak, %s of wave cycles waiting on memory" % (
+                               "%.0f%%" % (100 * valu["busy"]) if valu else "n/a",
+                               "%.0f%%" % (100 * valu["dram_frac_of_random_line_peak"])
+                               if valu and valu.get("dram_frac_of_random_line_peak") else "n/a",
+                               "%.0f%%" % (100 * valu["mem_wait_frac"]) if valu else "n/a"),
+                "note": "achieved = the SURVEY 8(d) algorithmic bytes (oracle counters, profiles/alg_bytes_<w>.json) / "
+                        "event-timed search kernel; traffic = calibrated DRAM bytes per launch (128 B per read "
+                        "request of the 128-B kind, WRITE_SIZE for writes: profiles/r03/pmc_calib.json) from "
+                        "profiles/pmc_search.json, scaled to this launch",
             },
             "node_pools": pools,
             "small_batch": small,
@@ -775,28 +781,36 @@ def stream_copy_gbs(torch, dev, nbytes=1 << 31, reps=10):
     return gbs
 
 
-def pmc_valu():
-    """VALU figures of the search launch from the committed PMC summary: busy = SQ_INSTS_VALU x 4
-    cycles per wave64 instruction / 1024 SIMDs over GRBM_GUI_ACTIVE per XCD; VALU instructions per
-    simulation per 64-root wave; share of wave cycles waiting on memory."""
-    path = os.path.join(ROOT, "profiles", "pmc_search.json")
+def pmc_valu(path=None):
+    """Measured issue figures of the search launch from the committed PMC summary
+    (tools/pmc_finalize.py): VALU busy = SQ_INSTS_VALU x 4 cycles / (1024 SIMDs x shader
+    cycles), the 4 cycles calibrated by tools/pmc_calib.hip (a saturated integer VALU pipe
+    reads 0.93-0.99 at 1-8 waves per SIMD); share of wave cycles waiting on memory; DRAM
+    rate against the measured random-line read peak."""
+    path = path or os.path.join(ROOT, "profiles", "pmc_search.json")
     try:
         with open(path) as fh:
             d = json.load(fh)
-        c = d["pmc_per_launch"]
-        sims = d["roots"] * d["iterations"]
-        return {"busy": c["SQ_INSTS_VALU"] * 4.0 / 1024.0 / (c["GRBM_GUI_ACTIVE"] / 8.0),
-                "mem_wait_frac": c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"],
-                "wave_insts_per_sim": c["SQ_INSTS_VALU"] * 64.0 / sims,
-                "source": "profiles/pmc_search.json"}
+        x = d["derived"]
+        return {"busy": x["valu_busy"], "mem_wait_frac": x["mem_wait_frac"],
+                "wave_insts_per_sim": d["valu_insts_per_sim_per_wave64"],
+                "dram_gbs_under_pmc": x.get("dram_gbs"),
+                "dram_frac_of_random_line_peak": d.get("dram_frac_of_random_line_peak"),
+                "random_line_read_peak_gbs": d.get("random_line_read_peak_gbs_measured"),
+                "source": os.path.relpath(path, ROOT), "calibration": d.get("calibration")}
     except Exception:
         return None
 
 
-def pmc_traffic(n_roots, iters):
-    """HBM bytes per search launch from the committed rocprofv3 PMC summary
-    (profiles/pmc_search.json), scaled to this launch size; None if absent."""
-    path = os.path.join(ROOT, "profiles", "pmc_search.json")
+def pmc_summary_path(workload):
+    """The committed PMC summary of a workload's search launch (tools/pmc_finalize.py):
+    profiles/pmc_search.json for C3, profiles/pmc_search_<workload>.json otherwise."""
+    return os.path.join(ROOT, "profiles", "pmc_search.json" if workload == "c3" else "pmc_search_%s.json" % workload)
+
+
+def pmc_traffic(n_roots, iters, path):
+    """Calibrated DRAM bytes per search launch from the committed PMC summary, scaled to
+    this launch size; None if absent."""
     if not os.path.exists(path):
         return None
     with open(path) as fh:

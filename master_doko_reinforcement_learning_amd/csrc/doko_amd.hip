@@ -69,7 +69,8 @@ struct GpuMem {
     W* states;
     uint32_t lslot, lstate, lovf;   // lane * cap_slots, lane * cap_states, lane * MAX_DEPTH
     template <class T> __device__ static T& at(T* base, uint32_t idx) {
-        return *reinterpret_cast<T*>(reinterpret_cast<char*>(base) + (uint32_t)(idx * (uint32_t)sizeof(T)));
+        if constexpr (H::WIDE) return base[idx];   // 64-bit byte offsets (regions >= 4 GiB)
+        else return *reinterpret_cast<T*>(reinterpret_cast<char*>(base) + (uint32_t)(idx * (uint32_t)sizeof(T)));
     }
     __device__ H& hr(uint32_t s) const { return at(hot, lslot + s); }
     __device__ dk::NodeCold& cr(uint32_t s) const { return at(cold, lslot + s); }
@@ -808,7 +809,8 @@ struct dk_ctx {
     uint32_t roots_per_wave = 64;   // pool region width; DK_ROOTS_PER_WAVE fixes the launch width too
     bool rpw_fixed = false;
     int hot_layout = 0;             // DK_HOT_RECORD=8|16|32 fixes the hot-record layout; 0 = per launch
-    bool p8_ok = false;             // the pools' slot capacities fit the 8-B records' child_base field
+    bool p8_ok = false;             // the pools' slot capacities suit the 8-B records (even-aligned blocks)
+    bool wide = false;              // a wave's pool region reaches 4 GiB: NodeHot32W (64-bit offsets) only
     bool ln_in_lds = false;         // DK_LN_LDS=1: ln(N) table copied into every workgroup's LDS (8 KB at
                                     // 1000 iterations); by default it is read through the L1/L2 caches
     int lds_path = 16;              // path entries kept in LDS (deeper ones spill to global): at most
@@ -917,8 +919,8 @@ hipError_t launch_search_t(dk_ctx* ctx, const dk_state* roots, const uint64_t* s
     grid = grid < regions ? grid : regions;
     if (grid == 0) return hipErrorInvalidValue;
     if (ctx->verbose)
-        fprintf(stderr, "doko_amd: search n=%u rpw=%u hot=%dB lds_path=%d lds=%zuB resident/CU=%d grid=%u root_window=%u\n",
-                n, rpw, (int)sizeof(H), lp, lds_bytes, per_cu, grid, ctx->root_window);
+        fprintf(stderr, "doko_amd: search n=%u rpw=%u hot=%dB lds_path=%d lds=%zuB resident/CU=%d grid=%u root_window=%u "
+                "wide=%d\n", n, rpw, (int)sizeof(H), lp, lds_bytes, per_cu, grid, ctx->root_window, (int)H::WIDE);
     hipError_t e = hipMemsetAsync(ctx->queue, 0, sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
     // group order only matters when waves take several groups each
@@ -978,6 +980,8 @@ hipError_t launch_search(dk_ctx* ctx, const dk_state* roots, const uint64_t* see
                      (ctx->hot_layout ? ctx->hot_layout <= 16 : grid_for(n, rpw) >= 2u * simds);
     // 8-B records where their fields hold the search (visits, state index, slots: P8_MAX_ITERS)
     const bool h8 = h16 && iters <= dk::P8_MAX_ITERS && ctx->hot_layout != 16 && ctx->p8_ok;
+    if (ctx->wide)   // per-wave pool regions of >= 4 GiB: 64-bit offsets (never with ln in LDS: iterations > 2047)
+        return launch_search_t<E, false, dk::NodeHot32W>(ctx, roots, seeds, n, iters, c, visits, values, best, st, 0, rpw);
     if (h8)
         return ln ? launch_search_t<E, true, dk::NodeHot8>(ctx, roots, seeds, n, iters, c, visits, values, best, st, ln_bytes, rpw)
                   : launch_search_t<E, false, dk::NodeHot8>(ctx, roots, seeds, n, iters, c, visits, values, best, st, ln_bytes, rpw);
@@ -1121,8 +1125,18 @@ dk_ctx* dk_create(const dk_config* cfg) {
         ok = hipMemcpy(ctx->ln_table, ln.data(), ln.size() * sizeof(double), hipMemcpyHostToDevice) == hipSuccess;
         ok = ok && hipMemset(ctx->err, 0, sizeof(int)) == hipSuccess;
     }
-    ctx->p8_ok = ctx->cap_slots <= (1u << 14) && (ctx->fb_slots == 0 || ctx->fb_slots <= (1u << 14)) &&
-                 ctx->cap_slots % 2 == 0 && ctx->fb_slots % 2 == 0;
+    // A launch of <= P8_MAX_ITERS iterations uses at most P8_SLOT_BOUND(iterations) < 2^14 slots per
+    // root, whatever the pools' capacity (sized for max_iterations), so the 8-B records' 13-bit
+    // child_base/2 field always holds its slots: only the even block alignment is a condition.
+    ctx->p8_ok = ctx->cap_slots % 2 == 0 && ctx->fb_slots % 2 == 0;
+    // 32-bit pool offsets (GpuMem::at) cover a wave's region only below 4 GiB: 64 lanes x the
+    // capacity x the widest record, in the main and the fallback pools, and the node states
+    {
+        const uint64_t lim = 1ULL << 32, lanes = WAVE;
+        const uint64_t slots = std::max<uint64_t>(ctx->cap_slots, ctx->fb_slots);
+        ctx->wide = lanes * slots * sizeof(dk::NodeHot32) >= lim || lanes * slots * sizeof(dk::NodeCold) >= lim ||
+                    lanes * ST * STATE_SLOT_BYTES >= lim;
+    }
     ctx->pool_bytes = R * S * (sizeof(dk::NodeHot32) + sizeof(dk::NodeCold)) + R * ST * STATE_SLOT_BYTES + ctx->fb_bytes;
     if (!ok) { dk_destroy(ctx); return nullptr; }
     return ctx;

@@ -48,7 +48,7 @@ struct DoE {
     DK_HD static void step_packed(dk_state& s, int a) { dko::step_packed(s.dk, a); }
     DK_HD static Node pack_node(const Work& w) { return dko::pack_node(w); }
     DK_HD static Work unpack_node(const Node& n) { return dko::unpack_node(n); }
-    DK_HD static bool node_ok(const Work&) { return true; }
+    DK_HD static bool node_ok(const Work& w) { return dko::node_ok(w); }
 };
 
 struct TttE {

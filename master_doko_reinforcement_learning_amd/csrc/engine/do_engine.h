@@ -292,6 +292,12 @@ DK_HD Work unpack_node(const Node& n) {
     x.re_players = (uint8_t)n.w[14]; x.pad0 = 0; x.pad1 = 0; x.pad2 = 0;
     return x;
 }
+// the record holds this state exactly (the search checks every root, as for rs-full-doko):
+// everything but the hands is stored whole, the hands as 48-bit masks
+DK_HD bool node_ok(const Work& x) {
+    const Work y = unpack_node(pack_node(x));
+    return x.h[0] == y.h[0] && x.h[1] == y.h[1] && x.h[2] == y.h[2] && x.h[3] == y.h[3];
+}
 
 DK_HD void unpack(const dk_do_state& s, Work& w) {
     for (int p = 0; p < 4; ++p) w.h[p] = s.hands[p];

@@ -11,15 +11,20 @@ namespace dk {
 struct Rng {
     uint64_t s0, s1, s2, s3;
 
-    DK_HD static uint64_t rotl(uint64_t x, int k) {
+    // rotate left by a compile-time amount (Xoshiro256++ uses 23 and 45).  The device form
+    // is two funnel shifts (v_alignbit_b32), whose shift operand is taken mod 32: a rotation
+    // by a multiple of 32 would come out wrong, so those amounts are rejected at compile time.
+    template <int K>
+    DK_HD static uint64_t rotl(uint64_t x) {
+        static_assert(K > 0 && K < 64 && K % 32 != 0, "rotl: 0 < K < 64, K != 32");
 #if defined(__HIP_DEVICE_COMPILE__)
-        // two funnel shifts (v_alignbit_b32) instead of 64-bit shifts and an or
+        constexpr int k = K >= 32 ? K - 32 : K;
         uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
-        if (k >= 32) { const uint32_t t = lo; lo = hi; hi = t; k -= 32; }
+        if constexpr (K >= 32) { const uint32_t t = lo; lo = hi; hi = t; }
         const uint32_t nh = __builtin_amdgcn_alignbit(hi, lo, 32 - k), nl = __builtin_amdgcn_alignbit(lo, hi, 32 - k);
         return (uint64_t)nh << 32 | nl;
 #else
-        return (x << k) | (x >> (64 - k));
+        return (x << K) | (x >> (64 - K));
 #endif
     }
 
@@ -45,7 +50,7 @@ struct Rng {
     }
 
     DK_HD uint64_t next_u64() {
-        const uint64_t res = rotl(s0 + s3, 23) + s0;
+        const uint64_t res = rotl<23>(s0 + s3) + s0;
         advance();
         return res;
     }
@@ -68,7 +73,7 @@ struct Rng {
         const uint64_t t = s1 << 17;
         const uint64_t n0 = xor3(s0, s3, s1), n1 = xor3(s1, s2, s0), n2 = xor3(s2, s0, t), n3 = s3 ^ s1;
         s0 = n0; s1 = n1; s2 = n2;
-        s3 = rotl(n3, 45);
+        s3 = rotl<45>(n3);
     }
 
     // random_range(0..n) on u32 (n >= 1).

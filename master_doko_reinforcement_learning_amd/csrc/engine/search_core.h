@@ -79,6 +79,7 @@ struct alignas(16) NodeHot16 {
     uint32_t info;        // nchild:6 | player:2 | has_unexpanded:1 | chain_head:1 | state_idx:22
     static constexpr bool CACHED_MEAN = false;
     static constexpr int MIN_WAVES = DK_HOT16_WAVES;   // search-kernel register budget (3 waves per SIMD: <= 168 VGPRs)
+    static constexpr bool WIDE = false;                // pool offsets: 32-bit (a wave's regions < 4 GiB)
 };
 struct alignas(32) NodeHot32 {
     uint64_t stats;
@@ -89,6 +90,13 @@ struct alignas(32) NodeHot32 {
     uint32_t pad;
     static constexpr bool CACHED_MEAN = true;
     static constexpr int MIN_WAVES = 1;   // no budget (its launches have one wave per SIMD)
+    static constexpr bool WIDE = false;
+};
+// NodeHot32 addressed with 64-bit offsets: contexts whose per-wave pool regions reach 4 GiB
+// (very long searches: the fallback pool's 32-B records at >= ~175 K iterations, node states
+// at >= ~1 M iterations), where 32-bit byte offsets would wrap into a neighbour lane's tree.
+struct alignas(32) NodeHot32W : NodeHot32 {
+    static constexpr bool WIDE = true;
 };
 // 8-B records (launches of <= P8_MAX_ITERS iterations): everything packed into two words
 //   w0 = win_score << 11 | visits                         (the stats: the backup stores w0 only)
@@ -102,6 +110,7 @@ struct alignas(8) NodeHot8 {
     uint32_t w0, w1;
     static constexpr bool CACHED_MEAN = false;
     static constexpr int MIN_WAVES = DK_HOT16_WAVES;
+    static constexpr bool WIDE = false;
 };
 // visits < 2^11, slots < 2^14, state indices < 2^10 (bit 10 of the state field marks a
 // resolved chain head, below)

@@ -259,6 +259,49 @@ def test_search_capacity_fallback(cap, env, monkeypatch):
         e.close()
 
 
+def test_search_wide_pools(monkeypatch, capfd):
+    """A context sized for 200,000 iterations (compare_impi's setting): its fallback pool's
+    per-wave region (64 lanes x 2.4 M slots x 32 B) passes 4 GiB, so every launch takes the
+    64-bit-offset records (NodeHot32W, launch line wide=1).  With a 256-slot main pool the
+    roots overflow into that fallback pool; results equal the oracle's."""
+    import master_doko_reinforcement_learning_amd as dk
+    monkeypatch.setenv("DK_VERBOSE", "1")
+    e = dk.Engine(device=0, max_roots=64, max_iterations=200000, slot_capacity=256)
+    try:
+        pool = [s for s in fdo_states(8, 31) if s.info()["phase"] != 3]
+        rng = np.random.default_rng(200000)
+        pick = [pool[i] for i in rng.choice(len(pool), size=16, replace=False)]
+        seeds = rng.integers(0, 2**63, size=len(pick), dtype=np.uint64)
+        visits, values, best = dk.CachedMCTS(e, dk.GAME_FULL_DOKO).monte_carlo_tree_search(pack_all(pick), 2.5, 1500, seeds)
+        assert e.pool_high_water()[2] > 0          # roots overflowed into the (wide) fallback pool
+    finally:
+        e.close()
+    err = capfd.readouterr().err
+    assert "wide=1" in err and "hot=32B" in err, err[-800:]
+    for i, (b, v, val) in enumerate(_oracle_search(pick, seeds, 1500, 2.5, "fdo")):
+        assert list(visits[i]) == v, i
+        assert values[i].tobytes() == np.array(val, dtype=np.float64).tobytes(), i
+        assert int(best[i]) == (b if b >= 0 else 255), i
+
+
+def test_search_malformed_doko_root(eng):
+    """An rs-doko root whose hand has bits above the 48 card bits cannot be held by the 64-B
+    node record: the search refuses it with DK_E_STATE (as for rs-full-doko roots) instead of
+    silently truncating the hand."""
+    import master_doko_reinforcement_learning_amd as dk
+    s = ol.DoState.new_game(0xBAD)
+    for _ in range(4):
+        s.play(24)
+    ok = np.frombuffer(s.pack(), dtype=np.uint8).copy()
+    bad = ok.copy()
+    bad[7] |= 0x01                                  # hand 0, bit 56
+    m = dk.CachedMCTS(eng, dk.GAME_DOKO)
+    v, _, _ = m.monte_carlo_tree_search(ok[None, :], 2.5, 50, np.array([5], dtype=np.uint64))
+    assert int(v[0].sum()) == 50
+    with pytest.raises(dk.DokoError, match="malformed"):
+        m.monte_carlo_tree_search(bad[None, :], 2.5, 50, np.array([5], dtype=np.uint64))
+
+
 def test_search_capacity_fallback_doko(monkeypatch):
     """The same fallback for rs-doko roots (longest-first queue order by default)."""
     import master_doko_reinforcement_learning_amd as dk
