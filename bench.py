@@ -62,6 +62,9 @@ def parse():
     p.add_argument("--small-infostates", type=int, default=512,
                    help="c3: also time the survey's small decision batch (512 infostates x 64 = 32,768 roots); 0 = skip")
     p.add_argument("--small-steps", type=int, default=5)
+    p.add_argument("--inflight", default="2,4,8",
+                   help="c3 small batch: also time K independent decision batches in flight on one engine "
+                        "(DefaultImpiPolicy.execute_many), for each K in this list; empty = skip")
     p.add_argument("--host-readback-check", action="store_true",
                    help="also copy every leg's visits to pageable host memory and check them there (the round-2 "
                         "sequence); a host-only violation is reported as host_copy_bad_roots, not raised")
@@ -151,6 +154,7 @@ def make_workload(args, dk, L, dev, sp, rank, world, local_rank, dist=None, eng=
                                        ptr(visits), ptr(values), ptr(best), sp))
 
     return eng, step, n_roots, {"visits": visits, "values": values, "best": best, "roots": roots, "I": I, "S_r": S_r,
+                                "info": info if determinized else None, "game": game,
                                 "actions": actions if determinized else None,
                                 "acc": (acc_u if fuse_mode == dk.FUSE_MAXN else acc_f) if determinized else None}
 
@@ -179,6 +183,41 @@ def result_invariants(visits, best, iters):
     b = best.long()
     vb = torch.gather(visits, 1, b.clamp(max=38)[:, None])[:, 0]
     return (s != iters) | (b > 38) | (vb != mx)
+
+
+def inflight_rates(args, dk, eng, sbufs, dev, world, dist, steps=3):
+    """K independent small decision batches in flight on ONE engine (DefaultImpiPolicy.execute_many:
+    batched into one device pass, results split per batch), the regime of an evaluator deciding
+    many games at once (compare_impi/run.rs:775).  A step = K whole decisions
+    (determinize -> search -> fuse -> select), complete; rate = K x roots x iterations / step time."""
+    import torch
+    info = sbufs["info"]
+    I, S, iters = info.shape[0], args.samples // world, args.iterations
+    n = I * S
+    fuse = dk.FUSE_MAXN if args.fusion == "maxn" else dk.FUSE_AVG
+    policy = dk.DefaultImpiPolicy(eng, args.c, iters, S, fuse)
+    out = {}
+    for k in [int(x) for x in args.inflight.split(",") if x]:
+        seeds = []
+        for b in range(k):
+            base = np.uint64(0xE1000000 + (b << 24))
+            sd = np.concatenate([np.arange(n, dtype=np.uint64) + base, np.arange(n, dtype=np.uint64) + base + np.uint64(n)])
+            seeds.append(torch.tensor(sd.view(np.int64), device=dev))
+        batches = [(info, seeds[b]) for b in range(k)]
+        policy.execute_many(batches, game=sbufs["game"])      # warm-up
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            res = policy.execute_many(batches, game=sbufs["game"])
+        torch.cuda.synchronize(dev)
+        el = time.perf_counter() - t0
+        for _, v in res:
+            assert not bool((v.sum(dim=1) != iters).any().item()), "inflight: a root without exactly %d simulations" % iters
+        out[str(k)] = {"batches_in_flight": k, "value": k * n * iters * steps * world / el, "unit": "rollouts/s",
+                       "ms_per_step": el / steps * 1e3}
+    return out
 
 
 def check_visits(bufs, iters, leg):
@@ -312,6 +351,8 @@ def main():
         small = {"infostates_per_gpu": args.small_infostates, "roots_per_gpu": s_roots, "steps": args.small_steps,
                  "value": s_roots * iters * args.small_steps * world / s_el, "unit": "rollouts/s",
                  "ms_per_step": s_el / args.small_steps * 1e3, "search_kernel_ms": float(np.mean(s_ms))}
+        if args.inflight:
+            small["inflight"] = inflight_rates(args, dk, eng, sbufs, dev, world, dist)
         del sbufs
 
     result = None

@@ -278,6 +278,99 @@ class DefaultImpiPolicy:
                                              _ptr(visits) if return_visits else None))
         return (actions, visits) if return_visits else actions
 
+    def execute_async(self, infostates, seeds, game=None):
+        """DefaultImpiPolicy::execute entirely on the device, asynchronously on torch's current
+        stream: `infostates` uint8 [n_info, 128] and `seeds` int64 [2 * n_info * num_samples]
+        (sampling seeds, then search seeds) are CUDA tensors; returns CUDA tensors (actions
+        uint8 [n_info], visits int32 [n_info * num_samples, 39]).  `game` (GAME_FULL_DOKO /
+        GAME_DOKO) avoids reading the game tag back from the device.  Calls issued on
+        different streams run concurrently on one engine: each search launch takes its own
+        slot and range of pool lanes (dk_search_batch_async), so independent decision
+        batches smaller than the resident grid overlap on the GPU.  Device-side errors
+        surface at dk_sync of the stream (execute_many does that)."""
+        if game is None:
+            game = int(infostates[0, STATE_BYTES - 1].item())
+        return _run_on_stream(infostates.device, self._execute_async, infostates, seeds, game)
+
+    def _execute_async(self, infostates, seeds, game, st):
+        import torch
+        L = _native.lib()
+        ctx = self.engine.ctx
+        dev = infostates.device
+        n_info, S = infostates.shape[0], self.num_samples
+        n = n_info * S
+        if seeds.numel() != 2 * n:
+            raise ValueError("need 2*n_info*num_samples seeds")
+        roots = torch.empty((n, STATE_BYTES), dtype=torch.uint8, device=dev)
+        visits = torch.empty((n, NUM_ACTIONS), dtype=torch.int32, device=dev)
+        values = torch.empty((n, NUM_ACTIONS), dtype=torch.float64, device=dev)
+        best = torch.empty(n, dtype=torch.uint8, device=dev)
+        allowed = torch.empty(n_info, dtype=torch.int64, device=dev)
+        acc_u = torch.empty((n_info, NUM_ACTIONS), dtype=torch.int32, device=dev)
+        acc_f = torch.empty((n_info, NUM_ACTIONS), dtype=torch.float32, device=dev)
+        actions = torch.empty(n_info, dtype=torch.uint8, device=dev)
+        sp = seeds.data_ptr()
+        _check(L.dk_determinize_batch_async(ctx, infostates.data_ptr(), n_info, S, sp, roots.data_ptr(), st))
+        _check(L.dk_search_batch_async(ctx, game, roots.data_ptr(), sp + 8 * n, n, self.iterations, self.c,
+                                       visits.data_ptr(), values.data_ptr(), best.data_ptr(), st))
+        _check(L.dk_legal_actions_async(ctx, infostates.data_ptr(), n_info, allowed.data_ptr(), st))
+        _check(L.dk_fuse_accumulate_async(ctx, visits.data_ptr(), n_info, S, allowed.data_ptr(), self.fusion,
+                                          acc_u.data_ptr(), acc_f.data_ptr(), st))
+        _check(L.dk_fuse_select_async(ctx, n_info, self.fusion, allowed.data_ptr(), acc_u.data_ptr(), acc_f.data_ptr(),
+                                      actions.data_ptr(), st))
+        return actions, visits
+
+    def execute_many(self, batches, game=None, streams=0):
+        """Independent decision batches [(infostates, seeds), ...] (CUDA tensors as in
+        execute_async) that are in flight at the same time -- the reference's evaluator
+        decides many games at once (compare_impi/run.rs:775).  By default they are batched
+        into ONE device pass (infostates and seeds concatenated, results split back): the
+        roots of different decisions are independent and the fusion is per infostate, so
+        every result equals its batch decided alone, while the launch gets the occupancy of
+        the combined batch.  streams=K instead issues each batch on one of K streams (the
+        engine's concurrent search slots); whether those overlap depends on how HIP maps
+        the streams onto hardware queues.  Returns [(actions, visits), ...], complete;
+        raises DokoError on a device-side error."""
+        import torch
+        if not batches:
+            return []
+        dev = batches[0][0].device
+        caller = torch.cuda.current_stream(dev)
+        L = _native.lib()
+        S = self.num_samples
+        if streams:
+            groups = [[b] for b in batches]
+        else:
+            # one pass: seeds of batch b are [sampling n_b][search n_b] -> [all sampling][all search]
+            sizes = [int(inf.shape[0]) for inf, _ in batches]
+            info = torch.cat([inf for inf, _ in batches])
+            seeds = torch.cat([sd[:n_b * S] for (_, sd), n_b in zip(batches, sizes)] +
+                              [sd[n_b * S:] for (_, sd), n_b in zip(batches, sizes)])
+            groups = [[(info, seeds)]]
+        k = max(1, min(streams or 1, len(groups)))
+        if len(getattr(self, "_streams", [])) < k:
+            self._streams = [torch.cuda.Stream(dev) for _ in range(k)]
+        res = []
+        for i, g in enumerate(groups):
+            s = self._streams[i % k]
+            s.wait_stream(caller)
+            with torch.cuda.stream(s):
+                res.append(self.execute_async(*g[0], game))
+        for s in self._streams[:k]:
+            _check(L.dk_sync(self.engine.ctx, s.cuda_stream))
+            caller.wait_stream(s)
+        for a, v in res:
+            a.record_stream(caller)
+            v.record_stream(caller)
+        if streams:
+            return res
+        actions, visits = res[0]
+        out, i0 = [], 0
+        for n_b in sizes:
+            out.append((actions[i0:i0 + n_b], visits[i0 * S:(i0 + n_b) * S]))
+            i0 += n_b
+        return out
+
 
 class ArImpiPolicy:
     """mcts_ar_maxn_policy / mcts_ar_avg_policy (rs-doko-py-bridge/src/compare_impi/all_policies.rs:78-127):

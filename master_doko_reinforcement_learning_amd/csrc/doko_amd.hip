@@ -191,7 +191,7 @@ __global__ void __launch_bounds__(WAVE, H::MIN_WAVES) search_kernel(const dk_sta
                                                       uint8_t* best, int* err, uint32_t* queue, uint64_t* prof,
                                                       const uint32_t* __restrict__ order, uint32_t* retry,
                                                       const uint32_t* __restrict__ list, uint32_t* high_water,
-                                                      const uint32_t* __restrict__ perm) {
+                                                      const uint32_t* __restrict__ perm, uint32_t lane_base) {
     const uint32_t lane = threadIdx.x;
     const uint32_t T = iters + 1;
     const uint32_t n_ln = LN_LDS ? T : 0u;
@@ -221,8 +221,9 @@ __global__ void __launch_bounds__(WAVE, H::MIN_WAVES) search_kernel(const dk_sta
         E::load(roots[root], w);
         dk::Rng rng = dk::Rng::seed_from_u64(seeds[root]);
         GpuMem<typename E::Node, LN_LDS, H> mem;
-        // wave bases (uniform) + lane offsets: pool region pr = blockIdx.x * rpw + lane
-        const size_t wr = (size_t)blockIdx.x * rpw;
+        // wave bases (uniform) + lane offsets: pool lane = lane_base + blockIdx.x * rpw + lane (a launch
+        // owns the lanes [lane_base, lane_base + grid * rpw) of the pools, dk_ctx::Slot)
+        const size_t wr = (size_t)lane_base + (size_t)blockIdx.x * rpw;
         mem.hot = reinterpret_cast<H*>(hot_pool) + wr * cap_slots;
         mem.cold = cold + wr * cap_slots;
         mem.states = states + wr * st_stride;
@@ -772,13 +773,38 @@ struct dk_ctx {
     uint32_t pool_roots = 0;        // roots the node pools hold at once (min(max_roots, DK_POOL_ROOTS or
                                     // the resident capacity: CUs x 12 single-wave workgroups x 64 lanes))
     int cu_count = 0;
-    uint32_t* queue = nullptr;      // root-group counter of the persistent search grid
+    // In-flight search launches.  dk_search_batch_async may be called on several streams at
+    // once (independent decision batches in flight, as the reference's evaluator runs many
+    // games at a time).  Each launch takes a Slot -- its own group-queue counters, retry list,
+    // root orders, error flag and events -- and a range of pool lanes [lane_base, lane_base +
+    // lanes), allocated round-robin over the pools.  Before it starts, the launch waits
+    // (hipStreamWaitEvent, on the GPU) for the previous user of its slot and for every earlier
+    // launch whose lanes overlap its own, so launches whose lane ranges are disjoint (batches
+    // smaller than the resident grid) run concurrently and larger ones serialise.  The fallback
+    // pool is shared: fallback passes wait for the previous one.
+    struct Slot {
+        uint32_t* queue = nullptr;      // root-group counter of the persistent search grid
+        uint32_t* queue_fb = nullptr;   // the fallback pass's counter
+        uint32_t* retry = nullptr;      // [0] = count, then the roots the main pools could not hold
+        uint32_t* order = nullptr;      // queue order of the root groups (group_order_kernel)
+        uint32_t* perm = nullptr;       // depth-sorted root order (root_sort_kernel)
+        hipEvent_t ev0 = nullptr, ev1 = nullptr, done = nullptr;
+        uint32_t lane_base = 0, lanes = 0;
+        bool used = false;              // `done` has been recorded
+        bool pending = false;           // err[slot] not yet collected by dk_sync on `stream`
+        hipStream_t stream = nullptr;
+    };
+    static constexpr int MAX_INFLIGHT = 8;
+    std::vector<Slot> slots;
+    int* slot_err = nullptr;        // [MAX_INFLIGHT] error flags of the search launches
+    uint32_t next_slot = 0, lane_cursor = 0;
+    int last_slot = -1;             // the latest launch (dk_last_search_ms)
+    hipEvent_t fb_done = nullptr;   // the latest fallback pass
+    bool fb_used = false;
     // Slot-capacity fallback: pools are sized from the measured demand (default 64 + 4 x
     // iterations slots per root, against the proven 42 + 12 x iterations); a root that runs out
-    // is appended to `retry` ([0] = count) and searched again, from its seed, by a second
-    // launch over a small pool with the proven capacity (fb_*).  Results do not change.
-    uint32_t* retry = nullptr;
-    uint32_t* queue_fb = nullptr;
+    // is appended to its launch's `retry` list ([0] = count) and searched again, from its seed,
+    // by a second launch over a small pool with the proven capacity (fb_*).  Results do not change.
     uint32_t* high_water = nullptr; // [0] largest slot demand of a root completed in the main pools, [1] roots
                                     // that overflowed them, [2] largest demand of a root the fallback pass
                                     // completed (cumulative since dk_create; dk_pool_high_water)
@@ -789,8 +815,6 @@ struct dk_ctx {
     void* fb_states = nullptr;
     uint32_t fb_slots = 0, fb_roots = 0;
     uint64_t fb_bytes = 0;
-    uint32_t* order = nullptr;      // queue order of the root groups (group_order_kernel)
-    uint32_t* perm = nullptr;       // depth-sorted root order (root_sort_kernel)
     uint32_t root_window = 1024;    // roots per depth-sort window (DK_ROOT_WINDOW; 0 = launch order = root order):
                                     // one rank's share of C4 at N = 8 (8 samples per infostate) 410 -> 389 ms,
                                     // C3 at N = 1 unchanged (381 / 382 ms); 4096 reorders C3's groups (+2.4 %)
@@ -802,8 +826,6 @@ struct dk_ctx {
     void* states = nullptr;
     double* ln_table = nullptr;
     int* err = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    bool timed = false;
     int last_error = DK_OK;
     uint64_t pool_bytes = 0;
     uint32_t roots_per_wave = 64;   // pool region width; DK_ROOTS_PER_WAVE fixes the launch width too
@@ -833,7 +855,8 @@ struct dk_ctx {
     bool az_root_done = false;
     std::vector<void*> scratch;
     std::vector<size_t> scratch_size;
-    std::mutex mu;
+    std::mutex mu;                  // host-pointer calls (scratch buffers, ctx->stream)
+    std::mutex slot_mu;             // search slots and lane ranges
 };
 
 namespace {
@@ -861,11 +884,28 @@ void* scratch(dk_ctx* ctx, int k, size_t bytes) {
     return ctx->scratch[k];
 }
 
+// Wait for stream `st`, then collect the error flags: the context's (env, sampler, AlphaZero
+// kernels) and those of the search launches issued on `st` since its last sync.
 int finish(dk_ctx* ctx, hipStream_t st) {
     if (hipStreamSynchronize(st) != hipSuccess) return ctx->last_error = DK_E_LAUNCH;
     int flag = 0;
     if (hipMemcpy(&flag, ctx->err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return ctx->last_error = DK_E_LAUNCH;
     (void)hipMemset(ctx->err, 0, sizeof(int));
+    {
+        std::lock_guard<std::mutex> g(ctx->slot_mu);
+        int se[dk_ctx::MAX_INFLIGHT];
+        bool any = false;
+        for (const dk_ctx::Slot& sl : ctx->slots) any |= sl.pending && sl.stream == st;
+        if (any) {
+            if (hipMemcpy(se, ctx->slot_err, sizeof(se), hipMemcpyDeviceToHost) != hipSuccess) return ctx->last_error = DK_E_LAUNCH;
+            for (int k = 0; k < (int)ctx->slots.size(); ++k) {
+                dk_ctx::Slot& sl = ctx->slots[k];
+                if (!sl.pending || sl.stream != st) continue;
+                flag |= se[k];
+                sl.pending = false;
+            }
+        }
+    }
     if (flag & 1) return ctx->last_error = DK_E_CAPACITY;
     if (flag & 2) return ctx->last_error = DK_E_STATE;
     return ctx->last_error = DK_OK;
@@ -888,7 +928,7 @@ uint32_t launch_rpw(const dk_ctx* ctx, uint32_t n) {
 template <class E, bool LN, class H>
 hipError_t launch_search_t(dk_ctx* ctx, const dk_state* roots, const uint64_t* seeds, uint32_t n, uint32_t iters,
                            double c, uint32_t* visits, double* values, uint8_t* best, hipStream_t st,
-                           size_t ln_bytes, uint32_t rpw) {
+                           size_t ln_bytes, uint32_t rpw, dk_ctx::Slot& sl, int* err) {
     const auto kern = search_kernel<E, LN, H>;
     // LDS per path entry and lane: slot word + stats (8-B records: their 32-bit stats word)
     constexpr size_t PATH_ENTRY_BYTES = dk::is_p8<H>::value ? 8 : 12;
@@ -918,10 +958,22 @@ hipError_t launch_search_t(dk_ctx* ctx, const dk_state* roots, const uint64_t* s
     uint32_t grid = groups < resident ? groups : resident;
     grid = grid < regions ? grid : regions;
     if (grid == 0) return hipErrorInvalidValue;
+    // this launch's pool lanes, round-robin over the pools; wait for the earlier launches on them
+    const uint32_t lanes = grid * rpw;
+    if (ctx->lane_cursor + lanes > ctx->pool_roots) ctx->lane_cursor = 0;
+    const uint32_t base = ctx->lane_cursor;
+    ctx->lane_cursor += lanes;
+    hipError_t e = hipSuccess;
+    for (const dk_ctx::Slot& o : ctx->slots)
+        if (&o != &sl && o.used && o.lane_base < base + lanes && base < o.lane_base + o.lanes && o.stream != st)
+            if ((e = hipStreamWaitEvent(st, o.done, 0)) != hipSuccess) return e;
+    sl.lane_base = base;
+    sl.lanes = lanes;
     if (ctx->verbose)
         fprintf(stderr, "doko_amd: search n=%u rpw=%u hot=%dB lds_path=%d lds=%zuB resident/CU=%d grid=%u root_window=%u "
-                "wide=%d\n", n, rpw, (int)sizeof(H), lp, lds_bytes, per_cu, grid, ctx->root_window, (int)H::WIDE);
-    hipError_t e = hipMemsetAsync(ctx->queue, 0, sizeof(uint32_t), st);
+                "wide=%d lanes=%u+%u\n", n, rpw, (int)sizeof(H), lp, lds_bytes, per_cu, grid, ctx->root_window,
+                (int)H::WIDE, base, lanes);
+    e = hipMemsetAsync(sl.queue, 0, sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
     // group order only matters when waves take several groups each
     const bool want = ctx->group_order < 0 ? E::ORDER_GROUPS : ctx->group_order == 1;
@@ -929,46 +981,52 @@ hipError_t launch_search_t(dk_ctx* ctx, const dk_state* roots, const uint64_t* s
     const uint32_t W = ctx->root_window;
     const bool sorted = W && E::GAME != DK_GAME_TTT && groups > 1;
     if (sorted) {
-        hipLaunchKernelGGL(root_sort_kernel, dim3(grid_for(n, W)), dim3(256), 0, st, roots, n, W, ctx->perm);
+        hipLaunchKernelGGL(root_sort_kernel, dim3(grid_for(n, W)), dim3(256), 0, st, roots, n, W, sl.perm);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
-    const uint32_t* perm = sorted ? (const uint32_t*)ctx->perm : (const uint32_t*)nullptr;
+    const uint32_t* perm = sorted ? (const uint32_t*)sl.perm : (const uint32_t*)nullptr;
     const bool ordered = want && E::GAME != DK_GAME_TTT && groups > grid;
     if (ordered) {
-        hipLaunchKernelGGL(group_order_kernel, dim3(1), dim3(1024), 0, st, roots, n, rpw, groups, ctx->order, perm);
+        hipLaunchKernelGGL(group_order_kernel, dim3(1), dim3(1024), 0, st, roots, n, rpw, groups, sl.order, perm);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
     const bool fallback = ctx->fb_hot != nullptr;
     if (fallback) {
-        e = hipMemsetAsync(ctx->retry, 0, sizeof(uint32_t), st);
-        if (e == hipSuccess) e = hipMemsetAsync(ctx->queue_fb, 0, sizeof(uint32_t), st);
+        e = hipMemsetAsync(sl.retry, 0, sizeof(uint32_t), st);
+        if (e == hipSuccess) e = hipMemsetAsync(sl.queue_fb, 0, sizeof(uint32_t), st);
         if (e != hipSuccess) return e;
     }
     hipLaunchKernelGGL(kern, dim3(grid), dim3(WAVE), lds_bytes, st, roots, seeds, n, iters, c, ctx->ln_table,
                        ctx->hot, ctx->cold, (typename E::Node*)ctx->states, ctx->ovf, ctx->ovf_st, ctx->cap_slots,
                        ctx->state_stride,
-                       rpw, lp, visits, values, best, ctx->err, ctx->queue, ctx->prof,
-                       ordered ? (const uint32_t*)ctx->order : (const uint32_t*)nullptr,
-                       fallback ? ctx->retry : (uint32_t*)nullptr, (const uint32_t*)nullptr, ctx->high_water, perm);
+                       rpw, lp, visits, values, best, err, sl.queue, ctx->prof,
+                       ordered ? (const uint32_t*)sl.order : (const uint32_t*)nullptr,
+                       fallback ? sl.retry : (uint32_t*)nullptr, (const uint32_t*)nullptr, ctx->high_water, perm, base);
     e = hipGetLastError();
     if (e != hipSuccess || !fallback) return e;
+    // the fallback pool is shared by all launches: one fallback pass at a time
+    if (ctx->fb_used && (e = hipStreamWaitEvent(st, ctx->fb_done, 0)) != hipSuccess) return e;
     // Second pass over the roots the main pool could not hold (retry[0] of them; the grid
     // drains at once when there are none): same kernel, proven-capacity pool, no retry list,
     // so running out there is DK_E_CAPACITY.
     const uint32_t fb_grid = ctx->fb_roots / rpw;
     hipLaunchKernelGGL(kern, dim3(fb_grid), dim3(WAVE), lds_bytes, st, roots, seeds, n, iters, c, ctx->ln_table,
                        ctx->fb_hot, ctx->fb_cold, (typename E::Node*)ctx->fb_states, ctx->fb_ovf, ctx->fb_ovf_st,
-                       ctx->fb_slots, ctx->state_stride, rpw, lp, visits, values, best, ctx->err, ctx->queue_fb, ctx->prof,
-                       (const uint32_t*)nullptr, (uint32_t*)nullptr, (const uint32_t*)ctx->retry, ctx->high_water + 2,
-                       (const uint32_t*)nullptr);
-    return hipGetLastError();
+                       ctx->fb_slots, ctx->state_stride, rpw, lp, visits, values, best, err, sl.queue_fb, ctx->prof,
+                       (const uint32_t*)nullptr, (uint32_t*)nullptr, (const uint32_t*)sl.retry, ctx->high_water + 2,
+                       (const uint32_t*)nullptr, 0u);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = hipEventRecord(ctx->fb_done, st)) != hipSuccess) return e;
+    ctx->fb_used = true;
+    return hipSuccess;
 }
 
 template <class E>
 hipError_t launch_search(dk_ctx* ctx, const dk_state* roots, const uint64_t* seeds, uint32_t n, uint32_t iters,
-                         double c, uint32_t* visits, double* values, uint8_t* best, hipStream_t st) {
+                         double c, uint32_t* visits, double* values, uint8_t* best, hipStream_t st, dk_ctx::Slot& sl,
+                         int* err) {
     const bool ln = iters + 1 <= LN_LDS_MAX && ctx->ln_in_lds;
     const uint32_t rpw = launch_rpw(ctx, n);
     const size_t ln_bytes = ln ? (size_t)((iters + 2) & ~1u) * 8 : 0;
@@ -981,15 +1039,15 @@ hipError_t launch_search(dk_ctx* ctx, const dk_state* roots, const uint64_t* see
     // 8-B records where their fields hold the search (visits, state index, slots: P8_MAX_ITERS)
     const bool h8 = h16 && iters <= dk::P8_MAX_ITERS && ctx->hot_layout != 16 && ctx->p8_ok;
     if (ctx->wide)   // per-wave pool regions of >= 4 GiB: 64-bit offsets (never with ln in LDS: iterations > 2047)
-        return launch_search_t<E, false, dk::NodeHot32W>(ctx, roots, seeds, n, iters, c, visits, values, best, st, 0, rpw);
+        return launch_search_t<E, false, dk::NodeHot32W>(ctx, roots, seeds, n, iters, c, visits, values, best, st, 0, rpw, sl, err);
     if (h8)
-        return ln ? launch_search_t<E, true, dk::NodeHot8>(ctx, roots, seeds, n, iters, c, visits, values, best, st, ln_bytes, rpw)
-                  : launch_search_t<E, false, dk::NodeHot8>(ctx, roots, seeds, n, iters, c, visits, values, best, st, ln_bytes, rpw);
+        return ln ? launch_search_t<E, true, dk::NodeHot8>(ctx, roots, seeds, n, iters, c, visits, values, best, st, ln_bytes, rpw, sl, err)
+                  : launch_search_t<E, false, dk::NodeHot8>(ctx, roots, seeds, n, iters, c, visits, values, best, st, ln_bytes, rpw, sl, err);
     if (h16)
-        return ln ? launch_search_t<E, true, dk::NodeHot16>(ctx, roots, seeds, n, iters, c, visits, values, best, st, ln_bytes, rpw)
-                  : launch_search_t<E, false, dk::NodeHot16>(ctx, roots, seeds, n, iters, c, visits, values, best, st, ln_bytes, rpw);
-    return ln ? launch_search_t<E, true, dk::NodeHot32>(ctx, roots, seeds, n, iters, c, visits, values, best, st, ln_bytes, rpw)
-              : launch_search_t<E, false, dk::NodeHot32>(ctx, roots, seeds, n, iters, c, visits, values, best, st, ln_bytes, rpw);
+        return ln ? launch_search_t<E, true, dk::NodeHot16>(ctx, roots, seeds, n, iters, c, visits, values, best, st, ln_bytes, rpw, sl, err)
+                  : launch_search_t<E, false, dk::NodeHot16>(ctx, roots, seeds, n, iters, c, visits, values, best, st, ln_bytes, rpw, sl, err);
+    return ln ? launch_search_t<E, true, dk::NodeHot32>(ctx, roots, seeds, n, iters, c, visits, values, best, st, ln_bytes, rpw, sl, err)
+              : launch_search_t<E, false, dk::NodeHot32>(ctx, roots, seeds, n, iters, c, visits, values, best, st, ln_bytes, rpw, sl, err);
 }
 
 }  // namespace
@@ -1093,7 +1151,6 @@ dk_ctx* dk_create(const dk_config* cfg) {
     ok = ok && hipMalloc(&ctx->states, R * ST * STATE_SLOT_BYTES) == hipSuccess;
     ok = ok && hipMalloc(&ctx->ln_table, (T + 1) * sizeof(double)) == hipSuccess;
     ok = ok && hipMalloc(&ctx->err, sizeof(int)) == hipSuccess;
-    ok = ok && hipMalloc(&ctx->queue, sizeof(uint32_t)) == hipSuccess;
     ok = ok && hipMalloc(&ctx->high_water, 4 * sizeof(uint32_t)) == hipSuccess;
     ok = ok && hipMemset(ctx->high_water, 0, 4 * sizeof(uint32_t)) == hipSuccess;
     if (ok && with_fallback) {
@@ -1102,18 +1159,27 @@ dk_ctx* dk_create(const dk_config* cfg) {
         const size_t FR = R < FALLBACK_ROOTS ? R : FALLBACK_ROOTS, FS = proven;
         ctx->fb_roots = (uint32_t)FR;
         ctx->fb_slots = proven;
-        ok = hipMalloc(&ctx->retry, ((size_t)cfg->max_roots + 1) * sizeof(uint32_t)) == hipSuccess;
-        ok = ok && hipMalloc(&ctx->queue_fb, sizeof(uint32_t)) == hipSuccess;
-        ok = ok && hipMalloc(&ctx->fb_hot, FR * FS * sizeof(dk::NodeHot32)) == hipSuccess;
+        ok = hipMalloc(&ctx->fb_hot, FR * FS * sizeof(dk::NodeHot32)) == hipSuccess;
         ok = ok && hipMalloc(&ctx->fb_cold, FR * FS * sizeof(dk::NodeCold)) == hipSuccess;
         ok = ok && hipMalloc(&ctx->fb_ovf, FR * dk::MAX_DEPTH * sizeof(uint32_t)) == hipSuccess;
         ok = ok && hipMalloc(&ctx->fb_ovf_st, FR * dk::MAX_DEPTH * sizeof(uint64_t)) == hipSuccess;
         ok = ok && hipMalloc(&ctx->fb_states, FR * ST * STATE_SLOT_BYTES) == hipSuccess;
         ctx->fb_bytes = FR * FS * (sizeof(dk::NodeHot32) + sizeof(dk::NodeCold)) + FR * ST * STATE_SLOT_BYTES;
     }
-    ok = ok && hipMalloc(&ctx->order, ((size_t)cfg->max_roots + 1) * sizeof(uint32_t)) == hipSuccess;
-    ok = ok && hipMalloc(&ctx->perm, (size_t)cfg->max_roots * sizeof(uint32_t)) == hipSuccess;
-    ok = ok && hipEventCreate(&ctx->ev0) == hipSuccess && hipEventCreate(&ctx->ev1) == hipSuccess;
+    // search slots (in-flight launches); the slot's lists are sized for max_roots
+    ctx->slots.resize(dk_ctx::MAX_INFLIGHT);
+    for (dk_ctx::Slot& sl : ctx->slots) {
+        const size_t list = ((size_t)cfg->max_roots + 1) * sizeof(uint32_t);
+        ok = ok && hipMalloc(&sl.queue, 2 * sizeof(uint32_t)) == hipSuccess;
+        if (ok) sl.queue_fb = sl.queue + 1;
+        ok = ok && hipMalloc(&sl.order, list) == hipSuccess && hipMalloc(&sl.perm, list) == hipSuccess;
+        ok = ok && (!with_fallback || hipMalloc(&sl.retry, list) == hipSuccess);
+        ok = ok && hipEventCreate(&sl.ev0) == hipSuccess && hipEventCreate(&sl.ev1) == hipSuccess &&
+             hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) == hipSuccess;
+    }
+    ok = ok && hipMalloc(&ctx->slot_err, dk_ctx::MAX_INFLIGHT * sizeof(int)) == hipSuccess &&
+         hipMemset(ctx->slot_err, 0, dk_ctx::MAX_INFLIGHT * sizeof(int)) == hipSuccess;
+    ok = ok && hipEventCreateWithFlags(&ctx->fb_done, hipEventDisableTiming) == hipSuccess;
 #ifdef DK_PHASE_PROF
     ok = ok && hipMalloc(&ctx->prof, (size_t)cfg->max_roots * 16 * sizeof(uint64_t)) == hipSuccess;
     ok = ok && hipMemset(ctx->prof, 0, (size_t)cfg->max_roots * 16 * sizeof(uint64_t)) == hipSuccess;
@@ -1154,19 +1220,23 @@ void dk_destroy(dk_ctx* ctx) {
     if (ctx->states) (void)hipFree(ctx->states);
     if (ctx->ln_table) (void)hipFree(ctx->ln_table);
     if (ctx->err) (void)hipFree(ctx->err);
-    if (ctx->queue) (void)hipFree(ctx->queue);
-    for (void* p : {(void*)ctx->high_water, (void*)ctx->retry, (void*)ctx->queue_fb, ctx->fb_hot, (void*)ctx->fb_cold,
+    for (dk_ctx::Slot& sl : ctx->slots) {
+        if (sl.stream) (void)hipStreamSynchronize(sl.stream);
+        for (void* p : {(void*)sl.queue, (void*)sl.order, (void*)sl.perm, (void*)sl.retry})
+            if (p) (void)hipFree(p);
+        for (hipEvent_t ev : {sl.ev0, sl.ev1, sl.done})
+            if (ev) (void)hipEventDestroy(ev);
+    }
+    if (ctx->slot_err) (void)hipFree(ctx->slot_err);
+    if (ctx->fb_done) (void)hipEventDestroy(ctx->fb_done);
+    for (void* p : {(void*)ctx->high_water, ctx->fb_hot, (void*)ctx->fb_cold,
                     (void*)ctx->fb_ovf, (void*)ctx->fb_ovf_st, ctx->fb_states})
         if (p) (void)hipFree(p);
-    if (ctx->order) (void)hipFree(ctx->order);
-    if (ctx->perm) (void)hipFree(ctx->perm);
     if (ctx->prof) (void)hipFree(ctx->prof);
     if (ctx->az_nodes) (void)hipFree(ctx->az_nodes);
     if (ctx->ar_lanes) (void)hipFree(ctx->ar_lanes);
     if (ctx->az_states) (void)hipFree(ctx->az_states);
     if (ctx->az_games) (void)hipFree(ctx->az_games);
-    if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
-    if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -1202,9 +1272,16 @@ int dk_sync(dk_ctx* ctx, void* stream) {
 }
 
 int dk_last_search_ms(dk_ctx* ctx, float* ms) {
-    if (!ctx || !ms || !ctx->timed) return DK_E_INVALID;
-    DK_HIP(hipEventSynchronize(ctx->ev1));
-    DK_HIP(hipEventElapsedTime(ms, ctx->ev0, ctx->ev1));
+    if (!ctx || !ms) return DK_E_INVALID;
+    hipEvent_t e0, e1;
+    {
+        std::lock_guard<std::mutex> g(ctx->slot_mu);
+        if (ctx->last_slot < 0) return DK_E_INVALID;
+        e0 = ctx->slots[ctx->last_slot].ev0;
+        e1 = ctx->slots[ctx->last_slot].ev1;
+    }
+    DK_HIP(hipEventSynchronize(e1));
+    DK_HIP(hipEventElapsedTime(ms, e0, e1));
     return DK_OK;
 }
 
@@ -1327,18 +1404,29 @@ int dk_search_batch_async(dk_ctx* ctx, int game, const dk_state* d_roots, const 
     if (!ctx) return DK_E_INVALID;
     if (n > ctx->max_roots || iterations > ctx->max_iters) return ctx->last_error = DK_E_CAPACITY;
     if (n == 0 || iterations == 0) return DK_E_INVALID;
+    if (game != DK_GAME_FULL_DOKO && game != DK_GAME_DOKO && game != DK_GAME_TTT) return DK_E_INVALID;
     hipStream_t st = pick(ctx, stream);
-    DK_HIP(hipEventRecord(ctx->ev0, st));
+    std::lock_guard<std::mutex> g(ctx->slot_mu);
+    // the next slot, round-robin; its previous launch must be done before its lists are reused
+    const int k = (int)(ctx->next_slot++ % dk_ctx::MAX_INFLIGHT);
+    dk_ctx::Slot& sl = ctx->slots[k];
+    if (sl.used && sl.stream != st) DK_HIP(hipStreamWaitEvent(st, sl.done, 0));
+    int* err = ctx->slot_err + k;
+    DK_HIP(hipMemsetAsync(err, 0, sizeof(int), st));
+    DK_HIP(hipEventRecord(sl.ev0, st));
     hipError_t e;
     switch (game) {
-        case DK_GAME_FULL_DOKO: e = launch_search<dk::FdoE>(ctx, d_roots, d_seeds, n, iterations, c, d_visits, d_values, d_best, st); break;
-        case DK_GAME_DOKO: e = launch_search<dk::DoE>(ctx, d_roots, d_seeds, n, iterations, c, d_visits, d_values, d_best, st); break;
-        case DK_GAME_TTT: e = launch_search<dk::TttE>(ctx, d_roots, d_seeds, n, iterations, c, d_visits, d_values, d_best, st); break;
-        default: return DK_E_INVALID;
+        case DK_GAME_FULL_DOKO: e = launch_search<dk::FdoE>(ctx, d_roots, d_seeds, n, iterations, c, d_visits, d_values, d_best, st, sl, err); break;
+        case DK_GAME_DOKO: e = launch_search<dk::DoE>(ctx, d_roots, d_seeds, n, iterations, c, d_visits, d_values, d_best, st, sl, err); break;
+        default: e = launch_search<dk::TttE>(ctx, d_roots, d_seeds, n, iterations, c, d_visits, d_values, d_best, st, sl, err); break;
     }
     if (e != hipSuccess) { fprintf(stderr, "doko_amd: search launch: %s\n", hipGetErrorString(e)); return DK_E_LAUNCH; }
-    DK_HIP(hipEventRecord(ctx->ev1, st));
-    ctx->timed = true;
+    DK_HIP(hipEventRecord(sl.ev1, st));
+    DK_HIP(hipEventRecord(sl.done, st));
+    sl.used = true;
+    sl.pending = true;
+    sl.stream = st;
+    ctx->last_slot = k;
     return DK_OK;
 }
 
