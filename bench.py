@@ -5,10 +5,12 @@ GPU, entirely on the device:
     CAP determinization (card_matching_full)  -> 18432 infostates x 64 samples = 1,179,648 roots
     UCT search, 1000 simulations per root (select/expand/random rollout/backup)
     policy fusion (MaxN) of the per-sample visit counts per infostate
-With N GPUs (config 4) the global batch holds 18432*N infostates; the 64 samples
-of every infostate are split evenly over the ranks (1,179,648 roots per GPU, weak
-scaling) and the per-infostate fusion accumulators are summed with one RCCL
-all-reduce over xGMI before the fused action is selected.
+With N GPUs (config 4) the global batch holds 18432*N infostates (weak scaling,
+1,179,648 roots per GPU).  By default every rank owns 18432 of them with all 64
+samples, so its work has exactly the N = 1 shape, and the fused actions are
+gathered with one RCCL all-gather over xGMI; --partition samples instead splits
+every infostate's samples over the ranks and sums the fusion accumulators with one
+RCCL all-reduce before the action is selected.
 
 Rank 0 prints one JSON line.  `value` = simulations of all ranks / max-over-ranks
 wall time of the K timed steps.  Inputs (the infostates) are synthesised on the
@@ -51,6 +53,11 @@ def parse():
                    help="infostates per GPU (c3: default 18432 x 64 samples = 1,179,648 roots, six 64-root groups per "
                         "resident wave (3072 waves); c2d, impi, impid: default 12288)")
     p.add_argument("--samples", type=int, default=64, help="samples per infostate (c3, c2d)")
+    p.add_argument("--partition", choices=["infostates", "samples"], default="infostates",
+                   help="N > 1 (c3, c2d): 'infostates' = each rank owns 1/N of the infostates with all their samples "
+                        "(every rank's work has the N = 1 shape; one RCCL all-gather of the fused actions); "
+                        "'samples' = the samples of every infostate split over the ranks (one RCCL all-reduce of "
+                        "the fusion accumulators)")
     p.add_argument("--roots", type=int, default=32768, help="roots per GPU (c2)")
     p.add_argument("--c", type=float, default=2.5)
     p.add_argument("--fusion", choices=["maxn", "avg"], default="maxn")
@@ -90,11 +97,15 @@ def make_workload(args, dk, L, dev, sp, rank, world, local_rank, dist=None, eng=
 
     determinized = args.workload in ("c3", "c2d")
     game = dk.GAME_FULL_DOKO if args.workload == "c3" else dk.GAME_DOKO
+    by_info = args.partition == "infostates"
     if determinized:
-        if args.samples % world:
+        if not by_info and args.samples % world:
             raise SystemExit("samples must be divisible by the number of GPUs")
-        I = args.infostates * world          # global infostates
-        S_r = args.samples // world          # samples of every infostate on this rank
+        # global infostates j = 0 .. infostates*world-1; this rank's: j0 .. j0+I-1 (all samples s0 .. s0+S_r-1)
+        I = args.infostates if by_info else args.infostates * world
+        S_r = args.samples if by_info else args.samples // world
+        j0 = rank * I if by_info else 0
+        s0 = 0 if by_info else rank * S_r
         n_roots = I * S_r
     else:
         I, S_r = 0, 0
@@ -109,17 +120,19 @@ def make_workload(args, dk, L, dev, sp, rank, world, local_rank, dist=None, eng=
             ck(L.dk_env_step_batch_async(eng.ctx, ptr(states_t), ptr(a), n, sp))
 
     if determinized:
-        info_seeds = torch.tensor(np.arange(I, dtype=np.uint64) + np.uint64(0xC3000000), device=dev)
+        gj = np.arange(j0, j0 + I, dtype=np.uint64)            # global infostate indices of this rank
+        info_seeds = torch.tensor(gj + np.uint64(0xC3000000), device=dev)
         info = torch.zeros((I, 128), dtype=torch.uint8, device=dev)
         ck(L.dk_new_game_batch_async(eng.ctx, game, ptr(info_seeds), I, ptr(info), sp))
         healthy_round(info, I)
-        plies = torch.tensor(np.array([[0, 8, 20, 32][j % 4] for j in range(I)], dtype=np.uint32).view(np.int32), device=dev)
-        ply_rng = torch.tensor(dk.splitmix_rng_states(np.arange(I, dtype=np.uint64) + np.uint64(0xC3100000)).view(np.int64), device=dev)
+        plies = torch.tensor(np.array([[0, 8, 20, 32][j % 4] for j in range(j0, j0 + I)], dtype=np.uint32).view(np.int32),
+                             device=dev)
+        ply_rng = torch.tensor(dk.splitmix_rng_states(gj + np.uint64(0xC3100000)).view(np.int64), device=dev)
         ck(L.dk_env_random_plies_batch_async(eng.ctx, ptr(info), ptr(ply_rng), ptr(plies), I, sp))
         allowed = torch.zeros(I, dtype=torch.int64, device=dev)
         ck(L.dk_legal_actions_async(eng.ctx, ptr(info), I, ptr(allowed), sp))
-        j = np.arange(I, dtype=np.uint64)[:, None]
-        s = np.arange(rank * S_r, (rank + 1) * S_r, dtype=np.uint64)[None, :]
+        j = gj[:, None]
+        s = np.arange(s0, s0 + S_r, dtype=np.uint64)[None, :]
         samp_seeds = (np.uint64(0xC3200000) + j * np.uint64(args.samples) + s).reshape(-1)
         srch_seeds = (np.uint64(0xC3300000) + j * np.uint64(args.samples) + s).reshape(-1)
         d_samp = torch.tensor(samp_seeds.view(np.int64), device=dev)
@@ -128,6 +141,8 @@ def make_workload(args, dk, L, dev, sp, rank, world, local_rank, dist=None, eng=
         acc_u = torch.zeros((I, 39), dtype=torch.int32, device=dev)
         acc_f = torch.zeros((I, 39), dtype=torch.float32, device=dev)
         actions = torch.zeros(I, dtype=torch.uint8, device=dev)
+        gather = by_info and world > 1
+        actions_all = torch.zeros((world, I), dtype=torch.uint8, device=dev) if gather else actions
     else:
         gidx = np.arange(rank * n_roots, (rank + 1) * n_roots, dtype=np.uint64)
         d_rs = torch.tensor((gidx + np.uint64(0xD0C00000)).view(np.int64), device=dev)
@@ -146,16 +161,18 @@ def make_workload(args, dk, L, dev, sp, rank, world, local_rank, dist=None, eng=
             ck(L.dk_search_batch_async(eng.ctx, game, ptr(roots), ptr(d_srch), n_roots, iters, args.c,
                                        ptr(visits), ptr(values), ptr(best), sp))
             ck(L.dk_fuse_accumulate_async(eng.ctx, ptr(visits), I, S_r, ptr(allowed), fuse_mode, ptr(acc_u), ptr(acc_f), sp))
-            if world > 1:
+            if world > 1 and not by_info:
                 dist.all_reduce(acc_u if fuse_mode == dk.FUSE_MAXN else acc_f)  # RCCL over xGMI
             ck(L.dk_fuse_select_async(eng.ctx, I, fuse_mode, ptr(allowed), ptr(acc_u), ptr(acc_f), ptr(actions), sp))
+            if gather:
+                dist.all_gather(list(actions_all.unbind(0)), actions)          # RCCL over xGMI: every rank's decisions
         else:
             ck(L.dk_search_batch_async(eng.ctx, dk.GAME_DOKO, ptr(roots), ptr(d_srch), n_roots, iters, args.c,
                                        ptr(visits), ptr(values), ptr(best), sp))
 
     return eng, step, n_roots, {"visits": visits, "values": values, "best": best, "roots": roots, "I": I, "S_r": S_r,
                                 "info": info if determinized else None, "game": game,
-                                "actions": actions if determinized else None,
+                                "actions": actions_all.reshape(-1) if determinized else None,
                                 "acc": (acc_u if fuse_mode == dk.FUSE_MAXN else acc_f) if determinized else None}
 
 
@@ -192,7 +209,7 @@ def inflight_rates(args, dk, eng, sbufs, dev, world, dist, steps=3):
     (determinize -> search -> fuse -> select), complete; rate = K x roots x iterations / step time."""
     import torch
     info = sbufs["info"]
-    I, S, iters = info.shape[0], args.samples // world, args.iterations
+    I, S, iters = info.shape[0], sbufs["S_r"], args.iterations
     n = I * S
     fuse = dk.FUSE_MAXN if args.fusion == "maxn" else dk.FUSE_AVG
     policy = dk.DefaultImpiPolicy(eng, args.c, iters, S, fuse)
@@ -326,8 +343,14 @@ def main():
     elapsed, search_ms = timed_steps(step, args.steps, args.warmup, eng, L, dev, world, dist, ck, sp)
     if rank == 0 and args.dump_actions and bufs["actions"] is not None:
         np.save(args.dump_actions, bufs["actions"].cpu().numpy())
-    if rank == 0 and args.dump_acc and bufs["acc"] is not None:
-        np.save(args.dump_acc, bufs["acc"].cpu().numpy())
+    if args.dump_acc and bufs["acc"] is not None:
+        acc = bufs["acc"]
+        if world > 1 and args.partition == "infostates" and args.workload in ("c3", "c2d"):
+            parts = [torch.zeros_like(acc) for _ in range(world)]
+            dist.all_gather(parts, acc)
+            acc = torch.cat(parts)
+        if rank == 0:
+            np.save(args.dump_acc, acc.cpu().numpy())
     check_visits(bufs, iters, "batch")
     host_bad = {}
     if args.host_readback_check:
@@ -400,7 +423,9 @@ def main():
                 "iterations": iters,
                 "uct_c": args.c,
                 "fusion": args.fusion if determinized else None,
-                "parallelism": "dp%d (samples split over GPUs, RCCL all-reduce of fusion accumulators)" % world,
+                "parallelism": ("dp%d (infostates split over GPUs, all samples of an infostate on one rank; RCCL "
+                                "all-gather of the fused actions)" if args.partition == "infostates" else
+                                "dp%d (samples split over GPUs, RCCL all-reduce of fusion accumulators)") % world,
             },
             "kernel_only_rollouts_per_s": n_roots * iters * world / (kernel_ms / 1e3),
             "search_kernel_ms": kernel_ms,

@@ -1,15 +1,20 @@
 """The bench's N>1 path with the real HIP kernels (config C4 rehearsed on one GPU).
 
 `bench.py --gpus 2` starts two ranks itself (torch.distributed.run, before touching
-the GPU); with DK_DIST_BACKEND=gloo both ranks share cuda:0.  Each rank determinizes
-and searches its half of every infostate's samples, runs dk_fuse_accumulate_async on
-them, the accumulators are all-reduced (gloo here, RCCL on an 8-GPU node) and every
-rank runs dk_fuse_select_async.  Reference: the sample fan-out of DefaultImpiPolicy
+the GPU); with DK_DIST_BACKEND=gloo both ranks share cuda:0.  Two partitions:
+  * infostates (default): each rank determinizes, searches and fuses its half of the
+    infostates with all their samples, and the fused actions are all-gathered (gloo
+    here, RCCL on an 8-GPU node): decisions AND accumulators equal the 1-rank run
+    over the same global workload bit for bit, for both fusions;
+  * samples: each rank searches its half of every infostate's samples, runs
+    dk_fuse_accumulate_async on them, the accumulators are all-reduced and every rank
+    runs dk_fuse_select_async.
+Reference: the sample fan-out of DefaultImpiPolicy
 (rs-doko-py-bridge/src/compare_impi/compare_impi.rs:217-291) and the fusions
 (policy_fusion.rs:23-123).
 
-MaxN fuses integer rank sums, so the 2-rank decision must equal the 1-rank run over
-the same global workload bit for bit.  Average-strategy fusion sums f32
+With the sample split, MaxN fuses integer rank sums, so the 2-rank decision must
+equal the 1-rank run over the same global workload bit for bit.  Average-strategy fusion sums f32
 probabilities: the two ranks' partial sums added by the all-reduce are a different
 f32 summation order than one rank's sequential sum (the reference's own order is
 JoinSet completion order, compare_impi.rs:276-288), so the accumulators agree within
@@ -31,7 +36,7 @@ pytestmark = pytest.mark.gpu
 INFO_PER_RANK, ITERS = 48, 200
 
 
-def _bench(tmp_path, gpus, infostates, fusion, tag):
+def _bench(tmp_path, gpus, infostates, fusion, tag, partition="samples"):
     env = dict(os.environ)
     env["DK_DIST_BACKEND"] = "gloo"
     env.pop("WORLD_SIZE", None)
@@ -39,7 +44,8 @@ def _bench(tmp_path, gpus, infostates, fusion, tag):
     acc = str(tmp_path / ("acc_%s.npy" % tag))
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--steps", "1", "--warmup", "0",
            "--no-cpu-baseline", "--small-infostates", "0", "--infostates", str(infostates),
-           "--iterations", str(ITERS), "--fusion", fusion, "--dump-actions", act, "--dump-acc", acc]
+           "--iterations", str(ITERS), "--fusion", fusion, "--dump-actions", act, "--dump-acc", acc,
+           "--partition", partition]
     out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=110)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
     line = [l for l in out.stdout.splitlines() if l.startswith("{")][-1]
@@ -52,6 +58,17 @@ def test_bench_two_ranks_maxn_exact(tmp_path):
     assert r2["config"]["roots_per_gpu"] == 2 * INFO_PER_RANK * 32
     r1, a1, acc1 = _bench(tmp_path, 1, 2 * INFO_PER_RANK, "maxn", "1")
     assert r1["n_gpus"] == 1
+    assert a2.shape == (2 * INFO_PER_RANK,)
+    assert np.array_equal(acc2, acc1)
+    assert np.array_equal(a2, a1)
+
+
+@pytest.mark.parametrize("fusion", ["maxn", "avg"])
+def test_bench_two_ranks_infostate_partition_exact(tmp_path, fusion):
+    r2, a2, acc2 = _bench(tmp_path, 2, INFO_PER_RANK, fusion, "i2" + fusion, "infostates")
+    assert r2["n_gpus"] == 2 and r2["ranks"] == 2
+    assert r2["config"]["roots_per_gpu"] == INFO_PER_RANK * 64          # the N = 1 shape per rank
+    r1, a1, acc1 = _bench(tmp_path, 1, 2 * INFO_PER_RANK, fusion, "i1" + fusion, "infostates")
     assert a2.shape == (2 * INFO_PER_RANK,)
     assert np.array_equal(acc2, acc1)
     assert np.array_equal(a2, a1)

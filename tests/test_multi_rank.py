@@ -1,9 +1,11 @@
-"""Multi-rank decision path on CPU (gloo, world_size 2): the samples of every
-infostate are split over the ranks exactly as bench.py does, each rank fuses
-its share into summable accumulators (the arithmetic of fuse_accumulate_kernel:
-1-based stable ranks, 0 for disallowed actions; probability sums for Avg), one
-all-reduce(sum) combines them and every rank selects.  The result must equal
-the oracle's fusion over all samples (policy_fusion.rs:23-123)."""
+"""Multi-rank decision path on CPU (gloo, world_size 2), both bench.py partitions:
+  * samples: the samples of every infostate are split over the ranks, each rank fuses
+    its share into summable accumulators (the arithmetic of fuse_accumulate_kernel:
+    1-based stable ranks, 0 for disallowed actions; probability sums for Avg), one
+    all-reduce(sum) combines them and every rank selects;
+  * infostates (the default): each rank fuses its own infostates over all their samples
+    and the fused actions are all-gathered.
+The result must equal the oracle's fusion over all samples (policy_fusion.rs:23-123)."""
 import os
 import socket
 
@@ -79,10 +81,24 @@ def _select(acc_u, acc_f, allowed, mode):
     return out
 
 
-def _worker(rank, world, port, allowed, visits, mode, q):
+def _worker(rank, world, port, allowed, visits, mode, q, partition="samples"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    if partition == "infostates":
+        # bench.py --partition infostates: rank r owns infostates [r*I_r, (r+1)*I_r) with all samples,
+        # fuses them locally and the actions are all-gathered (uint8, as on the device)
+        i_r = N_INFO // world
+        sl = slice(rank * i_r, (rank + 1) * i_r)
+        acc_u, acc_f = _accumulate(visits[sl], allowed[sl], mode)
+        mine = torch.tensor(_select(acc_u, acc_f, allowed[sl], mode), dtype=torch.uint8)
+        parts = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(parts, mine)
+        fparts = [torch.zeros((i_r, 39), dtype=torch.float32) for _ in range(world)]
+        dist.all_gather(fparts, torch.from_numpy(acc_f))
+        q.put((rank, torch.cat(parts).tolist(), torch.cat(fparts).numpy()))
+        dist.destroy_process_group()
+        return
     s_r = SAMPLES // world
     mine = visits[:, rank * s_r:(rank + 1) * s_r]          # bench.py: samples [rank*S_r, (rank+1)*S_r)
     acc_u, acc_f = _accumulate(mine, allowed, mode)
@@ -94,13 +110,14 @@ def _worker(rank, world, port, allowed, visits, mode, q):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("partition", ["samples", "infostates"])
 @pytest.mark.parametrize("mode", ["maxn", "avg"])
-def test_two_rank_fusion_equals_single_process(mode):
+def test_two_rank_fusion_equals_single_process(mode, partition):
     allowed, visits = _workload()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, allowed, visits, mode, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, allowed, visits, mode, q, partition)) for r in range(2)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in procs]
