@@ -468,6 +468,15 @@ int dk_net_add_ln_bf16_async(void* x_io, const void* delta, uint32_t rows, uint3
  * bf16 in and out, f32 accumulation, the activation written once. */
 int dk_net_fc_gelu_bf16_async(const void* x, const void* w, const void* bias, uint32_t rows, uint32_t k, uint32_t n,
                               void* y, void* stream);
+/* dk_net_mlp_ln_bf16_async: the MLP half of a transformer block and the LayerNorm after it in
+ * one pass (d = 160 with n_hidden % 64 == 0, or d = 256 with n_hidden % 32 == 0): delta = GELU(h w1^T + b1) w2^T + b2 (exact GELU; delta
+ * rounded to bf16 as the unfused proj GEMM outputs it), x += delta (bf16), h_out = LayerNorm(x;
+ * gamma, beta, eps).  w1 [n_hidden][d], w2 [d][n_hidden] (nn.Linear layout).  Replaces
+ * dk_net_fc_gelu_bf16_async + the second GEMM + dk_net_add_ln_bf16_async of
+ * TransformerBlock.py's MLP (az_doko.py:87-145). */
+int dk_net_mlp_ln_bf16_async(const void* h, void* x_io, const void* w1, const void* b1, const void* w2, const void* b2,
+                             uint32_t rows, uint32_t d, uint32_t n_hidden, const void* gamma, const void* beta, float eps,
+                             void* h_out, void* stream);
 /* dk_net_attn62_bf16_async: softmax(q k^T / sqrt(head_dim)) v for the networks' shape (62
  * tokens; heads x head_dim = 4 x 40 for the AlphaZero network, 4 x 64 for the IMPI network),
  * q/k/v read from the fused projection qkv[batch*62][3d] ([q | k | v], heads contiguous), the

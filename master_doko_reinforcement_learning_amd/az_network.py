@@ -156,12 +156,25 @@ class FusedTrunk:
                                                  self.rows, self.d, n, a.data_ptr(), self.st))
         return blk.proj(a)
 
+    def mlp_ln(self, x, blk, h, ln):
+        """x += proj(GELU(fc(h))); returns LN(x): the whole MLP half of the block and the
+        LayerNorm after it in one kernel (d = 160 or 256: the hidden activation never leaves the CU)."""
+        n = blk.fc.weight.shape[0]
+        if self.d not in (160, 256) or n % (64 if self.d == 160 else 32):
+            return self.add_ln(x, self.mlp_delta(blk, h), ln)
+        out = torch.empty_like(x)
+        self.ck(self.L.dk_net_mlp_ln_bf16_async(h.data_ptr(), x.data_ptr(), blk.fc.weight.data_ptr(),
+                                                blk.fc.bias.data_ptr(), blk.proj.weight.data_ptr(), blk.proj.bias.data_ptr(),
+                                                self.rows, self.d, n, ln.weight.data_ptr(), ln.bias.data_ptr(), ln.eps,
+                                                out.data_ptr(), self.st))
+        return out
+
     def run(self, h, blocks, final_ln, x=None):
         x = self.x if x is None else x
         for i, blk in enumerate(blocks):
             h = self.add_ln(x, self.attn_delta(blk, h), blk.ln_2)
             nxt = blocks[i + 1].ln_1 if i + 1 < len(blocks) else final_ln
-            h = self.add_ln(x, self.mlp_delta(blk, h), nxt)
+            h = self.mlp_ln(x, blk, h, nxt)
         return h
 
 

@@ -426,5 +426,246 @@ __global__ void __launch_bounds__(256, 2) fc_gelu_kernel(const uint16_t* __restr
     }
 }
 
+// ---------------------------------------------------------------------------
+// The whole MLP half of a transformer block in one pass (d = 160, the AlphaZero network, in
+// chunks of NC = 64 hidden units; d = 256, the IMPI network, NC = 32 to fit the registers):
+//   a = GELU(h W1^T + b1)          (4d hidden units, NC at a time, never leaving the CU)
+//   delta = a W2^T + b2            (accumulated over the hidden chunks in registers)
+//   x += delta;  h' = LN'(x)       (the residual add and the NEXT LayerNorm, as add_ln)
+// Unfused, the block's MLP wrote and re-read the 4d-wide activation (1,280 B per row each
+// way) and the 2d-byte delta; here a row costs its h and x reads and its x and h' writes.
+//   workgroup: 8 waves x 32 rows; a wave's h fragments (all of K = d) stay in registers;
+//   chunk loop over the hidden units: W1 rows [NC x d] and W2 columns [d x NC] of the chunk
+//   staged in LDS (double-buffered, shared by the 8 waves);
+//   GEMM1: D1 = W1_c h^T, NC / 32 tiles of 32 hidden units x 32 rows (v_mfma_f32_32x32x16_bf16);
+//   the bias + GELU'd accumulators ARE the B operand of GEMM2 without moving between lanes:
+//   MFMA sums over k, so the k order only has to agree between A and B.  Lane (r, hh)
+//   holds hidden units 32j + (g & 3) + 8 (g >> 2) + 4 hh of its row; k-step s = 2j + half
+//   takes its registers g = 8 half .. 8 half + 7, and the W2 fragment of the same k-step
+//   reads the matching hidden units (two runs of 4) from the LDS copy of W2;
+//   GEMM2: D2 = W2_c a^T, d / 32 tiles of 32 output columns x 32 rows, NC / 16 k-steps per chunk;
+//   epilogue: delta rounded to bf16 (torch's proj output), x + delta rounded to bf16, the
+//   row's mean / variance over the two half-wave lanes that hold it, h' = LN'(x).
+// GELU for the fused MLP: the same A&S 7.1.26 erf, rearranged for packed f32 (no selects):
+// GELU(v) = 0.5 v (1 + erf(v / sqrt2)) = 0.5 (v + |v|) - 0.5 |v| erfc(|v| / sqrt2), erf being odd.
+__device__ __forceinline__ f32x2_t gelu_erf2_pk(f32x2_t v) {
+    const f32x2_t a = __builtin_elementwise_abs(v);
+    const f32x2_t z = a * 0.70710678118654752f;
+    const f32x2_t d = __builtin_elementwise_fma(f32x2_t{0.3275911f, 0.3275911f}, z, f32x2_t{1.0f, 1.0f});
+    const f32x2_t t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+    f32x2_t p = __builtin_elementwise_fma(f32x2_t{1.061405429f, 1.061405429f}, t, f32x2_t{-1.453152027f, -1.453152027f});
+    p = __builtin_elementwise_fma(p, t, f32x2_t{1.421413741f, 1.421413741f});
+    p = __builtin_elementwise_fma(p, t, f32x2_t{-0.284496736f, -0.284496736f});
+    p = __builtin_elementwise_fma(p, t, f32x2_t{0.254829592f, 0.254829592f});
+    const f32x2_t q = z * (z * -1.4426950408889634f);
+    const f32x2_t e = {__builtin_amdgcn_exp2f(q.x), __builtin_amdgcn_exp2f(q.y)};
+    const f32x2_t c = (p * t) * e;                                   // erfc(|v| / sqrt2)
+    const f32x2_t ha = a * 0.5f;
+    return __builtin_elementwise_fma(-ha, c, __builtin_elementwise_fma(v, f32x2_t{0.5f, 0.5f}, ha));
+}
+
+// f32 pair -> two bf16 (round to nearest even, NaN kept), one v_cvt_pk_bf16_f32
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+    typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+    union { bf16x2_t v; uint32_t u; } r;
+    r.v = bf16x2_t{(__bf16)lo, (__bf16)hi};
+    return r.u;
+}
+
+constexpr uint32_t MLP_MAX_HIDDEN = 1024;
+template <int D, int NC>
+__global__ void __launch_bounds__(512, 1) mlp_ln_kernel(const uint16_t* __restrict__ h, uint16_t* __restrict__ x_io,
+                                                        const uint16_t* __restrict__ w1, const uint16_t* __restrict__ b1,
+                                                        const uint16_t* __restrict__ w2, const uint16_t* __restrict__ b2,
+                                                        uint32_t rows, uint32_t n_hidden, const uint16_t* __restrict__ gamma,
+                                                        const uint16_t* __restrict__ beta, float eps,
+                                                        uint16_t* __restrict__ h_out) {
+    static_assert(D % 32 == 0 && NC % 32 == 0, "d and the chunk: multiples of 32");
+    constexpr int KS = D / 16, OT = D / 32, LDW1 = D + 8, LDW2 = NC + 8, HT = NC / 32, GS = NC / 16;
+    __shared__ uint16_t w1s[2][NC * LDW1];
+    __shared__ uint16_t w2s[2][D * LDW2];
+    __shared__ float b1s[MLP_MAX_HIDDEN];           // the hidden units' biases
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
+    const uint32_t row = blockIdx.x * 256u + (uint32_t)wave * 32u + (uint32_t)r;
+    const bool ok = row < rows;
+    bf16x8_t hf[KS];
+    {
+        const uint16_t* hr = h + (size_t)(ok ? row : 0u) * D + 8 * hh;
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk) hf[kk] = load_frag8(hr + 16 * kk, ok);
+    }
+    // the chunk's weights: W1 rows c*NC .. +NC (D elements each) and columns c*NC .. +NC of every
+    // W2 row, as 16-byte pieces; the next chunk's pieces are loaded into registers before this
+    // chunk's GEMMs and written to the other LDS buffer after them (their latency hidden)
+    // The pieces live in named registers (pa0..2, pb0..2), each piece index a literal: an array
+    // indexed in a loop is an alloca that the compiler promoted to LDS here, which serialised
+    // every global load behind its LDS store.
+    constexpr int P1 = NC * (D / 8), P2 = D * (NC / 8);
+    static_assert(P1 <= 3 * 512 && P2 <= 3 * 512, "three pieces per thread and matrix");
+    uint4 pa0{}, pa1{}, pa2{}, pb0{}, pb1{}, pb2{};
+#define DK_MLP_LD(U, R1, R2, c)                                                                                \
+    {                                                                                                          \
+        const int v = threadIdx.x + 512 * (U);                                                                 \
+        if (v < P1) { const int i = v / (D / 8), p = v - i * (D / 8); R1 = *(const uint4*)(w1 + ((size_t)(c) * NC + i) * D + 8 * p); } \
+        if (v < P2) { const int o = v / (NC / 8), p = v - o * (NC / 8); R2 = *(const uint4*)(w2 + (size_t)o * n_hidden + (size_t)(c) * NC + 8 * p); } \
+    }
+#define DK_MLP_ST(U, R1, R2, buf)                                                                              \
+    {                                                                                                          \
+        const int v = threadIdx.x + 512 * (U);                                                                 \
+        if (v < P1) { const int i = v / (D / 8), p = v - i * (D / 8); *(uint4*)&w1s[buf][i * LDW1 + 8 * p] = R1; } \
+        if (v < P2) { const int o = v / (NC / 8), p = v - o * (NC / 8); *(uint4*)&w2s[buf][o * LDW2 + 8 * p] = R2; } \
+    }
+#define DK_MLP_LOAD_CHUNK(c) { DK_MLP_LD(0, pa0, pb0, c) DK_MLP_LD(1, pa1, pb1, c) DK_MLP_LD(2, pa2, pb2, c) }
+#define DK_MLP_STORE_CHUNK(buf) { DK_MLP_ST(0, pa0, pb0, buf) DK_MLP_ST(1, pa1, pb1, buf) DK_MLP_ST(2, pa2, pb2, buf) }
+    f32x16_t acc2[OT];
+#pragma unroll
+    for (int t = 0; t < OT; ++t) acc2[t] = f32x16_t{0};
+    const uint32_t chunks = n_hidden / NC;
+    for (uint32_t i = threadIdx.x; i < n_hidden; i += 512) b1s[i] = bf2f(b1[i]);
+    DK_MLP_LOAD_CHUNK(0u)
+    DK_MLP_STORE_CHUNK(0)
+    __syncthreads();
+    for (uint32_t c = 0; c < chunks; ++c) {
+        const int buf = (int)(c & 1u);
+        if (c + 1 < chunks) DK_MLP_LOAD_CHUNK(c + 1)
+        f32x16_t acc1[HT];
+#pragma unroll
+        for (int j = 0; j < HT; ++j) acc1[j] = f32x16_t{0};
+        // GEMM1, software-pipelined one k-step deep: the W1 fragments of k-step kk + 1 are read
+        // from LDS while the MFMAs of k-step kk run
+        {
+            bf16x8_t cur[HT], nxt[HT];
+#pragma unroll
+            for (int j = 0; j < HT; ++j) cur[j] = *(const bf16x8_t*)&w1s[buf][(32 * j + r) * LDW1 + 8 * hh];
+#pragma unroll
+            for (int kk = 0; kk < KS; ++kk) {
+                if (kk + 1 < KS) {
+#pragma unroll
+                    for (int j = 0; j < HT; ++j)
+                        nxt[j] = *(const bf16x8_t*)&w1s[buf][(32 * j + r) * LDW1 + 16 * (kk + 1) + 8 * hh];
+                }
+#pragma unroll
+                for (int j = 0; j < HT; ++j) acc1[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[j], hf[kk], acc1[j], 0, 0, 0);
+#pragma unroll
+                for (int j = 0; j < HT; ++j) cur[j] = nxt[j];
+            }
+        }
+        // bias + GELU -> bf16 B fragments of GEMM2 (k-step s = 2 j + half: registers 8 half .. +7)
+        bf16x8_t af[GS];
+#pragma unroll
+        for (int s = 0; s < GS; ++s) {
+            const int j = s >> 1, half = s & 1, h0 = 32 * j + 16 * half + 4 * hh;
+            const float4 bl = *(const float4*)&b1s[c * NC + h0], bh = *(const float4*)&b1s[c * NC + h0 + 8];
+            const float bb[8] = {bl.x, bl.y, bl.z, bl.w, bh.x, bh.y, bh.z, bh.w};
+            union { uint32_t u[4]; bf16x8_t v; } pk;
+#pragma unroll
+            for (int t = 0; t < 8; t += 2) {
+#ifdef DK_MLP_SOL_NO_GELU   // speed-of-light experiment (wrong results): the activation without GELU
+                const f32x2_t g = f32x2_t{acc1[j][8 * half + t] + bb[t], acc1[j][8 * half + t + 1] + bb[t + 1]};
+#else
+                const f32x2_t g = gelu_erf2_pk(f32x2_t{acc1[j][8 * half + t] + bb[t], acc1[j][8 * half + t + 1] + bb[t + 1]});
+#endif
+                pk.u[t / 2] = pack_bf16x2(g.x, g.y);
+            }
+            af[s] = pk.v;
+        }
+        // GEMM2, pipelined one output tile deep (the W2 fragment of the next tile read during this one)
+        {
+            auto w2frag = [&](int s, int t) {
+                const int h0 = 32 * (s >> 1) + 16 * (s & 1) + 4 * hh;
+                const uint16_t* wr = &w2s[buf][(32 * t + r) * LDW2 + h0];
+                union { uint2 u[2]; bf16x8_t v; } a;
+                a.u[0] = *(const uint2*)wr;
+                a.u[1] = *(const uint2*)(wr + 8);
+                return a.v;
+            };
+            bf16x8_t cur = w2frag(0, 0);
+#pragma unroll
+            for (int q = 0; q < GS * OT; ++q) {
+                const int s = q / OT, t = q % OT;
+                bf16x8_t nxt = cur;
+                if (q + 1 < GS * OT) nxt = w2frag((q + 1) / OT, (q + 1) % OT);
+                acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur, af[s], acc2[t], 0, 0, 0);
+                cur = nxt;
+            }
+        }
+        if (c + 1 < chunks) DK_MLP_STORE_CHUNK(buf ^ 1)
+        // LDS-only barrier: the next chunk is staged and this chunk's reads are done
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    }
+#ifdef DK_MLP_SOL_NO_EPILOGUE   // speed-of-light experiment: no residual / LayerNorm / row stores
+    {
+        float z = 0.0f;
+#pragma unroll
+        for (int t = 0; t < OT; ++t)
+#pragma unroll
+            for (int g = 0; g < 16; ++g) z += acc2[t][g];
+        if (z == 12345.678f) h_out[row] = 1;
+        return;
+    }
+#endif
+    // epilogue: acc2[t][g] = delta of row `row`, column 32 t + 8 (g >> 2) + 4 hh + (g & 3)
+    uint16_t* xr = x_io + (size_t)(ok ? row : 0u) * D;
+    float s1 = 0.0f;
+#pragma unroll
+    for (int t = 0; t < OT; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int col = 32 * t + 8 * q + 4 * hh;
+            const uint2 xv = ok ? *(const uint2*)(xr + col) : make_uint2(0u, 0u);
+            const uint2 bv = *(const uint2*)(b2 + col);
+            const uint16_t xs[4] = {(uint16_t)xv.x, (uint16_t)(xv.x >> 16), (uint16_t)xv.y, (uint16_t)(xv.y >> 16)};
+            const uint16_t bs[4] = {(uint16_t)bv.x, (uint16_t)(bv.x >> 16), (uint16_t)bv.y, (uint16_t)(bv.y >> 16)};
+            float xn[4];
+#pragma unroll
+            for (int e = 0; e < 4; e += 2) {
+                // delta rounded to bf16 (the unfused proj GEMM's output), then x + delta rounded
+                const uint32_t dl = pack_bf16x2(acc2[t][4 * q + e] + bf2f(bs[e]), acc2[t][4 * q + e + 1] + bf2f(bs[e + 1]));
+                const uint32_t xo = pack_bf16x2(bf2f(xs[e]) + bf2f((uint16_t)dl), bf2f(xs[e + 1]) + bf2f((uint16_t)(dl >> 16)));
+                xn[e] = bf2f((uint16_t)xo);
+                xn[e + 1] = bf2f((uint16_t)(xo >> 16));
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                acc2[t][4 * q + e] = xn[e];
+                s1 += xn[e];
+            }
+            if (ok) *(uint2*)(xr + col) = make_uint2(pack_bf16x2(xn[0], xn[1]), pack_bf16x2(xn[2], xn[3]));
+        }
+    s1 += __shfl_xor(s1, 32);
+    const float mean = s1 / (float)D;
+    float s2 = 0.0f;
+#pragma unroll
+    for (int t = 0; t < OT; ++t)
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+            const float dv = acc2[t][g] - mean;
+            s2 += dv * dv;
+        }
+    s2 += __shfl_xor(s2, 32);
+    const float rstd = rsqrtf(s2 / (float)D + eps);
+    uint16_t* hr = h_out + (size_t)(ok ? row : 0u) * D;
+#pragma unroll
+    for (int t = 0; t < OT; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int col = 32 * t + 8 * q + 4 * hh;
+            const uint2 gv = *(const uint2*)(gamma + col), bv = *(const uint2*)(beta + col);
+            const uint16_t gs[4] = {(uint16_t)gv.x, (uint16_t)(gv.x >> 16), (uint16_t)gv.y, (uint16_t)(gv.y >> 16)};
+            const uint16_t bs[4] = {(uint16_t)bv.x, (uint16_t)(bv.x >> 16), (uint16_t)bv.y, (uint16_t)(bv.y >> 16)};
+            float o[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = (acc2[t][4 * q + e] - mean) * rstd * bf2f(gs[e]) + bf2f(bs[e]);
+            if (ok) *(uint2*)(hr + col) = make_uint2(pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]));
+        }
+}
+#undef DK_MLP_LD
+#undef DK_MLP_ST
+#undef DK_MLP_LOAD_CHUNK
+#undef DK_MLP_STORE_CHUNK
+
 }  // namespace net
 }  // namespace dk

@@ -1828,6 +1828,26 @@ int dk_net_fc_gelu_bf16_async(const void* x, const void* w, const void* bias, ui
     return DK_OK;
 }
 
+int dk_net_mlp_ln_bf16_async(const void* h, void* x_io, const void* w1, const void* b1, const void* w2, const void* b2,
+                             uint32_t rows, uint32_t d, uint32_t n_hidden, const void* gamma, const void* beta, float eps,
+                             void* h_out, void* stream) {
+    if (!h || !x_io || !w1 || !b1 || !w2 || !b2 || !gamma || !beta || !h_out || (d != 160u && d != 256u) ||
+        n_hidden == 0 || n_hidden > dk::net::MLP_MAX_HIDDEN || n_hidden % (d == 160u ? 64u : 32u))
+        return DK_E_INVALID;
+    if (rows == 0) return DK_OK;
+    const dim3 grid((rows + 255u) / 256u), block(512);
+    if (d == 160u)
+        hipLaunchKernelGGL((dk::net::mlp_ln_kernel<160, 64>), grid, block, 0, (hipStream_t)stream, (const uint16_t*)h,
+                           (uint16_t*)x_io, (const uint16_t*)w1, (const uint16_t*)b1, (const uint16_t*)w2, (const uint16_t*)b2,
+                           rows, n_hidden, (const uint16_t*)gamma, (const uint16_t*)beta, eps, (uint16_t*)h_out);
+    else
+        hipLaunchKernelGGL((dk::net::mlp_ln_kernel<256, 32>), grid, block, 0, (hipStream_t)stream, (const uint16_t*)h,
+                           (uint16_t*)x_io, (const uint16_t*)w1, (const uint16_t*)b1, (const uint16_t*)w2, (const uint16_t*)b2,
+                           rows, n_hidden, (const uint16_t*)gamma, (const uint16_t*)beta, eps, (uint16_t*)h_out);
+    DK_HIP(hipGetLastError());
+    return DK_OK;
+}
+
 int dk_net_attn62_bf16_async(const void* qkv, void* y, uint32_t batch, uint32_t heads, uint32_t head_dim, void* stream) {
     if (!qkv || !y || heads != 4u || (head_dim != 40u && head_dim != 64u)) return DK_E_INVALID;
     if (batch == 0) return DK_OK;

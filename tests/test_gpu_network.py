@@ -93,3 +93,34 @@ def test_fc_gelu_matches_torch(k, n):
     ref = F.gelu(F.linear(x.float(), w.float(), b.float()))
     assert torch.isfinite(y.float()).all()
     torch.testing.assert_close(y.float(), ref, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("d,n", [(160, 640), (256, 1024)])
+def test_mlp_ln_matches_torch(d, n):
+    """The fused MLP half of a block (d = 160 AlphaZero, 256 IMPI): x += proj(GELU(fc(h))) and
+    h' = LN'(x), against fp32 torch on the same bf16 inputs (the delta rounded to bf16 like the
+    unfused proj GEMM)."""
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(7)
+    rows = 62 * 41 + 3                                   # not a multiple of the 256-row workgroup tile
+    h = torch.randn(rows, d, device=dev).bfloat16()
+    x = (torch.randn(rows, d, device=dev) * 2).bfloat16()
+    w1 = (torch.randn(n, d, device=dev) / d ** 0.5).bfloat16()
+    b1 = (torch.randn(n, device=dev) * 0.1).bfloat16()
+    w2 = (torch.randn(d, n, device=dev) / n ** 0.5).bfloat16()
+    b2 = (torch.randn(d, device=dev) * 0.1).bfloat16()
+    g = (1 + 0.1 * torch.randn(d, device=dev)).bfloat16()
+    be = (0.1 * torch.randn(d, device=dev)).bfloat16()
+    delta_ref = F.linear(F.gelu(F.linear(h.float(), w1.float(), b1.float())), w2.float(), b2.float())
+    x_ref = x.float() + delta_ref.bfloat16().float()
+    h_ref = F.layer_norm(x_ref.bfloat16().float(), (d,), g.float(), be.float(), 1e-5)
+    xo = x.clone()
+    out = torch.full((rows, d), float("nan"), device=dev).bfloat16()
+    rc = _lib().dk_net_mlp_ln_bf16_async(h.data_ptr(), xo.data_ptr(), w1.data_ptr(), b1.data_ptr(), w2.data_ptr(),
+                                         b2.data_ptr(), rows, d, n, g.data_ptr(), be.data_ptr(), 1e-5, out.data_ptr(),
+                                         torch.cuda.current_stream(dev).cuda_stream)
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert torch.isfinite(out.float()).all() and torch.isfinite(xo.float()).all()
+    torch.testing.assert_close(xo.float(), x_ref, rtol=1e-2, atol=3e-2)
+    torch.testing.assert_close(out.float(), h_ref, rtol=1e-2, atol=3e-2)

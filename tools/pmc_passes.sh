@@ -17,6 +17,8 @@ PASSES=(
   "SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_INSTS_SALU GRBM_GUI_ACTIVE"
   "SQ_ACTIVE_INST_VALU2 SQ_BUSY_CU_CYCLES SQ_INST_CYCLES_SALU SQ_WAIT_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_CYCLES SQ_WAVES GRBM_GUI_ACTIVE GRBM_COUNT"
 )
+# PMC_SETS="A B;C D" replaces the default passes (one pass per ';'-separated set)
+if [ -n "${PMC_SETS:-}" ]; then IFS=';' read -r -a PASSES <<< "$PMC_SETS"; fi
 i=0
 for set in "${PASSES[@]}"; do
   i=$((i+1))
