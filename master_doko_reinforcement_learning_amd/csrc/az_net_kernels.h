@@ -14,6 +14,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace dk {
 namespace net {
 
@@ -482,8 +484,9 @@ __global__ void __launch_bounds__(512, 1) mlp_ln_kernel(const uint16_t* __restri
                                                         uint16_t* __restrict__ h_out) {
     static_assert(D % 32 == 0 && NC % 32 == 0, "d and the chunk: multiples of 32");
     constexpr int KS = D / 16, OT = D / 32, LDW1 = D + 8, LDW2 = NC + 8, HT = NC / 32, GS = NC / 16;
-    __shared__ uint16_t w1s[2][NC * LDW1];
-    __shared__ uint16_t w2s[2][D * LDW2];
+    // LDS: the chunk's W1 / W2, double-buffered
+    constexpr int W1E = NC * LDW1, W2E = D * LDW2;
+    __shared__ __attribute__((aligned(16))) uint16_t lds[2 * (W1E + W2E)];
     __shared__ float b1s[MLP_MAX_HIDDEN];           // the hidden units' biases
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
     const uint32_t row = blockIdx.x * 256u + (uint32_t)wave * 32u + (uint32_t)r;
@@ -512,8 +515,8 @@ __global__ void __launch_bounds__(512, 1) mlp_ln_kernel(const uint16_t* __restri
 #define DK_MLP_ST(U, R1, R2, buf)                                                                              \
     {                                                                                                          \
         const int v = threadIdx.x + 512 * (U);                                                                 \
-        if (v < P1) { const int i = v / (D / 8), p = v - i * (D / 8); *(uint4*)&w1s[buf][i * LDW1 + 8 * p] = R1; } \
-        if (v < P2) { const int o = v / (NC / 8), p = v - o * (NC / 8); *(uint4*)&w2s[buf][o * LDW2 + 8 * p] = R2; } \
+        if (v < P1) { const int i = v / (D / 8), p = v - i * (D / 8); *(uint4*)&lds[(buf) * W1E + i * LDW1 + 8 * p] = R1; } \
+        if (v < P2) { const int o = v / (NC / 8), p = v - o * (NC / 8); *(uint4*)&lds[2 * W1E + (buf) * W2E + o * LDW2 + 8 * p] = R2; } \
     }
 #define DK_MLP_LOAD_CHUNK(c) { DK_MLP_LD(0, pa0, pb0, c) DK_MLP_LD(1, pa1, pb1, c) DK_MLP_LD(2, pa2, pb2, c) }
 #define DK_MLP_STORE_CHUNK(buf) { DK_MLP_ST(0, pa0, pb0, buf) DK_MLP_ST(1, pa1, pb1, buf) DK_MLP_ST(2, pa2, pb2, buf) }
@@ -525,7 +528,10 @@ __global__ void __launch_bounds__(512, 1) mlp_ln_kernel(const uint16_t* __restri
     DK_MLP_LOAD_CHUNK(0u)
     DK_MLP_STORE_CHUNK(0)
     __syncthreads();
-    for (uint32_t c = 0; c < chunks; ++c) {
+    // the residual rows' column groups of this lane (epilogue), loaded during the last chunk
+    constexpr bool PREFETCH_X = D <= 160;
+    uint2 xv[OT][4];
+    auto chunk = [&](uint32_t c, auto last) {
         const int buf = (int)(c & 1u);
         if (c + 1 < chunks) DK_MLP_LOAD_CHUNK(c + 1)
         f32x16_t acc1[HT];
@@ -536,19 +542,28 @@ __global__ void __launch_bounds__(512, 1) mlp_ln_kernel(const uint16_t* __restri
         {
             bf16x8_t cur[HT], nxt[HT];
 #pragma unroll
-            for (int j = 0; j < HT; ++j) cur[j] = *(const bf16x8_t*)&w1s[buf][(32 * j + r) * LDW1 + 8 * hh];
+            for (int j = 0; j < HT; ++j) cur[j] = *(const bf16x8_t*)&lds[(buf) * W1E + (32 * j + r) * LDW1 + 8 * hh];
 #pragma unroll
             for (int kk = 0; kk < KS; ++kk) {
                 if (kk + 1 < KS) {
 #pragma unroll
                     for (int j = 0; j < HT; ++j)
-                        nxt[j] = *(const bf16x8_t*)&w1s[buf][(32 * j + r) * LDW1 + 16 * (kk + 1) + 8 * hh];
+                        nxt[j] = *(const bf16x8_t*)&lds[(buf) * W1E + (32 * j + r) * LDW1 + 16 * (kk + 1) + 8 * hh];
                 }
 #pragma unroll
                 for (int j = 0; j < HT; ++j) acc1[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[j], hf[kk], acc1[j], 0, 0, 0);
 #pragma unroll
                 for (int j = 0; j < HT; ++j) cur[j] = nxt[j];
             }
+        }
+        if constexpr (decltype(last)::value && PREFETCH_X) {
+            // last chunk: the residual x of the epilogue is loaded now (the h fragments are dead),
+            // in flight during the last GELU and GEMM2 (d = 160; d = 256 has no registers to spare)
+            const uint16_t* xr = x_io + (size_t)(ok ? row : 0u) * D;
+#pragma unroll
+            for (int t = 0; t < OT; ++t)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) xv[t][q] = ok ? *(const uint2*)(xr + 32 * t + 8 * q + 4 * hh) : make_uint2(0u, 0u);
         }
         // bias + GELU -> bf16 B fragments of GEMM2 (k-step s = 2 j + half: registers 8 half .. +7)
         bf16x8_t af[GS];
@@ -560,11 +575,7 @@ __global__ void __launch_bounds__(512, 1) mlp_ln_kernel(const uint16_t* __restri
             union { uint32_t u[4]; bf16x8_t v; } pk;
 #pragma unroll
             for (int t = 0; t < 8; t += 2) {
-#ifdef DK_MLP_SOL_NO_GELU   // speed-of-light experiment (wrong results): the activation without GELU
-                const f32x2_t g = f32x2_t{acc1[j][8 * half + t] + bb[t], acc1[j][8 * half + t + 1] + bb[t + 1]};
-#else
                 const f32x2_t g = gelu_erf2_pk(f32x2_t{acc1[j][8 * half + t] + bb[t], acc1[j][8 * half + t + 1] + bb[t + 1]});
-#endif
                 pk.u[t / 2] = pack_bf16x2(g.x, g.y);
             }
             af[s] = pk.v;
@@ -573,7 +584,7 @@ __global__ void __launch_bounds__(512, 1) mlp_ln_kernel(const uint16_t* __restri
         {
             auto w2frag = [&](int s, int t) {
                 const int h0 = 32 * (s >> 1) + 16 * (s & 1) + 4 * hh;
-                const uint16_t* wr = &w2s[buf][(32 * t + r) * LDW2 + h0];
+                const uint16_t* wr = &lds[2 * W1E + (buf) * W2E + (32 * t + r) * LDW2 + h0];
                 union { uint2 u[2]; bf16x8_t v; } a;
                 a.u[0] = *(const uint2*)wr;
                 a.u[1] = *(const uint2*)(wr + 8);
@@ -595,29 +606,27 @@ __global__ void __launch_bounds__(512, 1) mlp_ln_kernel(const uint16_t* __restri
         __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-    }
-#ifdef DK_MLP_SOL_NO_EPILOGUE   // speed-of-light experiment: no residual / LayerNorm / row stores
-    {
-        float z = 0.0f;
+    };
+    for (uint32_t c = 0; c + 1 < chunks; ++c) chunk(c, std::false_type{});
+    chunk(chunks - 1, std::true_type{});
+
+    // epilogue: acc2[t][g] = delta of row `row`, column 32 t + 8 (g >> 2) + 4 hh + (g & 3)
+    uint16_t* xr = x_io + (size_t)(ok ? row : 0u) * D;
+    if constexpr (!PREFETCH_X) {
 #pragma unroll
         for (int t = 0; t < OT; ++t)
 #pragma unroll
-            for (int g = 0; g < 16; ++g) z += acc2[t][g];
-        if (z == 12345.678f) h_out[row] = 1;
-        return;
+            for (int q = 0; q < 4; ++q) xv[t][q] = ok ? *(const uint2*)(xr + 32 * t + 8 * q + 4 * hh) : make_uint2(0u, 0u);
     }
-#endif
-    // epilogue: acc2[t][g] = delta of row `row`, column 32 t + 8 (g >> 2) + 4 hh + (g & 3)
-    uint16_t* xr = x_io + (size_t)(ok ? row : 0u) * D;
     float s1 = 0.0f;
 #pragma unroll
     for (int t = 0; t < OT; ++t)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int col = 32 * t + 8 * q + 4 * hh;
-            const uint2 xv = ok ? *(const uint2*)(xr + col) : make_uint2(0u, 0u);
             const uint2 bv = *(const uint2*)(b2 + col);
-            const uint16_t xs[4] = {(uint16_t)xv.x, (uint16_t)(xv.x >> 16), (uint16_t)xv.y, (uint16_t)(xv.y >> 16)};
+            const uint16_t xs[4] = {(uint16_t)xv[t][q].x, (uint16_t)(xv[t][q].x >> 16), (uint16_t)xv[t][q].y,
+                                    (uint16_t)(xv[t][q].y >> 16)};
             const uint16_t bs[4] = {(uint16_t)bv.x, (uint16_t)(bv.x >> 16), (uint16_t)bv.y, (uint16_t)(bv.y >> 16)};
             float xn[4];
 #pragma unroll
