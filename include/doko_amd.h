@@ -477,6 +477,12 @@ int dk_net_fc_gelu_bf16_async(const void* x, const void* w, const void* bias, ui
 int dk_net_mlp_ln_bf16_async(const void* h, void* x_io, const void* w1, const void* b1, const void* w2, const void* b2,
                              uint32_t rows, uint32_t d, uint32_t n_hidden, const void* gamma, const void* beta, float eps,
                              void* h_out, void* stream);
+/* dk_net_attn_ln_bf16_async: the attention half of a transformer block after its qkv projection,
+ * in one pass per sample: y = attention core (as dk_net_attn62_bf16_async), delta = y wp^T + bp
+ * (the folded out_proj / c_proj, wp [d][d]), x += delta (bf16), h_out = LayerNorm(x; gamma,
+ * beta, eps).  heads = 4, head_dim 40 (d 160) or 64 (d 256). */
+int dk_net_attn_ln_bf16_async(const void* qkv, void* x_io, const void* wp, const void* bp, uint32_t batch, uint32_t heads,
+                              uint32_t head_dim, const void* gamma, const void* beta, float eps, void* h_out, void* stream);
 /* dk_net_attn62_bf16_async: softmax(q k^T / sqrt(head_dim)) v for the networks' shape (62
  * tokens; heads x head_dim = 4 x 40 for the AlphaZero network, 4 x 64 for the IMPI network),
  * q/k/v read from the fused projection qkv[batch*62][3d] ([q | k | v], heads contiguous), the

@@ -108,8 +108,9 @@ class FusedTrunk:
     """The bf16 GPU forward of a token trunk (shared by DokoAzNet and DokoImpiNet): HIP
     kernels (csrc/az_net_kernels.h) for the embedding sum + first LayerNorm, every
     residual add fused with the LayerNorm that follows it, (4 heads of 40 or 64) the
-    62-token attention core, and (d = 160 or 256) the MLP's first layer with its exact
-    GELU; the other GEMMs are torch (hipBLASLt).  `x` is the residual stream, `h` the
+    attention half after the qkv GEMM (attention core + folded projection + residual +
+    LayerNorm in one kernel), and (d = 160 or 256) the whole MLP half; the qkv GEMM and the
+    heads are torch (hipBLASLt).  `x` is the residual stream, `h` the
     current LayerNorm output."""
 
     def __init__(self, tokens, emb, ln0):
@@ -156,6 +157,19 @@ class FusedTrunk:
                                                  self.rows, self.d, n, a.data_ptr(), self.st))
         return blk.proj(a)
 
+    def attn_ln(self, x, blk, h, ln):
+        """x += c_proj(out(MHA(qkv(h)))); returns LN(x): after the qkv GEMM, the attention core,
+        the folded projection, the residual add and the LayerNorm in one kernel per sample."""
+        if not (blk.heads == 4 and self.d // 4 in (40, 64) and self.d % 4 == 0):
+            return self.add_ln(x, self.attn_delta(blk, h), ln)
+        qkv = blk.qkv(h)
+        w, b = blk.folded_proj()
+        out = torch.empty_like(x)
+        self.ck(self.L.dk_net_attn_ln_bf16_async(qkv.data_ptr(), x.data_ptr(), w.data_ptr(), b.data_ptr(), h.shape[0], 4,
+                                                 self.d // 4, ln.weight.data_ptr(), ln.bias.data_ptr(), ln.eps,
+                                                 out.data_ptr(), self.st))
+        return out
+
     def mlp_ln(self, x, blk, h, ln):
         """x += proj(GELU(fc(h))); returns LN(x): the whole MLP half of the block and the
         LayerNorm after it in one kernel (d = 160 or 256: the hidden activation never leaves the CU)."""
@@ -172,7 +186,7 @@ class FusedTrunk:
     def run(self, h, blocks, final_ln, x=None):
         x = self.x if x is None else x
         for i, blk in enumerate(blocks):
-            h = self.add_ln(x, self.attn_delta(blk, h), blk.ln_2)
+            h = self.attn_ln(x, blk, h, blk.ln_2)
             nxt = blocks[i + 1].ln_1 if i + 1 < len(blocks) else final_ln
             h = self.mlp_ln(x, blk, h, nxt)
         return h

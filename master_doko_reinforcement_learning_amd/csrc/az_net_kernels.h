@@ -172,25 +172,20 @@ __device__ __forceinline__ bf16x8_t load_frag8(const uint16_t* p, bool ok) {
     return r.v;
 }
 
-template <int HD, int H>
-__global__ void __launch_bounds__(256) attn62_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ y,
-                                                     uint32_t batch, float scale) {
+// One (sample, head) of the attention core, the body shared by attn62_kernel and attn_ln_kernel:
+// `base` = the sample's qkv rows, `vt` the wave's LDS V^T tile (HD x (64 + 4) bf16), put(s, e, v) receives output
+// element (token s < 62, head dim e < HD).  Every wave of the workgroup must call it (barrier).
+template <int HD, int H, class Put>
+__device__ __forceinline__ void attn62_head(const uint16_t* __restrict__ base, uint32_t hd, bool valid, uint16_t* vt,
+                                            float scale, Put put) {
     static_assert(HD % 8 == 0 && HD <= 64, "head dimension: a multiple of 8, at most 64");
     constexpr int S = 62, D = HD * H, LDT = 64 + 4;   // LDS row stride (keys) in bf16
     constexpr int PC = HD / 8;                        // 16-byte pieces per key row of V
     constexpr int KS = (HD + 15) / 16;                // k-steps over the head dimension
-    __shared__ uint16_t vt_all[4][64 * LDT];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint32_t bh = blockIdx.x * 4u + (uint32_t)wave;
-    const bool valid = bh < batch * (uint32_t)H;
-    const uint32_t b = valid ? bh / H : 0u, hd = valid ? bh % H : 0u;
-    const int r = lane & 31, h = lane >> 5;
-    const uint16_t* base = qkv + (size_t)b * S * (3 * D);
-    uint16_t* vt = vt_all[wave];
-
+    const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
     // V^T into LDS as [e][t]: the 62 x HD tile is read as 62 * HD / 8 16-byte pieces (8
     // dims of one key each, HD / 8 per lane) and scattered transposed; zero padding for
-    // t >= 62 and e >= HD
+    // t >= 62 (lanes of the second output tile with e >= HD read row HD - 1 and put nothing)
     {
 #pragma unroll
         for (int i = 0; i < PC; ++i) {
@@ -202,7 +197,6 @@ __global__ void __launch_bounds__(256) attn62_kernel(const uint16_t* __restrict_
 #pragma unroll
             for (int m = 0; m < 8; ++m) vt[(e0 + m) * LDT + t] = pc.s[m];
         }
-        for (int e = HD; e < 64; ++e) vt[e * LDT + lane] = 0;
     }
     // Q and K fragments: tile i covers tokens 32i + r, k-step kk covers dims 16kk + 8h + j
     bf16x8_t qf[2][KS], kf[2][KS];
@@ -267,13 +261,14 @@ __global__ void __launch_bounds__(256) attn62_kernel(const uint16_t* __restrict_
 #pragma unroll
     for (int et = 0; et < 2; ++et) {
         bf16x8_t vf[4];
-        const int e = 32 * et + r;
+        const int e = 32 * et + r, er = e < HD ? e : HD - 1;
+        if (32 * et >= HD) break;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int t0 = 16 * q + 4 * h;   // keys t0..t0+3 and t0+8..t0+11 (within tile q >> 1)
             union { uint2 u[2]; bf16x8_t v; } f;
-            f.u[0] = *(const uint2*)&vt[e * LDT + t0];
-            f.u[1] = *(const uint2*)&vt[e * LDT + t0 + 8];
+            f.u[0] = *(const uint2*)&vt[er * LDT + t0];
+            f.u[1] = *(const uint2*)&vt[er * LDT + t0 + 8];
             vf[q] = f.v;
         }
 #pragma unroll
@@ -285,8 +280,164 @@ __global__ void __launch_bounds__(256) attn62_kernel(const uint16_t* __restrict_
 #pragma unroll
                 for (int g = 0; g < 16; ++g) {
                     const int s = 32 * si + (g & 3) + 8 * (g >> 2) + 4 * h;
-                    if (s < S) y[((size_t)b * S + s) * D + hd * HD + e] = f2bf(acc[g]);
+                    if (s < S) put(s, e, acc[g]);
                 }
+            }
+        }
+    }
+}
+
+template <int HD, int H>
+__global__ void __launch_bounds__(256) attn62_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ y,
+                                                     uint32_t batch, float scale) {
+    constexpr int S = 62, D = HD * H, LDT = 64 + 4;
+    __shared__ uint16_t vt_all[4][HD * LDT];
+    const int wave = threadIdx.x >> 6;
+    const uint32_t bh = blockIdx.x * 4u + (uint32_t)wave;
+    const bool valid = bh < batch * (uint32_t)H;
+    const uint32_t b = valid ? bh / H : 0u, hd = valid ? bh % H : 0u;
+    attn62_head<HD, H>(qkv + (size_t)b * S * (3 * D), hd, valid, vt_all[wave], scale,
+                       [&](int s, int e, float v) { y[((size_t)b * S + s) * D + hd * HD + e] = f2bf(v); });
+}
+
+// ---------------------------------------------------------------------------
+// The attention half of a transformer block after the qkv projection, in one pass per sample:
+//   y = MHA core (attn62_head, one wave per head; y stays in LDS)
+//   delta = y Wp^T + bp   (the folded out_proj / c_proj GEMM, 16 rows per wave,
+//                          v_mfma_f32_16x16x32_bf16, Wp fragments read through the caches)
+//   x += delta;  h = LN(x)  (the residual add and ln_2, as add_ln)
+// Unfused, y and delta each went to HBM and back (2 x 4 d bytes per token) in three launches.
+// The sample's residual rows and both outputs move as coalesced 16-byte pieces of its 62
+// contiguous rows.  Numerics as the unfused path: y rounded to bf16 (the attention output),
+// delta + bias rounded to bf16 (the GEMM's output), x + delta rounded, LN of the rounded row.
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+template <int HD, int H>
+__global__ void __launch_bounds__(256, 2) attn_ln_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ x_io,
+                                                         const uint16_t* __restrict__ wp, const uint16_t* __restrict__ bp,
+                                                         uint32_t batch, float scale, const uint16_t* __restrict__ gamma,
+                                                         const uint16_t* __restrict__ beta, float eps,
+                                                         uint16_t* __restrict__ h_out) {
+    static_assert(H == 4, "one wave per head, four waves per workgroup");
+    constexpr int S = 62, D = HD * H, LDT = 64 + 4, LDY = D + 8, NT = D / 16, KS = D / 32;
+    constexpr int NJ = (NT + 3) / 4;          // column tiles per wave: w, w + 4, w + 8, ...
+    constexpr int XP = (S * (D / 8) + 255) / 256, LP = D / 32;   // 16-B pieces per thread: residual load, LN row
+    static_assert(D % 32 == 0, "d: a multiple of 32");
+    // LDS: the heads' V^T tiles, reused for the residual rows once attention is done (43 KB at
+    // d = 160, 69 KB at d = 256), and the attention output rows
+    constexpr int VT = 4 * HD * LDT, XS = 64 * LDY;
+    __shared__ __attribute__((aligned(16))) uint16_t lds_a[VT > XS ? VT : XS];
+    __shared__ __attribute__((aligned(16))) uint16_t ys[64 * LDY];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t b = blockIdx.x;                                   // one sample per workgroup
+    (void)batch;
+    for (int i = threadIdx.x; i < 2 * D; i += 256) ys[(S + i / D) * LDY + i % D] = 0;   // A operand padding rows
+    attn62_head<HD, H>(qkv + (size_t)b * S * (3 * D), (uint32_t)wave, true, lds_a + wave * HD * LDT, scale,
+                       [&](int s, int e, float v) { ys[s * LDY + wave * HD + e] = f2bf(v); });
+    __syncthreads();   // y complete in ys; the V^T tiles are dead
+    // the sample's residual rows: issued before the GEMM, stored to LDS after it
+    uint16_t* xs = lds_a;
+    const uint16_t* xg = x_io + (size_t)b * S * D;
+    uint4 xr[XP];
+#pragma unroll
+    for (int i = 0; i < XP; ++i) {
+        const int p = threadIdx.x + 256 * i;
+        xr[i] = p < S * (D / 8) ? *(const uint4*)(xg + 8 * p) : make_uint4(0u, 0u, 0u, 0u);
+    }
+    // delta = y Wp^T, the wave's column tiles T = wave + 4 j over all 64 rows (each Wp
+    // fragment read once per workgroup and used for 4 row tiles): A = y rows (lane: row rl,
+    // k 8 kg .. +7), B[k][n] = Wp[n][k]
+    const int rl = lane & 15, kg = lane >> 4;
+    f32x4_t acc[4][NJ];
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[m][j] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+        bf16x8_t a[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) a[m] = *(const bf16x8_t*)&ys[(16 * m + rl) * LDY + 32 * ks + 8 * kg];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int t = wave + 4 * j;
+            if (t < NT) {
+                const bf16x8_t w = load_frag8(wp + (size_t)(16 * t + rl) * D + 32 * ks + 8 * kg, true);
+#pragma unroll
+                for (int m = 0; m < 4; ++m) acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[m], w, acc[m][j], 0, 0, 0);
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < XP; ++i) {
+        const int p = threadIdx.x + 256 * i;
+        if (p < S * (D / 8)) {
+            const int rr = p / (D / 8), kp = p - rr * (D / 8);
+            *(uint4*)&xs[rr * LDY + 8 * kp] = xr[i];
+        }
+    }
+    __syncthreads();   // residual rows in xs
+    // x' = x + bf16(delta + bias), rounded like the unfused add; in place in xs
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        const int t = wave + 4 * j;
+        if (t < NT) {
+            const int col = 16 * t + rl;
+            const float bias = bf2f(bp[col]);
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    const int row = 16 * m + 4 * kg + v;
+                    const float delta = bf2f(f2bf(acc[m][j][v] + bias));
+                    xs[row * LDY + col] = f2bf(bf2f(xs[row * LDY + col]) + delta);
+                }
+        }
+    }
+    __syncthreads();   // x' complete
+    // LayerNorm: 4 threads per row, 16-B pieces q + 4 i; two-pass mean / variance
+    {
+        const int row = threadIdx.x >> 2, q = threadIdx.x & 3;
+        float xv[LP][8];
+        float s1 = 0.0f;
+#pragma unroll
+        for (int i = 0; i < LP; ++i) {
+            union { uint4 u; uint16_t s[8]; } pc;
+            pc.u = *(const uint4*)&xs[row * LDY + 8 * (q + 4 * i)];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                xv[i][e] = bf2f(pc.s[e]);
+                s1 += xv[i][e];
+            }
+        }
+        s1 += __shfl_xor(s1, 1);
+        s1 += __shfl_xor(s1, 2);
+        const float mean = s1 / (float)D;
+        float s2 = 0.0f;
+#pragma unroll
+        for (int i = 0; i < LP; ++i)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const float dv = xv[i][e] - mean;
+                s2 += dv * dv;
+            }
+        s2 += __shfl_xor(s2, 1);
+        s2 += __shfl_xor(s2, 2);
+        const float rstd = rsqrtf(s2 / (float)D + eps);
+        if (row < S) {
+            const size_t o = ((size_t)b * S + row) * D;
+#pragma unroll
+            for (int i = 0; i < LP; ++i) {
+                const int c0 = 8 * (q + 4 * i);
+                union { uint4 u; uint16_t s[8]; } gv, bv, xo, ho;
+                gv.u = *(const uint4*)(gamma + c0);
+                bv.u = *(const uint4*)(beta + c0);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    xo.s[e] = f2bf(xv[i][e]);
+                    ho.s[e] = f2bf((xv[i][e] - mean) * rstd * bf2f(gv.s[e]) + bf2f(bv.s[e]));
+                }
+                *(uint4*)(x_io + o + c0) = xo.u;
+                *(uint4*)(h_out + o + c0) = ho.u;
             }
         }
     }

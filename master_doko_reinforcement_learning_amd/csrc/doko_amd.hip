@@ -1848,6 +1848,24 @@ int dk_net_mlp_ln_bf16_async(const void* h, void* x_io, const void* w1, const vo
     return DK_OK;
 }
 
+int dk_net_attn_ln_bf16_async(const void* qkv, void* x_io, const void* wp, const void* bp, uint32_t batch, uint32_t heads,
+                              uint32_t head_dim, const void* gamma, const void* beta, float eps, void* h_out, void* stream) {
+    if (!qkv || !x_io || !wp || !bp || !gamma || !beta || !h_out || heads != 4u || (head_dim != 40u && head_dim != 64u))
+        return DK_E_INVALID;
+    if (batch == 0) return DK_OK;
+    const float scale = 1.0f / sqrtf((float)head_dim);
+    if (head_dim == 40u)
+        hipLaunchKernelGGL((dk::net::attn_ln_kernel<40, 4>), dim3(batch), dim3(256), 0, (hipStream_t)stream,
+                           (const uint16_t*)qkv, (uint16_t*)x_io, (const uint16_t*)wp, (const uint16_t*)bp, batch, scale,
+                           (const uint16_t*)gamma, (const uint16_t*)beta, eps, (uint16_t*)h_out);
+    else
+        hipLaunchKernelGGL((dk::net::attn_ln_kernel<64, 4>), dim3(batch), dim3(256), 0, (hipStream_t)stream,
+                           (const uint16_t*)qkv, (uint16_t*)x_io, (const uint16_t*)wp, (const uint16_t*)bp, batch, scale,
+                           (const uint16_t*)gamma, (const uint16_t*)beta, eps, (uint16_t*)h_out);
+    DK_HIP(hipGetLastError());
+    return DK_OK;
+}
+
 int dk_net_attn62_bf16_async(const void* qkv, void* y, uint32_t batch, uint32_t heads, uint32_t head_dim, void* stream) {
     if (!qkv || !y || heads != 4u || (head_dim != 40u && head_dim != 64u)) return DK_E_INVALID;
     if (batch == 0) return DK_OK;
