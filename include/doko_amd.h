@@ -477,6 +477,12 @@ int dk_net_fc_gelu_bf16_async(const void* x, const void* w, const void* bias, ui
 int dk_net_mlp_ln_bf16_async(const void* h, void* x_io, const void* w1, const void* b1, const void* w2, const void* b2,
                              uint32_t rows, uint32_t d, uint32_t n_hidden, const void* gamma, const void* beta, float eps,
                              void* h_out, void* stream);
+/* dk_net_qkv_attn_ln_bf16_async: the whole attention half of a transformer block from
+ * h = ln_1(x): qkv = h wqkv^T + bqkv (wqkv [3d][d], nn.MultiheadAttention.in_proj order q | k | v,
+ * heads contiguous), then as dk_net_attn_ln_bf16_async.  h and h_out must not alias. */
+int dk_net_qkv_attn_ln_bf16_async(const void* h, void* x_io, const void* wqkv, const void* bqkv, const void* wp, const void* bp,
+                                  uint32_t batch, uint32_t heads, uint32_t head_dim, const void* gamma, const void* beta,
+                                  float eps, void* h_out, void* stream);
 /* dk_net_attn_ln_bf16_async: the attention half of a transformer block after its qkv projection,
  * in one pass per sample: y = attention core (as dk_net_attn62_bf16_async), delta = y wp^T + bp
  * (the folded out_proj / c_proj, wp [d][d]), x += delta (bf16), h_out = LayerNorm(x; gamma,

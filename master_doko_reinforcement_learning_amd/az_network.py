@@ -107,10 +107,10 @@ class ClassHead(nn.Module):
 class FusedTrunk:
     """The bf16 GPU forward of a token trunk (shared by DokoAzNet and DokoImpiNet): HIP
     kernels (csrc/az_net_kernels.h) for the embedding sum + first LayerNorm, every
-    residual add fused with the LayerNorm that follows it, (4 heads of 40 or 64) the
-    attention half after the qkv GEMM (attention core + folded projection + residual +
-    LayerNorm in one kernel), and (d = 160 or 256) the whole MLP half; the qkv GEMM and the
-    heads are torch (hipBLASLt).  `x` is the residual stream, `h` the
+    residual add fused with the LayerNorm that follows it, (4 heads of 40 or 64) the whole
+    attention half (qkv projection + attention core + folded projection + residual +
+    LayerNorm in one kernel), and (d = 160 or 256) the whole MLP half; the heads' GEMMs are
+    torch (hipBLASLt).  `x` is the residual stream, `h` the
     current LayerNorm output."""
 
     def __init__(self, tokens, emb, ln0):
@@ -158,16 +158,17 @@ class FusedTrunk:
         return blk.proj(a)
 
     def attn_ln(self, x, blk, h, ln):
-        """x += c_proj(out(MHA(qkv(h)))); returns LN(x): after the qkv GEMM, the attention core,
+        """x += c_proj(out(MHA(qkv(h)))); returns LN(x): the qkv projection, the attention core,
         the folded projection, the residual add and the LayerNorm in one kernel per sample."""
         if not (blk.heads == 4 and self.d // 4 in (40, 64) and self.d % 4 == 0):
             return self.add_ln(x, self.attn_delta(blk, h), ln)
-        qkv = blk.qkv(h)
         w, b = blk.folded_proj()
         out = torch.empty_like(x)
-        self.ck(self.L.dk_net_attn_ln_bf16_async(qkv.data_ptr(), x.data_ptr(), w.data_ptr(), b.data_ptr(), h.shape[0], 4,
-                                                 self.d // 4, ln.weight.data_ptr(), ln.bias.data_ptr(), ln.eps,
-                                                 out.data_ptr(), self.st))
+        wq, bq = blk.qkv.weight, blk.qkv.bias
+        assert wq.dtype == torch.bfloat16 and wq.is_contiguous() and bq is not None and bq.is_contiguous()
+        self.ck(self.L.dk_net_qkv_attn_ln_bf16_async(h.data_ptr(), x.data_ptr(), wq.data_ptr(), bq.data_ptr(), w.data_ptr(),
+                                                     b.data_ptr(), h.shape[0], 4, self.d // 4, ln.weight.data_ptr(),
+                                                     ln.bias.data_ptr(), ln.eps, out.data_ptr(), self.st))
         return out
 
     def mlp_ln(self, x, blk, h, ln):

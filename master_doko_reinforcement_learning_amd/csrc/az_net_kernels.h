@@ -22,11 +22,18 @@ namespace net {
 constexpr int LN_MAX_PER_LANE = 8;    // bf16 pairs per lane: d <= 512
 
 __device__ __forceinline__ float bf2f(uint16_t v) { return __uint_as_float((uint32_t)v << 16); }
-__device__ __forceinline__ uint16_t f2bf(float f) {   // round to nearest even (torch's conversion), branch-free
-    const uint32_t u = __float_as_uint(f);
-    const uint32_t rne = (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
-    const uint32_t nan = (u >> 16) | 0x40u;
-    return (uint16_t)(((u & 0x7FFFFFFFu) > 0x7F800000u) ? nan : rne);
+// f32 -> bf16, round to nearest even (torch's conversion): gfx950's v_cvt_pk_bf16_f32, one
+// instruction for two values (the integer form took six per value); NaN stays NaN
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+    typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+    union { bf16x2_t v; uint32_t u; } r;
+    r.v = bf16x2_t{(__bf16)lo, (__bf16)hi};
+    return r.u;
+}
+__device__ __forceinline__ uint16_t f2bf(float f) {
+    union { __bf16 b; uint16_t u; } r;
+    r.b = (__bf16)f;
+    return r.u;
 }
 
 __device__ __forceinline__ float half_wave_sum(float v) {
@@ -62,7 +69,7 @@ __device__ __forceinline__ void ln_row(const float (&x)[2 * PER], int d, int lan
             const uint32_t g = gamma2[j], b = beta2[j];
             const float y0 = (x[2 * k] - mean) * rstd * bf2f((uint16_t)g) + bf2f((uint16_t)b);
             const float y1 = (x[2 * k + 1] - mean) * rstd * bf2f((uint16_t)(g >> 16)) + bf2f((uint16_t)(b >> 16));
-            out2[j] = (uint32_t)f2bf(y0) | ((uint32_t)f2bf(y1) << 16);
+            out2[j] = pack_bf16x2(y0, y1);
         }
     }
 }
@@ -99,7 +106,7 @@ __global__ void embed_ln_kernel(const int32_t* __restrict__ tokens, uint32_t B, 
                 a1 = bf2f(f2bf(a1 + bf2f((uint16_t)(v >> 16))));
             }
             x[2 * k] = a0; x[2 * k + 1] = a1;
-            xo[j] = (uint32_t)f2bf(a0) | ((uint32_t)f2bf(a1) << 16);
+            xo[j] = pack_bf16x2(a0, a1);
         }
     }
     ln_row<PER>(x, d, lane, (const uint32_t*)gamma, (const uint32_t*)beta, eps, (uint32_t*)(h_out + (size_t)row * d));
@@ -172,6 +179,10 @@ __device__ __forceinline__ bf16x8_t load_frag8(const uint16_t* p, bool ok) {
     return r.v;
 }
 
+template <int HD, class Put>
+__device__ __forceinline__ void attn62_core(const bf16x8_t (&qf)[2][(HD + 15) / 16], const bf16x8_t (&kf)[2][(HD + 15) / 16],
+                                            const uint16_t* vt, float scale, bool valid, Put put);
+
 // One (sample, head) of the attention core, the body shared by attn62_kernel and attn_ln_kernel:
 // `base` = the sample's qkv rows, `vt` the wave's LDS V^T tile (HD x (64 + 4) bf16), put(s, e, v) receives output
 // element (token s < 62, head dim e < HD).  Every wave of the workgroup must call it (barrier).
@@ -212,6 +223,18 @@ __device__ __forceinline__ void attn62_head(const uint16_t* __restrict__ base, u
             kf[i][kk] = load_frag8(row + D, ok);
         }
     }
+    attn62_core<HD>(qf, kf, vt, scale, valid, put);
+}
+
+// The attention core from the Q / K fragments on: qf[i][kk], kf[i][kk] = tokens 32 i + r,
+// k-step kk over the head dimension (any order of the dimensions, the same in both);
+// vt = the wave's V^T tile [e][t] in LDS, written by the caller.  Every wave of the
+// workgroup must call it (barrier).
+template <int HD, class Put>
+__device__ __forceinline__ void attn62_core(const bf16x8_t (&qf)[2][(HD + 15) / 16], const bf16x8_t (&kf)[2][(HD + 15) / 16],
+                                            const uint16_t* vt, float scale, bool valid, Put put) {
+    constexpr int S = 62, LDT = 64 + 4, KS = (HD + 15) / 16;
+    const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
     // X[ti][si] = K_ti Q_si^T
     f32x16_t x[2][2];
 #pragma unroll
@@ -250,9 +273,10 @@ __device__ __forceinline__ void attn62_head(const uint16_t* __restrict__ base, u
         const float inv = 1.0f / l;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            union { uint16_t u[8]; bf16x8_t v; } pk;
+            union { uint32_t u[4]; bf16x8_t v; } pk;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) pk.u[j] = f2bf(x[q >> 1][si][8 * (q & 1) + j] * inv);
+            for (int j = 0; j < 4; ++j)
+                pk.u[j] = pack_bf16x2(x[q >> 1][si][8 * (q & 1) + 2 * j] * inv, x[q >> 1][si][8 * (q & 1) + 2 * j + 1] * inv);
             pf[si][q] = pk.v;
         }
     }
@@ -311,29 +335,19 @@ __global__ void __launch_bounds__(256) attn62_kernel(const uint16_t* __restrict_
 // contiguous rows.  Numerics as the unfused path: y rounded to bf16 (the attention output),
 // delta + bias rounded to bf16 (the GEMM's output), x + delta rounded, LN of the rounded row.
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
-template <int HD, int H>
-__global__ void __launch_bounds__(256, 2) attn_ln_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ x_io,
-                                                         const uint16_t* __restrict__ wp, const uint16_t* __restrict__ bp,
-                                                         uint32_t batch, float scale, const uint16_t* __restrict__ gamma,
-                                                         const uint16_t* __restrict__ beta, float eps,
-                                                         uint16_t* __restrict__ h_out) {
-    static_assert(H == 4, "one wave per head, four waves per workgroup");
-    constexpr int S = 62, D = HD * H, LDT = 64 + 4, LDY = D + 8, NT = D / 16, KS = D / 32;
+// The block's tail after attention, shared by attn_ln_kernel and qkv_attn_ln_kernel: ys = the
+// sample's y rows (64 x LDY, rows 62 and 63 zero), lds_a = free LDS for the residual rows.
+// Call after a barrier that completes ys.
+template <int HD>
+__device__ __forceinline__ void proj_res_ln(const uint16_t* ys, uint16_t* lds_a, uint16_t* __restrict__ x_io,
+                                            const uint16_t* __restrict__ wp, const uint16_t* __restrict__ bp, uint32_t b,
+                                            const uint16_t* __restrict__ gamma, const uint16_t* __restrict__ beta, float eps,
+                                            uint16_t* __restrict__ h_out) {
+    constexpr int S = 62, D = HD * 4, LDY = D + 8, NT = D / 16, KS = D / 32;
     constexpr int NJ = (NT + 3) / 4;          // column tiles per wave: w, w + 4, w + 8, ...
     constexpr int XP = (S * (D / 8) + 255) / 256, LP = D / 32;   // 16-B pieces per thread: residual load, LN row
     static_assert(D % 32 == 0, "d: a multiple of 32");
-    // LDS: the heads' V^T tiles, reused for the residual rows once attention is done (43 KB at
-    // d = 160, 69 KB at d = 256), and the attention output rows
-    constexpr int VT = 4 * HD * LDT, XS = 64 * LDY;
-    __shared__ __attribute__((aligned(16))) uint16_t lds_a[VT > XS ? VT : XS];
-    __shared__ __attribute__((aligned(16))) uint16_t ys[64 * LDY];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint32_t b = blockIdx.x;                                   // one sample per workgroup
-    (void)batch;
-    for (int i = threadIdx.x; i < 2 * D; i += 256) ys[(S + i / D) * LDY + i % D] = 0;   // A operand padding rows
-    attn62_head<HD, H>(qkv + (size_t)b * S * (3 * D), (uint32_t)wave, true, lds_a + wave * HD * LDT, scale,
-                       [&](int s, int e, float v) { ys[s * LDY + wave * HD + e] = f2bf(v); });
-    __syncthreads();   // y complete in ys; the V^T tiles are dead
     // the sample's residual rows: issued before the GEMM, stored to LDS after it
     uint16_t* xs = lds_a;
     const uint16_t* xg = x_io + (size_t)b * S * D;
@@ -428,19 +442,156 @@ __global__ void __launch_bounds__(256, 2) attn_ln_kernel(const uint16_t* __restr
 #pragma unroll
             for (int i = 0; i < LP; ++i) {
                 const int c0 = 8 * (q + 4 * i);
-                union { uint4 u; uint16_t s[8]; } gv, bv, xo, ho;
+                union { uint4 u; uint16_t s[8]; uint32_t w[4]; } gv, bv, xo, ho;
                 gv.u = *(const uint4*)(gamma + c0);
                 bv.u = *(const uint4*)(beta + c0);
 #pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    xo.s[e] = f2bf(xv[i][e]);
-                    ho.s[e] = f2bf((xv[i][e] - mean) * rstd * bf2f(gv.s[e]) + bf2f(bv.s[e]));
+                for (int e = 0; e < 8; e += 2) {
+                    xo.w[e / 2] = pack_bf16x2(xv[i][e], xv[i][e + 1]);
+                    ho.w[e / 2] = pack_bf16x2((xv[i][e] - mean) * rstd * bf2f(gv.s[e]) + bf2f(bv.s[e]),
+                                              (xv[i][e + 1] - mean) * rstd * bf2f(gv.s[e + 1]) + bf2f(bv.s[e + 1]));
                 }
                 *(uint4*)(x_io + o + c0) = xo.u;
                 *(uint4*)(h_out + o + c0) = ho.u;
             }
         }
     }
+}
+
+template <int HD, int H>
+__global__ void __launch_bounds__(256, 2) attn_ln_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ x_io,
+                                                         const uint16_t* __restrict__ wp, const uint16_t* __restrict__ bp,
+                                                         uint32_t batch, float scale, const uint16_t* __restrict__ gamma,
+                                                         const uint16_t* __restrict__ beta, float eps,
+                                                         uint16_t* __restrict__ h_out) {
+    static_assert(H == 4, "one wave per head, four waves per workgroup");
+    constexpr int S = 62, D = HD * H, LDT = 64 + 4, LDY = D + 8;
+    // LDS: the heads' V^T tiles, reused for the residual rows once attention is done (43 KB at
+    // d = 160, 69 KB at d = 256), and the attention output rows
+    constexpr int VT = 4 * HD * LDT, XS = 64 * LDY;
+    __shared__ __attribute__((aligned(16))) uint16_t lds_a[VT > XS ? VT : XS];
+    __shared__ __attribute__((aligned(16))) uint16_t ys[64 * LDY];
+    const int wave = threadIdx.x >> 6;
+    const uint32_t b = blockIdx.x;                                   // one sample per workgroup
+    (void)batch;
+    for (int i = threadIdx.x; i < 2 * D; i += 256) ys[(S + i / D) * LDY + i % D] = 0;   // A operand padding rows
+    attn62_head<HD, H>(qkv + (size_t)b * S * (3 * D), (uint32_t)wave, true, lds_a + wave * HD * LDT, scale,
+                       [&](int s, int e, float v) { ys[s * LDY + wave * HD + e] = f2bf(v); });
+    __syncthreads();   // y complete in ys; the V^T tiles are dead
+    proj_res_ln<HD>(ys, lds_a, x_io, wp, bp, b, gamma, beta, eps, h_out);
+}
+
+// ---------------------------------------------------------------------------
+// The whole attention half of a block from h = ln_1(x), in one pass per sample: the qkv
+// projection runs inside the workgroup, so q, k and v (3 x 2 d bytes per token) never go
+// to HBM.  Wave w = head w computes its head's rows of Q^T, K^T and V^T = W h^T + b on
+// v_mfma_f32_32x32x16_bf16 (A = Wqkv rows of the head, padded to 64 with zero rows; B = the
+// sample's h rows from LDS):
+//   V^T accumulators go straight to the wave's LDS V^T tile [e][t];
+//   Q^T / K^T accumulators become the attention's fragments without moving between lanes:
+//   lane (r, hh) holds token 32 si + r, dims 32 dt + (g & 3) + 8 (g >> 2) + 4 hh, and
+//   registers g = 8 half .. 8 half + 7 of tile dt are k-step 2 dt + half of X = K Q^T.  The
+//   contraction pairs equal (hh, j) of both operands, so Q and K only have to use the same
+//   dimension order (k-steps of padding dimensions only are skipped).
+// Then the attention core (attn62_core) and the tail as attn_ln_kernel.  LDS: the h rows and
+// then y share one tile, the V^T tiles and then the residual rows another.
+template <int HD, int D>
+__device__ __forceinline__ void head_tiles(const uint16_t* hs, const uint16_t* __restrict__ w,
+                                           const uint16_t* __restrict__ bias, f32x16_t (&acc)[2][2]) {
+    constexpr int LDY = D + 8;
+    const int lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int si = 0; si < 2; ++si) acc[dt][si] = f32x16_t{0};
+#pragma unroll 2   // fully unrolled, the hoisted W loads cost a wave per SIMD (d 160) or spill (d 256)
+    for (int ks = 0; ks < D / 16; ++ks) {
+        bf16x8_t hb[2], wa[2];
+#pragma unroll
+        for (int si = 0; si < 2; ++si) hb[si] = *(const bf16x8_t*)&hs[(32 * si + r) * LDY + 16 * ks + 8 * hh];
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+            const int m = 32 * dt + r;
+            wa[dt] = load_frag8(w + (size_t)(m < HD ? m : 0) * D + 16 * ks + 8 * hh, m < HD);
+        }
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+            for (int si = 0; si < 2; ++si)
+                acc[dt][si] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[dt], hb[si], acc[dt][si], 0, 0, 0);
+    }
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+            const int m = 32 * dt + (g & 3) + 8 * (g >> 2) + 4 * hh;
+            const float bv = m < HD ? bf2f(bias[m]) : 0.0f;
+            acc[dt][0][g] += bv;
+            acc[dt][1][g] += bv;
+        }
+}
+
+template <int HD>
+__device__ __forceinline__ void pack_head(const f32x16_t (&acc)[2][2], bf16x8_t (&f)[2][(HD + 15) / 16]) {
+#pragma unroll
+    for (int si = 0; si < 2; ++si)
+#pragma unroll
+        for (int kk = 0; kk < (HD + 15) / 16; ++kk) {
+            union { uint32_t u[4]; bf16x8_t v; } pk;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                pk.u[j] = pack_bf16x2(acc[kk >> 1][si][8 * (kk & 1) + 2 * j], acc[kk >> 1][si][8 * (kk & 1) + 2 * j + 1]);
+            f[si][kk] = pk.v;
+        }
+}
+
+template <int HD>
+__global__ void __launch_bounds__(256, 2) qkv_attn_ln_kernel(const uint16_t* __restrict__ h_in, uint16_t* __restrict__ x_io,
+                                                             const uint16_t* __restrict__ wqkv, const uint16_t* __restrict__ bqkv,
+                                                             const uint16_t* __restrict__ wp, const uint16_t* __restrict__ bp,
+                                                             uint32_t batch, float scale, const uint16_t* __restrict__ gamma,
+                                                             const uint16_t* __restrict__ beta, float eps,
+                                                             uint16_t* __restrict__ h_out) {
+    constexpr int S = 62, D = HD * 4, LDT = 64 + 4, LDY = D + 8, KS = (HD + 15) / 16;
+    constexpr int VT = 4 * HD * LDT, XS = 64 * LDY;
+    __shared__ __attribute__((aligned(16))) uint16_t lds_a[VT > XS ? VT : XS];   // V^T tiles, then residual rows
+    __shared__ __attribute__((aligned(16))) uint16_t ys[64 * LDY];               // h rows, then y rows
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t b = blockIdx.x;                                                // one sample per workgroup
+    (void)batch;
+    const uint16_t* hg = h_in + (size_t)b * S * D;
+    for (int p = threadIdx.x; p < 64 * (D / 8); p += 256) {
+        const int rr = p / (D / 8), kp = p - rr * (D / 8);
+        *(uint4*)&ys[rr * LDY + 8 * kp] = rr < S ? *(const uint4*)(hg + 8 * p) : make_uint4(0u, 0u, 0u, 0u);
+    }
+    __syncthreads();
+    const int hh = lane >> 5, r = lane & 31;
+    const uint16_t* wh = wqkv + (size_t)wave * HD * D;   // the head's q rows; k, v rows d and 2 d further
+    const uint16_t* bh = bqkv + wave * HD;
+    uint16_t* vt = lds_a + wave * HD * LDT;
+    bf16x8_t qf[2][KS], kf[2][KS];
+    {
+        f32x16_t acc[2][2];
+        head_tiles<HD, D>(ys, wh + (size_t)2 * D * D, bh + 2 * D, acc);    // V^T -> [e][t]
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+            for (int g = 0; g < 16; ++g) {
+                const int m = 32 * dt + (g & 3) + 8 * (g >> 2) + 4 * hh;
+                if (m < HD) {
+                    vt[m * LDT + r] = f2bf(acc[dt][0][g]);
+                    vt[m * LDT + 32 + r] = f2bf(acc[dt][1][g]);
+                }
+            }
+        head_tiles<HD, D>(ys, wh + (size_t)D * D, bh + D, acc);            // K^T
+        pack_head<HD>(acc, kf);
+        head_tiles<HD, D>(ys, wh, bh, acc);                                // Q^T
+        pack_head<HD>(acc, qf);
+    }
+    // attn62_core's barrier also ends every wave's reads of the h rows: y may then overwrite them
+    attn62_core<HD>(qf, kf, vt, scale, true, [&](int s, int e, float v) { ys[s * LDY + wave * HD + e] = f2bf(v); });
+    __syncthreads();   // y complete (rows 62, 63 still the zero h padding); the V^T tiles are dead
+    proj_res_ln<HD>(ys, lds_a, x_io, wp, bp, b, gamma, beta, eps, h_out);
 }
 
 // ---------------------------------------------------------------------------
@@ -556,8 +707,8 @@ __global__ void __launch_bounds__(256, 2) fc_gelu_kernel(const uint16_t* __restr
                     const f32x2_t g01 = gelu_erf2(f32x2_t{acc[i][j][4 * q + 0] + b0, acc[i][j][4 * q + 1] + b1});
                     const f32x2_t g23 = gelu_erf2(f32x2_t{acc[i][j][4 * q + 2] + b2, acc[i][j][4 * q + 3] + b3});
                     uint2 o;
-                    o.x = (uint32_t)f2bf(g01.x) | ((uint32_t)f2bf(g01.y) << 16);
-                    o.y = (uint32_t)f2bf(g23.x) | ((uint32_t)f2bf(g23.y) << 16);
+                    o.x = pack_bf16x2(g01.x, g01.y);
+                    o.y = pack_bf16x2(g23.x, g23.y);
                     *(uint2*)&tw[(32 * i + r) * LDT + cl] = o;
                 }
             }
@@ -618,13 +769,6 @@ __device__ __forceinline__ f32x2_t gelu_erf2_pk(f32x2_t v) {
 }
 
 // f32 pair -> two bf16 (round to nearest even, NaN kept), one v_cvt_pk_bf16_f32
-__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
-    typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
-    union { bf16x2_t v; uint32_t u; } r;
-    r.v = bf16x2_t{(__bf16)lo, (__bf16)hi};
-    return r.u;
-}
-
 constexpr uint32_t MLP_MAX_HIDDEN = 1024;
 template <int D, int NC>
 __global__ void __launch_bounds__(512, 1) mlp_ln_kernel(const uint16_t* __restrict__ h, uint16_t* __restrict__ x_io,

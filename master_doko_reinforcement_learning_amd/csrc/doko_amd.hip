@@ -1848,6 +1848,28 @@ int dk_net_mlp_ln_bf16_async(const void* h, void* x_io, const void* w1, const vo
     return DK_OK;
 }
 
+int dk_net_qkv_attn_ln_bf16_async(const void* h, void* x_io, const void* wqkv, const void* bqkv, const void* wp, const void* bp,
+                                  uint32_t batch, uint32_t heads, uint32_t head_dim, const void* gamma, const void* beta,
+                                  float eps, void* h_out, void* stream) {
+    if (!h || !x_io || !wqkv || !bqkv || !wp || !bp || !gamma || !beta || !h_out || h == h_out || heads != 4u ||
+        (head_dim != 40u && head_dim != 64u))
+        return DK_E_INVALID;
+    if (batch == 0) return DK_OK;
+    const float scale = 1.0f / sqrtf((float)head_dim);
+    if (head_dim == 40u)
+        hipLaunchKernelGGL((dk::net::qkv_attn_ln_kernel<40>), dim3(batch), dim3(256), 0, (hipStream_t)stream,
+                           (const uint16_t*)h, (uint16_t*)x_io, (const uint16_t*)wqkv, (const uint16_t*)bqkv,
+                           (const uint16_t*)wp, (const uint16_t*)bp, batch, scale, (const uint16_t*)gamma,
+                           (const uint16_t*)beta, eps, (uint16_t*)h_out);
+    else
+        hipLaunchKernelGGL((dk::net::qkv_attn_ln_kernel<64>), dim3(batch), dim3(256), 0, (hipStream_t)stream,
+                           (const uint16_t*)h, (uint16_t*)x_io, (const uint16_t*)wqkv, (const uint16_t*)bqkv,
+                           (const uint16_t*)wp, (const uint16_t*)bp, batch, scale, (const uint16_t*)gamma,
+                           (const uint16_t*)beta, eps, (uint16_t*)h_out);
+    DK_HIP(hipGetLastError());
+    return DK_OK;
+}
+
 int dk_net_attn_ln_bf16_async(const void* qkv, void* x_io, const void* wp, const void* bp, uint32_t batch, uint32_t heads,
                               uint32_t head_dim, const void* gamma, const void* beta, float eps, void* h_out, void* stream) {
     if (!qkv || !x_io || !wp || !bp || !gamma || !beta || !h_out || heads != 4u || (head_dim != 40u && head_dim != 64u))

@@ -155,3 +155,40 @@ def test_attn_ln_matches_torch(hd):
     assert torch.isfinite(out.float()).all() and torch.isfinite(xo.float()).all()
     torch.testing.assert_close(xo.float(), x_ref, rtol=1e-2, atol=3e-2)
     torch.testing.assert_close(out.float(), h_ref, rtol=2e-2, atol=4e-2)
+
+
+@pytest.mark.parametrize("hd", [40, 64])
+def test_qkv_attn_ln_matches_torch(hd):
+    """The whole attention half from h = ln_1(x) (qkv projection inside the kernel) against fp32
+    torch: qkv = h Wqkv^T + b rounded to bf16 like the unfused GEMM, then as test_attn_ln."""
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(13)
+    B, d = 45, 4 * hd
+    h = torch.randn(B, 62, d, device=dev).bfloat16()
+    wq = (torch.randn(3 * d, d, device=dev) / d ** 0.5).bfloat16()
+    bq = (torch.randn(3 * d, device=dev) * 0.1).bfloat16()
+    x = (torch.randn(B, 62, d, device=dev) * 2).bfloat16()
+    w = (torch.randn(d, d, device=dev) / d ** 0.5).bfloat16()
+    b = (torch.randn(d, device=dev) * 0.1).bfloat16()
+    g = (1 + 0.1 * torch.randn(d, device=dev)).bfloat16()
+    be = (0.1 * torch.randn(d, device=dev)).bfloat16()
+    qkv = F.linear(h.float(), wq.float(), bq.float()).bfloat16().float()
+    q, k, v = qkv.view(B, 62, 3, 4, hd).permute(2, 0, 3, 1, 4)
+    y = (torch.softmax(q @ k.transpose(-1, -2) / hd ** 0.5, dim=-1) @ v).transpose(1, 2).reshape(B, 62, d)
+    delta = F.linear(y.bfloat16().float(), w.float(), b.float()).bfloat16().float()
+    x_ref = (x.float() + delta).bfloat16().float()
+    h_ref = F.layer_norm(x_ref, (d,), g.float(), be.float(), 1e-5)
+    xo = x.clone()
+    out = torch.full((B, 62, d), float("nan"), device=dev).bfloat16()
+    L = _lib()
+    assert L.dk_net_qkv_attn_ln_bf16_async(h.data_ptr(), xo.data_ptr(), wq.data_ptr(), bq.data_ptr(), w.data_ptr(),
+                                           b.data_ptr(), B, 4, hd, g.data_ptr(), be.data_ptr(), 1e-5, h.data_ptr(),
+                                           None) != 0            # h_out aliasing h is refused
+    rc = L.dk_net_qkv_attn_ln_bf16_async(h.data_ptr(), xo.data_ptr(), wq.data_ptr(), bq.data_ptr(), w.data_ptr(),
+                                         b.data_ptr(), B, 4, hd, g.data_ptr(), be.data_ptr(), 1e-5, out.data_ptr(),
+                                         torch.cuda.current_stream(dev).cuda_stream)
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert torch.isfinite(out.float()).all() and torch.isfinite(xo.float()).all()
+    torch.testing.assert_close(xo.float(), x_ref, rtol=1e-2, atol=3e-2)
+    torch.testing.assert_close(out.float(), h_ref, rtol=2e-2, atol=4e-2)

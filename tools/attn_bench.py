@@ -38,9 +38,26 @@ def case(L, d, B, reps):
         assert L.dk_net_attn_ln_bf16_async(qkv.data_ptr(), x.data_ptr(), w.data_ptr(), b.data_ptr(), B, 4, hd,
                                            g.data_ptr(), be.data_ptr(), 1e-5, out.data_ptr(), st) == 0
 
+    # with the qkv projection: hipBLASLt qkv GEMM + attn_ln_kernel against qkv_attn_ln_kernel
+    h = torch.randn(B, 62, d, device=dev).bfloat16()
+    wq = (torch.randn(3 * d, d, device=dev) / d ** 0.5).bfloat16()
+    bq = (torch.randn(3 * d, device=dev) * 0.1).bfloat16()
+
+    def gemm_fused(x):
+        q = F.linear(h, wq, bq)
+        assert L.dk_net_attn_ln_bf16_async(q.data_ptr(), x.data_ptr(), w.data_ptr(), b.data_ptr(), B, 4, hd,
+                                           g.data_ptr(), be.data_ptr(), 1e-5, out.data_ptr(), st) == 0
+
+    def all_fused(x):
+        assert L.dk_net_qkv_attn_ln_bf16_async(h.data_ptr(), x.data_ptr(), wq.data_ptr(), bq.data_ptr(), w.data_ptr(),
+                                               b.data_ptr(), B, 4, hd, g.data_ptr(), be.data_ptr(), 1e-5, out.data_ptr(),
+                                               st) == 0
+
     res = {"d": d, "samples": B}
     outs = {}
-    for name, fn in (("unfused", unfused), ("fused", fused), ("unfused2", unfused), ("fused2", fused)):
+    for name, fn in (("unfused", unfused), ("fused", fused), ("unfused2", unfused), ("fused2", fused),
+                     ("qkv_gemm+fused", gemm_fused), ("qkv_fused", all_fused), ("qkv_gemm+fused2", gemm_fused),
+                     ("qkv_fused2", all_fused)):
         x = x0.clone()
         fn(x)
         torch.cuda.synchronize()
@@ -56,6 +73,8 @@ def case(L, d, B, reps):
         res[name + "_ms"] = round(e0.elapsed_time(e1) / reps, 4)
     res["max_abs_diff_x"] = (outs["fused"][0].float() - outs["unfused"][0].float()).abs().max().item()
     res["max_abs_diff_h"] = (outs["fused"][1].float() - outs["unfused"][1].float()).abs().max().item()
+    res["qkv_max_abs_diff_x"] = (outs["qkv_fused"][0].float() - outs["qkv_gemm+fused"][0].float()).abs().max().item()
+    res["qkv_max_abs_diff_h"] = (outs["qkv_fused"][1].float() - outs["qkv_gemm+fused"][1].float()).abs().max().item()
     return res
 
 
