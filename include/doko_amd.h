@@ -477,6 +477,12 @@ int dk_net_fc_gelu_bf16_async(const void* x, const void* w, const void* bias, ui
 int dk_net_mlp_ln_bf16_async(const void* h, void* x_io, const void* w1, const void* b1, const void* w2, const void* b2,
                              uint32_t rows, uint32_t d, uint32_t n_hidden, const void* gamma, const void* beta, float eps,
                              void* h_out, void* stream);
+/* dk_net_class_pool_ln_bf16_async: PerClassAttentionMLPHead's attention pooling and each class
+ * MLP's opening LayerNorm (az_doko.py:42-50): x [batch][62][d], queries [classes][d] (classes
+ * <= 64), w = softmax(queries x^T * scale) over the 62 tokens, a = w x, out[c][b][:] =
+ * LayerNorm(a[b][c]; ln_w[c], ln_b[c], eps), class-major [classes][batch][d].  d 160 or 256. */
+int dk_net_class_pool_ln_bf16_async(const void* x, uint32_t batch, uint32_t d, const void* queries, uint32_t classes,
+                                    float scale, const void* ln_w, const void* ln_b, float eps, void* out, void* stream);
 /* dk_net_qkv_attn_ln_bf16_async: the whole attention half of a transformer block from
  * h = ln_1(x): qkv = h wqkv^T + bqkv (wqkv [3d][d], nn.MultiheadAttention.in_proj order q | k | v,
  * heads contiguous), then as dk_net_attn_ln_bf16_async.  h and h_out must not alias. */

@@ -91,7 +91,21 @@ class ClassHead(nn.Module):
         for p in (self.w1, self.b1, self.w2, self.b2):
             nn.init.uniform_(p, -bound, bound)
 
-    def forward(self, x):                                        # x [B, S, d]
+    def pooled(self, x):
+        """The attention pooling and each class's LayerNorm, class-major [C, B, d]."""
+        B, S, d = x.shape
+        C = self.queries.shape[0]
+        if (x.is_cuda and x.dtype == torch.bfloat16 and S == SEQ and d in (160, 256) and C <= 64
+                and self.queries.dtype == torch.bfloat16):
+            from . import _native
+            x = x.contiguous()
+            ac = torch.empty((C, B, d), dtype=x.dtype, device=x.device)
+            rc = _native.lib().dk_net_class_pool_ln_bf16_async(
+                x.data_ptr(), B, d, self.queries.data_ptr(), C, self.scale, self.ln_w.data_ptr(), self.ln_b.data_ptr(),
+                1e-5, ac.data_ptr(), torch.cuda.current_stream(x.device).cuda_stream)
+            if rc != 0:
+                raise RuntimeError("doko_amd class pooling kernel error %d" % rc)
+            return ac
         w = torch.softmax(torch.einsum("cd,bsd->bcs", self.queries, x) * self.scale, dim=-1)
         a = torch.einsum("bcs,bsd->bcd", w, x)                  # [B, C, d]
         a = F.layer_norm(a, a.shape[-1:]) * self.ln_w + self.ln_b
@@ -99,7 +113,10 @@ class ClassHead(nn.Module):
         # operand: einsum("bci,coi->bco") hands the GEMM a class-batched view whose batch
         # stride (d) is smaller than its row stride (C d), and a PyTorch TunableOp candidate
         # faulted on that layout
-        ac = a.transpose(0, 1).contiguous()                      # [C, B, d]
+        return a.transpose(0, 1).contiguous()                    # [C, B, d]
+
+    def forward(self, x):                                        # x [B, S, d]
+        ac = self.pooled(x)
         h = F.gelu(torch.bmm(ac, self.w1.transpose(1, 2)) + self.b1[:, None, :])   # [C, B, d]
         return ((h * self.w2[:, None, :]).sum(-1) + self.b2[:, None]).transpose(0, 1)   # [B, C]
 
@@ -220,10 +237,10 @@ class DokoAzNet(nn.Module):
         return self.value_head(self.v_ln(xv)), self.policy_head(self.p_ln(xp))
 
     def forward_fused(self, tokens):
-        """bf16 forward on the GPU with HIP kernels (csrc/az_net_kernels.h) for the
-        embedding sum + first LayerNorm (one pass), every residual add fused with the
-        LayerNorm that follows it, and the 62-token attention core (bf16 MFMA, reading
-        the fused qkv projection in place)."""
+        """bf16 forward on the GPU with HIP kernels (csrc/az_net_kernels.h): the embedding
+        sum + first LayerNorm, each block as two kernels (the attention half from the qkv
+        projection to the next LayerNorm, the MLP half likewise: FusedTrunk), and the heads'
+        attention pooling + per-class LayerNorm (ClassHead.pooled)."""
         if not (self.blocks and self.p_blocks and self.v_blocks):
             raise ValueError("the fused forward needs shared, policy and value blocks")
         f = FusedTrunk(tokens, self.emb, self.blocks[0].ln_1)

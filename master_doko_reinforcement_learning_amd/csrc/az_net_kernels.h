@@ -595,6 +595,169 @@ __global__ void __launch_bounds__(256, 2) qkv_attn_ln_kernel(const uint16_t* __r
 }
 
 // ---------------------------------------------------------------------------
+// PerClassAttentionMLPHead's pooling and its classes' LayerNorms (az_doko.py:42-50 and the
+// nn.LayerNorm that opens each class MLP), one 256-thread workgroup per sample:
+//   scores^T = X Q^T        (v_mfma_f32_32x32x16_bf16; the token in the registers, the class
+//                            on the lane; rounded to bf16, times scale, rounded: the bf16 torch ops)
+//   P = softmax over the 62 tokens (registers + one cross-half shuffle), packed in place as
+//       the A operand of
+//   A = P X                 (X^T staged in LDS as [d][t], as V^T in the attention core)
+//   out[c][b][:] = LN(A[c]) * w[c] + b[c]   (written class-major: the [C, B, d] operand of the
+//                                           classes' batched MLP GEMM, no transpose copy)
+// Class tiles of 32 (C <= 64): with one class tile the four waves split the d tiles, with two
+// each pair does.  LDS: the x rows (then the pooled rows) and x^T.
+template <int D>
+__global__ void __launch_bounds__(256, 2) class_pool_ln_kernel(const uint16_t* __restrict__ xin, uint32_t batch,
+                                                               const uint16_t* __restrict__ queries, uint32_t classes,
+                                                               float scale, const uint16_t* __restrict__ lnw,
+                                                               const uint16_t* __restrict__ lnb, float eps,
+                                                               uint16_t* __restrict__ out) {
+    constexpr int S = 62, LDX = D + 8, LDT = 64 + 4, KD = D / 16, DT = D / 32, LP = D / 32;
+    static_assert(D % 32 == 0, "d: a multiple of 32");
+    __shared__ __attribute__((aligned(16))) uint16_t xs[64 * LDX];   // x rows, then the pooled rows
+    __shared__ __attribute__((aligned(16))) uint16_t xt[D * LDT];    // x^T [d][t]
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
+    const uint32_t b = blockIdx.x;                                   // one sample per workgroup
+    const int C = (int)classes;
+    const uint16_t* xg = xin + (size_t)b * S * D;
+    for (int p = threadIdx.x; p < 64 * (D / 8); p += 256) {
+        const int t = p / (D / 8), d0 = 8 * (p - t * (D / 8));
+        union { uint4 u; uint16_t s[8]; } v;
+        v.u = t < S ? *(const uint4*)(xg + (size_t)t * D + d0) : make_uint4(0u, 0u, 0u, 0u);
+        *(uint4*)&xs[t * LDX + d0] = v.u;
+#pragma unroll
+        for (int m = 0; m < 8; ++m) xt[(d0 + m) * LDT + t] = v.s[m];
+    }
+    __syncthreads();
+    const int CT = C > 32 ? 2 : 1, WPC = 4 / CT;       // class tiles, waves per class tile
+    const int ct = wave % CT, part = wave / CT;
+    const int cls = 32 * ct + r;
+    f32x16_t sc[2];
+    sc[0] = f32x16_t{0};
+    sc[1] = f32x16_t{0};
+#pragma unroll 2
+    for (int ks = 0; ks < KD; ++ks) {
+        const bf16x8_t qf = load_frag8(queries + (size_t)(cls < C ? cls : 0) * D + 16 * ks + 8 * hh, cls < C);
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+            const bf16x8_t xa = *(const bf16x8_t*)&xs[(32 * mt + r) * LDX + 16 * ks + 8 * hh];
+            sc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa, qf, sc[mt], 0, 0, 0);
+        }
+    }
+    // softmax over the tokens t < 62 of the lane's class
+    bf16x8_t pf[4];
+    {
+        float mx = -INFINITY;
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+            for (int g = 0; g < 16; ++g) {
+                const int t = 32 * mt + (g & 3) + 8 * (g >> 2) + 4 * hh;
+                const float v = bf2f(f2bf(bf2f(f2bf(sc[mt][g])) * scale));
+                sc[mt][g] = v;
+                if (t < S) mx = fmaxf(mx, v);
+            }
+        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        float l = 0.0f;
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+            for (int g = 0; g < 16; ++g) {
+                const int t = 32 * mt + (g & 3) + 8 * (g >> 2) + 4 * hh;
+                const float e = t < S ? __expf(sc[mt][g] - mx) : 0.0f;
+                sc[mt][g] = e;
+                l += e;
+            }
+        l += __shfl_xor(l, 32);
+        const float inv = 1.0f / l;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            union { uint32_t u[4]; bf16x8_t v; } pk;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                pk.u[j] = pack_bf16x2(sc[q >> 1][8 * (q & 1) + 2 * j] * inv, sc[q >> 1][8 * (q & 1) + 2 * j + 1] * inv);
+            pf[q] = pk.v;
+        }
+    }
+    // A = P X for the wave's d tiles t = part, part + WPC, ...
+    constexpr int MAXT = (DT + 1) / 2;
+    f32x16_t acc[MAXT];
+#pragma unroll
+    for (int i = 0; i < MAXT; ++i) {
+        const int t = part + WPC * i;
+        acc[i] = f32x16_t{0};
+        if (t < DT) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int t0 = 16 * q + 4 * hh;
+                union { uint2 u[2]; bf16x8_t v; } f;
+                f.u[0] = *(const uint2*)&xt[(32 * t + r) * LDT + t0];
+                f.u[1] = *(const uint2*)&xt[(32 * t + r) * LDT + t0 + 8];
+                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pf[q], f.v, acc[i], 0, 0, 0);
+            }
+        }
+    }
+    __syncthreads();   // every wave's reads of the x rows done: the pooled rows replace them
+#pragma unroll
+    for (int i = 0; i < MAXT; ++i) {
+        const int t = part + WPC * i;
+        if (t < DT) {
+#pragma unroll
+            for (int g = 0; g < 16; ++g) {
+                const int c = 32 * ct + (g & 3) + 8 * (g >> 2) + 4 * hh;
+                if (c < C) xs[c * LDX + 32 * t + r] = f2bf(acc[i][g]);
+            }
+        }
+    }
+    __syncthreads();
+    // LayerNorm of each class row with the class's affine: 4 threads per row
+    {
+        const int c = threadIdx.x >> 2, q = threadIdx.x & 3;
+        float xv[LP][8];
+        float s1 = 0.0f;
+#pragma unroll
+        for (int i = 0; i < LP; ++i) {
+            union { uint4 u; uint16_t s[8]; } pc;
+            pc.u = *(const uint4*)&xs[c * LDX + 8 * (q + 4 * i)];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                xv[i][e] = bf2f(pc.s[e]);
+                s1 += xv[i][e];
+            }
+        }
+        s1 += __shfl_xor(s1, 1);
+        s1 += __shfl_xor(s1, 2);
+        const float mean = s1 / (float)D;
+        float s2 = 0.0f;
+#pragma unroll
+        for (int i = 0; i < LP; ++i)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const float dv = xv[i][e] - mean;
+                s2 += dv * dv;
+            }
+        s2 += __shfl_xor(s2, 1);
+        s2 += __shfl_xor(s2, 2);
+        const float rstd = rsqrtf(s2 / (float)D + eps);
+        if (c < C) {
+            const size_t o = ((size_t)c * batch + b) * D;
+#pragma unroll
+            for (int i = 0; i < LP; ++i) {
+                const int c0 = 8 * (q + 4 * i);
+                union { uint4 u; uint16_t s[8]; uint32_t w[4]; } gv, bv, ho;
+                gv.u = *(const uint4*)(lnw + (size_t)c * D + c0);
+                bv.u = *(const uint4*)(lnb + (size_t)c * D + c0);
+#pragma unroll
+                for (int e = 0; e < 8; e += 2)
+                    ho.w[e / 2] = pack_bf16x2((xv[i][e] - mean) * rstd * bf2f(gv.s[e]) + bf2f(bv.s[e]),
+                                              (xv[i][e + 1] - mean) * rstd * bf2f(gv.s[e + 1]) + bf2f(bv.s[e + 1]));
+                *(uint4*)(out + o + c0) = ho.u;
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // The MLP's first layer with its activation: y = GELU(x W^T + b), exact (erf) GELU as
 // the reference's nn.GELU(), for the networks' small K (= d: 160 AlphaZero, 256 IMPI).
 // hipBLASLt runs this GEMM at 160-320 TFLOP/s and the separate GELU pass re-reads and

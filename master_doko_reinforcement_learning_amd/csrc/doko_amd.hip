@@ -1848,6 +1848,23 @@ int dk_net_mlp_ln_bf16_async(const void* h, void* x_io, const void* w1, const vo
     return DK_OK;
 }
 
+int dk_net_class_pool_ln_bf16_async(const void* x, uint32_t batch, uint32_t d, const void* queries, uint32_t classes,
+                                    float scale, const void* ln_w, const void* ln_b, float eps, void* out, void* stream) {
+    if (!x || !queries || !ln_w || !ln_b || !out || classes == 0 || classes > 64u || (d != 160u && d != 256u))
+        return DK_E_INVALID;
+    if (batch == 0) return DK_OK;
+    if (d == 160u)
+        hipLaunchKernelGGL((dk::net::class_pool_ln_kernel<160>), dim3(batch), dim3(256), 0, (hipStream_t)stream,
+                           (const uint16_t*)x, batch, (const uint16_t*)queries, classes, scale, (const uint16_t*)ln_w,
+                           (const uint16_t*)ln_b, eps, (uint16_t*)out);
+    else
+        hipLaunchKernelGGL((dk::net::class_pool_ln_kernel<256>), dim3(batch), dim3(256), 0, (hipStream_t)stream,
+                           (const uint16_t*)x, batch, (const uint16_t*)queries, classes, scale, (const uint16_t*)ln_w,
+                           (const uint16_t*)ln_b, eps, (uint16_t*)out);
+    DK_HIP(hipGetLastError());
+    return DK_OK;
+}
+
 int dk_net_qkv_attn_ln_bf16_async(const void* h, void* x_io, const void* wqkv, const void* bqkv, const void* wp, const void* bp,
                                   uint32_t batch, uint32_t heads, uint32_t head_dim, const void* gamma, const void* beta,
                                   float eps, void* h_out, void* stream) {

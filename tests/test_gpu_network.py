@@ -192,3 +192,30 @@ def test_qkv_attn_ln_matches_torch(hd):
     assert torch.isfinite(out.float()).all() and torch.isfinite(xo.float()).all()
     torch.testing.assert_close(xo.float(), x_ref, rtol=1e-2, atol=3e-2)
     torch.testing.assert_close(out.float(), h_ref, rtol=2e-2, atol=4e-2)
+
+
+@pytest.mark.parametrize("d,C", [(160, 39), (160, 4), (256, 33)])
+def test_class_pool_ln_matches_torch(d, C):
+    """PerClassAttentionMLPHead's pooling + per-class LayerNorm (policy 39 / value 4 classes at
+    d 160, IMPI 33 at d 256) against fp32 torch with the bf16 path's roundings (scores, scaled
+    scores, softmax weights and the pooled rows rounded to bf16)."""
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(17)
+    B = 37
+    x = (torch.randn(B, 62, d, device=dev) * 1.5).bfloat16()
+    q = torch.randn(C, d, device=dev).bfloat16()
+    lw = (1 + 0.1 * torch.randn(C, d, device=dev)).bfloat16()
+    lb = (0.1 * torch.randn(C, d, device=dev)).bfloat16()
+    scale = d ** -0.5
+    bf = lambda t: t.bfloat16().float()   # noqa: E731
+    sc = bf(bf(torch.einsum("cd,bsd->bcs", q.float(), x.float())) * scale)
+    w = bf(torch.softmax(sc, dim=-1))
+    a = bf(torch.einsum("bcs,bsd->bcd", w, x.float()))
+    ref = (F.layer_norm(a, (d,)) * lw.float() + lb.float()).transpose(0, 1)      # [C, B, d]
+    out = torch.full((C, B, d), float("nan"), device=dev).bfloat16()
+    rc = _lib().dk_net_class_pool_ln_bf16_async(x.data_ptr(), B, d, q.data_ptr(), C, scale, lw.data_ptr(), lb.data_ptr(),
+                                                1e-5, out.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert torch.isfinite(out.float()).all()
+    torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=4e-2)
