@@ -495,6 +495,12 @@ __global__ void __launch_bounds__(256, 2) attn_ln_kernel(const uint16_t* __restr
 //   dimension order (k-steps of padding dimensions only are skipped).
 // Then the attention core (attn62_core) and the tail as attn_ln_kernel.  LDS: the h rows and
 // then y share one tile, the V^T tiles and then the residual rows another.
+#ifndef DK_QKV_GS
+#define DK_QKV_GS 2
+#endif
+#ifndef DK_QKV_WPE
+#define DK_QKV_WPE 3
+#endif
 template <int HD, int D>
 __device__ __forceinline__ void head_tiles(const uint16_t* hs, const uint16_t* __restrict__ w,
                                            const uint16_t* __restrict__ bias, f32x16_t (&acc)[2][2]) {
@@ -504,22 +510,39 @@ __device__ __forceinline__ void head_tiles(const uint16_t* hs, const uint16_t* _
     for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
         for (int si = 0; si < 2; ++si) acc[dt][si] = f32x16_t{0};
-#pragma unroll 2   // fully unrolled, the hoisted W loads cost a wave per SIMD (d 160) or spill (d 256)
-    for (int ks = 0; ks < D / 16; ++ks) {
-        bf16x8_t hb[2], wa[2];
+    // k order: groups of GS = 4 k-steps (64 k; a tail group of 2 at d = 160); in a group lane
+    // half hh covers 8 GS consecutive k, 8 per k-step, so a lane reads 16 GS contiguous bytes
+    // of its W row in GS back-to-back loads (the line is fetched once, then hit).  One 16-B
+    // piece per row half per k-step instead thrashed L1 across k-steps: each 128-B line came
+    // from L2 four times.  The h fragments (B operand, LDS) use the same order.
+    const uint16_t* w0 = w + (size_t)r * D;
+    const uint16_t* w1 = w + (size_t)(32 + r < HD ? 32 + r : 0) * D;
+    const bool ok1 = 32 + r < HD;
+    auto group = [&](auto gs_c, int k0) {
+        constexpr int GS = decltype(gs_c)::value;
+        const int kb = k0 + hh * 8 * GS;
+        bf16x8_t wa[2][GS];
 #pragma unroll
-        for (int si = 0; si < 2; ++si) hb[si] = *(const bf16x8_t*)&hs[(32 * si + r) * LDY + 16 * ks + 8 * hh];
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt) {
-            const int m = 32 * dt + r;
-            wa[dt] = load_frag8(w + (size_t)(m < HD ? m : 0) * D + 16 * ks + 8 * hh, m < HD);
+        for (int st = 0; st < GS; ++st) {
+            wa[0][st] = load_frag8(w0 + kb + 8 * st, true);
+            wa[1][st] = load_frag8(w1 + kb + 8 * st, ok1);
         }
 #pragma unroll
-        for (int dt = 0; dt < 2; ++dt)
+        for (int st = 0; st < GS; ++st) {
+            bf16x8_t hb[2];
 #pragma unroll
-            for (int si = 0; si < 2; ++si)
-                acc[dt][si] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[dt], hb[si], acc[dt][si], 0, 0, 0);
-    }
+            for (int si = 0; si < 2; ++si) hb[si] = *(const bf16x8_t*)&hs[(32 * si + r) * LDY + kb + 8 * st];
+#pragma unroll
+            for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+                for (int si = 0; si < 2; ++si)
+                    acc[dt][si] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[dt][st], hb[si], acc[dt][si], 0, 0, 0);
+        }
+    };
+    constexpr int G = DK_QKV_GS, NG = D / (16 * G), TAIL = (D % (16 * G)) / 16;
+#pragma unroll 1
+    for (int gi = 0; gi < NG; ++gi) group(std::integral_constant<int, G>{}, 16 * G * gi);
+    if constexpr (TAIL > 0) group(std::integral_constant<int, TAIL>{}, 16 * G * NG);
 #pragma unroll
     for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
@@ -546,7 +569,7 @@ __device__ __forceinline__ void pack_head(const f32x16_t (&acc)[2][2], bf16x8_t 
 }
 
 template <int HD>
-__global__ void __launch_bounds__(256, 2) qkv_attn_ln_kernel(const uint16_t* __restrict__ h_in, uint16_t* __restrict__ x_io,
+__global__ void __launch_bounds__(256, HD == 40 ? DK_QKV_WPE : 2) qkv_attn_ln_kernel(const uint16_t* __restrict__ h_in, uint16_t* __restrict__ x_io,
                                                              const uint16_t* __restrict__ wqkv, const uint16_t* __restrict__ bqkv,
                                                              const uint16_t* __restrict__ wp, const uint16_t* __restrict__ bp,
                                                              uint32_t batch, float scale, const uint16_t* __restrict__ gamma,

@@ -801,7 +801,7 @@ struct dk_ctx {
     int last_slot = -1;             // the latest launch (dk_last_search_ms)
     hipEvent_t fb_done = nullptr;   // the latest fallback pass
     bool fb_used = false;
-    // Slot-capacity fallback: pools are sized from the measured demand (default 64 + 4 x
+    // Slot-capacity fallback: pools are sized from the measured demand (default 64 + 8 x
     // iterations slots per root, against the proven 42 + 12 x iterations); a root that runs out
     // is appended to its launch's `retry` list ([0] = count) and searched again, from its seed,
     // by a second launch over a small pool with the proven capacity (fb_*).  Results do not change.
@@ -1086,25 +1086,28 @@ dk_ctx* dk_create(const dk_config* cfg) {
     ctx->max_iters = cfg->max_iterations;
     // Proven bound: the root block (<= 39) plus one block of <= 12 children per
     // iteration (non-root nodes offer at most 12 cards / 9 reservations / 1 pass).
-    // The measured demand is far lower (largest over the C3 bench roots: ~2,400 slots at
-    // 1,000 iterations), so by default the main pools hold 64 + 4 x iterations
-    // slots per root and the rare root that needs more is searched again in the fallback
-    // pool, which has the proven bound.  cfg->slot_capacity (or env DK_SLOT_CAPACITY) sets
-    // the main pools' capacity; at or above the proven bound there is no fallback pool.
+    // The measured demand is far lower (largest over the C3 bench roots: 3,546 slots at
+    // 1,000 iterations), so by default the main pools hold 64 + 8 x iterations
+    // slots per root (8,192 at 1,000: 43 % high water, where 4,096 was 87 %; the same speed,
+    // profiles/r03/cap_ab_4096_8192.log) and the rare root that needs more is
+    // searched again in the fallback pool, which has the proven bound.  The default halves
+    // (down to 64 + 4 x iterations) while the main pools would take more than half of the free
+    // device memory.  cfg->slot_capacity (or env DK_SLOT_CAPACITY) sets the main pools'
+    // capacity; at or above the proven bound there is no fallback pool.
     // The capacity is also the stride between the lanes' pool regions, and it is rounded up
     // to a multiple of 256 slots (4 KB of 16-B records): strides 512 B off a multiple of
     // 64 KB (4,064 or 4,128 slots) ran the C3 search 1.6x slower than 4,096 or 12,040
     // (tools/cap_sweep.py; the lanes' accesses fall into the same memory channels).
     // (+2 for the 8-B records' even-aligned blocks: search_core.h P8_SLOT_BOUND)
     const uint32_t proven = dk::P8_SLOT_BOUND(cfg->max_iterations);
-    uint32_t cap = cfg->slot_capacity ? cfg->slot_capacity : 64u + 4u * cfg->max_iterations;
+    bool cap_default = cfg->slot_capacity == 0;
+    uint32_t cap = cfg->slot_capacity ? cfg->slot_capacity : 64u + 8u * cfg->max_iterations;
     if (const char* e = getenv("DK_SLOT_CAPACITY")) {
         const long v = atol(e);
-        if (v >= 1) cap = (uint32_t)v;
+        if (v >= 1) { cap = (uint32_t)v; cap_default = false; }
     }
     cap = cap < proven ? (cap + 255u) & ~255u : proven;
     ctx->cap_slots = cap < proven ? cap : proven;
-    const bool with_fallback = ctx->cap_slots < proven;
     ctx->cu_count = prop.multiProcessorCount;
     if (const char* e = getenv("DK_ROOTS_PER_WAVE")) {
         const int v = atoi(e);
@@ -1135,6 +1138,17 @@ dk_ctx* dk_create(const dk_config* cfg) {
     if (pool > cfg->max_roots) pool = cfg->max_roots;
     const uint32_t rpw = ctx->roots_per_wave;
     ctx->pool_roots = (uint32_t)((pool + rpw - 1) / rpw * rpw);   // whole regions of rpw roots
+    if (cap_default) {
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
+            const uint32_t floor_cap = ((64u + 4u * cfg->max_iterations) + 255u) & ~255u;
+            const size_t per_slot = sizeof(dk::NodeHot32) + sizeof(dk::NodeCold);
+            while (ctx->cap_slots > floor_cap && (size_t)ctx->pool_roots * ctx->cap_slots * per_slot > free_b / 2)
+                ctx->cap_slots = (ctx->cap_slots / 2 + 255u) & ~255u;
+            if (ctx->cap_slots < floor_cap) ctx->cap_slots = floor_cap < proven ? floor_cap : proven;
+        }
+    }
+    const bool with_fallback = ctx->cap_slots < proven;
     const size_t R = ctx->pool_roots, S = ctx->cap_slots, T = (size_t)cfg->max_iterations + 1;
     // node states per lane region (>= T): DK_STATE_STRIDE, else T
     size_t ST = T;

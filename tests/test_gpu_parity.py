@@ -502,9 +502,10 @@ def test_full_size_properties(eng, monkeypatch):
     finally:
         e16.close()
     assert np.array_equal(v1, v3) and np.array_equal(val1.view(np.uint64), val3.view(np.uint64)) and np.array_equal(b1, b3)
-    # the default main-pool capacity (64 + 4 x iterations) holds every one of these searches
+    # the default main-pool capacity (64 + 8 x iterations, 64 + 4 x when device memory is
+    # short) holds every one of these searches
     hw, cap, overflowed = eng.pool_high_water()
-    assert cap == 4096 and 0 < hw <= cap and overflowed == 0, (hw, cap, overflowed)
+    assert cap in (4096, 8192) and 0 < hw <= cap and overflowed == 0, (hw, cap, overflowed)
 
 
 # ---------------------------------------------------------------- rs-doko rule-based sampler
