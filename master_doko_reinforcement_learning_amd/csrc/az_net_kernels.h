@@ -956,6 +956,12 @@ __device__ __forceinline__ f32x2_t gelu_erf2_pk(f32x2_t v) {
 
 // f32 pair -> two bf16 (round to nearest even, NaN kept), one v_cvt_pk_bf16_f32
 constexpr uint32_t MLP_MAX_HIDDEN = 1024;
+#ifndef DK_MLP_SKEW
+#define DK_MLP_SKEW 1
+#endif
+#ifndef DK_MLP_W2PAD
+#define DK_MLP_W2PAD 4
+#endif
 template <int D, int NC>
 __global__ void __launch_bounds__(512, 1) mlp_ln_kernel(const uint16_t* __restrict__ h, uint16_t* __restrict__ x_io,
                                                         const uint16_t* __restrict__ w1, const uint16_t* __restrict__ b1,
@@ -964,10 +970,15 @@ __global__ void __launch_bounds__(512, 1) mlp_ln_kernel(const uint16_t* __restri
                                                         const uint16_t* __restrict__ beta, float eps,
                                                         uint16_t* __restrict__ h_out) {
     static_assert(D % 32 == 0 && NC % 32 == 0, "d and the chunk: multiples of 32");
-    constexpr int KS = D / 16, OT = D / 32, LDW1 = D + 8, LDW2 = NC + 8, HT = NC / 32, GS = NC / 16;
-    // LDS: the chunk's W1 / W2, double-buffered
+    // W2 rows padded by 4 elements: a 2-dword-odd row stride puts the 32 rows of a W2
+    // fragment read (ds_read_b64) in 32 distinct bank pairs (+8 was 2-way conflicted)
+    constexpr int KS = D / 16, OT = D / 32, LDW1 = D + 8, LDW2 = NC + DK_MLP_W2PAD, HT = NC / 32, GS = NC / 16;
+    // LDS: the chunk's W1 / W2, in NB buffers: 3 when the waves 4..7 run half a chunk behind
+    // (below), 2 otherwise
+    constexpr bool SKEW = DK_MLP_SKEW && D <= 160;   // d = 256 has no registers to spare
+    constexpr int NB = SKEW ? 3 : 2;
     constexpr int W1E = NC * LDW1, W2E = D * LDW2;
-    __shared__ __attribute__((aligned(16))) uint16_t lds[2 * (W1E + W2E)];
+    __shared__ __attribute__((aligned(16))) uint16_t lds[NB * (W1E + W2E)];
     __shared__ float b1s[MLP_MAX_HIDDEN];           // the hidden units' biases
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
     const uint32_t row = blockIdx.x * 256u + (uint32_t)wave * 32u + (uint32_t)r;
@@ -997,7 +1008,8 @@ __global__ void __launch_bounds__(512, 1) mlp_ln_kernel(const uint16_t* __restri
     {                                                                                                          \
         const int v = threadIdx.x + 512 * (U);                                                                 \
         if (v < P1) { const int i = v / (D / 8), p = v - i * (D / 8); *(uint4*)&lds[(buf) * W1E + i * LDW1 + 8 * p] = R1; } \
-        if (v < P2) { const int o = v / (NC / 8), p = v - o * (NC / 8); *(uint4*)&lds[2 * W1E + (buf) * W2E + o * LDW2 + 8 * p] = R2; } \
+        if (v < P2) { const int o = v / (NC / 8), p = v - o * (NC / 8); uint2* d_ = (uint2*)&lds[NB * W1E + (buf) * W2E + o * LDW2 + 8 * p]; \
+                      d_[0] = make_uint2(R2.x, R2.y); d_[1] = make_uint2(R2.z, R2.w); } \
     }
 #define DK_MLP_LOAD_CHUNK(c) { DK_MLP_LD(0, pa0, pb0, c) DK_MLP_LD(1, pa1, pb1, c) DK_MLP_LD(2, pa2, pb2, c) }
 #define DK_MLP_STORE_CHUNK(buf) { DK_MLP_ST(0, pa0, pb0, buf) DK_MLP_ST(1, pa1, pb1, buf) DK_MLP_ST(2, pa2, pb2, buf) }
@@ -1012,40 +1024,50 @@ __global__ void __launch_bounds__(512, 1) mlp_ln_kernel(const uint16_t* __restri
     // the residual rows' column groups of this lane (epilogue), loaded during the last chunk
     constexpr bool PREFETCH_X = D <= 160;
     uint2 xv[OT][4];
-    auto chunk = [&](uint32_t c, auto last) {
-        const int buf = (int)(c & 1u);
-        if (c + 1 < chunks) DK_MLP_LOAD_CHUNK(c + 1)
-        f32x16_t acc1[HT];
+    // Per chunk: GEMM1 (MFMA), bias + GELU (VALU), GEMM2 (MFMA).  With one barrier per chunk
+    // every wave runs the same phase at the same time, and the two waves of a SIMD (waves w
+    // and w + 4) contend for the MFMA pipe and then for the VALU.  So (DK_MLP_SKEW) waves
+    // 4..7 run half a chunk behind: in chunk interval c they finish chunk c - 1 (GELU + GEMM2)
+    // and then run GEMM1 of chunk c, while waves 0..3 run GEMM1 then GELU + GEMM2 of chunk c:
+    // one wave's GELU meets the other's MFMAs.  The lagging waves read chunk c - 1's W2 while
+    // chunk c + 1 is staged, hence three LDS buffers.
+    f32x16_t acc1[HT];
+    auto gemm1 = [&](uint32_t c) {
+        const int buf = (int)(c % NB);
 #pragma unroll
         for (int j = 0; j < HT; ++j) acc1[j] = f32x16_t{0};
-        // GEMM1, software-pipelined one k-step deep: the W1 fragments of k-step kk + 1 are read
-        // from LDS while the MFMAs of k-step kk run
-        {
-            bf16x8_t cur[HT], nxt[HT];
+        // software-pipelined one k-step deep: the W1 fragments of k-step kk + 1 are read from
+        // LDS while the MFMAs of k-step kk run
+        bf16x8_t cur[HT], nxt[HT];
 #pragma unroll
-            for (int j = 0; j < HT; ++j) cur[j] = *(const bf16x8_t*)&lds[(buf) * W1E + (32 * j + r) * LDW1 + 8 * hh];
+        for (int j = 0; j < HT; ++j) cur[j] = *(const bf16x8_t*)&lds[(buf) * W1E + (32 * j + r) * LDW1 + 8 * hh];
 #pragma unroll
-            for (int kk = 0; kk < KS; ++kk) {
-                if (kk + 1 < KS) {
+        for (int kk = 0; kk < KS; ++kk) {
+            if (kk + 1 < KS) {
 #pragma unroll
-                    for (int j = 0; j < HT; ++j)
-                        nxt[j] = *(const bf16x8_t*)&lds[(buf) * W1E + (32 * j + r) * LDW1 + 16 * (kk + 1) + 8 * hh];
-                }
-#pragma unroll
-                for (int j = 0; j < HT; ++j) acc1[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[j], hf[kk], acc1[j], 0, 0, 0);
-#pragma unroll
-                for (int j = 0; j < HT; ++j) cur[j] = nxt[j];
+                for (int j = 0; j < HT; ++j)
+                    nxt[j] = *(const bf16x8_t*)&lds[(buf) * W1E + (32 * j + r) * LDW1 + 16 * (kk + 1) + 8 * hh];
             }
+#pragma unroll
+            for (int j = 0; j < HT; ++j) acc1[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[j], hf[kk], acc1[j], 0, 0, 0);
+#pragma unroll
+            for (int j = 0; j < HT; ++j) cur[j] = nxt[j];
         }
-        if constexpr (decltype(last)::value && PREFETCH_X) {
-            // last chunk: the residual x of the epilogue is loaded now (the h fragments are dead),
-            // in flight during the last GELU and GEMM2 (d = 160; d = 256 has no registers to spare)
+    };
+    auto prefetch_x = [&]() {
+        if constexpr (PREFETCH_X) {
+            // after the last GEMM1 the h fragments are dead: the residual x of the epilogue is
+            // loaded now, in flight during the last GELU and GEMM2 (d = 160; d = 256 has no
+            // registers to spare)
             const uint16_t* xr = x_io + (size_t)(ok ? row : 0u) * D;
 #pragma unroll
             for (int t = 0; t < OT; ++t)
 #pragma unroll
                 for (int q = 0; q < 4; ++q) xv[t][q] = ok ? *(const uint2*)(xr + 32 * t + 8 * q + 4 * hh) : make_uint2(0u, 0u);
         }
+    };
+    auto gelu_gemm2 = [&](uint32_t c) {
+        const int buf = (int)(c % NB);
         // bias + GELU -> bf16 B fragments of GEMM2 (k-step s = 2 j + half: registers 8 half .. +7)
         bf16x8_t af[GS];
 #pragma unroll
@@ -1062,34 +1084,67 @@ __global__ void __launch_bounds__(512, 1) mlp_ln_kernel(const uint16_t* __restri
             af[s] = pk.v;
         }
         // GEMM2, pipelined one output tile deep (the W2 fragment of the next tile read during this one)
-        {
-            auto w2frag = [&](int s, int t) {
-                const int h0 = 32 * (s >> 1) + 16 * (s & 1) + 4 * hh;
-                const uint16_t* wr = &lds[2 * W1E + (buf) * W2E + (32 * t + r) * LDW2 + h0];
-                union { uint2 u[2]; bf16x8_t v; } a;
-                a.u[0] = *(const uint2*)wr;
-                a.u[1] = *(const uint2*)(wr + 8);
-                return a.v;
-            };
-            bf16x8_t cur = w2frag(0, 0);
+        auto w2frag = [&](int s, int t) {
+            const int h0 = 32 * (s >> 1) + 16 * (s & 1) + 4 * hh;
+            const uint16_t* wr = &lds[NB * W1E + (buf) * W2E + (32 * t + r) * LDW2 + h0];
+            union { uint2 u[2]; bf16x8_t v; } a;
+            a.u[0] = *(const uint2*)wr;
+            a.u[1] = *(const uint2*)(wr + 8);
+            return a.v;
+        };
+        bf16x8_t cur = w2frag(0, 0);
 #pragma unroll
-            for (int q = 0; q < GS * OT; ++q) {
-                const int s = q / OT, t = q % OT;
-                bf16x8_t nxt = cur;
-                if (q + 1 < GS * OT) nxt = w2frag((q + 1) / OT, (q + 1) % OT);
-                acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur, af[s], acc2[t], 0, 0, 0);
-                cur = nxt;
-            }
+        for (int q = 0; q < GS * OT; ++q) {
+            const int s = q / OT, t = q % OT;
+            bf16x8_t nxt = cur;
+            if (q + 1 < GS * OT) nxt = w2frag((q + 1) / OT, (q + 1) % OT);
+            acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur, af[s], acc2[t], 0, 0, 0);
+            cur = nxt;
         }
-        if (c + 1 < chunks) DK_MLP_STORE_CHUNK(buf ^ 1)
-        // LDS-only barrier: the next chunk is staged and this chunk's reads are done
+    };
+    // one code path for all waves: iteration c = [GELU + GEMM2 of chunk c - 1][GEMM1 of chunk c];
+    // waves 0..3 (SKEW) stage the next chunk and meet the barrier between the two halves,
+    // waves 4..7 after them, so the groups run half an iteration apart
+    const bool early = SKEW && wave < 4;   // wave-uniform
+    auto sync = [&]() {
+        // LDS-only barrier: the next chunk is staged and the reads of the buffer it overwrites are done
         asm volatile("" ::: "memory");
         __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
     };
-    for (uint32_t c = 0; c + 1 < chunks; ++c) chunk(c, std::false_type{});
-    chunk(chunks - 1, std::true_type{});
+    auto iteration = [&](uint32_t c, auto last) {
+        constexpr bool L = decltype(last)::value;
+        if constexpr (!L) DK_MLP_LOAD_CHUNK(c + 1)
+        if constexpr (!SKEW) {   // d = 256: chunk c whole (acc1 dead between iterations)
+            gemm1(c);
+            if constexpr (L) prefetch_x();
+            gelu_gemm2(c);
+            if constexpr (!L) {
+                DK_MLP_STORE_CHUNK((c + 1) % NB)
+                sync();
+            }
+            return;
+        }
+        if (c > 0) gelu_gemm2(c - 1);
+        if constexpr (!L) {
+            if (early) {
+                DK_MLP_STORE_CHUNK((c + 1) % NB)
+                sync();
+            }
+        }
+        gemm1(c);
+        if constexpr (L) prefetch_x();
+        if constexpr (!L) {
+            if (!early) {
+                DK_MLP_STORE_CHUNK((c + 1) % NB)
+                sync();
+            }
+        }
+    };
+    for (uint32_t c = 0; c + 1 < chunks; ++c) iteration(c, std::false_type{});
+    iteration(chunks - 1, std::true_type{});
+    if constexpr (SKEW) gelu_gemm2(chunks - 1);
 
     // epilogue: acc2[t][g] = delta of row `row`, column 32 t + 8 (g >> 2) + 4 hh + (g & 3)
     uint16_t* xr = x_io + (size_t)(ok ? row : 0u) * D;
