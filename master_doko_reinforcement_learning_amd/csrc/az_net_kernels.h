@@ -962,6 +962,12 @@ constexpr uint32_t MLP_MAX_HIDDEN = 1024;
 #ifndef DK_MLP_W2PAD
 #define DK_MLP_W2PAD 4
 #endif
+#ifndef DK_MLP_P1
+#define DK_MLP_P1 1
+#endif
+#ifndef DK_MLP_P2
+#define DK_MLP_P2 1
+#endif
 template <int D, int NC>
 __global__ void __launch_bounds__(512, 1) mlp_ln_kernel(const uint16_t* __restrict__ h, uint16_t* __restrict__ x_io,
                                                         const uint16_t* __restrict__ w1, const uint16_t* __restrict__ b1,
@@ -1036,22 +1042,27 @@ __global__ void __launch_bounds__(512, 1) mlp_ln_kernel(const uint16_t* __restri
         const int buf = (int)(c % NB);
 #pragma unroll
         for (int j = 0; j < HT; ++j) acc1[j] = f32x16_t{0};
-        // software-pipelined one k-step deep: the W1 fragments of k-step kk + 1 are read from
-        // LDS while the MFMAs of k-step kk run
-        bf16x8_t cur[HT], nxt[HT];
+        // software-pipelined P1 k-steps deep: the W1 fragments of k-step kk + P1 are read from
+        // LDS while the MFMAs of k-step kk run (an LDS read under load outlasts two MFMAs)
+        constexpr int P1D = DK_MLP_P1;
+        bf16x8_t ring[P1D][HT];
 #pragma unroll
-        for (int j = 0; j < HT; ++j) cur[j] = *(const bf16x8_t*)&lds[(buf) * W1E + (32 * j + r) * LDW1 + 8 * hh];
+        for (int kk = 0; kk < P1D && kk < KS; ++kk)
+#pragma unroll
+            for (int j = 0; j < HT; ++j)
+                ring[kk][j] = *(const bf16x8_t*)&lds[(buf) * W1E + (32 * j + r) * LDW1 + 16 * kk + 8 * hh];
 #pragma unroll
         for (int kk = 0; kk < KS; ++kk) {
-            if (kk + 1 < KS) {
+            bf16x8_t cur[HT];
+#pragma unroll
+            for (int j = 0; j < HT; ++j) cur[j] = ring[kk % P1D][j];
+            if (kk + P1D < KS) {
 #pragma unroll
                 for (int j = 0; j < HT; ++j)
-                    nxt[j] = *(const bf16x8_t*)&lds[(buf) * W1E + (32 * j + r) * LDW1 + 16 * (kk + 1) + 8 * hh];
+                    ring[kk % P1D][j] = *(const bf16x8_t*)&lds[(buf) * W1E + (32 * j + r) * LDW1 + 16 * (kk + P1D) + 8 * hh];
             }
 #pragma unroll
             for (int j = 0; j < HT; ++j) acc1[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[j], hf[kk], acc1[j], 0, 0, 0);
-#pragma unroll
-            for (int j = 0; j < HT; ++j) cur[j] = nxt[j];
         }
     };
     auto prefetch_x = [&]() {
@@ -1092,14 +1103,16 @@ __global__ void __launch_bounds__(512, 1) mlp_ln_kernel(const uint16_t* __restri
             a.u[1] = *(const uint2*)(wr + 8);
             return a.v;
         };
-        bf16x8_t cur = w2frag(0, 0);
+        constexpr int P2D = DK_MLP_P2;   // W2 fragments read P2D MFMAs ahead
+        bf16x8_t ring2[P2D];
+#pragma unroll
+        for (int q = 0; q < P2D && q < GS * OT; ++q) ring2[q] = w2frag(q / OT, q % OT);
 #pragma unroll
         for (int q = 0; q < GS * OT; ++q) {
             const int s = q / OT, t = q % OT;
-            bf16x8_t nxt = cur;
-            if (q + 1 < GS * OT) nxt = w2frag((q + 1) / OT, (q + 1) % OT);
+            const bf16x8_t cur = ring2[q % P2D];
+            if (q + P2D < GS * OT) ring2[q % P2D] = w2frag((q + P2D) / OT, (q + P2D) % OT);
             acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur, af[s], acc2[t], 0, 0, 0);
-            cur = nxt;
         }
     };
     // one code path for all waves: iteration c = [GELU + GEMM2 of chunk c - 1][GEMM1 of chunk c];
