@@ -501,6 +501,9 @@ __global__ void __launch_bounds__(256, 2) attn_ln_kernel(const uint16_t* __restr
 #ifndef DK_QKV_WPE
 #define DK_QKV_WPE 3
 #endif
+#ifndef DK_QKV_PF
+#define DK_QKV_PF -1   // -1: per head size (below)
+#endif
 template <int HD, int D>
 __device__ __forceinline__ void head_tiles(const uint16_t* hs, const uint16_t* __restrict__ w,
                                            const uint16_t* __restrict__ bias, f32x16_t (&acc)[2][2]) {
@@ -539,10 +542,42 @@ __device__ __forceinline__ void head_tiles(const uint16_t* hs, const uint16_t* _
                     acc[dt][si] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[dt][st], hb[si], acc[dt][si], 0, 0, 0);
         }
     };
+    // d = 256 (two waves per SIMD): W fragments PF k-steps ahead in a register ring; a
+    // scheduling barrier per k-step keeps the compiler from hoisting every load to the top
+    // (0.77 -> 0.73 ms at 8192 samples).  d = 160 keeps its third wave per SIMD instead
+    // (the ring spills there, and one k-step ahead was no faster: tools/attn_bench.py).
+    constexpr int PF = DK_QKV_PF >= 0 ? DK_QKV_PF : (HD == 64 ? 2 : 0);
+    if constexpr (PF > 0) {
+    constexpr int NKS = D / 16;
+    bf16x8_t ring[PF][2];
+#pragma unroll
+    for (int p = 0; p < PF; ++p) {
+        ring[p][0] = load_frag8(w0 + 16 * p + 8 * hh, true);
+        ring[p][1] = load_frag8(w1 + 16 * p + 8 * hh, ok1);
+    }
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+        const bf16x8_t a0 = ring[ks % PF][0], a1 = ring[ks % PF][1];
+        if (ks + PF < NKS) {
+            ring[ks % PF][0] = load_frag8(w0 + 16 * (ks + PF) + 8 * hh, true);
+            ring[ks % PF][1] = load_frag8(w1 + 16 * (ks + PF) + 8 * hh, ok1);
+        }
+        bf16x8_t hb[2];
+#pragma unroll
+        for (int si = 0; si < 2; ++si) hb[si] = *(const bf16x8_t*)&hs[(32 * si + r) * LDY + 16 * ks + 8 * hh];
+#pragma unroll
+        for (int si = 0; si < 2; ++si) {
+            acc[0][si] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, hb[si], acc[0][si], 0, 0, 0);
+            acc[1][si] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, hb[si], acc[1][si], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    } else {
     constexpr int G = DK_QKV_GS, NG = D / (16 * G), TAIL = (D % (16 * G)) / 16;
 #pragma unroll 1
     for (int gi = 0; gi < NG; ++gi) group(std::integral_constant<int, G>{}, 16 * G * gi);
     if constexpr (TAIL > 0) group(std::integral_constant<int, TAIL>{}, 16 * G * NG);
+    }
 #pragma unroll
     for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
