@@ -2,11 +2,11 @@
 
 One step = one determinized decision batch of BASELINE.json config 3 on every
 GPU, entirely on the device:
-    CAP determinization (card_matching_full)  -> 18432 infostates x 64 samples = 1,179,648 roots
+    CAP determinization (card_matching_full)  -> 36864 infostates x 64 samples = 2,359,296 roots
     UCT search, 1000 simulations per root (select/expand/random rollout/backup)
     policy fusion (MaxN) of the per-sample visit counts per infostate
-With N GPUs (config 4) the global batch holds 18432*N infostates (weak scaling,
-1,179,648 roots per GPU).  By default every rank owns 18432 of them with all 64
+With N GPUs (config 4) the global batch holds 36864*N infostates (weak scaling,
+2,359,296 roots per GPU).  By default every rank owns 36864 of them with all 64
 samples, so its work has exactly the N = 1 shape, and the fused actions are
 gathered with one RCCL all-gather over xGMI; --partition samples instead splits
 every infostate's samples over the ranks and sums the fusion accumulators with one
@@ -50,8 +50,9 @@ def parse():
     p.add_argument("--ar-temperature", type=float, default=0.4, help="AR sampling temperature (impi; all_policies.rs:30)")
     p.add_argument("--iterations", type=int, default=1000)
     p.add_argument("--infostates", type=int, default=None,
-                   help="infostates per GPU (c3: default 18432 x 64 samples = 1,179,648 roots, six 64-root groups per "
-                        "resident wave (3072 waves); c2d, impi, impid: default 12288)")
+                   help="infostates per GPU (c3: default 36864 x 64 samples = 2,359,296 roots, twelve 64-root groups "
+                        "per resident wave (3072 waves): the persistent grid's drain tail is 4.6 %% of the launch, "
+                        "against 7.5 %% at six groups (per-wave clocks, DESIGN.md §4.1); c2d, impi, impid: default 12288)")
     p.add_argument("--samples", type=int, default=64, help="samples per infostate (c3, c2d)")
     p.add_argument("--partition", choices=["infostates", "samples"], default="infostates",
                    help="N > 1 (c3, c2d): 'infostates' = each rank owns 1/N of the infostates with all their samples "
@@ -77,7 +78,7 @@ def parse():
                         "sequence); a host-only violation is reported as host_copy_bad_roots, not raised")
     a = p.parse_args()
     if a.infostates is None:
-        a.infostates = 18432 if a.workload == "c3" else 12288   # c2d: 2.18 G/s at 18432 against 2.24 at 12288
+        a.infostates = 36864 if a.workload == "c3" else 12288   # c2d: 2.18 G/s at 18432 against 2.24 at 12288
     return a
 
 
@@ -341,6 +342,9 @@ def main():
     I = bufs["I"]
 
     elapsed, search_ms = timed_steps(step, args.steps, args.warmup, eng, L, dev, world, dist, ck, sp)
+    # per-wave clocks of the last timed search launch: how much of it the persistent grid's
+    # drain tail costs (the waves that ran out of groups wait for the slowest one)
+    waves = eng.last_search_waves()
     if rank == 0 and args.dump_actions and bufs["actions"] is not None:
         np.save(args.dump_actions, bufs["actions"].cpu().numpy())
     if args.dump_acc and bufs["acc"] is not None:
@@ -368,12 +372,14 @@ def main():
         sa.infostates = args.small_infostates
         _, sstep, s_roots, sbufs = make_workload(sa, dk, L, dev, sp, rank, world, local_rank, dist, eng=eng)
         s_el, s_ms = timed_steps(sstep, args.small_steps, 1, eng, L, dev, world, dist, ck, sp)
+        s_waves = eng.last_search_waves()
         check_visits(sbufs, iters, "small batch")
         if args.host_readback_check:
             host_bad["small"] = check_visits_host(sbufs["visits"].cpu().numpy(), iters, "small batch").size
         small = {"infostates_per_gpu": args.small_infostates, "roots_per_gpu": s_roots, "steps": args.small_steps,
                  "value": s_roots * iters * args.small_steps * world / s_el, "unit": "rollouts/s",
-                 "ms_per_step": s_el / args.small_steps * 1e3, "search_kernel_ms": float(np.mean(s_ms))}
+                 "ms_per_step": s_el / args.small_steps * 1e3, "search_kernel_ms": float(np.mean(s_ms)),
+                 "search_waves_busy_frac": round(s_waves["busy_frac"], 4)}
         if args.inflight:
             small["inflight"] = inflight_rates(args, dk, eng, sbufs, dev, world, dist)
         del sbufs
@@ -429,6 +435,11 @@ def main():
             },
             "kernel_only_rollouts_per_s": n_roots * iters * world / (kernel_ms / 1e3),
             "search_kernel_ms": kernel_ms,
+            "search_waves": {"waves": waves["waves"], "busy_frac": round(waves["busy_frac"], 4),
+                             "first_end_ms": round(waves["first_end_ms"], 2),
+                             "median_end_ms": round(waves["median_end_ms"], 2), "span_ms": round(waves["span_ms"], 2),
+                             "note": "each wave of the persistent grid stamps the 100 MHz counter at start and once "
+                                     "the group queue is dry for it; 1 - busy_frac = drain tail + launch ramp"},
             "roofline": {
                 # achieved/peak/frac: the north-star's HBM figures, algorithmic bytes / event-timed
                 # kernel vs 8 TB/s; traffic: calibrated DRAM bytes per launch (PMC); neither VALU nor

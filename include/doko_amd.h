@@ -510,6 +510,13 @@ int dk_net_attn62_bf16_async(const void* qkv, void* y, uint32_t batch, uint32_t 
  */
 int dk_sync(dk_ctx* ctx, void* stream);
 int dk_last_search_ms(dk_ctx* ctx, float* ms);
+/* Per-wave clocks of the last search launch's persistent grid (each workgroup stamps the
+ * 100 MHz realtime counter when it starts and when the group queue has run dry for it):
+ * out[0] = span first start -> last end (ms), out[1] = mean fraction of the span a wave had
+ * work (1 - out[1] is the drain tail plus the launch ramp), out[2] = the first wave's end and
+ * out[3] = the median wave's end (ms after the first start), out[4] = waves.  Measurement
+ * only (the reference has no counterpart); waits for the launch. */
+int dk_last_search_waves(dk_ctx* ctx, double* out);
 /* memory footprint of the node / state pools reserved by dk_create (bytes) */
 uint64_t dk_pool_bytes(const dk_ctx* ctx);
 /* Pool demand since dk_create (waits for `stream`): the most child slots one search used

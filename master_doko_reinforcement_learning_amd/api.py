@@ -143,6 +143,14 @@ class Engine:
         _check(_native.lib().dk_last_search_ms(self._ctx, ctypes.byref(ms)))
         return float(ms.value)
 
+    def last_search_waves(self):
+        """Per-wave clocks of the last search launch (dk_last_search_waves): span_ms, the mean
+        fraction of the span a wave had work, first / median wave end (ms), waves."""
+        out = (ctypes.c_double * 5)()
+        _check(_native.lib().dk_last_search_waves(self._ctx, out))
+        return {"span_ms": out[0], "busy_frac": out[1], "first_end_ms": out[2], "median_end_ms": out[3],
+                "waves": int(out[4])}
+
     # ---- game construction (FdoState::new_game / DoState::new_game)
     def new_games(self, game, seeds):
         seeds = np.ascontiguousarray(seeds, dtype=np.uint64)

@@ -191,8 +191,13 @@ __global__ void __launch_bounds__(WAVE, H::MIN_WAVES) search_kernel(const dk_sta
                                                       uint8_t* best, int* err, uint32_t* queue, uint64_t* prof,
                                                       const uint32_t* __restrict__ order, uint32_t* retry,
                                                       const uint32_t* __restrict__ list, uint32_t* high_water,
-                                                      const uint32_t* __restrict__ perm, uint32_t lane_base) {
+                                                      const uint32_t* __restrict__ perm, uint32_t lane_base,
+                                                      uint64_t* wave_clock) {
     const uint32_t lane = threadIdx.x;
+    // per-wave start / end of the realtime counter (100 MHz), one entry per 16 pool lanes
+    // (dk_last_search_waves): how long each wave had work before the group queue drained
+    const uint32_t clock_idx = (lane_base + blockIdx.x * rpw) / 16u;
+    if (wave_clock && lane == 0) wave_clock[2 * clock_idx] = __builtin_amdgcn_s_memrealtime();
     const uint32_t T = iters + 1;
     const uint32_t n_ln = LN_LDS ? T : 0u;
     for (uint32_t i = lane; i < n_ln; i += WAVE) dk_lds[i] = (uint64_t)__double_as_longlong(ln_table[i]);
@@ -260,6 +265,7 @@ __global__ void __launch_bounds__(WAVE, H::MIN_WAVES) search_kernel(const dk_sta
         best[root] = b;
     }
     if (hw) atomicMax(high_water, hw);
+    if (wave_clock && lane == 0) wave_clock[2 * clock_idx + 1] = __builtin_amdgcn_s_memrealtime();
 }
 
 // is_consistent (rs-full-doko/src/matching/is_consistent.rs:38-305) of assumed hands and
@@ -792,6 +798,7 @@ struct dk_ctx {
         uint32_t lane_base = 0, lanes = 0;
         bool used = false;              // `done` has been recorded
         bool pending = false;           // err[slot] not yet collected by dk_sync on `stream`
+        uint32_t clock_first = 0, clock_n = 0, clock_stride = 1;   // its waves' entries in wave_clock
         hipStream_t stream = nullptr;
     };
     static constexpr int MAX_INFLIGHT = 8;
@@ -840,6 +847,7 @@ struct dk_ctx {
     bool lds_path_fixed = false;    // DK_LDS_PATH (1..MAX_PATH) fixes it
     bool verbose = false;           // DK_VERBOSE=1: one stderr line per search launch (shape, residency)
     uint64_t* prof = nullptr;       // phase timers (DK_PHASE_PROF builds only)
+    uint64_t* wave_clock = nullptr; // [pool_roots / 16][2] realtime-counter start / end of the search waves
     // AlphaZero PUCT search (dk_az_*): per-game node / state regions, allocated on first use
     dk::az::Node* az_nodes = nullptr;
     dk_az_state* az_states = nullptr;
@@ -1003,7 +1011,11 @@ hipError_t launch_search_t(dk_ctx* ctx, const dk_state* roots, const uint64_t* s
                        ctx->state_stride,
                        rpw, lp, visits, values, best, err, sl.queue, ctx->prof,
                        ordered ? (const uint32_t*)sl.order : (const uint32_t*)nullptr,
-                       fallback ? sl.retry : (uint32_t*)nullptr, (const uint32_t*)nullptr, ctx->high_water, perm, base);
+                       fallback ? sl.retry : (uint32_t*)nullptr, (const uint32_t*)nullptr, ctx->high_water, perm, base,
+                       ctx->wave_clock);
+    sl.clock_first = base / 16u;
+    sl.clock_n = grid;
+    sl.clock_stride = rpw / 16u;
     e = hipGetLastError();
     if (e != hipSuccess || !fallback) return e;
     // the fallback pool is shared by all launches: one fallback pass at a time
@@ -1016,7 +1028,7 @@ hipError_t launch_search_t(dk_ctx* ctx, const dk_state* roots, const uint64_t* s
                        ctx->fb_hot, ctx->fb_cold, (typename E::Node*)ctx->fb_states, ctx->fb_ovf, ctx->fb_ovf_st,
                        ctx->fb_slots, ctx->state_stride, rpw, lp, visits, values, best, err, sl.queue_fb, ctx->prof,
                        (const uint32_t*)nullptr, (uint32_t*)nullptr, (const uint32_t*)sl.retry, ctx->high_water + 2,
-                       (const uint32_t*)nullptr, 0u);
+                       (const uint32_t*)nullptr, 0u, (uint64_t*)nullptr);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if ((e = hipEventRecord(ctx->fb_done, st)) != hipSuccess) return e;
     ctx->fb_used = true;
@@ -1167,6 +1179,7 @@ dk_ctx* dk_create(const dk_config* cfg) {
     ok = ok && hipMalloc(&ctx->err, sizeof(int)) == hipSuccess;
     ok = ok && hipMalloc(&ctx->high_water, 4 * sizeof(uint32_t)) == hipSuccess;
     ok = ok && hipMemset(ctx->high_water, 0, 4 * sizeof(uint32_t)) == hipSuccess;
+    ok = ok && hipMalloc(&ctx->wave_clock, (R / 16 + 1) * 2 * sizeof(uint64_t)) == hipSuccess;
     if (ok && with_fallback) {
         // 64 waves of 64 roots (fewer when the context is smaller): overflow is rare, and the
         // pass only has to finish the few roots that need it
@@ -1243,7 +1256,7 @@ void dk_destroy(dk_ctx* ctx) {
     }
     if (ctx->slot_err) (void)hipFree(ctx->slot_err);
     if (ctx->fb_done) (void)hipEventDestroy(ctx->fb_done);
-    for (void* p : {(void*)ctx->high_water, ctx->fb_hot, (void*)ctx->fb_cold,
+    for (void* p : {(void*)ctx->high_water, (void*)ctx->wave_clock, ctx->fb_hot, (void*)ctx->fb_cold,
                     (void*)ctx->fb_ovf, (void*)ctx->fb_ovf_st, ctx->fb_states})
         if (p) (void)hipFree(p);
     if (ctx->prof) (void)hipFree(ctx->prof);
@@ -1277,6 +1290,39 @@ int dk_pool_high_water(dk_ctx* ctx, void* stream, uint32_t* slots, uint32_t* cap
     *slots = h[0] > h[2] ? h[0] : h[2];
     *capacity = ctx->cap_slots;
     *overflowed = h[1];
+    return DK_OK;
+}
+
+int dk_last_search_waves(dk_ctx* ctx, double* out) {
+    if (!ctx || !out) return DK_E_INVALID;
+    uint32_t first, nw, stride;
+    hipEvent_t e1;
+    {
+        std::lock_guard<std::mutex> g(ctx->slot_mu);
+        if (ctx->last_slot < 0) return DK_E_INVALID;
+        const dk_ctx::Slot& sl = ctx->slots[ctx->last_slot];
+        first = sl.clock_first; nw = sl.clock_n; stride = sl.clock_stride; e1 = sl.ev1;
+    }
+    if (nw == 0) return DK_E_INVALID;
+    DK_HIP(hipEventSynchronize(e1));
+    std::vector<uint64_t> t((size_t)nw * stride * 2);
+    DK_HIP(hipMemcpy(t.data(), ctx->wave_clock + 2 * (size_t)first, t.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    uint64_t t0 = ~0ull, t1 = 0, e_min = ~0ull;
+    std::vector<uint64_t> ends(nw);
+    double busy = 0.0;
+    for (uint32_t w = 0; w < nw; ++w) {
+        const uint64_t a = t[2 * (size_t)w * stride], b = t[2 * (size_t)w * stride + 1];
+        t0 = a < t0 ? a : t0; t1 = b > t1 ? b : t1; e_min = b < e_min ? b : e_min;
+        busy += (double)(b - a);
+        ends[w] = b;
+    }
+    std::sort(ends.begin(), ends.end());
+    const double span = (double)(t1 - t0);
+    out[0] = span / 1e5;                                   // first start -> last end (ms, 100 MHz counter)
+    out[1] = span > 0 ? busy / ((double)nw * span) : 1.0;  // mean fraction of the span a wave had work
+    out[2] = (double)(e_min - t0) / 1e5;                   // first wave out of work (ms)
+    out[3] = (double)(ends[nw / 2] - t0) / 1e5;            // median wave end (ms)
+    out[4] = (double)nw;
     return DK_OK;
 }
 

@@ -127,19 +127,19 @@ def _c3_check_picks(out, args, I, S, picks, rng, lds_path=None, per_info=4):
 
 def test_c3_bench_two_legs(monkeypatch, capfd):
     """bench.main's exact sequence on one engine: the timed C3 batch at bench's default
-    size (18,432 infostates x 64 CAP samples = 1,179,648 roots, six groups per resident
+    size (36,864 infostates x 64 CAP samples = 2,359,296 roots, twelve groups per resident
     wave), then the small-batch leg (512 infostates: 32-root waves, 32-B records) on the
     same engine with its own buffers.  Every root of both legs passes the device
     invariants (visit sum, best = an argmax) and the host re-check; roots spread over each
     queue equal oracle searches bitwise; whole infostates fuse to the oracle's action."""
-    I, S = 18432, 64
+    I, S = 36864, 64
     args, n_roots, out, eng = _bench_workload([], monkeypatch, keep=True)
     assert args.infostates == I and n_roots == I * S
     ln = _launch_line(capfd)
     assert ln["hot"] == "8B", ln
     grid, rpw = int(ln["grid"]), int(ln["rpw"])
     assert rpw == 64 and int(ln["resident/CU"]) * 256 >= grid
-    assert n_roots // rpw >= 6 * grid, ln           # six groups per resident wave, as timed
+    assert n_roots // rpw >= 12 * grid, ln          # twelve groups per resident wave, as timed
     lds_path = int(ln["lds_path"])
     assert lds_path <= 16
     _host_invariants(out, ITERS)
