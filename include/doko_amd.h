@@ -242,8 +242,9 @@ typedef struct dk_config {
     int32_t device;          /* HIP device ordinal                                          */
     uint32_t max_roots;      /* largest batch of roots one search call may carry            */
     uint32_t max_iterations; /* largest `iterations` one search call may use                */
-    uint32_t slot_capacity;  /* child slots per root in the main pools (0 = 64 + 4 x        */
-                             /* max_iterations); see dk_pool_high_water                     */
+    uint32_t slot_capacity;  /* child slots per root in the main pools (0 = 64 + 8 x        */
+                             /* max_iterations, halved while the pools would take more than */
+                             /* half of the free device memory); see dk_pool_high_water     */
 } dk_config;
 
 typedef struct dk_ctx dk_ctx;
@@ -254,7 +255,7 @@ typedef struct dk_ctx dk_ctx;
  * roots at a time, so max_roots bounds the batch, not the memory.
  * Child slots: a search needs at most 42 + 12 x iterations of them (proven bound) but
  * measured far fewer, so the main pools hold slot_capacity per root (default
- * 64 + 4 x max_iterations, rounded up to a multiple of 256; env DK_SLOT_CAPACITY overrides).  A root that runs out is
+ * 64 + 8 x max_iterations, rounded up to a multiple of 256; env DK_SLOT_CAPACITY overrides).  A root that runs out is
  * searched again, from its seed, by a second launch over a small pool with the proven
  * bound (4,096 roots at once): results are identical whatever the capacity.  With
  * slot_capacity at or above the proven bound there is no second pool. */
