@@ -506,6 +506,14 @@ def test_full_size_properties(eng, monkeypatch):
     # short) holds every one of these searches
     hw, cap, overflowed = eng.pool_high_water()
     assert cap in (4096, 8192) and 0 < hw <= cap and overflowed == 0, (hw, cap, overflowed)
+    # per-wave clocks of the last launch (dk_last_search_waves): one entry per wave of the grid
+    # (4096 roots as 256 waves of 16: one wave per SIMD, launch_rpw), every wave busy for a
+    # share of the span, and the span (100 MHz counter) within the launch's HIP-event time
+    ms = eng.last_search_ms()
+    w = eng.last_search_waves()
+    assert w["waves"] == n // 16, w
+    assert 0.0 < w["busy_frac"] <= 1.0 and 0.0 < w["first_end_ms"] <= w["median_end_ms"] <= w["span_ms"], w
+    assert 0.5 * ms < w["span_ms"] <= ms * 1.02 + 0.05, (ms, w)
 
 
 # ---------------------------------------------------------------- rs-doko rule-based sampler
