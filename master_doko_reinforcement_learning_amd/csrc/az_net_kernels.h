@@ -1003,8 +1003,8 @@ constexpr uint32_t MLP_MAX_HIDDEN = 1024;
 #ifndef DK_MLP_P2
 #define DK_MLP_P2 1
 #endif
-template <int D, int NC, int WAVES = 8>
-__global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) mlp_ln_kernel(const uint16_t* __restrict__ h, uint16_t* __restrict__ x_io,
+template <int D, int NC>
+__global__ void __launch_bounds__(512, 1) mlp_ln_kernel(const uint16_t* __restrict__ h, uint16_t* __restrict__ x_io,
                                                         const uint16_t* __restrict__ w1, const uint16_t* __restrict__ b1,
                                                         const uint16_t* __restrict__ w2, const uint16_t* __restrict__ b2,
                                                         uint32_t rows, uint32_t n_hidden, const uint16_t* __restrict__ gamma,
@@ -1016,15 +1016,13 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) mlp_ln_kernel(const uin
     constexpr int KS = D / 16, OT = D / 32, LDW1 = D + 8, LDW2 = NC + DK_MLP_W2PAD, HT = NC / 32, GS = NC / 16;
     // LDS: the chunk's W1 / W2, in NB buffers: 3 when the waves 4..7 run half a chunk behind
     // (below), 2 otherwise
-    // (four-wave workgroups: two per CU, whose waves pair up on the SIMDs without a skew)
-    constexpr bool SKEW = DK_MLP_SKEW && D <= 160 && WAVES == 8;   // d = 256 has no registers to spare
-    constexpr int T = 64 * WAVES;                   // threads
+    constexpr bool SKEW = DK_MLP_SKEW && D <= 160;   // d = 256 has no registers to spare
     constexpr int NB = SKEW ? 3 : 2;
     constexpr int W1E = NC * LDW1, W2E = D * LDW2;
     __shared__ __attribute__((aligned(16))) uint16_t lds[NB * (W1E + W2E)];
     __shared__ float b1s[MLP_MAX_HIDDEN];           // the hidden units' biases
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
-    const uint32_t row = blockIdx.x * (32u * WAVES) + (uint32_t)wave * 32u + (uint32_t)r;
+    const uint32_t row = blockIdx.x * 256u + (uint32_t)wave * 32u + (uint32_t)r;
     const bool ok = row < rows;
     bf16x8_t hf[KS];
     {
@@ -1039,17 +1037,17 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) mlp_ln_kernel(const uin
     // indexed in a loop is an alloca that the compiler promoted to LDS here, which serialised
     // every global load behind its LDS store.
     constexpr int P1 = NC * (D / 8), P2 = D * (NC / 8);
-    static_assert(P1 <= 3 * T && P2 <= 3 * T, "three pieces per thread and matrix");
+    static_assert(P1 <= 3 * 512 && P2 <= 3 * 512, "three pieces per thread and matrix");
     uint4 pa0{}, pa1{}, pa2{}, pb0{}, pb1{}, pb2{};
 #define DK_MLP_LD(U, R1, R2, c)                                                                                \
     {                                                                                                          \
-        const int v = threadIdx.x + T * (U);                                                                   \
+        const int v = threadIdx.x + 512 * (U);                                                                 \
         if (v < P1) { const int i = v / (D / 8), p = v - i * (D / 8); R1 = *(const uint4*)(w1 + ((size_t)(c) * NC + i) * D + 8 * p); } \
         if (v < P2) { const int o = v / (NC / 8), p = v - o * (NC / 8); R2 = *(const uint4*)(w2 + (size_t)o * n_hidden + (size_t)(c) * NC + 8 * p); } \
     }
 #define DK_MLP_ST(U, R1, R2, buf)                                                                              \
     {                                                                                                          \
-        const int v = threadIdx.x + T * (U);                                                                   \
+        const int v = threadIdx.x + 512 * (U);                                                                 \
         if (v < P1) { const int i = v / (D / 8), p = v - i * (D / 8); *(uint4*)&lds[(buf) * W1E + i * LDW1 + 8 * p] = R1; } \
         if (v < P2) { const int o = v / (NC / 8), p = v - o * (NC / 8); uint2* d_ = (uint2*)&lds[NB * W1E + (buf) * W2E + o * LDW2 + 8 * p]; \
                       d_[0] = make_uint2(R2.x, R2.y); d_[1] = make_uint2(R2.z, R2.w); } \
@@ -1060,7 +1058,7 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) mlp_ln_kernel(const uin
 #pragma unroll
     for (int t = 0; t < OT; ++t) acc2[t] = f32x16_t{0};
     const uint32_t chunks = n_hidden / NC;
-    for (uint32_t i = threadIdx.x; i < n_hidden; i += T) b1s[i] = bf2f(b1[i]);
+    for (uint32_t i = threadIdx.x; i < n_hidden; i += 512) b1s[i] = bf2f(b1[i]);
     DK_MLP_LOAD_CHUNK(0u)
     DK_MLP_STORE_CHUNK(0)
     __syncthreads();

@@ -1896,16 +1896,7 @@ int dk_net_mlp_ln_bf16_async(const void* h, void* x_io, const void* w1, const vo
         return DK_E_INVALID;
     if (rows == 0) return DK_OK;
     const dim3 grid((rows + 255u) / 256u), block(512);
-    static const int variant = [] { const char* e = getenv("DK_MLP_VARIANT"); return e ? atoi(e) : 0; }();
-    if (d == 160u && variant == 1)
-        hipLaunchKernelGGL((dk::net::mlp_ln_kernel<160, 32, 4>), dim3((rows + 127u) / 128u), dim3(256), 0, (hipStream_t)stream,
-                           (const uint16_t*)h, (uint16_t*)x_io, (const uint16_t*)w1, (const uint16_t*)b1, (const uint16_t*)w2,
-                           (const uint16_t*)b2, rows, n_hidden, (const uint16_t*)gamma, (const uint16_t*)beta, eps, (uint16_t*)h_out);
-    else if (d == 160u && variant == 2)
-        hipLaunchKernelGGL((dk::net::mlp_ln_kernel<160, 32>), grid, block, 0, (hipStream_t)stream, (const uint16_t*)h,
-                           (uint16_t*)x_io, (const uint16_t*)w1, (const uint16_t*)b1, (const uint16_t*)w2, (const uint16_t*)b2,
-                           rows, n_hidden, (const uint16_t*)gamma, (const uint16_t*)beta, eps, (uint16_t*)h_out);
-    else if (d == 160u)
+    if (d == 160u)
         hipLaunchKernelGGL((dk::net::mlp_ln_kernel<160, 64>), grid, block, 0, (hipStream_t)stream, (const uint16_t*)h,
                            (uint16_t*)x_io, (const uint16_t*)w1, (const uint16_t*)b1, (const uint16_t*)w2, (const uint16_t*)b2,
                            rows, n_hidden, (const uint16_t*)gamma, (const uint16_t*)beta, eps, (uint16_t*)h_out);
