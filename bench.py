@@ -51,7 +51,7 @@ def parse():
     p.add_argument("--iterations", type=int, default=1000)
     p.add_argument("--infostates", type=int, default=None,
                    help="infostates per GPU (c3: default 36864 x 64 samples = 2,359,296 roots, twelve 64-root groups "
-                        "per resident wave (3072 waves): the persistent grid's drain tail is 4.6 %% of the launch, "
+                        "per resident wave (3072 waves): the persistent grid's drain tail is 4.5 %% of the launch, "
                         "against 7.5 %% at six groups (per-wave clocks, DESIGN.md §4.1); c2d, impi, impid: default 12288)")
     p.add_argument("--samples", type=int, default=64, help="samples per infostate (c3, c2d)")
     p.add_argument("--partition", choices=["infostates", "samples"], default="infostates",
