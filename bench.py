@@ -73,6 +73,10 @@ def parse():
     p.add_argument("--inflight", default="2,4,8",
                    help="c3 small batch: also time K independent decision batches in flight on one engine "
                         "(DefaultImpiPolicy.execute_many), for each K in this list; empty = skip")
+    p.add_argument("--dist-one-rank", action="store_true",
+                   help="c3 / c2d at --gpus 1: initialise the process group anyway (RCCL, one rank) so that the "
+                        "multi-GPU collectives (all-gather of the actions, all-reduce of the accumulators, barriers, "
+                        "max-over-ranks timing) run on the device; results equal the plain N = 1 run")
     p.add_argument("--host-readback-check", action="store_true",
                    help="also copy every leg's visits to pageable host memory and check them there (the round-2 "
                         "sequence); a host-only violation is reported as host_copy_bad_roots, not raised")
@@ -142,7 +146,8 @@ def make_workload(args, dk, L, dev, sp, rank, world, local_rank, dist=None, eng=
         acc_u = torch.zeros((I, 39), dtype=torch.int32, device=dev)
         acc_f = torch.zeros((I, 39), dtype=torch.float32, device=dev)
         actions = torch.zeros(I, dtype=torch.uint8, device=dev)
-        gather = by_info and world > 1
+        dist_on = dist is not None and dist.is_available() and dist.is_initialized()
+        gather = by_info and dist_on
         actions_all = torch.zeros((world, I), dtype=torch.uint8, device=dev) if gather else actions
     else:
         gidx = np.arange(rank * n_roots, (rank + 1) * n_roots, dtype=np.uint64)
@@ -162,7 +167,7 @@ def make_workload(args, dk, L, dev, sp, rank, world, local_rank, dist=None, eng=
             ck(L.dk_search_batch_async(eng.ctx, game, ptr(roots), ptr(d_srch), n_roots, iters, args.c,
                                        ptr(visits), ptr(values), ptr(best), sp))
             ck(L.dk_fuse_accumulate_async(eng.ctx, ptr(visits), I, S_r, ptr(allowed), fuse_mode, ptr(acc_u), ptr(acc_f), sp))
-            if world > 1 and not by_info:
+            if dist_on and not by_info:
                 dist.all_reduce(acc_u if fuse_mode == dk.FUSE_MAXN else acc_f)  # RCCL over xGMI
             ck(L.dk_fuse_select_async(eng.ctx, I, fuse_mode, ptr(allowed), ptr(acc_u), ptr(acc_f), ptr(actions), sp))
             if gather:
@@ -177,14 +182,18 @@ def make_workload(args, dk, L, dev, sp, rank, world, local_rank, dist=None, eng=
                                 "acc": (acc_u if fuse_mode == dk.FUSE_MAXN else acc_f) if determinized else None}
 
 
+def free_port():
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
 def launch_ranks(args):
     """`--gpus N` outside a torchrun environment: start the N ranks (one process per GPU)
     as children under torch.distributed.run and return their exit status.  Called before
     this process touches the GPU (no HIP call, no torch.cuda query)."""
-    import socket
-    with socket.socket() as so:
-        so.bind(("127.0.0.1", 0))
-        port = so.getsockname()[1]
+    port = free_port()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
     return subprocess.call(cmd)
@@ -269,7 +278,8 @@ def timed_steps(step, steps, warmup, eng, L, dev, world, dist, ck, sp):
     for _ in range(warmup):
         step()
     ck(L.dk_sync(eng.ctx, sp))
-    if world > 1:
+    dist_on = dist.is_available() and dist.is_initialized()
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -278,11 +288,11 @@ def timed_steps(step, steps, warmup, eng, L, dev, world, dist, ck, sp):
         search_ms.append(eng.last_search_ms())  # waits for this step's search kernel (HIP events on its stream)
     torch.cuda.synchronize(dev)
     ck(L.dk_sync(eng.ctx, sp))
-    if world > 1:
+    if dist_on:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
+    if dist_on:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item()), search_ms
 
@@ -311,7 +321,13 @@ def main():
                          % (world, world, ndev))
     device = local_rank % max(1, ndev) if backend != "nccl" else local_rank
     torch.cuda.set_device(device)
-    if world > 1:
+    dist_on = world > 1 or (args.dist_one_rank and args.workload in ("c3", "c2d"))
+    if dist_on:
+        if world == 1:   # one-rank group outside torchrun (--dist-one-rank)
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(free_port()))
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", device))   # RCCL over xGMI
         else:
@@ -349,7 +365,7 @@ def main():
         np.save(args.dump_actions, bufs["actions"].cpu().numpy())
     if args.dump_acc and bufs["acc"] is not None:
         acc = bufs["acc"]
-        if world > 1 and args.partition == "infostates" and args.workload in ("c3", "c2d"):
+        if dist_on and args.partition == "infostates" and args.workload in ("c3", "c2d"):
             parts = [torch.zeros_like(acc) for _ in range(world)]
             dist.all_gather(parts, acc)
             acc = torch.cat(parts)
@@ -469,11 +485,11 @@ def main():
             "small_batch": small,
             "host_copy_bad_roots": host_bad or None,
             "ranks": world,
-            "dist_backend": backend if world > 1 else None,
+            "dist_backend": backend if dist_on else None,
             "cpu_baseline": cpu,
         }
         print(json.dumps(result))
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
     eng.close()
     return result

@@ -36,16 +36,17 @@ pytestmark = pytest.mark.gpu
 INFO_PER_RANK, ITERS = 48, 200
 
 
-def _bench(tmp_path, gpus, infostates, fusion, tag, partition="samples"):
+def _bench(tmp_path, gpus, infostates, fusion, tag, partition="samples", backend="gloo", extra=()):
     env = dict(os.environ)
-    env["DK_DIST_BACKEND"] = "gloo"
-    env.pop("WORLD_SIZE", None)
+    env["DK_DIST_BACKEND"] = backend
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
     act = str(tmp_path / ("act_%s.npy" % tag))
     acc = str(tmp_path / ("acc_%s.npy" % tag))
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--steps", "1", "--warmup", "0",
            "--no-cpu-baseline", "--small-infostates", "0", "--infostates", str(infostates),
            "--iterations", str(ITERS), "--fusion", fusion, "--dump-actions", act, "--dump-acc", acc,
-           "--partition", partition]
+           "--partition", partition] + list(extra)
     out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=110)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
     line = [l for l in out.stdout.splitlines() if l.startswith("{")][-1]
@@ -82,3 +83,17 @@ def test_bench_two_ranks_avg_tolerance(tmp_path):
         if a1[i] != a2[i]:
             top = np.sort(acc1[i])[-2:]
             assert top[1] - top[0] <= 1e-5, (i, a1[i], a2[i], top)
+
+
+@pytest.mark.parametrize("partition", ["infostates", "samples"])
+def test_bench_rccl_one_rank(tmp_path, partition):
+    """The N > 1 code path over RCCL on the MI355X (`--dist-one-rank`: a one-rank nccl process
+    group, so the all-gather of the actions / all-reduce of the accumulators, the barriers and
+    the max-over-ranks timing all run through RCCL on the device): decisions and accumulators
+    equal the plain one-GPU run bit for bit."""
+    r, a, acc = _bench(tmp_path, 1, 2 * INFO_PER_RANK, "maxn", "r" + partition, partition, backend="nccl",
+                       extra=("--dist-one-rank",))
+    assert r["dist_backend"] == "nccl" and r["ranks"] == 1, r
+    r0, a0, acc0 = _bench(tmp_path, 1, 2 * INFO_PER_RANK, "maxn", "p" + partition, partition, backend="nccl")
+    assert r0["dist_backend"] is None
+    assert np.array_equal(acc, acc0) and np.array_equal(a, a0)
