@@ -38,12 +38,21 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--workload", choices=["c3", "c2", "c2d", "c5", "impi", "impid"], default="c3",
+    p.add_argument("--workload", choices=["c3", "c2", "c2d", "c5", "impi", "impid", "c1", "prod"], default="c3",
                    help="c3: rs-full-doko + CAP (default, the metric's config); c2: rs-doko roots after 4x Healthy; "
                         "c2d: rs-doko infostates determinized by the rule-based sampler; "
                         "c5: AlphaZero self-play moves (PUCT + policy/value network); "
                         "impi: autoregressive (IMPI) determinization of the c3 infostates with the IMPI network; "
-                        "impid: the AR-determinized decision (mcts_ar_maxn_policy: AR samples -> UCT -> MaxN)")
+                        "impid: the AR-determinized decision (mcts_ar_maxn_policy: AR samples -> UCT -> MaxN); "
+                        "c1: tic-tac-toe games (tic_tac_toe_player: one SmallRng stream through every search, and "
+                        "independent games in lockstep); prod: the thesis's production search shape (S samples x "
+                        "200,000 iterations, run.rs:270-291): decision latency and decisions in flight")
+    p.add_argument("--c1-games", type=int, default=1000, help="c1: independent games in lockstep per step")
+    p.add_argument("--c1-serial-games", type=int, default=5,
+                   help="c1: games of the one-stream tic_tac_toe_player timed on the GPU and on the oracle")
+    p.add_argument("--prod-iterations", type=int, default=200000, help="prod: iterations per sample (run.rs:270-291)")
+    p.add_argument("--prod-samples", default="5,10,50", help="prod: samples per decision, one leg each")
+    p.add_argument("--prod-inflight", type=int, default=16, help="prod: decisions in flight in the batched leg")
     p.add_argument("--games", type=int, default=8192, help="concurrent self-play games per GPU (c5)")
     p.add_argument("--az-iterations", type=int, default=200, help="PUCT iterations per move (c5)")
     p.add_argument("--ar-samples", type=int, default=4, help="AR samples per infostate (impi)")
@@ -160,6 +169,16 @@ def make_workload(args, dk, L, dev, sp, rank, world, local_rank, dist=None, eng=
     values = torch.zeros((n_roots, 39), dtype=torch.float64, device=dev)
     best = torch.zeros(n_roots, dtype=torch.uint8, device=dev)
     ck(L.dk_sync(eng.ctx, sp))
+    # HIP events on the step's stream around the collectives (RCCL work is ordered between
+    # them): per-rank collective time, so an N-GPU curve separates search from exchange
+    coll_events = []
+
+    def collective(fn):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn()
+        e1.record()
+        coll_events.append((e0, e1))
 
     def step():
         if determinized:
@@ -168,10 +187,11 @@ def make_workload(args, dk, L, dev, sp, rank, world, local_rank, dist=None, eng=
                                        ptr(visits), ptr(values), ptr(best), sp))
             ck(L.dk_fuse_accumulate_async(eng.ctx, ptr(visits), I, S_r, ptr(allowed), fuse_mode, ptr(acc_u), ptr(acc_f), sp))
             if dist_on and not by_info:
-                dist.all_reduce(acc_u if fuse_mode == dk.FUSE_MAXN else acc_f)  # RCCL over xGMI
+                collective(lambda: dist.all_reduce(acc_u if fuse_mode == dk.FUSE_MAXN else acc_f))  # RCCL over xGMI
             ck(L.dk_fuse_select_async(eng.ctx, I, fuse_mode, ptr(allowed), ptr(acc_u), ptr(acc_f), ptr(actions), sp))
             if gather:
-                dist.all_gather(list(actions_all.unbind(0)), actions)          # RCCL over xGMI: every rank's decisions
+                # RCCL over xGMI: every rank's decisions
+                collective(lambda: dist.all_gather(list(actions_all.unbind(0)), actions))
         else:
             ck(L.dk_search_batch_async(eng.ctx, dk.GAME_DOKO, ptr(roots), ptr(d_srch), n_roots, iters, args.c,
                                        ptr(visits), ptr(values), ptr(best), sp))
@@ -179,6 +199,7 @@ def make_workload(args, dk, L, dev, sp, rank, world, local_rank, dist=None, eng=
     return eng, step, n_roots, {"visits": visits, "values": values, "best": best, "roots": roots, "I": I, "S_r": S_r,
                                 "info": info if determinized else None, "game": game,
                                 "actions": actions_all.reshape(-1) if determinized else None,
+                                "coll_events": coll_events,
                                 "acc": (acc_u if fuse_mode == dk.FUSE_MAXN else acc_f) if determinized else None}
 
 
@@ -270,14 +291,17 @@ def check_visits_host(v, iters, leg):
     return np.nonzero(s != iters)[0]
 
 
-def timed_steps(step, steps, warmup, eng, L, dev, world, dist, ck, sp):
+def timed_steps(step, steps, warmup, eng, L, dev, world, dist, ck, sp, coll_events=None):
     """W untimed steps, then exactly K steps bracketed by barrier + synchronize; returns
-    (max-over-ranks wall seconds, per-step search-kernel ms)."""
+    (max-over-ranks wall seconds, per-step search-kernel ms, per-step collective ms of
+    this rank)."""
     import torch
     search_ms = []
     for _ in range(warmup):
         step()
     ck(L.dk_sync(eng.ctx, sp))
+    if coll_events is not None:
+        coll_events.clear()
     dist_on = dist.is_available() and dist.is_initialized()
     if dist_on:
         dist.barrier()
@@ -294,7 +318,19 @@ def timed_steps(step, steps, warmup, eng, L, dev, world, dist, ck, sp):
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if dist_on:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item()), search_ms
+    coll_ms = sum(e0.elapsed_time(e1) for e0, e1 in coll_events) / steps if coll_events else 0.0
+    return float(t.item()), search_ms, coll_ms
+
+
+def per_rank(value, dev, world, dist):
+    """Every rank's `value` (a float), gathered on all ranks."""
+    import torch
+    if world == 1 or not (dist.is_available() and dist.is_initialized()):
+        return [value]
+    t = torch.tensor([value], dtype=torch.float64, device=dev)
+    parts = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(parts, t)
+    return [float(p.item()) for p in parts]
 
 
 def main():
@@ -349,6 +385,10 @@ def main():
 
     if args.workload == "c5":
         return run_c5(args, dk, L, dev, stream, rank, world, local_rank, dist)
+    if args.workload == "c1":
+        return run_c1(args, dk, L, dev, stream, rank, world, local_rank, dist)
+    if args.workload == "prod":
+        return run_prod(args, dk, L, dev, stream, rank, world, local_rank, dist)
     if args.workload in ("impi", "impid"):
         return run_impi(args, dk, L, dev, stream, rank, world, local_rank, dist)
     eng, step, n_roots, bufs = make_workload(args, dk, L, dev, sp, rank, world, local_rank, dist)
@@ -357,7 +397,8 @@ def main():
     visits = bufs["visits"]
     I = bufs["I"]
 
-    elapsed, search_ms = timed_steps(step, args.steps, args.warmup, eng, L, dev, world, dist, ck, sp)
+    elapsed, search_ms, coll_ms = timed_steps(step, args.steps, args.warmup, eng, L, dev, world, dist, ck, sp,
+                                              bufs["coll_events"])
     # per-wave clocks of the last timed search launch: how much of it the persistent grid's
     # drain tail costs (the waves that ran out of groups wait for the slowest one)
     waves = eng.last_search_waves()
@@ -377,6 +418,9 @@ def main():
         host_bad["batch"] = check_visits_host(visits.cpu().numpy(), iters, "batch").size
     sims_total = n_roots * iters * args.steps * world
     kernel_ms = float(np.mean(search_ms))
+    # attribution of an N-GPU step: every rank's search kernel and collective time (HIP events)
+    rank_kernel_ms = per_rank(kernel_ms, dev, world, dist)
+    rank_coll_ms = per_rank(coll_ms, dev, world, dist)
     del bufs, visits
 
     # the survey's C3 decision batch (512 infostates x 64 samples = 32,768 roots): the regime a
@@ -387,7 +431,7 @@ def main():
         sa = copy.copy(args)
         sa.infostates = args.small_infostates
         _, sstep, s_roots, sbufs = make_workload(sa, dk, L, dev, sp, rank, world, local_rank, dist, eng=eng)
-        s_el, s_ms = timed_steps(sstep, args.small_steps, 1, eng, L, dev, world, dist, ck, sp)
+        s_el, s_ms, _ = timed_steps(sstep, args.small_steps, 1, eng, L, dev, world, dist, ck, sp)
         s_waves = eng.last_search_waves()
         check_visits(sbufs, iters, "small batch")
         if args.host_readback_check:
@@ -451,6 +495,12 @@ def main():
             },
             "kernel_only_rollouts_per_s": n_roots * iters * world / (kernel_ms / 1e3),
             "search_kernel_ms": kernel_ms,
+            "search_kernel_ms_per_rank": rank_kernel_ms,
+            "collective_ms": max(rank_coll_ms),
+            "collective_ms_per_rank": rank_coll_ms,
+            "collective": (None if not (dist_on and determinized) else
+                           "all_gather of the fused actions (%d B per rank)" % I if args.partition == "infostates" else
+                           "all_reduce of the fusion accumulators (%d B)" % (I * 39 * 4)),
             "search_waves": {"waves": waves["waves"], "busy_frac": round(waves["busy_frac"], 4),
                              "first_end_ms": round(waves["first_end_ms"], 2),
                              "median_end_ms": round(waves["median_end_ms"], 2), "span_ms": round(waves["span_ms"], 2),
@@ -612,6 +662,222 @@ def run_c5(args, dk, L, dev, stream, rank, world, local_rank, dist):
                          "note": "network GEMMs/attention: %.1f MFLOP per leaf evaluation (algorithmic), bf16 dense "
                                  "peak; achieved over the network's event-timed share of the step" % (flop / 1e6)},
             "cpu_baseline": None,
+        }
+        print(json.dumps(result))
+    if world > 1:
+        dist.destroy_process_group()
+    eng.close()
+    return result
+
+
+def _finish_dist(world, dist, t_elapsed, dev):
+    """Max-over-ranks wall time (the driver's contract) for the replica workloads."""
+    import torch
+    t = torch.tensor([t_elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def run_c1(args, dk, L, dev, stream, rank, world, local_rank, dist):
+    """Config 1: tic-tac-toe with rs-doko-mcts plain UCT (c = 2.0).  Two legs:
+      * serial: tic_tac_toe_player (tic_tac_toe_player.rs:8-52) -- ONE seed_from_u64(999) stream
+        threaded through every search of every game (dk_search_batch_rng, one root per launch), so
+        the games are strictly sequential; timed on the GPU and on the oracle (one CPU thread,
+        the reference's configuration) over the same --c1-serial-games games;
+      * lockstep (`value`): --c1-games independent games, game g on its own stream
+        seed_from_u64(999 + g), one search launch per move over every unfinished game.
+    A step = one lockstep pass (all games played to the end)."""
+    import torch
+    iters = args.iterations if args.iterations != 1000 else 1400          # tic_tac_toe_player.rs:18
+    G = args.c1_games
+    eng = dk.Engine(device=local_rank, max_roots=max(G, 64), max_iterations=iters)
+    seeds = np.arange(G, dtype=np.uint64) + np.uint64(999 + rank * G)
+    for _ in range(args.warmup):
+        dk.tic_tac_toe_games(eng, seeds, iters, 2.0)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    searches, fin = 0, None
+    for _ in range(args.steps):
+        fin, moves, n = dk.tic_tac_toe_games(eng, seeds, iters, 2.0)
+        searches += n
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = _finish_dist(world, dist, time.perf_counter() - t0, dev)
+    # serial leg: the reference's one-stream player
+    gs = args.c1_serial_games
+    dk.tic_tac_toe_player(eng, 1, iters, 2.0)                              # warm-up game
+    trace = []
+    t1 = time.perf_counter()
+    res_serial = dk.tic_tac_toe_player(eng, gs, iters, 2.0, trace=trace)
+    serial_s = time.perf_counter() - t1
+    result = None
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu_baseline:
+            sys.path.insert(0, os.path.join(ROOT, "tests"))
+            import ctypes
+
+            import oracle_lib as ol
+            rng = ol.rng_seed(999)
+            t2 = time.perf_counter()
+            ms, same = 0, True
+            for g in range(gs):
+                b = [0] * 9
+                while ol.lib().or_ttt_finish(ol.arr(ctypes.c_int32, 9, b)) == 0:
+                    best, _, _ = ol.ttt_search(b, rng, iters, 2.0)
+                    if ms < len(trace):
+                        same &= trace[ms][3] == best and [int(w) for w in trace[ms][4]] == [int(rng[k]) for k in range(4)]
+                    b[best] = 1 if b.count(1) == b.count(2) else 2
+                    ms += 1
+            cpu_s = time.perf_counter() - t2
+            cpu = {"value": ms * iters / cpu_s, "unit": "rollouts/s", "cores": 1, "kind": "port",
+                   "sample": "the same %d one-stream games (%d searches x %d sims), oracle C++ restatement on one "
+                             "thread (the reference's configuration)" % (gs, ms, iters),
+                   "ms_per_search": cpu_s / ms * 1e3, "moves_equal_gpu": bool(same and ms == len(trace))}
+        fin = np.asarray(fin)
+        result = {
+            "metric": "tic-tac-toe UCT simulations/sec (rs-doko-mcts plain UCT, %d sims/move, c = 2.0)" % iters,
+            "value": searches * iters * world / elapsed,
+            "unit": "rollouts/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "u64+f64",
+            "data": "tic-tac-toe from the empty board; game g's stream SmallRng::seed_from_u64(999 + g)",
+            "config": {"workload": "C1 tic-tac-toe: %d independent games in lockstep per GPU, one search launch per "
+                                   "move over the unfinished games, %d sims per search" % (G, iters),
+                       "searches_per_step": searches // args.steps,
+                       "results_x_o_draw": [int((fin == 1).sum()), int((fin == 2).sum()), int((fin == 3).sum())],
+                       "parallelism": "replicas x%d" % world},
+            "serial_one_stream": {
+                "games": gs, "searches": len(trace), "results_x_o_draw": res_serial,
+                "ms_per_search": serial_s / max(1, len(trace)) * 1e3,
+                "rollouts_per_s": len(trace) * iters / serial_s,
+                "note": "tic_tac_toe_player as the reference runs it: each search continues the previous one's "
+                        "stream, so one root per launch, two host round trips per move (search, step)"},
+            "roofline": None,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(result))
+    if world > 1:
+        dist.destroy_process_group()
+    eng.close()
+    return result
+
+
+def run_prod(args, dk, L, dev, stream, rank, world, local_rank, dist):
+    """The thesis's production search shape: DefaultImpiPolicy with S CAP samples of
+    200,000 UCT iterations each (compare_impi/run.rs:270-291; S in {5, 10, 50}).  Per S:
+      * latency: ONE decision (S roots, determinize -> search -> fuse -> select) on the GPU;
+      * in flight: --prod-inflight decisions batched into one pass (execute_many), the regime of
+        the evaluator's 2 x available_parallelism concurrent games (run.rs:775);
+      * cpu: the oracle on S threads, one sample per thread (the reference runs the samples of a
+        decision as tokio tasks on MCTSWorkers threads), on the same roots.
+    Each root's 200,000 simulations are sequential (the reference's semantics), so a decision's
+    latency is one lane's sequential speed: the GPU loses on latency and wins on throughput."""
+    import torch
+    iters = args.prod_iterations
+    Ss = [int(x) for x in args.prod_samples.split(",") if x]
+    K = args.prod_inflight
+    max_roots = max(Ss) * K
+    # pools: 32-B records (iterations > 4095); 4 slots per iteration cover the measured demand
+    eng = dk.Engine(device=local_rank, max_roots=max_roots, max_iterations=iters, slot_capacity=64 + 4 * iters)
+    sp = stream.cuda_stream
+
+    def ck(rc):
+        if rc != 0:
+            raise RuntimeError("doko_amd error %d: %s" % (rc, L.dk_status_string(rc).decode()))
+
+    # K infostates: C3-style seeded deals, 4x Healthy, k in {0,8,20,32} random plies
+    info_seeds = torch.tensor((np.arange(K, dtype=np.uint64) + np.uint64(0xC3000000)).view(np.int64), device=dev)
+    info = torch.zeros((K, 128), dtype=torch.uint8, device=dev)
+    ck(L.dk_new_game_batch_async(eng.ctx, dk.GAME_FULL_DOKO, info_seeds.data_ptr(), K, info.data_ptr(), sp))
+    a = torch.full((K,), 1 << 24, dtype=torch.int64, device=dev)
+    for _ in range(4):
+        ck(L.dk_env_step_batch_async(eng.ctx, info.data_ptr(), a.data_ptr(), K, sp))
+    plies = torch.tensor(np.array([[0, 8, 20, 32][j % 4] for j in range(K)], dtype=np.uint32).view(np.int32), device=dev)
+    ply_rng = torch.tensor(dk.splitmix_rng_states(np.arange(K, dtype=np.uint64) + np.uint64(0xC3100000)).view(np.int64),
+                           device=dev)
+    ck(L.dk_env_random_plies_batch_async(eng.ctx, info.data_ptr(), ply_rng.data_ptr(), plies.data_ptr(), K, sp))
+    ck(L.dk_sync(eng.ctx, sp))
+    legs, v1_rows = [], {}
+    for S in Ss:
+        pol = dk.DefaultImpiPolicy(eng, args.c, iters, S, dk.FUSE_MAXN)
+
+        def seeds_for(j):
+            base = np.uint64(0xC3200000 + j * 4096)
+            sd = np.concatenate([np.arange(S, dtype=np.uint64) + base, np.arange(S, dtype=np.uint64) + base + np.uint64(2048)])
+            return torch.tensor(sd.view(np.int64), device=dev)
+
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        act1, v1 = pol.execute_many([(info[:1], seeds_for(0))], game=dk.GAME_FULL_DOKO)[0]
+        torch.cuda.synchronize(dev)
+        lat = time.perf_counter() - t0
+        k1 = eng.last_search_ms()
+        v1_rows[S] = v1.cpu().numpy()
+        batches = [(info[j:j + 1], seeds_for(j)) for j in range(K)]
+        t0 = time.perf_counter()
+        res = pol.execute_many(batches, game=dk.GAME_FULL_DOKO)
+        torch.cuda.synchronize(dev)
+        el = time.perf_counter() - t0
+        kK = eng.last_search_ms()
+        assert np.array_equal(res[0][1].cpu().numpy(), v1.cpu().numpy()), "prod: batched decision 0 differs"
+        for _, v in res:
+            assert bool((v.sum(dim=1) == iters).all().item()), "prod: a root without exactly %d simulations" % iters
+        leg = {"samples": S, "decision_latency_s": lat, "search_kernel_ms_one": k1,
+               "inflight_decisions": K, "inflight_s": el, "search_kernel_ms_inflight": kK,
+               "inflight_decisions_per_s": K / el, "inflight_rollouts_per_s": K * S * iters / el,
+               "one_decision_rollouts_per_s": S * iters / lat}
+        legs.append(leg)
+    hw, cap, overflowed = eng.pool_high_water(sp)
+    result = None
+    if rank == 0:
+        if not args.no_cpu_baseline:
+            sys.path.insert(0, os.path.join(ROOT, "tests"))
+            import ctypes
+
+            import oracle_lib as ol
+            st = ol.FdoState.new_game(0xC3000000)
+            for _ in range(4):
+                st.play(24)
+            rng = ol.arr(ctypes.c_uint64, 4, [int(x) for x in dk.splitmix_rng_states(np.array([0xC3100000], dtype=np.uint64))[0]])
+            st.random_plies(rng, 0, True)
+            for leg in legs:
+                S = leg["samples"]
+                roots = [st.card_matching(ol.rng_seed(0xC3200000 + s)) for s in range(S)]
+                handles = (ctypes.c_void_p * S)(*[r.h for r in roots])
+                vis = (ctypes.c_uint32 * (39 * S))()
+                sd = ol.arr(ctypes.c_uint64, S, [0xC3200000 + 2048 + s for s in range(S)])
+                cores, quota = cpu_quota_cores()
+                thr = min(S, int(np.ceil(quota)) if quota else cores)
+                secs = ol.lib().or_fdo_search_many(None, handles, sd, S, iters, args.c, vis, thr)
+                same = all(list(vis[39 * s:39 * s + 39]) == [int(x) for x in v1_rows[S][s]] for s in range(S)) \
+                    if S in v1_rows else None
+                leg["cpu"] = {"decision_latency_s": secs, "threads": thr, "kind": "port",
+                              "rollouts_per_s": S * iters / secs, "visits_equal_gpu": same}
+                leg["gpu_over_cpu_latency"] = leg["decision_latency_s"] / secs
+        result = {
+            "metric": "determinized decision latency and throughput at the production search shape "
+                      "(S CAP samples x %d UCT iterations, MaxN)" % iters,
+            "value": legs[-1]["inflight_rollouts_per_s"],
+            "unit": "rollouts/s",
+            "n_gpus": world, "steps": 1, "warmup": 0,
+            "ms_per_step": legs[-1]["inflight_s"] * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64+f64",
+            "data": "synthetic: C3-style seeded deals (4x Healthy, k in {0,8,20,32} random plies), CAP samples",
+            "config": {"workload": "prod: S in %s samples x %d iterations; one decision, and %d decisions in flight "
+                                   "(execute_many)" % (Ss, iters, K), "parallelism": "replicas x%d" % world},
+            "legs": legs,
+            "node_pools": {"bytes": eng.pool_bytes(), "slot_capacity": cap, "slot_high_water": hw,
+                           "overflowed_roots": overflowed},
+            "roofline": None,
+            "note": "a root's simulations are sequential (bit-exact reference semantics), so one decision's "
+                    "latency is one GPU lane's sequential speed; throughput comes from decisions in flight",
         }
         print(json.dumps(result))
     if world > 1:

@@ -306,6 +306,19 @@ int dk_search_batch(dk_ctx* ctx, int game, const dk_state* roots, const uint64_t
 int dk_search_batch_async(dk_ctx* ctx, int game, const dk_state* d_roots, const uint64_t* d_seeds, uint32_t n,
                           uint32_t iterations, double c, uint32_t* d_visits, double* d_values, uint8_t* d_best,
                           void* stream);
+/* The same search continuing the caller's SmallRng: CachedMCTS::monte_carlo_tree_search(state, c,
+ * iterations, random: &mut SmallRng) (rs-doko-mcts/src/mcts/mcts.rs:294-315), whose callers thread
+ * one stream through many searches (rs-doko-mcts/src/example/tic_tac_toe_player.rs:9-36 uses one
+ * seed_from_u64(999) stream for every move of 1000 games).  rng_states[4*i .. 4*i+3] is root i's
+ * Xoshiro256++ state (s0..s3); on return it holds the state after the search, which has consumed
+ * exactly what the reference consumes: every expansion's random_single and every rollout, then one
+ * u64 for the final random_bool((1f32/1000f32) as f64) (mcts.rs:231).  A root that fails (DK_E_STATE)
+ * keeps its input state. */
+int dk_search_batch_rng(dk_ctx* ctx, int game, const dk_state* roots, uint64_t* rng_states, uint32_t n,
+                        uint32_t iterations, double c, uint32_t* visits, double* values, uint8_t* best);
+int dk_search_batch_rng_async(dk_ctx* ctx, int game, const dk_state* d_roots, uint64_t* d_rng_states, uint32_t n,
+                              uint32_t iterations, double c, uint32_t* d_visits, double* d_values, uint8_t* d_best,
+                              void* stream);
 
 /* ---- determinization: SamplingFn::sample ------------------------------------
  * out[i*samples + s] = sample(infostates[i], SmallRng::seed_from_u64(seeds[i*samples+s])), by game:
@@ -505,7 +518,9 @@ int dk_net_attn62_bf16_async(const void* qkv, void* y, uint32_t batch, uint32_t 
 
 /* ---- completion / errors / timing of *_async work -------------------------------
  * dk_sync: waits for the stream and returns the first device-side error
- * (DK_E_CAPACITY when a search ran out of child slots) since the last dk_sync.
+ * (DK_E_CAPACITY when a search ran out of child slots) since the last dk_sync, including
+ * errors of search launches on that stream whose slot a later launch reused (more than
+ * eight searches in flight without a dk_sync).
  * dk_last_search_ms: device time of the last search launch (HIP events recorded
  * on the launch stream around the kernel).
  */

@@ -75,6 +75,8 @@ def lib():
         "dk_env_random_plies_batch": (ctypes.c_int, [vp, vp, vp, vp, u32]),
         "dk_search_batch": (ctypes.c_int, [vp, ctypes.c_int, vp, vp, u32, u32, ctypes.c_double, vp, vp, vp]),
         "dk_search_batch_async": (ctypes.c_int, [vp, ctypes.c_int, vp, vp, u32, u32, ctypes.c_double, vp, vp, vp, vp]),
+        "dk_search_batch_rng": (ctypes.c_int, [vp, ctypes.c_int, vp, vp, u32, u32, ctypes.c_double, vp, vp, vp]),
+        "dk_search_batch_rng_async": (ctypes.c_int, [vp, ctypes.c_int, vp, vp, u32, u32, ctypes.c_double, vp, vp, vp, vp]),
         "dk_determinize_batch": (ctypes.c_int, [vp, vp, u32, u32, vp, vp]),
         "dk_determinize_batch_async": (ctypes.c_int, [vp, vp, u32, u32, vp, vp, vp]),
         "dk_fuse": (ctypes.c_int, [vp, vp, u32, u32, vp, ctypes.c_int, vp]),
@@ -126,7 +128,7 @@ EXPORTED = [
     "dk_create", "dk_destroy", "dk_last_error", "dk_status_string", "dk_abi_version", "dk_new_game_batch",
     "dk_new_game_batch_async", "dk_env_allowed_batch", "dk_env_step_batch", "dk_env_rewards_batch",
     "dk_env_rollout_batch", "dk_env_rollout_batch_async", "dk_env_random_plies_batch", "dk_search_batch",
-    "dk_search_batch_async", "dk_determinize_batch", "dk_determinize_batch_async", "dk_fuse",
+    "dk_search_batch_async", "dk_search_batch_rng", "dk_search_batch_rng_async", "dk_determinize_batch", "dk_determinize_batch_async", "dk_fuse",
     "dk_fuse_accumulate_async", "dk_fuse_select_async", "dk_decide_batch", "dk_sync", "dk_last_search_ms", "dk_last_search_waves",
     "dk_pool_bytes", "dk_legal_actions_async", "dk_env_step_batch_async", "dk_env_random_plies_batch_async",
     "dk_az_begin_async", "dk_az_root_async", "dk_az_select_async", "dk_az_backup_async", "dk_az_finish_async",

@@ -5,6 +5,7 @@ Names follow the Rust types they replace:
 * ``Engine``                      — a dk_ctx (device, node/state pools)
 * ``McEnv``                       — McEnvState (rs-doko-mcts/src/env/env_state.rs:7-28), batched
 * ``CachedMCTS``                  — CachedMCTS::monte_carlo_tree_search (mcts.rs:284-315), batched over roots
+* ``SmallRng``                    — rand 0.9 SmallRng state, continued by a search like ``&mut SmallRng``
 * ``card_matching_full``          — CAP determinization (rs-full-doko/src/matching/card_matching.rs:469-497)
 * ``sample_assignment_full``      — rs-doko rule-based determinization (rs-doko-assignment/src/assignment.rs:472-580)
 * ``PolicyFusionMaxN`` / ``PolicyFusionAverageStrategy`` — policy_fusion.rs:18-123
@@ -200,24 +201,145 @@ class McEnv:
         return s, g
 
 
+class SmallRng:
+    """rand 0.9 ``SmallRng`` (Xoshiro256++) held on the host as its four state words.  Passed to
+    ``CachedMCTS.monte_carlo_tree_search`` it is advanced in place, exactly as the reference's
+    ``&mut SmallRng`` is (rs-doko-mcts/src/mcts/mcts.rs:294-315)."""
+
+    def __init__(self, state):
+        self.state = np.array(state, dtype=np.uint64).reshape(4)
+
+    @classmethod
+    def seed_from_u64(cls, seed):
+        return cls(splitmix_rng_states([seed])[0])
+
+    def __eq__(self, other):
+        return isinstance(other, SmallRng) and bool(np.array_equal(self.state, other.state))
+
+    def __repr__(self):
+        return "SmallRng(%s)" % ", ".join("0x%016x" % int(w) for w in self.state)
+
+
 class CachedMCTS:
-    """CachedMCTS::monte_carlo_tree_search for a batch of roots (one independent
-    search per root, SmallRng::seed_from_u64(seed) each)."""
+    """CachedMCTS::monte_carlo_tree_search (mcts.rs:294-315) for a batch of roots, one
+    independent search per root.  `random` is either
+      * u64 seeds [n]: root i searches with SmallRng::seed_from_u64(seeds[i]), or
+      * the caller's generators, continued in place: a SmallRng (one root), a list of them, or a
+        uint64 array [n, 4] of Xoshiro256++ states (dk_search_batch_rng).
+    Returns (visits [n, 39], values [n, 39], best [n]): the Move list by action index and
+    max_by_key(visits) over it (the last maximum), DK_NONE without children."""
 
     def __init__(self, engine, game=GAME_FULL_DOKO):
         self.engine = engine
         self.game = game
 
-    def monte_carlo_tree_search(self, roots, uct_exploration_constant, iterations, seeds):
+    def monte_carlo_tree_search(self, roots, uct_exploration_constant, iterations, random):
         s = _states(roots)
         n = s.shape[0]
-        seeds = np.ascontiguousarray(seeds, dtype=np.uint64)
         visits = np.zeros((n, NUM_ACTIONS), dtype=np.uint32)
         values = np.zeros((n, NUM_ACTIONS), dtype=np.float64)
         best = np.zeros(n, dtype=np.uint8)
-        _check(_native.lib().dk_search_batch(self.engine.ctx, self.game, _ptr(s), _ptr(seeds), n, iterations,
-                                             float(uct_exploration_constant), _ptr(visits), _ptr(values), _ptr(best)))
+        L = _native.lib()
+        c = float(uct_exploration_constant)
+        gens = [random] if isinstance(random, SmallRng) else random
+        if isinstance(gens, (list, tuple)) and gens and isinstance(gens[0], SmallRng):
+            st = np.stack([g.state for g in gens]).astype(np.uint64)
+            if st.shape[0] != n:
+                raise ValueError("need one SmallRng per root")
+            _check(L.dk_search_batch_rng(self.engine.ctx, self.game, _ptr(s), _ptr(st), n, iterations, c,
+                                         _ptr(visits), _ptr(values), _ptr(best)))
+            for g, w in zip(gens, st):
+                g.state[:] = w
+            return visits, values, best
+        arr = np.asarray(random)
+        if arr.ndim == 2:
+            if arr.shape != (n, 4) or arr.dtype != np.uint64 or not arr.flags.c_contiguous:
+                raise ValueError("rng states must be a C-contiguous uint64 array [n, 4]")
+            _check(L.dk_search_batch_rng(self.engine.ctx, self.game, _ptr(s), _ptr(arr), n, iterations, c,
+                                         _ptr(visits), _ptr(values), _ptr(best)))
+            return visits, values, best
+        seeds = np.ascontiguousarray(arr, dtype=np.uint64)
+        if seeds.shape != (n,):
+            raise ValueError("need one seed per root")
+        _check(L.dk_search_batch(self.engine.ctx, self.game, _ptr(s), _ptr(seeds), n, iterations, c,
+                                 _ptr(visits), _ptr(values), _ptr(best)))
         return visits, values, best
+
+
+# ---- tic-tac-toe (config 1: rs-doko-mcts/src/example/tic_tac_toe*.rs) -------------------------
+TTT_NOT_FINISHED, TTT_XWON, TTT_OWON, TTT_DRAW = 0, 1, 2, 3
+_TTT_LINES = ((0, 1, 2), (3, 4, 5), (6, 7, 8), (0, 3, 6), (1, 4, 7), (2, 5, 8), (0, 4, 8), (2, 4, 6))
+
+
+def ttt_state(board=None, last_action=None):
+    """The dk_ttt_state wire record of a TicTacToeState (0 empty, 1 X, 2 O per cell); its
+    finish state is calc_finish_state (tic_tac_toe.rs:29-80)."""
+    b = [0] * 9 if board is None else [int(v) for v in board]
+    rec = np.zeros(STATE_BYTES, dtype=np.uint8)
+    rec[:9] = b
+    fin = TTT_NOT_FINISHED
+    for ln in _TTT_LINES:
+        if all(b[k] == 1 for k in ln):
+            fin = TTT_XWON
+            break
+        if all(b[k] == 2 for k in ln):
+            fin = TTT_OWON
+            break
+    if fin == TTT_NOT_FINISHED and 0 not in b:
+        fin = TTT_DRAW
+    rec[9] = fin
+    rec[10] = 0xFF if last_action is None else int(last_action)
+    rec[STATE_BYTES - 1] = GAME_TTT
+    return rec
+
+
+def tic_tac_toe_player(engine, games, iterations=1400, uct_exploration_constant=2.0, random=None, trace=None):
+    """tic_tac_toe_player (rs-doko-mcts/src/example/tic_tac_toe_player.rs:8-52): `games` games
+    from the empty board, ONE SmallRng (default seed_from_u64(999)) threaded through every
+    search of every game, each move max_by_key(visits) of
+    monte_carlo_tree_search(state, c, iterations, rng).  Every search and every move runs on
+    the GPU (one root per launch: the stream makes the games strictly sequential).  Returns
+    [X won, O won, draws]; `trace` (a list) receives (game, board, visits[39], best, rng state
+    after the search) per move."""
+    rng = SmallRng.seed_from_u64(999) if random is None else random
+    mcts = CachedMCTS(engine, GAME_TTT)
+    env = McEnv(engine)
+    results = [0, 0, 0]
+    for g in range(games):
+        st = ttt_state()[None, :]
+        while st[0, 9] == TTT_NOT_FINISHED:
+            visits, _, best = mcts.monte_carlo_tree_search(st, uct_exploration_constant, iterations, rng)
+            if trace is not None:
+                trace.append((g, st[0, :9].copy(), visits[0].copy(), int(best[0]), rng.state.copy()))
+            st = env.by_action(st, np.array([1 << int(best[0])], dtype=np.uint64))
+        results[int(st[0, 9]) - 1] += 1
+    return results
+
+
+def tic_tac_toe_games(engine, seeds, iterations=1400, uct_exploration_constant=2.0):
+    """Independent tic-tac-toe games in lockstep, game g with its own
+    SmallRng::seed_from_u64(seeds[g]) threaded through its searches: one search launch per
+    move over every unfinished game (the GPU-shaped form of tic_tac_toe_player).  Returns
+    (finish state per game, moves per game, total searches)."""
+    seeds = np.ascontiguousarray(seeds, dtype=np.uint64)
+    n = seeds.shape[0]
+    rng = splitmix_rng_states(seeds)
+    states = np.stack([ttt_state()] * n)
+    mcts = CachedMCTS(engine, GAME_TTT)
+    env = McEnv(engine)
+    moves = np.zeros(n, dtype=np.int32)
+    searches = 0
+    while True:
+        live = np.nonzero(states[:, 9] == TTT_NOT_FINISHED)[0]
+        if live.size == 0:
+            break
+        r = np.ascontiguousarray(rng[live])
+        _, _, best = mcts.monte_carlo_tree_search(states[live], uct_exploration_constant, iterations, r)
+        rng[live] = r
+        states[live] = env.by_action(states[live], np.left_shift(np.uint64(1), best.astype(np.uint64)))
+        moves[live] += 1
+        searches += int(live.size)
+    return states[:, 9].copy(), moves, searches
 
 
 def card_matching_full(engine, infostates, samples, seeds):

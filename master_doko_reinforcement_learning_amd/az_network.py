@@ -95,8 +95,10 @@ class ClassHead(nn.Module):
         """The attention pooling and each class's LayerNorm, class-major [C, B, d]."""
         B, S, d = x.shape
         C = self.queries.shape[0]
+        # the HIP kernel has no backward: inference only, and only on bf16 contiguous operands
         if (x.is_cuda and x.dtype == torch.bfloat16 and S == SEQ and d in (160, 256) and C <= 64
-                and self.queries.dtype == torch.bfloat16):
+                and not torch.is_grad_enabled()
+                and all(p.dtype == torch.bfloat16 and p.is_contiguous() for p in (self.queries, self.ln_w, self.ln_b))):
             from . import _native
             x = x.contiguous()
             ac = torch.empty((C, B, d), dtype=x.dtype, device=x.device)

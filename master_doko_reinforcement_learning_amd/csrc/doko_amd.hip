@@ -192,11 +192,11 @@ __global__ void __launch_bounds__(WAVE, H::MIN_WAVES) search_kernel(const dk_sta
                                                       const uint32_t* __restrict__ order, uint32_t* retry,
                                                       const uint32_t* __restrict__ list, uint32_t* high_water,
                                                       const uint32_t* __restrict__ perm, uint32_t lane_base,
-                                                      uint64_t* wave_clock) {
+                                                      uint64_t* wave_clock, uint64_t* rng_io) {
     const uint32_t lane = threadIdx.x;
-    // per-wave start / end of the realtime counter (100 MHz), one entry per 16 pool lanes
-    // (dk_last_search_waves): how long each wave had work before the group queue drained
-    const uint32_t clock_idx = (lane_base + blockIdx.x * rpw) / 16u;
+    // per-wave start / end of the realtime counter (100 MHz), indexed by the wave's first pool
+    // lane (dk_last_search_waves): how long each wave had work before the group queue drained
+    const uint32_t clock_idx = lane_base + blockIdx.x * rpw;
     if (wave_clock && lane == 0) wave_clock[2 * clock_idx] = __builtin_amdgcn_s_memrealtime();
     const uint32_t T = iters + 1;
     const uint32_t n_ln = LN_LDS ? T : 0u;
@@ -224,7 +224,10 @@ __global__ void __launch_bounds__(WAVE, H::MIN_WAVES) search_kernel(const dk_sta
         const uint32_t root = list ? list[1 + idx] : perm ? perm[idx] : idx;   // perm: depth-sorted order
         typename E::Work w;
         E::load(roots[root], w);
-        dk::Rng rng = dk::Rng::seed_from_u64(seeds[root]);
+        // rng_io: the caller's SmallRng states, continued (dk_search_batch_rng_async); else seeded
+        dk::Rng rng = rng_io ? dk::Rng{rng_io[4 * (size_t)root], rng_io[4 * (size_t)root + 1], rng_io[4 * (size_t)root + 2],
+                                       rng_io[4 * (size_t)root + 3]}
+                             : dk::Rng::seed_from_u64(seeds[root]);
         GpuMem<typename E::Node, LN_LDS, H> mem;
         // wave bases (uniform) + lane offsets: pool lane = lane_base + blockIdx.x * rpw + lane (a launch
         // owns the lanes [lane_base, lane_base + grid * rpw) of the pools, dk_ctx::Slot)
@@ -261,6 +264,12 @@ __global__ void __launch_bounds__(WAVE, H::MIN_WAVES) search_kernel(const dk_sta
             }
         } else {
             hw = used[0] > hw ? used[0] : hw;
+            // the advanced stream goes back only for a completed search: a root that ran out
+            // of slots is searched again by the fallback pass from the caller's state
+            if (rng_io) {
+                rng_io[4 * (size_t)root] = rng.s0; rng_io[4 * (size_t)root + 1] = rng.s1;
+                rng_io[4 * (size_t)root + 2] = rng.s2; rng_io[4 * (size_t)root + 3] = rng.s3;
+            }
         }
         best[root] = b;
     }
@@ -803,6 +812,16 @@ struct dk_ctx {
     };
     static constexpr int MAX_INFLIGHT = 8;
     std::vector<Slot> slots;
+    // The latest launch on each fixed region of REGION_LANES pool lanes (a slot index, -1 =
+    // none).  A launch waits for every region it covers, so an earlier launch that still runs
+    // on those lanes is waited for even after its slot has been reused for other lanes: a
+    // slot's latest launch is ordered after all of its earlier ones (same stream, or the
+    // reuse waited for them), so waiting on its `done` covers them.
+    static constexpr uint32_t REGION_LANES = 1024;
+    std::vector<int> region_slot;
+    // Errors of search launches folded in when their slot was reused before dk_sync collected
+    // them (more than MAX_INFLIGHT launches in flight), per stream; dk_sync(stream) reports them.
+    std::vector<std::pair<hipStream_t, int>> stream_err;
     int* slot_err = nullptr;        // [MAX_INFLIGHT] error flags of the search launches
     uint32_t next_slot = 0, lane_cursor = 0;
     int last_slot = -1;             // the latest launch (dk_last_search_ms)
@@ -847,7 +866,7 @@ struct dk_ctx {
     bool lds_path_fixed = false;    // DK_LDS_PATH (1..MAX_PATH) fixes it
     bool verbose = false;           // DK_VERBOSE=1: one stderr line per search launch (shape, residency)
     uint64_t* prof = nullptr;       // phase timers (DK_PHASE_PROF builds only)
-    uint64_t* wave_clock = nullptr; // [pool_roots / 16][2] realtime-counter start / end of the search waves
+    uint64_t* wave_clock = nullptr; // [pool_roots][2] realtime-counter start / end of the search waves (by first lane)
     // AlphaZero PUCT search (dk_az_*): per-game node / state regions, allocated on first use
     dk::az::Node* az_nodes = nullptr;
     dk_az_state* az_states = nullptr;
@@ -870,6 +889,7 @@ struct dk_ctx {
 namespace {
 
 constexpr size_t FALLBACK_ROOTS = 64 * 64;   // roots the fallback pool holds at once
+constexpr size_t FALLBACK_BYTES = 16ull << 30; // ... within this many bytes (at least one 64-root region)
 
 // node-state records (adapters.h Node: 64 B for both card games)
 constexpr size_t STATE_SLOT_BYTES =
@@ -901,6 +921,14 @@ int finish(dk_ctx* ctx, hipStream_t st) {
     (void)hipMemset(ctx->err, 0, sizeof(int));
     {
         std::lock_guard<std::mutex> g(ctx->slot_mu);
+        for (size_t i = 0; i < ctx->stream_err.size();) {
+            if (ctx->stream_err[i].first == st) {
+                flag |= ctx->stream_err[i].second;
+                ctx->stream_err.erase(ctx->stream_err.begin() + (long)i);
+            } else {
+                ++i;
+            }
+        }
         int se[dk_ctx::MAX_INFLIGHT];
         bool any = false;
         for (const dk_ctx::Slot& sl : ctx->slots) any |= sl.pending && sl.stream == st;
@@ -936,7 +964,7 @@ uint32_t launch_rpw(const dk_ctx* ctx, uint32_t n) {
 template <class E, bool LN, class H>
 hipError_t launch_search_t(dk_ctx* ctx, const dk_state* roots, const uint64_t* seeds, uint32_t n, uint32_t iters,
                            double c, uint32_t* visits, double* values, uint8_t* best, hipStream_t st,
-                           size_t ln_bytes, uint32_t rpw, dk_ctx::Slot& sl, int* err) {
+                           size_t ln_bytes, uint32_t rpw, dk_ctx::Slot& sl, int* err, uint64_t* rng_io) {
     const auto kern = search_kernel<E, LN, H>;
     // LDS per path entry and lane: slot word + stats (8-B records: their 32-bit stats word)
     constexpr size_t PATH_ENTRY_BYTES = dk::is_p8<H>::value ? 8 : 12;
@@ -972,9 +1000,17 @@ hipError_t launch_search_t(dk_ctx* ctx, const dk_state* roots, const uint64_t* s
     const uint32_t base = ctx->lane_cursor;
     ctx->lane_cursor += lanes;
     hipError_t e = hipSuccess;
-    for (const dk_ctx::Slot& o : ctx->slots)
-        if (&o != &sl && o.used && o.lane_base < base + lanes && base < o.lane_base + o.lanes && o.stream != st)
-            if ((e = hipStreamWaitEvent(st, o.done, 0)) != hipSuccess) return e;
+    const int self = (int)(&sl - ctx->slots.data());
+    const uint32_t r0 = base / dk_ctx::REGION_LANES, r1 = (base + lanes - 1) / dk_ctx::REGION_LANES;
+    uint32_t waited = 0;   // slots already waited for
+    for (uint32_t r = r0; r <= r1; ++r) {
+        const int k = ctx->region_slot[r];
+        if (k < 0 || k == self || ((waited >> k) & 1u)) continue;
+        const dk_ctx::Slot& o = ctx->slots[k];
+        waited |= 1u << k;
+        if (o.used && o.stream != st && (e = hipStreamWaitEvent(st, o.done, 0)) != hipSuccess) return e;
+    }
+    for (uint32_t r = r0; r <= r1; ++r) ctx->region_slot[r] = self;
     sl.lane_base = base;
     sl.lanes = lanes;
     if (ctx->verbose)
@@ -1012,10 +1048,10 @@ hipError_t launch_search_t(dk_ctx* ctx, const dk_state* roots, const uint64_t* s
                        rpw, lp, visits, values, best, err, sl.queue, ctx->prof,
                        ordered ? (const uint32_t*)sl.order : (const uint32_t*)nullptr,
                        fallback ? sl.retry : (uint32_t*)nullptr, (const uint32_t*)nullptr, ctx->high_water, perm, base,
-                       ctx->wave_clock);
-    sl.clock_first = base / 16u;
+                       ctx->wave_clock, rng_io);
+    sl.clock_first = base;
     sl.clock_n = grid;
-    sl.clock_stride = rpw / 16u;
+    sl.clock_stride = rpw;
     e = hipGetLastError();
     if (e != hipSuccess || !fallback) return e;
     // the fallback pool is shared by all launches: one fallback pass at a time
@@ -1028,7 +1064,7 @@ hipError_t launch_search_t(dk_ctx* ctx, const dk_state* roots, const uint64_t* s
                        ctx->fb_hot, ctx->fb_cold, (typename E::Node*)ctx->fb_states, ctx->fb_ovf, ctx->fb_ovf_st,
                        ctx->fb_slots, ctx->state_stride, rpw, lp, visits, values, best, err, sl.queue_fb, ctx->prof,
                        (const uint32_t*)nullptr, (uint32_t*)nullptr, (const uint32_t*)sl.retry, ctx->high_water + 2,
-                       (const uint32_t*)nullptr, 0u, (uint64_t*)nullptr);
+                       (const uint32_t*)nullptr, 0u, (uint64_t*)nullptr, rng_io);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if ((e = hipEventRecord(ctx->fb_done, st)) != hipSuccess) return e;
     ctx->fb_used = true;
@@ -1038,7 +1074,7 @@ hipError_t launch_search_t(dk_ctx* ctx, const dk_state* roots, const uint64_t* s
 template <class E>
 hipError_t launch_search(dk_ctx* ctx, const dk_state* roots, const uint64_t* seeds, uint32_t n, uint32_t iters,
                          double c, uint32_t* visits, double* values, uint8_t* best, hipStream_t st, dk_ctx::Slot& sl,
-                         int* err) {
+                         int* err, uint64_t* rng_io) {
     const bool ln = iters + 1 <= LN_LDS_MAX && ctx->ln_in_lds;
     const uint32_t rpw = launch_rpw(ctx, n);
     const size_t ln_bytes = ln ? (size_t)((iters + 2) & ~1u) * 8 : 0;
@@ -1051,15 +1087,15 @@ hipError_t launch_search(dk_ctx* ctx, const dk_state* roots, const uint64_t* see
     // 8-B records where their fields hold the search (visits, state index, slots: P8_MAX_ITERS)
     const bool h8 = h16 && iters <= dk::P8_MAX_ITERS && ctx->hot_layout != 16 && ctx->p8_ok;
     if (ctx->wide)   // per-wave pool regions of >= 4 GiB: 64-bit offsets (never with ln in LDS: iterations > 2047)
-        return launch_search_t<E, false, dk::NodeHot32W>(ctx, roots, seeds, n, iters, c, visits, values, best, st, 0, rpw, sl, err);
+        return launch_search_t<E, false, dk::NodeHot32W>(ctx, roots, seeds, n, iters, c, visits, values, best, st, 0, rpw, sl, err, rng_io);
     if (h8)
-        return ln ? launch_search_t<E, true, dk::NodeHot8>(ctx, roots, seeds, n, iters, c, visits, values, best, st, ln_bytes, rpw, sl, err)
-                  : launch_search_t<E, false, dk::NodeHot8>(ctx, roots, seeds, n, iters, c, visits, values, best, st, ln_bytes, rpw, sl, err);
+        return ln ? launch_search_t<E, true, dk::NodeHot8>(ctx, roots, seeds, n, iters, c, visits, values, best, st, ln_bytes, rpw, sl, err, rng_io)
+                  : launch_search_t<E, false, dk::NodeHot8>(ctx, roots, seeds, n, iters, c, visits, values, best, st, ln_bytes, rpw, sl, err, rng_io);
     if (h16)
-        return ln ? launch_search_t<E, true, dk::NodeHot16>(ctx, roots, seeds, n, iters, c, visits, values, best, st, ln_bytes, rpw, sl, err)
-                  : launch_search_t<E, false, dk::NodeHot16>(ctx, roots, seeds, n, iters, c, visits, values, best, st, ln_bytes, rpw, sl, err);
-    return ln ? launch_search_t<E, true, dk::NodeHot32>(ctx, roots, seeds, n, iters, c, visits, values, best, st, ln_bytes, rpw, sl, err)
-              : launch_search_t<E, false, dk::NodeHot32>(ctx, roots, seeds, n, iters, c, visits, values, best, st, ln_bytes, rpw, sl, err);
+        return ln ? launch_search_t<E, true, dk::NodeHot16>(ctx, roots, seeds, n, iters, c, visits, values, best, st, ln_bytes, rpw, sl, err, rng_io)
+                  : launch_search_t<E, false, dk::NodeHot16>(ctx, roots, seeds, n, iters, c, visits, values, best, st, ln_bytes, rpw, sl, err, rng_io);
+    return ln ? launch_search_t<E, true, dk::NodeHot32>(ctx, roots, seeds, n, iters, c, visits, values, best, st, ln_bytes, rpw, sl, err, rng_io)
+              : launch_search_t<E, false, dk::NodeHot32>(ctx, roots, seeds, n, iters, c, visits, values, best, st, ln_bytes, rpw, sl, err, rng_io);
 }
 
 }  // namespace
@@ -1179,11 +1215,17 @@ dk_ctx* dk_create(const dk_config* cfg) {
     ok = ok && hipMalloc(&ctx->err, sizeof(int)) == hipSuccess;
     ok = ok && hipMalloc(&ctx->high_water, 4 * sizeof(uint32_t)) == hipSuccess;
     ok = ok && hipMemset(ctx->high_water, 0, 4 * sizeof(uint32_t)) == hipSuccess;
-    ok = ok && hipMalloc(&ctx->wave_clock, (R / 16 + 1) * 2 * sizeof(uint64_t)) == hipSuccess;
+    ok = ok && hipMalloc(&ctx->wave_clock, (R + 1) * 2 * sizeof(uint64_t)) == hipSuccess;
+    ctx->region_slot.assign((R + dk_ctx::REGION_LANES - 1) / dk_ctx::REGION_LANES, -1);
     if (ok && with_fallback) {
         // 64 waves of 64 roots (fewer when the context is smaller): overflow is rare, and the
         // pass only has to finish the few roots that need it
-        const size_t FR = R < FALLBACK_ROOTS ? R : FALLBACK_ROOTS, FS = proven;
+        // (long searches: at most FALLBACK_BYTES, in whole 64-root regions; 64 roots at 200,000
+        // iterations are 8 GB)
+        const size_t FS = proven, per_root = FS * (sizeof(dk::NodeHot32) + sizeof(dk::NodeCold)) + ST * STATE_SLOT_BYTES;
+        size_t FR = R < FALLBACK_ROOTS ? R : FALLBACK_ROOTS;
+        const size_t by_bytes = std::max<size_t>(64, FALLBACK_BYTES / per_root / 64 * 64);
+        FR = FR < by_bytes ? FR : by_bytes;
         ctx->fb_roots = (uint32_t)FR;
         ctx->fb_slots = proven;
         ok = hipMalloc(&ctx->fb_hot, FR * FS * sizeof(dk::NodeHot32)) == hipSuccess;
@@ -1458,9 +1500,10 @@ int dk_env_random_plies_batch(dk_ctx* ctx, dk_state* states, uint64_t* rng_state
 }
 
 // ---------------------------------------------------------------- search
-int dk_search_batch_async(dk_ctx* ctx, int game, const dk_state* d_roots, const uint64_t* d_seeds, uint32_t n,
-                          uint32_t iterations, double c, uint32_t* d_visits, double* d_values, uint8_t* d_best,
-                          void* stream) {
+namespace {
+// One search launch on `stream` (seeded from d_seeds, or continuing the states d_rng in place).
+int search_async(dk_ctx* ctx, int game, const dk_state* d_roots, const uint64_t* d_seeds, uint64_t* d_rng, uint32_t n,
+                 uint32_t iterations, double c, uint32_t* d_visits, double* d_values, uint8_t* d_best, void* stream) {
     if (!ctx) return DK_E_INVALID;
     if (n > ctx->max_roots || iterations > ctx->max_iters) return ctx->last_error = DK_E_CAPACITY;
     if (n == 0 || iterations == 0) return DK_E_INVALID;
@@ -1470,15 +1513,25 @@ int dk_search_batch_async(dk_ctx* ctx, int game, const dk_state* d_roots, const 
     // the next slot, round-robin; its previous launch must be done before its lists are reused
     const int k = (int)(ctx->next_slot++ % dk_ctx::MAX_INFLIGHT);
     dk_ctx::Slot& sl = ctx->slots[k];
-    if (sl.used && sl.stream != st) DK_HIP(hipStreamWaitEvent(st, sl.done, 0));
     int* err = ctx->slot_err + k;
+    if (sl.used && sl.pending) {
+        // More than MAX_INFLIGHT launches since the previous user's stream was synchronised:
+        // wait for that launch and keep its error flag for dk_sync of its stream before the
+        // flag is cleared for this launch.
+        int f = 0;
+        DK_HIP(hipEventSynchronize(sl.done));
+        DK_HIP(hipMemcpy(&f, err, sizeof(int), hipMemcpyDeviceToHost));
+        if (f) ctx->stream_err.emplace_back(sl.stream, f);
+        sl.pending = false;
+    }
+    if (sl.used && sl.stream != st) DK_HIP(hipStreamWaitEvent(st, sl.done, 0));
     DK_HIP(hipMemsetAsync(err, 0, sizeof(int), st));
     DK_HIP(hipEventRecord(sl.ev0, st));
     hipError_t e;
     switch (game) {
-        case DK_GAME_FULL_DOKO: e = launch_search<dk::FdoE>(ctx, d_roots, d_seeds, n, iterations, c, d_visits, d_values, d_best, st, sl, err); break;
-        case DK_GAME_DOKO: e = launch_search<dk::DoE>(ctx, d_roots, d_seeds, n, iterations, c, d_visits, d_values, d_best, st, sl, err); break;
-        default: e = launch_search<dk::TttE>(ctx, d_roots, d_seeds, n, iterations, c, d_visits, d_values, d_best, st, sl, err); break;
+        case DK_GAME_FULL_DOKO: e = launch_search<dk::FdoE>(ctx, d_roots, d_seeds, n, iterations, c, d_visits, d_values, d_best, st, sl, err, d_rng); break;
+        case DK_GAME_DOKO: e = launch_search<dk::DoE>(ctx, d_roots, d_seeds, n, iterations, c, d_visits, d_values, d_best, st, sl, err, d_rng); break;
+        default: e = launch_search<dk::TttE>(ctx, d_roots, d_seeds, n, iterations, c, d_visits, d_values, d_best, st, sl, err, d_rng); break;
     }
     if (e != hipSuccess) { fprintf(stderr, "doko_amd: search launch: %s\n", hipGetErrorString(e)); return DK_E_LAUNCH; }
     DK_HIP(hipEventRecord(sl.ev1, st));
@@ -1490,25 +1543,57 @@ int dk_search_batch_async(dk_ctx* ctx, int game, const dk_state* d_roots, const 
     return DK_OK;
 }
 
-int dk_search_batch(dk_ctx* ctx, int game, const dk_state* roots, const uint64_t* seeds, uint32_t n, uint32_t iterations,
-                    double c, uint32_t* visits, double* values, uint8_t* best) {
-    if (!ctx || !roots || !seeds || !visits || !values || !best) return DK_E_INVALID;
+// Host-pointer search: seeds (d_seeds) or caller states (rng_states, copied in and back out).
+int search_host(dk_ctx* ctx, int game, const dk_state* roots, const uint64_t* seeds, uint64_t* rng_states, uint32_t n,
+                uint32_t iterations, double c, uint32_t* visits, double* values, uint8_t* best) {
     std::lock_guard<std::mutex> g(ctx->mu);
     if (n > ctx->max_roots || iterations > ctx->max_iters) return ctx->last_error = DK_E_CAPACITY;
+    const size_t words = rng_states ? 4 : 1;
     dk_state* d_r = (dk_state*)scratch(ctx, 0, n * sizeof(dk_state));
-    uint64_t* d_s = (uint64_t*)scratch(ctx, 1, n * sizeof(uint64_t));
+    uint64_t* d_s = (uint64_t*)scratch(ctx, 1, words * n * sizeof(uint64_t));
     uint32_t* d_v = (uint32_t*)scratch(ctx, 2, (size_t)n * 39 * sizeof(uint32_t));
     double* d_val = (double*)scratch(ctx, 3, (size_t)n * 39 * sizeof(double));
     uint8_t* d_b = (uint8_t*)scratch(ctx, 4, n);
     if (!d_r || !d_s || !d_v || !d_val || !d_b) return DK_E_CAPACITY;
     DK_HIP(hipMemcpyAsync(d_r, roots, n * sizeof(dk_state), hipMemcpyHostToDevice, ctx->stream));
-    DK_HIP(hipMemcpyAsync(d_s, seeds, n * sizeof(uint64_t), hipMemcpyHostToDevice, ctx->stream));
-    int rc = dk_search_batch_async(ctx, game, d_r, d_s, n, iterations, c, d_v, d_val, d_b, ctx->stream);
+    DK_HIP(hipMemcpyAsync(d_s, rng_states ? (const uint64_t*)rng_states : seeds, words * n * sizeof(uint64_t),
+                          hipMemcpyHostToDevice, ctx->stream));
+    int rc = search_async(ctx, game, d_r, rng_states ? nullptr : d_s, rng_states ? d_s : nullptr, n, iterations, c, d_v,
+                          d_val, d_b, ctx->stream);
     if (rc) return rc;
     DK_HIP(hipMemcpyAsync(visits, d_v, (size_t)n * 39 * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
     DK_HIP(hipMemcpyAsync(values, d_val, (size_t)n * 39 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
     DK_HIP(hipMemcpyAsync(best, d_b, n, hipMemcpyDeviceToHost, ctx->stream));
+    if (rng_states)
+        DK_HIP(hipMemcpyAsync(rng_states, d_s, 4 * (size_t)n * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream));
     return finish(ctx, ctx->stream);
+}
+}  // namespace
+
+int dk_search_batch_async(dk_ctx* ctx, int game, const dk_state* d_roots, const uint64_t* d_seeds, uint32_t n,
+                          uint32_t iterations, double c, uint32_t* d_visits, double* d_values, uint8_t* d_best,
+                          void* stream) {
+    if (!d_seeds) return DK_E_INVALID;
+    return search_async(ctx, game, d_roots, d_seeds, nullptr, n, iterations, c, d_visits, d_values, d_best, stream);
+}
+
+int dk_search_batch_rng_async(dk_ctx* ctx, int game, const dk_state* d_roots, uint64_t* d_rng_states, uint32_t n,
+                              uint32_t iterations, double c, uint32_t* d_visits, double* d_values, uint8_t* d_best,
+                              void* stream) {
+    if (!d_rng_states) return DK_E_INVALID;
+    return search_async(ctx, game, d_roots, nullptr, d_rng_states, n, iterations, c, d_visits, d_values, d_best, stream);
+}
+
+int dk_search_batch(dk_ctx* ctx, int game, const dk_state* roots, const uint64_t* seeds, uint32_t n, uint32_t iterations,
+                    double c, uint32_t* visits, double* values, uint8_t* best) {
+    if (!ctx || !roots || !seeds || !visits || !values || !best) return DK_E_INVALID;
+    return search_host(ctx, game, roots, seeds, nullptr, n, iterations, c, visits, values, best);
+}
+
+int dk_search_batch_rng(dk_ctx* ctx, int game, const dk_state* roots, uint64_t* rng_states, uint32_t n, uint32_t iterations,
+                        double c, uint32_t* visits, double* values, uint8_t* best) {
+    if (!ctx || !roots || !rng_states || !visits || !values || !best) return DK_E_INVALID;
+    return search_host(ctx, game, roots, nullptr, rng_states, n, iterations, c, visits, values, best);
 }
 
 // ---------------------------------------------------------------- determinization

@@ -113,3 +113,82 @@ def test_full_pool_and_small_batches_concurrently():
             assert np.array_equal(v.cpu().numpy(), r)
     finally:
         eng.close()
+
+
+def test_error_of_reused_slot_reaches_dk_sync():
+    """A malformed root on stream A (DK_E_STATE), then nine more launches on stream B before
+    anyone syncs: the ninth reuses A's slot.  dk_sync(B) is clean and dk_sync(A) still
+    reports A's error (it is folded into A's pending errors when the slot is reused)."""
+    import torch
+
+    import master_doko_reinforcement_learning_amd as dk
+    dev = torch.device("cuda", 0)
+    L = dk._native.lib()
+    eng = dk.Engine(device=0, max_roots=1024, max_iterations=ITERS)
+    try:
+        s = ol.DoState.new_game(0xBAD)
+        for _ in range(4):
+            s.play(24)
+        good = np.frombuffer(s.pack(), dtype=np.uint8).copy()
+        bad = good.copy()
+        bad[7] |= 0x01                                   # hand 0, bit 56: DK_E_STATE
+        a, b = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+        n = 64
+        keep = []
+
+        def launch(stream, root):
+            roots = torch.tensor(np.tile(root, (n, 1)), device=dev)
+            seeds = torch.arange(n, dtype=torch.int64, device=dev)
+            vis = torch.empty((n, 39), dtype=torch.int32, device=dev)
+            val = torch.empty((n, 39), dtype=torch.float64, device=dev)
+            best = torch.empty(n, dtype=torch.uint8, device=dev)
+            keep.append((roots, seeds, vis, val, best))
+            return L.dk_search_batch_async(eng.ctx, dk.GAME_DOKO, roots.data_ptr(), seeds.data_ptr(), n, 50, 2.5,
+                                           vis.data_ptr(), val.data_ptr(), best.data_ptr(), stream.cuda_stream)
+
+        torch.cuda.synchronize(dev)
+        assert launch(a, bad) == 0
+        for _ in range(9):
+            assert launch(b, good) == 0
+        assert L.dk_sync(eng.ctx, b.cuda_stream) == 0
+        assert L.dk_sync(eng.ctx, a.cuda_stream) == -3      # DK_E_STATE
+        assert L.dk_sync(eng.ctx, a.cuda_stream) == 0       # reported once
+        torch.cuda.synchronize(dev)
+        for _, _, vis, _, _ in keep[1:]:
+            assert bool((vis.sum(dim=1) == 50).all())
+    finally:
+        eng.close()
+
+
+def test_reused_slot_lane_regions():
+    """The lane-overlap pattern of a reused slot: X fills 60 % of the pool lanes on stream A,
+    seven small launches take the other slots, X's slot is reused on stream A for the last
+    lanes, and a launch on stream B wraps round to lanes X may still be using.  Its wait must
+    come from the lane regions X covered, not from the slot's latest lane range.  Every
+    result equals the same batch decided alone."""
+    import torch
+
+    import master_doko_reinforcement_learning_amd as dk
+    dev = torch.device("cuda", 0)
+    S = 16
+    eng = dk.Engine(device=0, max_roots=65536, max_iterations=ITERS)
+    try:
+        pol = dk.DefaultImpiPolicy(eng, 2.5, ITERS, S, dk.FUSE_MAXN)
+        sizes = [2456] + [205] * 7 + [205, 1229]           # infostates x 16 samples per launch
+        batches = [_batches(torch, dev, 1, k, S)[1][0] for k in sizes]
+        ref = [v.cpu().numpy() for _, v in pol.execute_many(batches, game=dk.GAME_FULL_DOKO, streams=1)]
+        a, b = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+        order = [a] + [b] * 7 + [a, b]
+        res = []
+        torch.cuda.synchronize(dev)
+        for st, bt in zip(order, batches):
+            with torch.cuda.stream(st):
+                res.append(pol.execute_async(*bt, game=dk.GAME_FULL_DOKO))
+        L = dk._native.lib()
+        for st in (a, b):
+            assert L.dk_sync(eng.ctx, st.cuda_stream) == 0
+        torch.cuda.synchronize(dev)
+        for (_, v), r in zip(res, ref):
+            assert np.array_equal(v.cpu().numpy(), r)
+    finally:
+        eng.close()

@@ -749,3 +749,28 @@ def test_search_record_width_limits(iters, env, hot, monkeypatch, capfd):
             assert int(best[i]) == (b if b >= 0 else 255), i
     finally:
         e.close()
+
+
+@pytest.mark.parametrize("iters,n", [(12000, 6), (50000, 2), (200000, 1)])
+def test_search_parity_production_shape(iters, n):
+    """Searches of the thesis's production length (run.rs:270-291 runs 200,000 iterations per
+    sample; its grid goes to 2,000,000, run.rs:107-118): 32-B records with cached means
+    (iterations > 4095), deep LDS-path overflow, and at 200,000 iterations 64-bit pool offsets
+    (a wave's fallback region passes 4 GiB).  Visits, values (bitwise) and the best move
+    equal the oracle's."""
+    import master_doko_reinforcement_learning_amd as dk
+    pool = [s for s in fdo_states(8, 53) if s.info()["phase"] != 3 and s.info()["card_index"] < 24]
+    rng = np.random.default_rng(iters)
+    pick = [pool[i] for i in rng.choice(len(pool), size=n, replace=False)]
+    seeds = rng.integers(0, 2**63, size=n, dtype=np.uint64)
+    e = dk.Engine(device=0, max_roots=64, max_iterations=iters, slot_capacity=64 + 4 * iters)
+    try:
+        visits, values, best = dk.CachedMCTS(e, dk.GAME_FULL_DOKO).monte_carlo_tree_search(pack_all(pick), 2.5, iters, seeds)
+        _, _, overflowed = e.pool_high_water()
+    finally:
+        e.close()
+    for i, (b, v, val) in enumerate(_oracle_search(pick, seeds, iters, 2.5, "fdo")):
+        assert list(visits[i]) == v, i
+        assert values[i].tobytes() == np.array(val, dtype=np.float64).tobytes(), i
+        assert int(best[i]) == b, i
+    assert overflowed == 0
