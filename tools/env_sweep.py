@@ -31,6 +31,9 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--samples", type=int, default=64, help="samples per infostate (8 = one rank's share at N = 8)")
     ap.add_argument("--no-check", action="store_true", help="speed-of-light variants: results may differ")
+    ap.add_argument("--workload", choices=["c3", "c2"], default="c3",
+                    help="c2: bench.py's C2 roots (rs-doko deals after 4x Healthy), --roots of them")
+    ap.add_argument("--roots", type=int, default=32768)
     a = ap.parse_args()
     import torch
     import master_doko_reinforcement_learning_amd as dk
@@ -49,8 +52,23 @@ def main():
     torch.cuda.set_stream(stream)
     sp = stream.cuda_stream
     I, S, iters = a.infostates, a.samples, 1000
-    n = I * S
-    roots, d_srch = c3_roots(dk, L, dev, sp, I, S)
+    game = 0
+    if a.workload == "c2":
+        n, game = a.roots, 1
+        gen = dk.Engine(device=0, max_roots=n, max_iterations=1, slot_capacity=64)
+        gidx = np.arange(n, dtype=np.uint64)
+        d_rs = torch.tensor((gidx + np.uint64(0xD0C00000)).view(np.int64), device=dev)
+        roots = torch.zeros((n, 128), dtype=torch.uint8, device=dev)
+        assert L.dk_new_game_batch_async(gen.ctx, 1, d_rs.data_ptr(), n, roots.data_ptr(), sp) == 0
+        h = torch.full((n,), 1 << 24, dtype=torch.int64, device=dev)
+        for _ in range(4):
+            assert L.dk_env_step_batch_async(gen.ctx, roots.data_ptr(), h.data_ptr(), n, sp) == 0
+        assert L.dk_sync(gen.ctx, sp) == 0
+        gen.close()
+        d_srch = torch.tensor((gidx * np.uint64(0x9E3779B97F4A7C15) + np.uint64(1)).view(np.int64), device=dev)
+    else:
+        n = I * S
+        roots, d_srch = c3_roots(dk, L, dev, sp, I, S)
     v = torch.zeros((n, 39), dtype=torch.int32, device=dev)
     q = torch.zeros((n, 39), dtype=torch.float64, device=dev)
     bst = torch.zeros(n, dtype=torch.uint8, device=dev)
@@ -72,7 +90,7 @@ def main():
                     os.environ[key] = val
             got = []
             for r in range(a.reps):
-                assert Lk.dk_search_batch_async(ctx, 0, roots.data_ptr(), d_srch.data_ptr(), n, iters, 2.5,
+                assert Lk.dk_search_batch_async(ctx, game, roots.data_ptr(), d_srch.data_ptr(), n, iters, 2.5,
                                                 v.data_ptr(), q.data_ptr(), bst.data_ptr(), sp) == 0
                 assert Lk.dk_sync(ctx, sp) == 0
                 ms = ctypes.c_float()
