@@ -56,6 +56,11 @@ def parse():
     p.add_argument("--games", type=int, default=8192, help="concurrent self-play games per GPU (c5)")
     p.add_argument("--az-iterations", type=int, default=200, help="PUCT iterations per move (c5)")
     p.add_argument("--ar-samples", type=int, default=4, help="AR samples per infostate (impi)")
+    p.add_argument("--net-precision", choices=["bf16", "f32"], default="bf16",
+                   help="c5 / impi / impid network: bf16 = the fused bf16 HIP kernels (default); f32 = the reference's "
+                        "precision: f32 activations, torch.set_float32_matmul_precision('medium') and allow_tf32 as "
+                        "az_doko.py:539-541 / main.py:508 set them (hipBLASLt then computes the f32 GEMMs from bf16 "
+                        "products, ~5e-6 relative error: profiles/r04/fp32_gemm_probe.json)")
     p.add_argument("--ar-temperature", type=float, default=0.4, help="AR sampling temperature (impi; all_policies.rs:30)")
     p.add_argument("--iterations", type=int, default=1000)
     p.add_argument("--infostates", type=int, default=None,
@@ -554,6 +559,18 @@ def az_flop_per_eval(d=160, seq=62, blocks=6, classes=43):
     return blocks * (26 * seq * d * d + 4 * seq * seq * d) + 4 * classes * seq * d + 2 * classes * d * d + 2 * classes * d
 
 
+def net_precision(args, torch):
+    """(torch dtype, dtype label, matrix peak TFLOP/s, note) of the network precision."""
+    if args.net_precision == "f32":
+        # the reference's settings (az_doko.py:539-541, main.py:402/508)
+        torch.set_float32_matmul_precision("medium")
+        torch.backends.cuda.matmul.allow_tf32 = True
+        return (torch.float32, "f32 network (reference precision: f32 activations, matmul precision 'medium')", 2500.0 / 3,
+                "f32 activations; hipBLASLt computes the f32 GEMMs of precision 'medium' from bf16 products "
+                "(max relative error ~5e-6 against f64, profiles/r04/fp32_gemm_probe.json): peak = bf16 dense / 3")
+    return torch.bfloat16, "bf16 network", 2500.0, "bf16 dense peak"
+
+
 def run_c5(args, dk, L, dev, stream, rank, world, local_rank, dist):
     """Config 5: AlphaZero self-play.  One step = one move decision of every concurrent
     game: root evaluation, `az_iterations` x (PUCT select on the GPU -> encode_state_pi on
@@ -590,7 +607,8 @@ def run_c5(args, dk, L, dev, stream, rank, world, local_rank, dist):
             ev_time.append((e0, e1))
             return out
 
-    evaluator = TimedEval(eng, net)
+    ndt, nlabel, npeak, nnote = net_precision(args, torch)
+    evaluator = TimedEval(eng, net, dtype=ndt)
     search = dk.AlphaZeroSearch(eng, 4.0, 0.3, 10, 0.5)
     dirichlet = torch.distributions.Dirichlet(torch.full((39,), 0.8, device=dev))
     next_seed = [int(seeds[-1]) + 1]
@@ -648,7 +666,7 @@ def run_c5(args, dk, L, dev, stream, rank, world, local_rank, dist):
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16 network, f32 tree statistics",
+            "dtype": nlabel + ", f32 tree statistics",
             "data": "synthetic: seeded full-doko deals, random-initialised DokoAzNet (d 160, 6 blocks); Dirichlet "
                     "noise from torch",
             "config": {"workload": "C5 AlphaZero self-play: %d concurrent games x %d PUCT iterations per move per GPU"
@@ -657,10 +675,10 @@ def run_c5(args, dk, L, dev, stream, rank, world, local_rank, dist):
                        "moves_per_step": G, "games_finished": moves[1], "parallelism": "replicas x%d" % world},
             "network_ms_per_step": net_ms / args.steps,
             "search_ms_per_step": elapsed / args.steps * 1e3 - net_ms / args.steps,
-            "roofline": {"bound": "mfma", "achieved": achieved, "peak": 2500.0, "unit": "TFLOP/s",
-                         "frac": achieved / 2500.0, "traffic": None,
-                         "note": "network GEMMs/attention: %.1f MFLOP per leaf evaluation (algorithmic), bf16 dense "
-                                 "peak; achieved over the network's event-timed share of the step" % (flop / 1e6)},
+            "roofline": {"bound": "mfma", "achieved": achieved, "peak": npeak, "unit": "TFLOP/s",
+                         "frac": achieved / npeak, "traffic": None,
+                         "note": "network GEMMs/attention: %.1f MFLOP per leaf evaluation (algorithmic), %s; achieved "
+                                 "over the network's event-timed share of the step" % (flop / 1e6, nnote)},
             "cpu_baseline": None,
         }
         print(json.dumps(result))
@@ -925,7 +943,8 @@ def run_impi(args, dk, L, dev, stream, rank, world, local_rank, dist):
                            device=dev)
     ck(L.dk_env_random_plies_batch_async(eng.ctx, info.data_ptr(), ply_rng.data_ptr(), plies.data_ptr(), I, sp))
     records = dk.az_records(eng, info)
-    net = DokoImpiNet().to(dev).eval().bfloat16()
+    ndt, nlabel, npeak, nnote = net_precision(args, torch)
+    net = DokoImpiNet().to(dev).eval().to(ndt)
     ev = []
 
     def network(tokens):
@@ -991,7 +1010,7 @@ def run_impi(args, dk, L, dev, stream, rank, world, local_rank, dist):
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16 network, f32 softmax / weighted draw" + (", u64+f64 search" if decide else ""),
+            "dtype": nlabel + ", f32 softmax / weighted draw" + (", u64+f64 search" if decide else ""),
             "data": "synthetic: the C3 infostates (seeded deals, 4x Healthy, k in {0,8,20,32} random plies), "
                     "random-initialised DokoImpiNet (d 256, 4 blocks, 4 heads)",
             "config": {"workload": ("IMPI AR decision: %d infostates x %d AR samples x %d sims per GPU" % (I, S, args.iterations))
@@ -1003,11 +1022,12 @@ def run_impi(args, dk, L, dev, stream, rank, world, local_rank, dist):
             "network_ms_per_step": net_ms / args.steps,
             ("search_sampler_fusion_ms_per_step" if decide else "sampler_ms_per_step"):
                 elapsed / args.steps * 1e3 - net_ms / args.steps,
-            "roofline": {"bound": "mfma", "achieved": achieved, "peak": 2500.0, "unit": "TFLOP/s",
-                         "frac": achieved / 2500.0, "traffic": None,
+            "roofline": {"bound": "mfma", "achieved": achieved, "peak": npeak, "unit": "TFLOP/s",
+                         "frac": achieved / npeak, "traffic": None,
                          "note": "IMPI network: %.1f MFLOP per guess (algorithmic), rows = guesses actually needed "
                                  "(infostates ordered by guess count, each round runs the prefix of lanes still "
-                                 "guessing); achieved over the network's event-timed share of the step" % (flop / 1e6)},
+                                 "guessing); achieved over the network's event-timed share of the step; %s"
+                                 % (flop / 1e6, nnote)},
             "cpu_baseline": None,
         }
         print(json.dumps(result))

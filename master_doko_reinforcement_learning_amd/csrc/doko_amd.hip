@@ -1078,14 +1078,17 @@ hipError_t launch_search(dk_ctx* ctx, const dk_state* roots, const uint64_t* see
     const bool ln = iters + 1 <= LN_LDS_MAX && ctx->ln_in_lds;
     const uint32_t rpw = launch_rpw(ctx, n);
     const size_t ln_bytes = ln ? (size_t)((iters + 2) & ~1u) * 8 : 0;
-    // hot-record layout (search_core.h): 16 B once the batch gives every SIMD two waves,
-    // 32 B (cached means) when a single wave per SIMD leaves the pick's latency exposed
+    // hot-record layout (search_core.h): 8 B once the batch gives every SIMD two waves, 16 B
+    // when a single wave per SIMD leaves the pick's latency exposed (round 4, alternated
+    // contexts: C2 33.0 ms against 33.8 ms for the 32-B records and 35.3 ms for 8 B, the
+    // 512-infostate batch 41.6 / 42.8 / 43.6 ms; profiles/r04/layout_single_wave.log), 32 B
+    // (cached exact means) beyond the 16-B records' 24-bit cross products (P24_MAX_ITERS)
     const uint32_t simds = 4u * (uint32_t)ctx->cu_count;
-    // (16-B records compare means by 24-bit cross products: exact up to P24_MAX_ITERS iterations)
-    const bool h16 = iters <= dk::P24_MAX_ITERS &&
-                     (ctx->hot_layout ? ctx->hot_layout <= 16 : grid_for(n, rpw) >= 2u * simds);
+    const bool multi = grid_for(n, rpw) >= 2u * simds;
+    const bool h16 = iters <= dk::P24_MAX_ITERS && (ctx->hot_layout ? ctx->hot_layout <= 16 : true);
     // 8-B records where their fields hold the search (visits, state index, slots: P8_MAX_ITERS)
-    const bool h8 = h16 && iters <= dk::P8_MAX_ITERS && ctx->hot_layout != 16 && ctx->p8_ok;
+    const bool h8 = h16 && iters <= dk::P8_MAX_ITERS && ctx->hot_layout != 16 && ctx->p8_ok &&
+                    (ctx->hot_layout == 8 || multi);
     if (ctx->wide)   // per-wave pool regions of >= 4 GiB: 64-bit offsets (never with ln in LDS: iterations > 2047)
         return launch_search_t<E, false, dk::NodeHot32W>(ctx, roots, seeds, n, iters, c, visits, values, best, st, 0, rpw, sl, err, rng_io);
     if (h8)

@@ -128,7 +128,7 @@ def _c3_check_picks(out, args, I, S, picks, rng, lds_path=None, per_info=4):
 def test_c3_bench_two_legs(monkeypatch, capfd):
     """bench.main's exact sequence on one engine: the timed C3 batch at bench's default
     size (36,864 infostates x 64 CAP samples = 2,359,296 roots, twelve groups per resident
-    wave), then the small-batch leg (512 infostates: 32-root waves, 32-B records) on the
+    wave), then the small-batch leg (512 infostates: 32-root waves, 16-B records) on the
     same engine with its own buffers.  Every root of both legs passes the device
     invariants (visit sum, best = an argmax) and the host re-check; roots spread over each
     queue equal oracle searches bitwise; whole infostates fuse to the oracle's action."""
@@ -166,7 +166,7 @@ def test_c3_bench_two_legs(monkeypatch, capfd):
         eng.close()
     ln2 = _launch_line(capfd)
     assert n2 == I2 * S
-    assert ln2["hot"] == "32B" and int(ln2["rpw"]) == 32, ln2
+    assert ln2["hot"] == "16B" and int(ln2["rpw"]) == 32, ln2      # single wave per SIMD: 16-B records
     _host_invariants(out2, ITERS)
     rng = np.random.default_rng(512)
     checked, _ = _c3_check_picks(out2, args2, I2, S, sorted(set([0, 1, 255, 256, I2 - 2, I2 - 1] +
@@ -238,7 +238,7 @@ def test_c2d_bench_launch_parity(monkeypatch, capfd):
 
 def test_c2_bench_parity_1000(monkeypatch, capfd):
     """C2 (rs-doko, 32,768 deals after 4x Healthy) at the config's 1000 iterations: the
-    32-root waves and 32-B records the launch picks for this batch."""
+    32-root waves and 16-B records the launch picks for this batch."""
     args, n_roots, out = _bench_workload(["--workload", "c2", "--iterations", str(ITERS)], monkeypatch)
     ln = _launch_line(capfd)
     assert n_roots == 32768

@@ -1,0 +1,8 @@
+#!/bin/bash
+# round-4: PC sampling availability and a sampled C3 search launch
+mkdir -p gpurun_out/pcs
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+timeout -s KILL 60 rocprofv3 -L > gpurun_out/pcs/list.txt 2>&1 || true
+timeout -k 10 180 rocprofv3 --pc-sampling-beta-enabled --pc-sampling-method stochastic --pc-sampling-unit cycles --pc-sampling-interval 1048576 -d gpurun_out/pcs/c3 -o c3 --output-format csv -- python3 tools/env_sweep.py --infostates 6144 --contexts 1 --reps 2 "D=" > gpurun_out/pcs/c3.log 2>&1
+echo "rc=$?" >> gpurun_out/pcs/c3.log
+ls -laR gpurun_out/pcs | head -40 >> gpurun_out/pcs/c3.log
