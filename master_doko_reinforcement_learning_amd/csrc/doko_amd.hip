@@ -83,6 +83,7 @@ struct GpuMem {
     uint32_t* ovf;        // global overflow of the path (entries >= lds_n)
     uint64_t* ovf_st;
     uint32_t path_stride;
+    uint32_t half;        // lane pairs (NodeHot16P): 0 = the lower lane of the pair, 1 = its partner
     int lds_n;            // path entries held in LDS
     const double* ln_glob;
     uint32_t cap_slots, cap_states;
@@ -194,6 +195,11 @@ __global__ void __launch_bounds__(WAVE, H::MIN_WAVES) search_kernel(const dk_sta
                                                       const uint32_t* __restrict__ perm, uint32_t lane_base,
                                                       uint64_t* wave_clock, uint64_t* rng_io) {
     const uint32_t lane = threadIdx.x;
+    // lane pairs (NodeHot16P, rpw <= 32): lanes l and l + 32 search the same root
+    constexpr bool PAIR = H::PAIR;
+    const uint32_t rl = PAIR ? (lane & 31u) : lane;                    // the root's lane in the group
+    const bool lead = !PAIR || lane < 32u;                              // one lane per root for atomics
+    const uint32_t pw = PAIR ? (uint32_t)WAVE : rpw;                    // LDS path width (lanes)
     // per-wave start / end of the realtime counter (100 MHz), indexed by the wave's first pool
     // lane (dk_last_search_waves): how long each wave had work before the group queue drained
     const uint32_t clock_idx = lane_base + blockIdx.x * rpw;
@@ -207,7 +213,7 @@ __global__ void __launch_bounds__(WAVE, H::MIN_WAVES) search_kernel(const dk_sta
     // path stats: u64 words (8-B records: u32 words), then the u32 slots
     constexpr bool P8 = dk::is_p8<H>::value;
     const uint32_t path_st_base = P8 ? 2u * n_ln16 : n_ln16;
-    const uint32_t path_base32 = P8 ? path_st_base + (uint32_t)lds_n * rpw : 2u * (path_st_base + (uint32_t)lds_n * rpw);
+    const uint32_t path_base32 = P8 ? path_st_base + (uint32_t)lds_n * pw : 2u * (path_st_base + (uint32_t)lds_n * pw);
     // fallback pass (list != nullptr): the roots the main pass could not fit, list[0] of them
     // at list[1..], searched again in a pool with the proven capacity
     if (list) n = list[0];
@@ -219,8 +225,8 @@ __global__ void __launch_bounds__(WAVE, H::MIN_WAVES) search_kernel(const dk_sta
         g = __shfl(g, 0);
         if (g >= groups) break;                                         // every wave reaches this
         if (order) g = order[g];                                        // longest groups first
-        const uint32_t idx = g * rpw + lane;
-        if (lane >= rpw || idx >= n) continue;
+        const uint32_t idx = g * rpw + rl;
+        if (rl >= rpw || idx >= n) continue;
         const uint32_t root = list ? list[1 + idx] : perm ? perm[idx] : idx;   // perm: depth-sorted order
         typename E::Work w;
         E::load(roots[root], w);
@@ -235,12 +241,13 @@ __global__ void __launch_bounds__(WAVE, H::MIN_WAVES) search_kernel(const dk_sta
         mem.hot = reinterpret_cast<H*>(hot_pool) + wr * cap_slots;
         mem.cold = cold + wr * cap_slots;
         mem.states = states + wr * st_stride;
-        mem.lslot = lane * cap_slots; mem.lstate = lane * st_stride; mem.lovf = lane * (uint32_t)dk::MAX_DEPTH;
+        mem.lslot = rl * cap_slots; mem.lstate = rl * st_stride; mem.lovf = rl * (uint32_t)dk::MAX_DEPTH;
         mem.path_st_off = path_st_base + lane;
         mem.path_off = path_base32 + lane;
         mem.ln_glob = ln_table;
         mem.lds_n = lds_n;
-        mem.path_stride = rpw;
+        mem.path_stride = pw;
+        mem.half = PAIR ? lane >> 5 : 0u;
         mem.ovf = ovf + wr * dk::MAX_DEPTH;
         mem.ovf_st = ovf_st + wr * dk::MAX_DEPTH;
         mem.cap_slots = cap_slots; mem.cap_states = T;
@@ -257,8 +264,10 @@ __global__ void __launch_bounds__(WAVE, H::MIN_WAVES) search_kernel(const dk_sta
             atomicOr(err, 2);                                           // malformed root (DK_E_STATE)
         } else if (st != dk::SR_OK) {
             if (retry) {                                                // searched again by the fallback pass
-                retry[1 + atomicAdd(retry, 1u)] = root;
-                atomicAdd(high_water + 1, 1u);
+                if (lead) {
+                    retry[1 + atomicAdd(retry, 1u)] = root;
+                    atomicAdd(high_water + 1, 1u);
+                }
             } else {
                 atomicOr(err, 1);
             }
@@ -857,6 +866,7 @@ struct dk_ctx {
     uint32_t roots_per_wave = 64;   // pool region width; DK_ROOTS_PER_WAVE fixes the launch width too
     bool rpw_fixed = false;
     int hot_layout = 0;             // DK_HOT_RECORD=8|16|32 fixes the hot-record layout; 0 = per launch
+    int pair = -1;                  // DK_PAIR=0 / 1: lane pairs off / on for launches of <= 32 roots per wave
     bool p8_ok = false;             // the pools' slot capacities suit the 8-B records (even-aligned blocks)
     bool wide = false;              // a wave's pool region reaches 4 GiB: NodeHot32W (64-bit offsets) only
     bool ln_in_lds = false;         // DK_LN_LDS=1: ln(N) table copied into every workgroup's LDS (8 KB at
@@ -968,9 +978,10 @@ hipError_t launch_search_t(dk_ctx* ctx, const dk_state* roots, const uint64_t* s
     const auto kern = search_kernel<E, LN, H>;
     // LDS per path entry and lane: slot word + stats (8-B records: their 32-bit stats word)
     constexpr size_t PATH_ENTRY_BYTES = dk::is_p8<H>::value ? 8 : 12;
+    const size_t pw = H::PAIR ? (size_t)WAVE : rpw;   // lanes with a path (lane pairs: both lanes)
     auto occupancy = [&](int lp) {
         int b = 0;
-        const size_t bytes = ln_bytes + (size_t)lp * rpw * PATH_ENTRY_BYTES;
+        const size_t bytes = ln_bytes + (size_t)lp * pw * PATH_ENTRY_BYTES;
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kern, WAVE, bytes) == hipSuccess ? b : 0;
     };
     // LDS path length: DK_LDS_PATH, or else the longest (<= 16) that keeps the residency
@@ -985,7 +996,7 @@ hipError_t launch_search_t(dk_ctx* ctx, const dk_state* roots, const uint64_t* s
         const int best = occupancy(1);
         while (lp > 1 && occupancy(lp + 1) < best) --lp;
     }
-    const size_t lds_bytes = ln_bytes + (size_t)lp * rpw * PATH_ENTRY_BYTES;
+    const size_t lds_bytes = ln_bytes + (size_t)lp * pw * PATH_ENTRY_BYTES;
     int per_cu = occupancy(lp);
     if (per_cu < 1) per_cu = 1;
     const uint32_t groups = grid_for(n, rpw);
@@ -1015,8 +1026,8 @@ hipError_t launch_search_t(dk_ctx* ctx, const dk_state* roots, const uint64_t* s
     sl.lanes = lanes;
     if (ctx->verbose)
         fprintf(stderr, "doko_amd: search n=%u rpw=%u hot=%dB lds_path=%d lds=%zuB resident/CU=%d grid=%u root_window=%u "
-                "wide=%d lanes=%u+%u\n", n, rpw, (int)sizeof(H), lp, lds_bytes, per_cu, grid, ctx->root_window,
-                (int)H::WIDE, base, lanes);
+                "wide=%d lanes=%u+%u pair=%d\n", n, rpw, (int)sizeof(H), lp, lds_bytes, per_cu, grid, ctx->root_window,
+                (int)H::WIDE, base, lanes, (int)H::PAIR);
     e = hipMemsetAsync(sl.queue, 0, sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
     // group order only matters when waves take several groups each
@@ -1091,6 +1102,11 @@ hipError_t launch_search(dk_ctx* ctx, const dk_state* roots, const uint64_t* see
                     (ctx->hot_layout == 8 || multi);
     if (ctx->wide)   // per-wave pool regions of >= 4 GiB: 64-bit offsets (never with ln in LDS: iterations > 2047)
         return launch_search_t<E, false, dk::NodeHot32W>(ctx, roots, seeds, n, iters, c, visits, values, best, st, 0, rpw, sl, err, rng_io);
+    // lane pairs where a single wave per SIMD holds at most 32 roots (DK_PAIR=0 / 1 forces)
+    const bool pair = h16 && !h8 && rpw <= 32u && (ctx->pair < 0 ? !multi : ctx->pair == 1);
+    if (pair)
+        return ln ? launch_search_t<E, true, dk::NodeHot16P>(ctx, roots, seeds, n, iters, c, visits, values, best, st, ln_bytes, rpw, sl, err, rng_io)
+                  : launch_search_t<E, false, dk::NodeHot16P>(ctx, roots, seeds, n, iters, c, visits, values, best, st, ln_bytes, rpw, sl, err, rng_io);
     if (h8)
         return ln ? launch_search_t<E, true, dk::NodeHot8>(ctx, roots, seeds, n, iters, c, visits, values, best, st, ln_bytes, rpw, sl, err, rng_io)
                   : launch_search_t<E, false, dk::NodeHot8>(ctx, roots, seeds, n, iters, c, visits, values, best, st, ln_bytes, rpw, sl, err, rng_io);
@@ -1174,6 +1190,7 @@ dk_ctx* dk_create(const dk_config* cfg) {
         if (v == 8 || v == 16 || v == 32) ctx->hot_layout = v;
     }
     if (const char* e = getenv("DK_VERBOSE")) ctx->verbose = atoi(e) != 0;
+    if (const char* e = getenv("DK_PAIR")) ctx->pair = atoi(e) != 0 ? 1 : 0;
     if (const char* e = getenv("DK_LN_LDS")) ctx->ln_in_lds = atoi(e) != 0;
     if (const char* e = getenv("DK_LDS_PATH")) {
         const int v = atoi(e);

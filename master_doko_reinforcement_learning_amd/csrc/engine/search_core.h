@@ -80,6 +80,17 @@ struct alignas(16) NodeHot16 {
     static constexpr bool CACHED_MEAN = false;
     static constexpr int MIN_WAVES = DK_HOT16_WAVES;   // search-kernel register budget (3 waves per SIMD: <= 168 VGPRs)
     static constexpr bool WIDE = false;                // pool offsets: 32-bit (a wave's regions < 4 GiB)
+    static constexpr bool PAIR = false;                // two lanes per root (NodeHot16P)
+};
+// 16-B records searched by lane PAIRS: launches of at most 32 roots per wave (a single wave per
+// SIMD, half of its lanes otherwise idle) give every root two lanes, lane l and l + 32.  Both
+// run the root's whole search on identical data (same control flow, the same loads and stores),
+// except the pick, which they split: each scans half of the child block and the halves combine
+// their partial minima / maxima / candidates through v_permlane32_swap, keeping the reference's
+// first-strict-maximum order (pick_child_pair).
+struct alignas(16) NodeHot16P : NodeHot16 {
+    static constexpr int MIN_WAVES = 1;
+    static constexpr bool PAIR = true;
 };
 struct alignas(32) NodeHot32 {
     uint64_t stats;
@@ -91,6 +102,7 @@ struct alignas(32) NodeHot32 {
     static constexpr bool CACHED_MEAN = true;
     static constexpr int MIN_WAVES = 1;   // no budget (its launches have one wave per SIMD)
     static constexpr bool WIDE = false;
+    static constexpr bool PAIR = false;
 };
 // NodeHot32 addressed with 64-bit offsets: contexts whose per-wave pool regions reach 4 GiB
 // (very long searches: the fallback pool's 32-B records at >= ~175 K iterations, node states
@@ -111,6 +123,7 @@ struct alignas(8) NodeHot8 {
     static constexpr bool CACHED_MEAN = false;
     static constexpr int MIN_WAVES = DK_HOT16_WAVES;
     static constexpr bool WIDE = false;
+    static constexpr bool PAIR = false;
 };
 // visits < 2^11, slots < 2^14, state indices < 2^10 (bit 10 of the state field marks a
 // resolved chain head, below)
@@ -505,6 +518,147 @@ DK_HD uint32_t pick_child_x(const B& b, uint32_t n, double lnN, double c, Mem& m
     return pick;
 }
 
+// ---- lane pairs (NodeHot16P) ----------------------------------------------------------
+static constexpr int SCAN_HALF = SCAN_REG / 2;   // children per lane of a pair
+// Half a child block (16-B records) in registers.
+struct BlockH {
+    uint64_t st[SCAN_HALF];
+    uint32_t cb[SCAN_HALF], inf[SCAN_HALF];
+};
+// The partner lane's value (lane ^ 32): one v_permlane32_swap (a half exchange) and a select.
+DK_HD uint32_t pair_x(uint32_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return __lane_id() < 32 ? r[1] : r[0];
+#else
+    return v;   // (host builds never search in pairs)
+#endif
+}
+DK_HD uint64_t pair_x64(uint64_t v) { return (uint64_t)pair_x((uint32_t)(v >> 32)) << 32 | pair_x((uint32_t)v); }
+DK_HD int32_t pair_xi(int32_t v) { return (int32_t)pair_x((uint32_t)v); }
+DK_HD float pair_xf(float v) { union { float f; uint32_t u; } a; a.f = v; a.u = pair_x(a.u); return a.f; }
+DK_HD double pair_xd(double v) { union { double d; uint64_t u; } a; a.d = v; a.u = pair_x64(a.u); return a.d; }
+
+// pick_child_x for a lane pair: this lane holds children j0 .. j0 + 5 of the block (j0 = 0 in the
+// lower half of the wave, 6 in the upper), its partner the others.  Every step keeps the
+// sequential order of pick_child_x: a partial result of the upper half (later children) replaces
+// the lower half's only when it is STRICTLY smaller (sibling minimum), strictly larger (sibling
+// maximum, first estimate maximum, first exact maximum), so both lanes end with the reference's
+// first strict maximum (node.rs:258-277) and the same record.
+template <class Mem>
+DK_HD uint32_t pick_child_pair(const BlockH& b, uint32_t n, uint32_t j0, double lnN, double c, Mem& mem,
+                               uint64_t* p_st, uint32_t* p_cb, uint32_t* p_inf, NodeHot16* end, bool* end_ok) {
+    const bool upper = j0 != 0;
+    const bool have = j0 < n;                 // the lower half always holds child 0
+    // 1. sibling min / max (exact, cross products) over this half, then the pair
+    int32_t wmin = have ? (int32_t)(b.st[0] >> 32) : 0, wmax = wmin;
+    uint32_t vmin = have ? (uint32_t)b.st[0] : 1u, vmax = vmin;
+#pragma unroll
+    for (int k = 1; k < SCAN_HALF; ++k) {
+        if (j0 + (uint32_t)k < n) {
+            const int32_t w = (int32_t)(b.st[k] >> 32);
+            const uint32_t v = (uint32_t)b.st[k];
+            const bool lt = mean_lt(w, v, wmin, vmin);
+            const bool gt = mean_lt(wmax, vmax, w, v);
+            wmin = lt ? w : wmin; vmin = lt ? v : vmin;
+            wmax = gt ? w : wmax; vmax = gt ? v : vmax;
+        }
+    }
+    {
+        const int32_t pwmin = pair_xi(wmin), pwmax = pair_xi(wmax);
+        const uint32_t pvmin = pair_x(vmin), pvmax = pair_x(vmax);
+        const bool phave = upper || n > (uint32_t)SCAN_HALF;   // the partner holds a child
+        // lower-half (a) and upper-half (b) partials: b replaces a only when strictly beyond it
+        const int32_t awmin = upper ? pwmin : wmin, awmax = upper ? pwmax : wmax;
+        const uint32_t avmin = upper ? pvmin : vmin, avmax = upper ? pvmax : vmax;
+        const int32_t bwmin = upper ? wmin : pwmin, bwmax = upper ? wmax : pwmax;
+        const uint32_t bvmin = upper ? vmin : pvmin, bvmax = upper ? vmax : pvmax;
+        const bool bh = upper ? have : phave;
+        const bool bmin = bh && mean_lt(bwmin, bvmin, awmin, avmin);
+        const bool bmax = bh && mean_lt(awmax, avmax, bwmax, bvmax);
+        wmin = bmin ? bwmin : awmin; vmin = bmin ? bvmin : avmin;
+        wmax = bmax ? bwmax : awmax; vmax = bmax ? bvmax : avmax;
+    }
+    const uint32_t D = (uint32_t)mul24(wmax, (int)vmin) - (uint32_t)mul24(wmin, (int)vmax);
+    const bool flat = D == 0;
+    const float vv = (float)vmin * (float)vmax;
+    const float A = flat ? 0.0f : 2.0f * vv * rcp_approx((float)D);
+    const float minf = (float)wmin * rcp_approx((float)vmin);
+    const float maxf = (float)wmax * rcp_approx((float)vmax);
+    const float Bc = flat ? 1.0f : -(minf * A + 1.0f);
+    const float qabs = fmaxf(fabsf(minf), fabsf(maxf));
+    const float ex = (float)c * sqrt_approx((float)lnN);
+    // 2. estimates of this half, first maximum with its record
+    float ue[SCAN_HALF];
+    float umax = -INFINITY;
+    uint32_t jm = j0, cbm = b.cb[0], inm = b.inf[0];
+    uint64_t sm = b.st[0];
+#pragma unroll
+    for (int k = 0; k < SCAN_HALF; ++k) {
+        ue[k] = -INFINITY;
+        if (wave_any(j0 + (uint32_t)k < n)) {
+            const uint32_t vis = (uint32_t)b.st[k];
+            const float rs = rsqrt_approx((float)vis);
+            const float nq = fmaf((float)(int32_t)(b.st[k] >> 32) * (rs * rs), A, Bc);
+            ue[k] = j0 + (uint32_t)k < n ? fmaf(ex, rs, nq) : -INFINITY;
+            const bool gt = ue[k] > umax;
+            umax = gt ? ue[k] : umax;
+            jm = gt ? j0 + (uint32_t)k : jm;
+            sm = gt ? b.st[k] : sm; cbm = gt ? b.cb[k] : cbm; inm = gt ? b.inf[k] : inm;
+        }
+    }
+    {
+        const float pu = pair_xf(umax);
+        const uint32_t pj = pair_x(jm), pcb = pair_x(cbm), pin = pair_x(inm);
+        const uint64_t ps = pair_x64(sm);
+        // the upper half's maximum wins only when strictly larger (its children come later)
+        const bool take = upper ? !(umax > pu) : pu > umax;
+        umax = take ? pu : umax; jm = take ? pj : jm; cbm = take ? pcb : cbm; inm = take ? pin : inm; sm = take ? ps : sm;
+    }
+    const float cut = umax - (3e-6f * (3.0f + fabsf(ex)) + 4e-6f * qabs * A);
+    uint32_t cmask = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_HALF; ++k) cmask |= (ue[k] >= cut ? 1u : 0u) << (j0 + (uint32_t)k);
+    cmask |= pair_x(cmask);
+    const uint32_t nc = (uint32_t)popc32(cmask);
+    // prefetch the chain end of the leading candidate if it is a forced chain head
+    const bool f1 = ni_nchild(inm) == 1 && !ni_open(inm);
+    NodeHot16 e1;
+    if (f1) e1 = mem.load_hot(cbm);
+    uint32_t pick = jm, pc = cbm, pi = inm;
+    uint64_t ps = sm;
+    uint32_t emask = jm != (uint32_t)ctz32(cmask) ? 1u : 0u;
+    if (nc >= 2) {
+        uint32_t em = 0;
+#pragma unroll
+        for (int k = 0; k < SCAN_HALF; ++k) em |= (((cmask >> (j0 + k)) & 1u) && b.st[k] != sm ? 1u : 0u);
+        emask |= em | pair_x(em);
+    }
+    if (emask) {
+        // the exact f64 values of this half's candidates, first strict maximum, then the pair's
+        const double min_q = (double)wmin / (double)vmin, max_q = (double)wmax / (double)vmax;
+        double best = -INFINITY;
+        uint32_t bj = 0, bcb = 0, binf = 0;
+        uint64_t bst = 0;
+#pragma unroll
+        for (int k = 0; k < SCAN_HALF; ++k) {
+            if ((cmask >> (j0 + k)) & 1u) {
+                const double u = uct_exact(b.st[k], mean_of(b.st[k]), flat, min_q, max_q, lnN, c);
+                if (u > best) { best = u; bj = j0 + (uint32_t)k; bst = b.st[k]; bcb = b.cb[k]; binf = b.inf[k]; }
+            }
+        }
+        const double pb = pair_xd(best);
+        const uint32_t pj = pair_x(bj), pcb = pair_x(bcb), pin = pair_x(binf);
+        const uint64_t pst = pair_x64(bst);
+        const bool take = upper ? !(best > pb) : pb > best;
+        pick = take ? pj : bj; ps = take ? pst : bst; pc = take ? pcb : bcb; pi = take ? pin : binf;
+    }
+    *p_st = ps; *p_cb = pc; *p_inf = pi;
+    *end_ok = pick == jm && f1;
+    if (*end_ok) *end = e1;
+    return pick;
+}
+
 template <class E, class Mem>
 DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, double c,
                       Mem& mem, uint32_t* visits39, double* values39, uint8_t* best_out, uint64_t* ctr_scanned,
@@ -619,6 +773,26 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
                         lnN_x = mem.ln(N);
                     }
                     pick = pick_child_x<Raw8>(blk, n, lnN_x, c, mem, &y.stats, &y.child_base, &y.info, &end, &end_ok);
+                    DK_STAMP_DRAINED(tl2);
+                    DK_PROF(mem, 9, tl2 - tl1);
+                } else if constexpr (Mem::Rec::PAIR) {
+                    // lane pairs: this lane loads and scans its half of the block
+                    DK_STAMP_DRAINED(tl0);
+                    const double lnN = mem.ln(x_visits);
+                    const uint32_t j0 = mem.half ? (uint32_t)SCAN_HALF : 0u;
+                    BlockH blk;
+#pragma unroll
+                    for (int k = 0; k < SCAN_HALF; ++k) {
+                        if (j0 + (uint32_t)k < n) {
+                            const NodeHot h = mem.load_hot(x.child_base + j0 + (uint32_t)k);
+                            blk.st[k] = h.stats; blk.cb[k] = h.child_base; blk.inf[k] = h.info;
+                        } else {
+                            blk.st[k] = 0; blk.cb[k] = 0; blk.inf[k] = 0;
+                        }
+                    }
+                    DK_STAMP_DRAINED(tl1);
+                    DK_PROF(mem, 8, tl1 - tl0);
+                    pick = pick_child_pair(blk, n, j0, lnN, c, mem, &y.stats, &y.child_base, &y.info, &end, &end_ok);
                     DK_STAMP_DRAINED(tl2);
                     DK_PROF(mem, 9, tl2 - tl1);
                 } else {

@@ -201,14 +201,18 @@ def test_search_parity_fdo(eng, iters):
                                  {"DK_HOT_RECORD": "8"}, {"DK_HOT_RECORD": "8", "DK_LDS_PATH": "2"},
                                  {"DK_HOT_RECORD": "8", "DK_POOL_ROOTS": "1", "DK_ROOTS_PER_WAVE": "4"},
                                  {"DK_HOT_RECORD": "8", "DK_ROOTS_PER_WAVE": "7"},
-                                 {"DK_GROUP_ORDER": "1", "DK_POOL_ROOTS": "16", "DK_ROOTS_PER_WAVE": "5"}])
+                                 {"DK_GROUP_ORDER": "1", "DK_POOL_ROOTS": "16", "DK_ROOTS_PER_WAVE": "5"},
+                                 {"DK_PAIR": "0"}, {"DK_PAIR": "1", "DK_LDS_PATH": "2"},
+                                 {"DK_PAIR": "1", "DK_POOL_ROOTS": "1", "DK_ROOTS_PER_WAVE": "4"},
+                                 {"DK_PAIR": "1", "DK_ROOTS_PER_WAVE": "7", "DK_LN_LDS": "1"}])
 def test_search_parity_fdo_launch_variants(env, monkeypatch):
     """Path overflow into global memory (2 LDS entries), partial / narrow waves, the LDS
     ln table, and batches larger than the node pools: with DK_POOL_ROOTS=1 one wave
     streams all six 4-root groups through a single pool region (stale trees of the
     previous group stay in it), with 16 four waves share five groups.  DK_HOT_RECORD
-    forces a hot-record layout (8, 16 or 32 B; small batches pick the 32-B one by themselves);
-    DK_GROUP_ORDER=1 queues the root groups longest-first (group_order_kernel)."""
+    forces a hot-record layout (8, 16 or 32 B; small batches pick 16-B records searched by lane
+    pairs by themselves, DK_PAIR=0 / 1 switches the pairs off / on); DK_GROUP_ORDER=1 queues the
+    root groups longest-first (group_order_kernel)."""
     import master_doko_reinforcement_learning_amd as dk
     for k, v in env.items():
         monkeypatch.setenv(k, v)
