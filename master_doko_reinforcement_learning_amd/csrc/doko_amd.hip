@@ -49,6 +49,17 @@ constexpr int MAX_PATH = 64;   // LDS path entries per lane (deeper paths spill 
 
 // Dynamic LDS of the search kernel: [ln table (optional)][path stats][path slots]
 extern __shared__ uint64_t dk_lds[];
+// destination of the prefetch loads (GpuMem::touch_next): one dword per lane, never read.
+// Off by default: alternated contexts (profiles/r04/ab_touch.log) put it at -1.9 % on C2, +4 % on
+// the 512-infostate batch and neutral to +1 % on C3; -DDK_TOUCH=1 builds it.
+#ifndef DK_TOUCH
+#define DK_TOUCH 0
+#endif
+__shared__ uint32_t dk_touch_lds[64];
+typedef __attribute__((address_space(3))) void dk_lds_void;
+__device__ __forceinline__ void touch(const void* g) {
+    __builtin_amdgcn_global_load_lds(g, (dk_lds_void*)dk_touch_lds, 4, 0, 0);
+}
 constexpr uint32_t LN_LDS_MAX = 2048;   // ln(N) entries staged in LDS (16 KB)
 
 // ---------------------------------------------------------------- node pool access
@@ -167,6 +178,25 @@ struct GpuMem {
             at(ovf, lovf + (uint32_t)(k - lds_n)) = v;
             at(ovf_st, lovf + (uint32_t)(k - lds_n)) = st;
         }
+    }
+    // Prefetch for the pick's leading candidate (pick_child_x / pick_child_pair): the record the
+    // next step will load -- its state and cold record if it is open (the expansion), the head of
+    // its child block if it branches -- is requested now, while the pick finishes, and the real
+    // load later finds it on its way into the caches.  A 4-byte global_load_lds per lane (no
+    // destination register; the LDS bytes are never read).  Forced chain heads are loaded by the
+    // pick itself (the chain-end prefetch).
+    __device__ void touch_next(uint32_t slot, uint32_t cb, uint32_t info) const {
+#if DK_TOUCH
+        const uint32_t nch = dk::ni_nchild(info);
+        if (dk::ni_open(info)) {
+            touch(&sr(dk::ni_state(info)));
+            if (nch) touch(&cr(slot));
+        } else if (nch >= 2 || (P8 && dk::ni_resolved(info))) {
+            touch(&hr(cb));
+        }
+#else
+        (void)slot; (void)cb; (void)info;
+#endif
     }
 #ifdef DK_PHASE_PROF
     __device__ void prof_add(int k, uint64_t v) const { prof[k] += v; }

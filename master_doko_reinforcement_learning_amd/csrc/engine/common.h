@@ -23,6 +23,15 @@ DK_HD int ctz64(uint64_t x) { return __builtin_ctzll(x); }
 DK_HD int clz32(uint32_t x) { return x == 0 ? 32 : __builtin_clz(x); }
 DK_HD int clz64(uint64_t x) { return x == 0 ? 64 : __builtin_clzll(x); }
 
+// true if any active lane of the wave has p (host builds: p itself)
+DK_HD bool wave_any(bool p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_ballot_w64(p) != 0;
+#else
+    return p;
+#endif
+}
+
 // Bit of rank r counted from the MSB (rs-game-utils/src/bit_flag.rs:104-171):
 // equivalently the (popc-1-r)-th set bit counted from the LSB.  Branch-free
 // binary search over popcounts (6 steps for 64-bit masks).

@@ -579,6 +579,9 @@ DK_HD int round_draws(const Work& w) {
 // position once per trick.  The lanes of a wave then complete their tricks in the same trip,
 // so the wave pays one trick completion per four plies.  Draw order, rewards and plies are
 // the reference's (state.rs:401-431; host check fdo_engine_check).
+#ifndef DK_ROLLOUT_FAST
+#define DK_ROLLOUT_FAST 1   // tricks without announcement offers skip the per-card offer tests
+#endif
 DK_HD int rollout_cards(const Work& w0, Rng& rng, int pts[4]) {
     uint32_t any0, any1, any2, any3, two0, two1, two2, two3;
     {
@@ -600,6 +603,7 @@ DK_HD int rollout_cards(const Work& w0, Rng& rng, int pts[4]) {
     uint32_t eyes = w0.eyes, ntr = w0.ntricks, doko = w0.doko;
     uint32_t fox_n = w0.fox_n, fox0 = w0.fox0, fox1 = w0.fox1, karl = w0.karl;
     uint32_t lead = 0xFFFFFFu, best_pos = 0, win_card = 0, t_eyes = 0, da_bits = 0;
+    uint32_t lt = 0;   // lead | tm of the running trick (DK_ROLLOUT_FAST)
     int best_key = -2;
     for (uint32_t i = 0; i < trick_len; ++i) {
         const uint32_t c = (w0.trick_cards >> (8u * i)) & 0xFFu;
@@ -609,6 +613,7 @@ DK_HD int rollout_cards(const Work& w0, Rng& rng, int pts[4]) {
         t_eyes += eyes_fast(c);
         if (c == (uint32_t)DIAMOND_ACE) da_bits |= 1u << ((trick_start + i) & 3u);
     }
+    lt = lead | tm;
     auto complete = [&](uint32_t winner) {
         const uint32_t sh = 8u * winner;
         eyes += t_eyes << sh;
@@ -632,26 +637,40 @@ DK_HD int rollout_cards(const Work& w0, Rng& rng, int pts[4]) {
         }
     };
     int plies = 0;
-    // one card of player p, whose hand is (a, t2); updates the hand and the running trick
-    auto play = [&](uint32_t& a, uint32_t& t2, uint32_t p, bool first) {
+    // one card of player p, whose hand is (a, t2), at position `pos` of the trick; updates the
+    // hand and the running trick.  `track` keeps the hand sizes (nb) per card, which only the
+    // announcement offers read (draws).
+    auto play = [&](uint32_t& a, uint32_t& t2, uint32_t p, bool first, uint32_t pos, bool track) {
         const uint32_t f = a & lead;
         const uint32_t legal = f ? f : a;
         const uint32_t r = rng.range_u32((uint32_t)popc32(legal));
         const uint32_t card = nth_set_bit24(legal, (uint32_t)popc32(legal) - 1u - r), bit = 1u << card;
+#if DK_ROLLOUT_FAST
+        // the second copy goes first: t2 loses the bit if it holds it, a otherwise (no selects)
+        const uint32_t second = t2 & bit;
+        t2 ^= second;
+        a ^= bit ^ second;
+#else
         const bool dup = (t2 & bit) != 0u;
         a = dup ? a : (a ^ bit);
         t2 = dup ? (t2 ^ bit) : t2;
-        nb -= 1u << (8u * p);
+#endif
+        if (track) nb -= 1u << (8u * p);
         const CardInfo ci = card_info(gt, card);
         lead = first ? (ci.x & 0xFFFFFFu) : lead;
+#if DK_ROLLOUT_FAST
+        // a card can win the trick iff it is a trump or of the led class: one bit of lead | tm
+        lt = first ? (lead | tm) : lt;
+        const int key = ((lt >> card) & 1u) ? (int)ci.y : -1;
+#else
         const int key = (((ci.x >> 28) & 1u) || ((lead >> card) & 1u)) ? (int)ci.y : -1;
+#endif
         const bool better = first || key > best_key;
         best_key = better ? key : best_key;
-        best_pos = better ? trick_len : best_pos;
+        best_pos = better ? pos : best_pos;
         win_card = better ? card : win_card;
         t_eyes = (first ? 0u : t_eyes) + ((ci.x >> 24) & 15u);
         da_bits = (first ? 0u : da_bits) | (card == (uint32_t)DIAMOND_ACE ? 1u << p : 0u);
-        trick_len += 1u;
         plies += 1;
     };
     // collapsed announcement round after a card: one forced draw per offered player
@@ -664,7 +683,8 @@ DK_HD int rollout_cards(const Work& w0, Rng& rng, int pts[4]) {
     // the partial first trick, absolute hands (a wave runs at most three of these plies)
     while (trick_len != 0u) {
         uint32_t a = sel4u(any0, any1, any2, any3, cur), t2 = sel4u(two0, two1, two2, two3, cur);
-        play(a, t2, cur, false);
+        play(a, t2, cur, false, trick_len, true);
+        trick_len += 1u;
         any0 = cur == 0u ? a : any0; any1 = cur == 1u ? a : any1; any2 = cur == 2u ? a : any2; any3 = cur == 3u ? a : any3;
         two0 = cur == 0u ? t2 : two0; two1 = cur == 1u ? t2 : two1; two2 = cur == 2u ? t2 : two2; two3 = cur == 3u ? t2 : two3;
         cur = (cur + 1u) & 3u;
@@ -686,13 +706,26 @@ DK_HD int rollout_cards(const Work& w0, Rng& rng, int pts[4]) {
         uint32_t T2 = sel4u(two0, two1, two2, two3, (s0 + 2u) & 3u), T3 = sel4u(two0, two1, two2, two3, (s0 + 3u) & 3u);
         while (n_tricks < 12u) {
             const uint32_t s = trick_start;
-            play(A0, T0, s, true);
-            draws();
-            play(A1, T1, (s + 1u) & 3u, false);
-            draws();
-            play(A2, T2, (s + 2u) & 3u, false);
-            draws();
-            play(A3, T3, (s + 3u) & 3u, false);
+            // Announcement offers need n_p >= theta_p; hand sizes only fall and theta changes only
+            // when a trick completes (a wedding resolved), so a trick that starts with no offer
+            // for any lane of the wave has none before its last card: it skips the per-card
+            // offer tests and hand-size updates (one trick's worth of sizes at its end).
+            // (With nobody announcing, offers end within the first trick: theta = 11 - ws.)
+            if (!DK_ROLLOUT_FAST || wave_any((((nb | 0x80808080u) - theta) & 0x80808080u) != 0u)) {
+                play(A0, T0, s, true, 0u, true);
+                draws();
+                play(A1, T1, (s + 1u) & 3u, false, 1u, true);
+                draws();
+                play(A2, T2, (s + 2u) & 3u, false, 2u, true);
+                draws();
+                play(A3, T3, (s + 3u) & 3u, false, 3u, true);
+            } else {
+                play(A0, T0, s, true, 0u, false);
+                play(A1, T1, (s + 1u) & 3u, false, 1u, false);
+                play(A2, T2, (s + 2u) & 3u, false, 2u, false);
+                play(A3, T3, (s + 3u) & 3u, false, 3u, false);
+                nb -= 0x01010101u;
+            }
             const uint32_t bp = best_pos;
             const uint32_t winner = (s + bp) & 3u;
             complete(winner);

@@ -246,15 +246,6 @@ struct Block {
     float isv[SCAN_REG];
 };
 
-// true if any active lane of the wave has p (host builds: p itself)
-DK_HD bool wave_any(bool p) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    return __builtin_amdgcn_ballot_w64(p) != 0;
-#else
-    return p;
-#endif
-}
-
 // UCT pick over a register block (32-B records); returns the index and the picked node's
 // stats / child_base / info.  Bit-exact with the reference's first-strict-
 // maximum over f64 UCT values:
@@ -420,7 +411,7 @@ DK_HD Raw8 sel_raw(bool p, const Raw8& a, const Raw8& b) { return Raw8{p ? a.w0 
 // +inf for an unvisited child never arises; host builds check this).
 template <class R, class B, class Mem>
 DK_HD uint32_t pick_child_x(const B& b, uint32_t n, double lnN, double c, Mem& mem, uint64_t* p_st, uint32_t* p_cb,
-                            uint32_t* p_inf, NodeHot16* end, bool* end_ok) {
+                            uint32_t* p_inf, NodeHot16* end, bool* end_ok, uint32_t cbx) {
 #if !defined(__HIP_DEVICE_COMPILE__)
     for (uint32_t j = 0; j < n; ++j)
         if (R::at(b, (int)j).vis() == 0) { fprintf(stderr, "pick_child_x: unvisited child\n"); abort(); }
@@ -472,6 +463,8 @@ DK_HD uint32_t pick_child_x(const B& b, uint32_t n, double lnN, double c, Mem& m
             rm = sel_raw(gt, r, rm);
         }
     }
+    // the leading candidate is the pick but in the rare exact case: start its next load now
+    mem.touch_next(cbx + jm, rm.child_base(), rm.info());
     const float cut = umax - (3e-6f * (3.0f + fabsf(ex)) + 4e-6f * qabs * A);
     uint32_t cmask = 0;
 #pragma unroll
@@ -547,7 +540,8 @@ DK_HD double pair_xd(double v) { union { double d; uint64_t u; } a; a.d = v; a.u
 // first strict maximum (node.rs:258-277) and the same record.
 template <class Mem>
 DK_HD uint32_t pick_child_pair(const BlockH& b, uint32_t n, uint32_t j0, double lnN, double c, Mem& mem,
-                               uint64_t* p_st, uint32_t* p_cb, uint32_t* p_inf, NodeHot16* end, bool* end_ok) {
+                               uint64_t* p_st, uint32_t* p_cb, uint32_t* p_inf, NodeHot16* end, bool* end_ok,
+                               uint32_t cbx) {
     const bool upper = j0 != 0;
     const bool have = j0 < n;                 // the lower half always holds child 0
     // 1. sibling min / max (exact, cross products) over this half, then the pair
@@ -615,6 +609,7 @@ DK_HD uint32_t pick_child_pair(const BlockH& b, uint32_t n, uint32_t j0, double 
         const bool take = upper ? !(umax > pu) : pu > umax;
         umax = take ? pu : umax; jm = take ? pj : jm; cbm = take ? pcb : cbm; inm = take ? pin : inm; sm = take ? ps : sm;
     }
+    mem.touch_next(cbx + jm, cbm, inm);   // (see pick_child_x)
     const float cut = umax - (3e-6f * (3.0f + fabsf(ex)) + 4e-6f * qabs * A);
     uint32_t cmask = 0;
 #pragma unroll
@@ -772,7 +767,7 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
                         x_visits = N;
                         lnN_x = mem.ln(N);
                     }
-                    pick = pick_child_x<Raw8>(blk, n, lnN_x, c, mem, &y.stats, &y.child_base, &y.info, &end, &end_ok);
+                    pick = pick_child_x<Raw8>(blk, n, lnN_x, c, mem, &y.stats, &y.child_base, &y.info, &end, &end_ok, x.child_base);
                     DK_STAMP_DRAINED(tl2);
                     DK_PROF(mem, 9, tl2 - tl1);
                 } else if constexpr (Mem::Rec::PAIR) {
@@ -792,7 +787,7 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
                     }
                     DK_STAMP_DRAINED(tl1);
                     DK_PROF(mem, 8, tl1 - tl0);
-                    pick = pick_child_pair(blk, n, j0, lnN, c, mem, &y.stats, &y.child_base, &y.info, &end, &end_ok);
+                    pick = pick_child_pair(blk, n, j0, lnN, c, mem, &y.stats, &y.child_base, &y.info, &end, &end_ok, x.child_base);
                     DK_STAMP_DRAINED(tl2);
                     DK_PROF(mem, 9, tl2 - tl1);
                 } else {
@@ -813,7 +808,7 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
                     if constexpr (NodeHot::CACHED_MEAN)
                         pick = pick_child_reg(blk, n, lnN, c, mem, &y.stats, &y.child_base, &y.info, &end, &end_ok);
                     else
-                        pick = pick_child_x<Raw16>(blk, n, lnN, c, mem, &y.stats, &y.child_base, &y.info, &end, &end_ok);
+                        pick = pick_child_x<Raw16>(blk, n, lnN, c, mem, &y.stats, &y.child_base, &y.info, &end, &end_ok, x.child_base);
                     DK_STAMP_DRAINED(tl2);
                     DK_PROF(mem, 9, tl2 - tl1);
                 }

@@ -31,6 +31,7 @@ struct HostMemBase {
     uint32_t path_get_lds(int k, uint64_t* st) { *st = path_st[k]; return path[k]; }
     uint32_t path_get_ovf(int k, uint64_t* st) { *st = path_st[k]; return path[k]; }
     void path_set(int k, uint32_t v, uint64_t st) { path[k] = v; path_st[k] = st; }
+    void touch_next(uint32_t, uint32_t, uint32_t) {}   // (the GPU's L2 prefetch)
 };
 
 // the 16-B / 32-B layouts store the in-register form itself (the host build's DK_HOT16)

@@ -25,6 +25,7 @@ float dk::rsqrt_approx(float x) { return perturb(1.0f / sqrtf(x)); }
 
 struct NullMem {   // chain-end prefetch target (never a forced node here: info = j*13 << 6 has nchild 0)
     dk::NodeHot load_hot(uint32_t) const { dk::NodeHot h; memset(&h, 0, sizeof(h)); return h; }
+    void touch_next(uint32_t, uint32_t, uint32_t) const {}
 };
 
 static uint32_t naive(const dk::NodeHot* rec, uint32_t n, double lnN, double c) {
@@ -110,7 +111,7 @@ int main(int argc, char** argv) {
             blk.w0[j] = dk::p8_w0(rec[j].stats);
             blk.w1[j] = dk::p8_w1(cb_of((uint32_t)j), info_of((uint32_t)j));
         }
-        const uint32_t a = dk::pick_child_x<dk::Raw8>(blk, n, lnN, c, nm, &gs, &gc, &gi, &end, &end_ok);
+        const uint32_t a = dk::pick_child_x<dk::Raw8>(blk, n, lnN, c, nm, &gs, &gc, &gi, &end, &end_ok, 0u);
         const uint32_t want_info = dk::p8_info(dk::p8_w1(cb_of(b), info_of(b)));
 #else
         dk::Block blk;
@@ -119,7 +120,7 @@ int main(int argc, char** argv) {
             blk.q[j] = dk::hot_q(rec[j]); blk.isv[j] = dk::hot_isv(rec[j]);
         }
 #if DK_HOT16
-        const uint32_t a = dk::pick_child_x<dk::Raw16>(blk, n, lnN, c, nm, &gs, &gc, &gi, &end, &end_ok);
+        const uint32_t a = dk::pick_child_x<dk::Raw16>(blk, n, lnN, c, nm, &gs, &gc, &gi, &end, &end_ok, 0u);
 #else
         const uint32_t a = dk::pick_child_reg(blk, n, lnN, c, nm, &gs, &gc, &gi, &end, &end_ok);
 #endif

@@ -1,0 +1,5 @@
+#!/bin/bash
+mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_bench_config.py tests/test_gpu_fixtures.py > gpurun_out/r4_rfast_parity.log 2>&1 || exit 1
+timeout -k 10 500 python -u tools/env_sweep.py --infostates 18432 --contexts 4 --reps 3 "F=" "S=LIB=libdoko_amd_rs.so" > gpurun_out/r4_rfast_c3.log 2>&1 || exit 2
+timeout -k 10 300 python -u tools/env_sweep.py --infostates 512 --contexts 2 --reps 4 "F=" "S=LIB=libdoko_amd_rs.so" > gpurun_out/r4_rfast_small.log 2>&1 || exit 3
