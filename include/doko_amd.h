@@ -516,6 +516,20 @@ int dk_net_attn_ln_bf16_async(const void* qkv, void* x_io, const void* wp, const
 int dk_net_attn62_bf16_async(const void* qkv, void* y, uint32_t batch, uint32_t heads, uint32_t head_dim,
                              void* stream);
 
+/* ---- f32 network row kernels: the networks at the reference's precision (f32 activations;
+ * az_doko.py:379-400, 539-541).  d % 4 == 0, d <= 512; f32 tables / gamma / beta / activations.
+ * dk_net_embed_ln_f32_async: x = e0[t0] + e1[t1] + ... + e5[t5] (f32, left to right), h = LN(x).
+ * dk_net_add_ln_f32_async:   x += delta (delta may be NULL), h = LN(x).
+ * dk_net_attn62_f32_async:   softmax(q k^T / sqrt(head_dim)) v, 62 tokens, q/k/v read from qkv[batch*62][3d]
+ *                            (heads contiguous), y[batch*62][d]; head_dim 40 or 64.
+ * dk_net_gelu_f32_async:     y = GELU(y) in place (exact erf form), n elements, n % 4 == 0. */
+int dk_net_embed_ln_f32_async(const int32_t* d_tokens, uint32_t batch, const void* const* tables, uint32_t d,
+                              const void* gamma, const void* beta, float eps, void* x_out, void* h_out, void* stream);
+int dk_net_add_ln_f32_async(void* x_io, const void* delta, uint32_t rows, uint32_t d, const void* gamma, const void* beta,
+                            float eps, void* h_out, void* stream);
+int dk_net_attn62_f32_async(const void* qkv, void* y, uint32_t batch, uint32_t heads, uint32_t head_dim, void* stream);
+int dk_net_gelu_f32_async(void* y, uint64_t n, void* stream);
+
 /* ---- completion / errors / timing of *_async work -------------------------------
  * dk_sync: waits for the stream and returns the first device-side error
  * (DK_E_CAPACITY when a search ran out of child slots) since the last dk_sync, including

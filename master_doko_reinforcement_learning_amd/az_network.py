@@ -212,6 +212,49 @@ class FusedTrunk:
         return h
 
 
+class FusedTrunkF32(FusedTrunk):
+    """The f32 GPU forward of a token trunk: the reference's precision (f32 activations; the
+    GEMMs as torch F.linear, i.e. hipBLASLt at the caller's matmul precision -- the reference
+    sets "medium", az_doko.py:539-541) with HIP kernels (csrc/az_net_f32_kernels.h) for the
+    embedding sum + first LayerNorm, every residual add fused with the LayerNorm after it, the
+    attention core (f32, one wave per sample and head) and the GELU in place.  The attention
+    half's out_proj and c_proj run folded into one GEMM (Block.folded_proj, f32)."""
+
+    def __init__(self, tokens, emb, ln0):
+        from . import _native
+        self.L = _native.lib()
+        self.st = torch.cuda.current_stream(tokens.device).cuda_stream
+        tok = tokens.int().contiguous()
+        B, d = tok.shape[0], emb[0].weight.shape[1]
+        self.rows, self.d = B * SEQ, d
+        self.x = torch.empty((B, SEQ, d), dtype=torch.float32, device=tok.device)
+        self.h = torch.empty_like(self.x)
+        tables = (ctypes_vp * 6)(*[e.weight.data_ptr() for e in emb])
+        self.ck(self.L.dk_net_embed_ln_f32_async(tok.data_ptr(), B, tables, d, ln0.weight.data_ptr(), ln0.bias.data_ptr(),
+                                                 ln0.eps, self.x.data_ptr(), self.h.data_ptr(), self.st))
+
+    def add_ln(self, x, delta, ln):
+        h = torch.empty_like(x)
+        self.ck(self.L.dk_net_add_ln_f32_async(x.data_ptr(), delta.data_ptr() if delta is not None else None, self.rows,
+                                               self.d, ln.weight.data_ptr(), ln.bias.data_ptr(), ln.eps, h.data_ptr(), self.st))
+        return h
+
+    def attn_ln(self, x, blk, h, ln):
+        if not (self.d % blk.heads == 0 and self.d // blk.heads in (40, 64)):
+            return self.add_ln(x, blk.attn_delta(h), ln)
+        qkv = F.linear(h, blk.qkv.weight, blk.qkv.bias).contiguous()     # [B, 62, 3d]: q | k | v, heads contiguous
+        y = torch.empty_like(h)
+        self.ck(self.L.dk_net_attn62_f32_async(qkv.data_ptr(), y.data_ptr(), h.shape[0], blk.heads, self.d // blk.heads,
+                                               self.st))
+        w, b = blk.folded_proj()
+        return self.add_ln(x, F.linear(y, w, b), ln)
+
+    def mlp_ln(self, x, blk, h, ln):
+        a = F.linear(h, blk.fc.weight, blk.fc.bias).contiguous()
+        self.ck(self.L.dk_net_gelu_f32_async(a.data_ptr(), a.numel(), self.st))
+        return self.add_ln(x, blk.proj(a), ln)
+
+
 class DokoAzNet(nn.Module):
     def __init__(self, d=160, heads=4, layers=4, policy_layers=1, value_layers=1):
         super().__init__()
@@ -227,6 +270,12 @@ class DokoAzNet(nn.Module):
     def forward(self, tokens):                                   # int32/int64 [B, 311]
         if tokens.is_cuda and self.emb[0].weight.dtype == torch.bfloat16:
             return self.forward_fused(tokens)
+        if tokens.is_cuda and self.emb[0].weight.dtype == torch.float32 and not torch.is_grad_enabled():
+            return self.forward_fused(tokens, FusedTrunkF32)
+        return self.forward_torch(tokens)
+
+    def forward_torch(self, tokens):
+        """The plain module forward (reference structure; any device and dtype, autograd)."""
         t = tokens.long()
         x = sum(self.emb[i](t[:, SEQ * i:SEQ * (i + 1)]) for i in range(5)) + self.emb[5](t[:, 310:311])
         for blk in self.blocks:
@@ -238,14 +287,15 @@ class DokoAzNet(nn.Module):
             xv = blk(xv)
         return self.value_head(self.v_ln(xv)), self.policy_head(self.p_ln(xp))
 
-    def forward_fused(self, tokens):
+    def forward_fused(self, tokens, trunk=None):
         """bf16 forward on the GPU with HIP kernels (csrc/az_net_kernels.h): the embedding
         sum + first LayerNorm, each block as two kernels (the attention half from the qkv
         projection to the next LayerNorm, the MLP half likewise: FusedTrunk), and the heads'
-        attention pooling + per-class LayerNorm (ClassHead.pooled)."""
+        attention pooling + per-class LayerNorm (ClassHead.pooled).  trunk=FusedTrunkF32: the
+        f32 forward (reference precision)."""
         if not (self.blocks and self.p_blocks and self.v_blocks):
             raise ValueError("the fused forward needs shared, policy and value blocks")
-        f = FusedTrunk(tokens, self.emb, self.blocks[0].ln_1)
+        f = (trunk or FusedTrunk)(tokens, self.emb, self.blocks[0].ln_1)
         hp = f.run(f.h, self.blocks, self.p_blocks[0].ln_1)       # f.x now holds the shared trunk's output
         xv = f.x.clone()
         hv = f.add_ln(xv, None, self.v_blocks[0].ln_1)

@@ -1,0 +1,214 @@
+// Row kernels of the networks' f32 forward (az_network.FusedTrunkF32): the reference's
+// precision -- f32 activations everywhere, the GEMMs on hipBLASLt at matmul precision
+// "medium" (az_doko.py:539-541, main.py:508) -- with the memory-bound passes fused:
+//   embed_ln_f32 : x = sum of the six token embeddings (left to right, f32); h = LN(x)
+//   add_ln_f32   : x += delta; h = LN(x)                 (delta may be NULL: h = LN(x))
+//   attn62_f32   : softmax(q k^T / sqrt(hd)) v per (sample, head), q / k / v read from the
+//                  fused qkv projection [B*62, 3d], the heads' outputs written [B*62, d]
+//   gelu_f32     : y = GELU(y) in place, the exact erf form of nn.GELU()
+// One row per 32-lane half-wave in the row kernels: lane l holds float4 groups l, l + 32
+// (d / 4 groups), so a half-wave instruction moves up to 512 contiguous bytes.  LayerNorm as
+// torch: two-pass mean / biased variance, (x - mean) * rsqrt(var + eps) * gamma + beta.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dk {
+namespace net {
+
+constexpr int LN4_MAX = 4;   // float4 groups per lane: d <= 512
+
+__device__ __forceinline__ float hw_sum(float v) {
+#pragma unroll
+    for (int o = 16; o >= 1; o >>= 1) v += __shfl_xor(v, o, 32);
+    return v;
+}
+
+template <int P4>
+__device__ __forceinline__ void ln_row_f32(const float4 (&x)[P4], int d, int lane, const float4* gamma4,
+                                           const float4* beta4, float eps, float4* out4) {
+    const int n4 = d / 4;
+    float s = 0.0f;
+#pragma unroll
+    for (int k = 0; k < P4; ++k)
+        if (lane + 32 * k < n4) s += (x[k].x + x[k].y) + (x[k].z + x[k].w);
+    const float mean = hw_sum(s) / (float)d;
+    float q = 0.0f;
+#pragma unroll
+    for (int k = 0; k < P4; ++k)
+        if (lane + 32 * k < n4) {
+            const float a = x[k].x - mean, b = x[k].y - mean, c = x[k].z - mean, e = x[k].w - mean;
+            q += (a * a + b * b) + (c * c + e * e);
+        }
+    const float rstd = rsqrtf(hw_sum(q) / (float)d + eps);
+#pragma unroll
+    for (int k = 0; k < P4; ++k) {
+        const int j = lane + 32 * k;
+        if (j < n4) {
+            const float4 g = gamma4[j], b = beta4[j];
+            out4[j] = make_float4((x[k].x - mean) * rstd * g.x + b.x, (x[k].y - mean) * rstd * g.y + b.y,
+                                  (x[k].z - mean) * rstd * g.z + b.z, (x[k].w - mean) * rstd * g.w + b.w);
+        }
+    }
+}
+
+// tokens [B, 311] int32 (encode_state_pi / encode_state_ipi); tables (f32): object, position,
+// player, subposition, team, phase (or player to guess)
+template <int P4>
+__global__ void embed_ln_f32_kernel(const int32_t* __restrict__ tokens, uint32_t B, int d, const float* __restrict__ e0,
+                                    const float* __restrict__ e1, const float* __restrict__ e2,
+                                    const float* __restrict__ e3, const float* __restrict__ e4,
+                                    const float* __restrict__ e5, const float* gamma, const float* beta, float eps,
+                                    float* __restrict__ x_out, float* __restrict__ h_out) {
+    const uint32_t row = blockIdx.x * (blockDim.x / 32) + threadIdx.x / 32;
+    const int lane = threadIdx.x & 31, n4 = d / 4;
+    if (row >= B * 62u) return;
+    const uint32_t b = row / 62u, s = row % 62u;
+    const int32_t* t = tokens + (size_t)b * 311;
+    const float4* rows[6] = {(const float4*)(e0 + (size_t)t[s] * d), (const float4*)(e1 + (size_t)t[62 + s] * d),
+                             (const float4*)(e2 + (size_t)t[124 + s] * d), (const float4*)(e3 + (size_t)t[186 + s] * d),
+                             (const float4*)(e4 + (size_t)t[248 + s] * d), (const float4*)(e5 + (size_t)t[310] * d)};
+    float4* xo = (float4*)(x_out + (size_t)row * d);
+    float4 x[P4];
+#pragma unroll
+    for (int k = 0; k < P4; ++k) {
+        const int j = lane + 32 * k;
+        x[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (j < n4) {
+            float4 a = rows[0][j];
+#pragma unroll
+            for (int e = 1; e < 6; ++e) {   // torch: ((((e0 + e1) + e2) + e3) + e4) + e5
+                const float4 v = rows[e][j];
+                a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+            }
+            x[k] = a;
+            xo[j] = a;
+        }
+    }
+    ln_row_f32<P4>(x, d, lane, (const float4*)gamma, (const float4*)beta, eps, (float4*)(h_out + (size_t)row * d));
+}
+
+template <int P4>
+__global__ void add_ln_f32_kernel(float* __restrict__ x_io, const float* __restrict__ delta, uint32_t rows, int d,
+                                  const float* gamma, const float* beta, float eps, float* __restrict__ h_out) {
+    const uint32_t row = blockIdx.x * (blockDim.x / 32) + threadIdx.x / 32;
+    const int lane = threadIdx.x & 31, n4 = d / 4;
+    if (row >= rows) return;
+    float4* xr = (float4*)(x_io + (size_t)row * d);
+    const float4* dr = delta ? (const float4*)(delta + (size_t)row * d) : nullptr;
+    float4 x[P4];
+#pragma unroll
+    for (int k = 0; k < P4; ++k) {
+        const int j = lane + 32 * k;
+        x[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (j < n4) {
+            float4 v = xr[j];
+            if (dr) {
+                const float4 e = dr[j];
+                v.x += e.x; v.y += e.y; v.z += e.z; v.w += e.w;
+                xr[j] = v;
+            }
+            x[k] = v;
+        }
+    }
+    ln_row_f32<P4>(x, d, lane, (const float4*)gamma, (const float4*)beta, eps, (float4*)(h_out + (size_t)row * d));
+}
+
+// GELU(v) = 0.5 v (1 + erf(v / sqrt 2)), the exact form (libm erff)
+__global__ void gelu_f32_kernel(float* __restrict__ y, size_t n4) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n4) return;
+    float4 v = ((float4*)y)[i];
+    v.x = 0.5f * v.x * (1.0f + erff(v.x * 0.70710678118654752f));
+    v.y = 0.5f * v.y * (1.0f + erff(v.y * 0.70710678118654752f));
+    v.z = 0.5f * v.z * (1.0f + erff(v.z * 0.70710678118654752f));
+    v.w = 0.5f * v.w * (1.0f + erff(v.w * 0.70710678118654752f));
+    ((float4*)y)[i] = v;
+}
+
+// Attention core in f32: one wave per (sample, head), the query on the lane (62 of 64 lanes).
+// The head's K and V rows (62 x HD f32 each) are staged in LDS; every lane reads the same key
+// row (an LDS broadcast).  Keys in chunks of 8: the chunk's scores in registers, one rescale of
+// the running output per chunk (online softmax with the chunk maximum), exp via exp2f.
+template <int HD>
+__global__ void __launch_bounds__(64) attn62_f32_kernel(const float* __restrict__ qkv, float* __restrict__ y,
+                                                        uint32_t batch, uint32_t heads, float scale) {
+    static_assert(HD % 4 == 0, "head dimension: multiple of 4");
+    __shared__ float4 ks[62 * (HD / 4)];
+    __shared__ float4 vs[62 * (HD / 4)];
+    const uint32_t sample = blockIdx.x / heads, head = blockIdx.x % heads;
+    const int lane = threadIdx.x;
+    const uint32_t d = heads * HD;
+    const float* base = qkv + (size_t)sample * 62 * 3 * d;
+    // stage K and V of this head
+    for (int i = lane; i < 62 * (HD / 4); i += 64) {
+        const int t = i / (HD / 4), e4 = i % (HD / 4);
+        ks[i] = *(const float4*)(base + (size_t)t * 3 * d + d + head * HD + 4 * e4);
+        vs[i] = *(const float4*)(base + (size_t)t * 3 * d + 2 * d + head * HD + 4 * e4);
+    }
+    const bool ok = lane < 62;
+    float4 q[HD / 4];
+    {
+        const float* qr = base + (size_t)(ok ? lane : 0) * 3 * d + head * HD;
+        const float sl = scale * 1.4426950408889634f;   // scores in log2 units: exp(s) = exp2(s log2 e)
+#pragma unroll
+        for (int e4 = 0; e4 < HD / 4; ++e4) {
+            const float4 v = *(const float4*)(qr + 4 * e4);
+            q[e4] = make_float4(v.x * sl, v.y * sl, v.z * sl, v.w * sl);
+        }
+    }
+    __syncthreads();
+    float4 acc[HD / 4];
+#pragma unroll
+    for (int e4 = 0; e4 < HD / 4; ++e4) acc[e4] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    float m = -INFINITY, l = 0.0f;
+    for (int t0 = 0; t0 < 64; t0 += 8) {
+        float s[8];
+        float cm = -INFINITY;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int t = t0 + u;
+            float a = -INFINITY;
+            if (t < 62) {
+                a = 0.0f;
+#pragma unroll
+                for (int e4 = 0; e4 < HD / 4; ++e4) {
+                    const float4 kv = ks[t * (HD / 4) + e4];
+                    a = fmaf(q[e4].x, kv.x, a); a = fmaf(q[e4].y, kv.y, a);
+                    a = fmaf(q[e4].z, kv.z, a); a = fmaf(q[e4].w, kv.w, a);
+                }
+            }
+            s[u] = a;
+            cm = fmaxf(cm, a);
+        }
+        const float mn = fmaxf(m, cm);
+        const float corr = exp2f(m - mn);   // 0 on the first chunk (m = -inf)
+        l *= corr;
+#pragma unroll
+        for (int e4 = 0; e4 < HD / 4; ++e4) { acc[e4].x *= corr; acc[e4].y *= corr; acc[e4].z *= corr; acc[e4].w *= corr; }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int t = t0 + u;
+            if (t < 62) {
+                const float p = exp2f(s[u] - mn);
+                l += p;
+#pragma unroll
+                for (int e4 = 0; e4 < HD / 4; ++e4) {
+                    const float4 vv = vs[t * (HD / 4) + e4];
+                    acc[e4].x = fmaf(p, vv.x, acc[e4].x); acc[e4].y = fmaf(p, vv.y, acc[e4].y);
+                    acc[e4].z = fmaf(p, vv.z, acc[e4].z); acc[e4].w = fmaf(p, vv.w, acc[e4].w);
+                }
+            }
+        }
+        m = mn;
+    }
+    if (!ok) return;
+    const float inv = 1.0f / l;
+    float* yr = y + ((size_t)sample * 62 + lane) * d + head * HD;
+#pragma unroll
+    for (int e4 = 0; e4 < HD / 4; ++e4)
+        *(float4*)(yr + 4 * e4) = make_float4(acc[e4].x * inv, acc[e4].y * inv, acc[e4].z * inv, acc[e4].w * inv);
+}
+
+}  // namespace net
+}  // namespace dk

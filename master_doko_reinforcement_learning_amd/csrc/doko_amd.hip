@@ -22,6 +22,7 @@
 #include "engine/az_core.h"
 #include "engine/encode_pi.h"
 #include "az_net_kernels.h"
+#include "az_net_f32_kernels.h"
 #include "engine/cap_engine.h"
 #include "engine/search_core.h"
 #include "state_fields.h"
@@ -2112,6 +2113,74 @@ int dk_net_attn62_bf16_async(const void* qkv, void* y, uint32_t batch, uint32_t 
     else
         hipLaunchKernelGGL((dk::net::attn62_kernel<64, 4>), dim3((waves + 3u) / 4u), dim3(256), 0, (hipStream_t)stream,
                            (const uint16_t*)qkv, (uint16_t*)y, batch, scale);
+    DK_HIP(hipGetLastError());
+    return DK_OK;
+}
+
+// ---------------------------------------------------------------- f32 network row kernels (az_net_f32_kernels.h)
+namespace {
+int p4_of(uint32_t d) { return (d % 4u == 0u && d >= 4u && d <= 128u * (uint32_t)dk::net::LN4_MAX) ? (int)((d / 4u + 31u) / 32u) : 0; }
+}  // namespace
+#define DK_P4_CASES(M) M(1) M(2) M(3) M(4)
+
+int dk_net_embed_ln_f32_async(const int32_t* d_tokens, uint32_t batch, const void* const* tables, uint32_t d,
+                              const void* gamma, const void* beta, float eps, void* x_out, void* h_out, void* stream) {
+    const int p4 = p4_of(d);
+    if (!tables || !d_tokens || !x_out || !h_out || !gamma || !beta || p4 == 0) return DK_E_INVALID;
+    if (batch == 0) return DK_OK;
+    const uint32_t rows = batch * 62u;
+    const dim3 grid((rows + 7u) / 8u), block(256);
+    hipStream_t st = (hipStream_t)stream;
+    const float* const* t = (const float* const*)tables;
+    switch (p4) {
+#define M(P) case P: hipLaunchKernelGGL(dk::net::embed_ln_f32_kernel<P>, grid, block, 0, st, d_tokens, batch, (int)d, t[0], t[1], \
+                                        t[2], t[3], t[4], t[5], (const float*)gamma, (const float*)beta, eps, (float*)x_out,      \
+                                        (float*)h_out); break;
+        DK_P4_CASES(M)
+#undef M
+    }
+    DK_HIP(hipGetLastError());
+    return DK_OK;
+}
+
+int dk_net_add_ln_f32_async(void* x_io, const void* delta, uint32_t rows, uint32_t d, const void* gamma, const void* beta,
+                            float eps, void* h_out, void* stream) {
+    const int p4 = p4_of(d);
+    if (!x_io || !h_out || !gamma || !beta || p4 == 0) return DK_E_INVALID;
+    if (rows == 0) return DK_OK;
+    const dim3 grid((rows + 7u) / 8u), block(256);
+    hipStream_t st = (hipStream_t)stream;
+    switch (p4) {
+#define M(P) case P: hipLaunchKernelGGL(dk::net::add_ln_f32_kernel<P>, grid, block, 0, st, (float*)x_io, (const float*)delta, \
+                                        rows, (int)d, (const float*)gamma, (const float*)beta, eps, (float*)h_out); break;
+        DK_P4_CASES(M)
+#undef M
+    }
+    DK_HIP(hipGetLastError());
+    return DK_OK;
+}
+
+int dk_net_gelu_f32_async(void* y, uint64_t n, void* stream) {
+    if (!y || n % 4u) return DK_E_INVALID;
+    if (n == 0) return DK_OK;
+    const uint64_t n4 = n / 4u;
+    hipLaunchKernelGGL(dk::net::gelu_f32_kernel, dim3((unsigned)((n4 + 255u) / 256u)), dim3(256), 0, (hipStream_t)stream,
+                       (float*)y, (size_t)n4);
+    DK_HIP(hipGetLastError());
+    return DK_OK;
+}
+
+int dk_net_attn62_f32_async(const void* qkv, void* y, uint32_t batch, uint32_t heads, uint32_t head_dim, void* stream) {
+    if (!qkv || !y || heads == 0 || (head_dim != 40u && head_dim != 64u)) return DK_E_INVALID;
+    if (batch == 0) return DK_OK;
+    if ((uint64_t)batch * heads > 0x7FFFFFFFull) return DK_E_INVALID;
+    const float scale = 1.0f / sqrtf((float)head_dim);
+    if (head_dim == 40u)
+        hipLaunchKernelGGL((dk::net::attn62_f32_kernel<40>), dim3(batch * heads), dim3(64), 0, (hipStream_t)stream,
+                           (const float*)qkv, (float*)y, batch, heads, scale);
+    else
+        hipLaunchKernelGGL((dk::net::attn62_f32_kernel<64>), dim3(batch * heads), dim3(64), 0, (hipStream_t)stream,
+                           (const float*)qkv, (float*)y, batch, heads, scale);
     DK_HIP(hipGetLastError());
     return DK_OK;
 }

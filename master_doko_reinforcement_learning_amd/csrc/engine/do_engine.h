@@ -173,24 +173,36 @@ DK_HD int rollout_cards(const Work& w0, Rng& rng, int pts[4]) {
         if (k > best_key) { best_key = k; best_pos = i; }
         t_eyes += fdo::eyes_fast(c);
     }
+    uint32_t lt = lead | tm;   // a card can win the trick iff it is a trump or of the led class
     int plies = 0;
-    // one card of the player whose hand is (a, t2); updates the hand and the running trick
-    auto play = [&](uint32_t& a, uint32_t& t2, bool first) {
+    // one card of the player whose hand is (a, t2), at position `pos` of the trick; updates the
+    // hand (the second copy first: no selects) and the running trick
+    auto play = [&](uint32_t& a, uint32_t& t2, bool first, uint32_t pos) {
         const uint32_t f = a & lead;
         const uint32_t legal = f ? f : a;
         const uint32_t r = rng.range_u32((uint32_t)popc32(legal));
         const uint32_t card = fdo::nth_set_bit24(legal, (uint32_t)popc32(legal) - 1u - r), bit = 1u << card;
+#if DK_ROLLOUT_FAST
+        const uint32_t second = t2 & bit;
+        t2 ^= second;
+        a ^= bit ^ second;
+#else
         const bool dup = (t2 & bit) != 0u;
         a = dup ? a : (a ^ bit);
         t2 = dup ? (t2 ^ bit) : t2;
+#endif
         const fdo::CardInfo ci = fdo::card_info(fdo::GT_NORMAL, card);
         lead = first ? (ci.x & 0xFFFFFFu) : lead;
+#if DK_ROLLOUT_FAST
+        lt = first ? (lead | tm) : lt;
+        const int key = ((lt >> card) & 1u) ? (int)ci.y : -1;
+#else
         const int key = (((ci.x >> 28) & 1u) || ((lead >> card) & 1u)) ? (int)ci.y : -1;
+#endif
         const bool better = first || key > best_key;
         best_key = better ? key : best_key;
-        best_pos = better ? trick_len : best_pos;
+        best_pos = better ? pos : best_pos;
         t_eyes = (first ? 0u : t_eyes) + ((ci.x >> 24) & 15u);
-        trick_len += 1u;
         plies += 1;
     };
     auto complete = [&](uint32_t winner) {
@@ -206,7 +218,8 @@ DK_HD int rollout_cards(const Work& w0, Rng& rng, int pts[4]) {
     // the partial first trick, absolute hands (a wave runs at most three of these plies)
     while (trick_len != 0u) {
         uint32_t a = fdo::sel4u(any0, any1, any2, any3, cur), t2 = fdo::sel4u(two0, two1, two2, two3, cur);
-        play(a, t2, false);
+        play(a, t2, false, trick_len);
+        trick_len += 1u;
         any0 = cur == 0u ? a : any0; any1 = cur == 1u ? a : any1; any2 = cur == 2u ? a : any2; any3 = cur == 3u ? a : any3;
         two0 = cur == 0u ? t2 : two0; two1 = cur == 1u ? t2 : two1; two2 = cur == 2u ? t2 : two2; two3 = cur == 3u ? t2 : two3;
         cur = (cur + 1u) & 3u;
@@ -224,10 +237,10 @@ DK_HD int rollout_cards(const Work& w0, Rng& rng, int pts[4]) {
         uint32_t T0 = fdo::sel4u(two0, two1, two2, two3, s0), T1 = fdo::sel4u(two0, two1, two2, two3, (s0 + 1u) & 3u);
         uint32_t T2 = fdo::sel4u(two0, two1, two2, two3, (s0 + 2u) & 3u), T3 = fdo::sel4u(two0, two1, two2, two3, (s0 + 3u) & 3u);
         for (;;) {
-            play(A0, T0, true);
-            play(A1, T1, false);
-            play(A2, T2, false);
-            play(A3, T3, false);
+            play(A0, T0, true, 0u);
+            play(A1, T1, false, 1u);
+            play(A2, T2, false, 2u);
+            play(A3, T3, false, 3u);
             const uint32_t bp = best_pos;
             const uint32_t winner = (trick_start + bp) & 3u;
             complete(winner);

@@ -18,7 +18,7 @@ load_reference_state_dict maps a reference state_dict onto this module.
 import torch
 from torch import nn
 
-from .az_network import SEQ, Block, ClassHead, FusedTrunk
+from .az_network import SEQ, Block, ClassHead, FusedTrunk, FusedTrunkF32
 
 VOCAB_IPI = (43, 57, 5, 13, 3, 5)   # object, position, player, subposition, team, player to guess (main.py:91-96)
 IPI_CLASSES = 33
@@ -35,14 +35,19 @@ class DokoImpiNet(nn.Module):
     def forward(self, tokens):                                   # int32/int64 [B, 311] -> [B, 33]
         if tokens.is_cuda and self.emb[0].weight.dtype == torch.bfloat16:
             return self.forward_fused(tokens)
+        if tokens.is_cuda and self.emb[0].weight.dtype == torch.float32 and not torch.is_grad_enabled():
+            return self.forward_fused(tokens, FusedTrunkF32)
+        return self.forward_torch(tokens)
+
+    def forward_torch(self, tokens):
         t = tokens.long()
         x = sum(self.emb[i](t[:, SEQ * i:SEQ * (i + 1)]) for i in range(5)) + self.emb[5](t[:, 310:311])
         for blk in self.blocks:
             x = blk(x)
         return self.head(self.ln_f(x))
 
-    def forward_fused(self, tokens):
-        f = FusedTrunk(tokens, self.emb, self.blocks[0].ln_1)
+    def forward_fused(self, tokens, trunk=None):
+        f = (trunk or FusedTrunk)(tokens, self.emb, self.blocks[0].ln_1)
         return self.head(f.run(f.h, self.blocks, self.ln_f))
 
     @torch.no_grad()

@@ -102,8 +102,9 @@ def test_fused_network_matches_fp32_module():
 
 @pytest.mark.parametrize("net_name", ["az", "impi"])
 def test_f32_network_reference_precision(net_name):
-    """The f32 network path at the reference's precision settings (f32 activations, matmul
-    precision "medium", allow_tf32: az_doko.py:539-541, main.py:508) against full f32: within
+    """The f32 network path (FusedTrunkF32: f32 embedding + LayerNorm, add + LayerNorm,
+    attention-core and GELU kernels, GEMMs at the reference's matmul precision "medium",
+    az_doko.py:539-541, main.py:508) against the plain f32 module at full f32 precision: within
     F32_REL of the output scale, argmax exact wherever the top-two gap exceeds twice that."""
     dev = torch.device("cuda", 0)
     torch.manual_seed(1)
@@ -117,11 +118,11 @@ def test_f32_network_reference_precision(net_name):
     try:
         torch.set_float32_matmul_precision("highest")
         with torch.inference_mode():
-            ref = net(tok)
+            ref = net.forward_torch(tok)            # the plain f32 module, exact f32 GEMMs
         torch.set_float32_matmul_precision("medium")
         torch.backends.cuda.matmul.allow_tf32 = True
         with torch.inference_mode():
-            got = net(tok)
+            got = net(tok)                          # FusedTrunkF32: f32 HIP row kernels + "medium" GEMMs
     finally:
         torch.set_float32_matmul_precision("highest")
         torch.backends.cuda.matmul.allow_tf32 = False
@@ -280,3 +281,59 @@ def test_class_pool_ln_matches_torch(d, C):
     torch.cuda.synchronize()
     assert torch.isfinite(out.float()).all()
     torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=4e-2)
+
+
+@pytest.mark.parametrize("hd", [40, 64])
+def test_attn62_f32_matches_torch(hd):
+    """f32 attention core (one wave per sample and head, online softmax over chunks of 8 keys)
+    against torch f32 softmax(q k^T / sqrt(hd)) v at full f32 precision."""
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(13)
+    B, d = 53, 4 * hd
+    qkv = torch.randn(B, 62, 3 * d, device=dev) * 1.5
+    y = torch.full((B, 62, d), float("nan"), device=dev)
+    rc = _lib().dk_net_attn62_f32_async(qkv.data_ptr(), y.data_ptr(), B, 4, hd, torch.cuda.current_stream(dev).cuda_stream)
+    assert rc == 0
+    torch.cuda.synchronize()
+    torch.set_float32_matmul_precision("highest")
+    q, k, v = qkv.double().view(B, 62, 3, 4, hd).permute(2, 0, 3, 1, 4)
+    ref = (torch.softmax(q @ k.transpose(-1, -2) / hd ** 0.5, dim=-1) @ v).transpose(1, 2).reshape(B, 62, d)
+    torch.testing.assert_close(y.double(), ref, rtol=2e-5, atol=2e-5)
+
+
+@pytest.mark.parametrize("d", [160, 256])
+def test_f32_row_kernels_match_torch(d):
+    """embed + LayerNorm, add + LayerNorm and GELU in f32 against torch f32."""
+    from master_doko_reinforcement_learning_amd.az_network import VOCAB
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(d + 1)
+    B = 37
+    tables = [torch.randn(v, d, device=dev) for v in VOCAB]
+    tok = _tokens(dev, B, VOCAB)
+    g, b = 1 + 0.1 * torch.randn(d, device=dev), 0.1 * torch.randn(d, device=dev)
+    x = torch.empty(B, 62, d, device=dev)
+    h = torch.empty_like(x)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    tp = (ctypes.c_void_p * 6)(*[t.data_ptr() for t in tables])
+    assert _lib().dk_net_embed_ln_f32_async(tok.data_ptr(), B, tp, d, g.data_ptr(), b.data_ptr(), 1e-5, x.data_ptr(),
+                                           h.data_ptr(), st) == 0
+    t = tok.long()
+    xr = tables[0][t[:, 0:62]]
+    for i in range(1, 5):
+        xr = xr + tables[i][t[:, 62 * i:62 * (i + 1)]]
+    xr = xr + tables[5][t[:, 310:311]]
+    torch.cuda.synchronize()
+    assert torch.equal(x, xr)                               # the same left-to-right f32 sum
+    torch.testing.assert_close(h, F.layer_norm(xr, (d,), g, b, 1e-5), rtol=1e-5, atol=1e-5)
+    delta = torch.randn_like(x)
+    x2 = x.clone()
+    assert _lib().dk_net_add_ln_f32_async(x2.data_ptr(), delta.data_ptr(), B * 62, d, g.data_ptr(), b.data_ptr(), 1e-5,
+                                         h.data_ptr(), st) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(x2, x + delta)
+    torch.testing.assert_close(h, F.layer_norm(x + delta, (d,), g, b, 1e-5), rtol=1e-5, atol=1e-5)
+    a = torch.randn(B * 62, 4 * d, device=dev) * 3
+    a2 = a.clone()
+    assert _lib().dk_net_gelu_f32_async(a2.data_ptr(), a2.numel(), st) == 0
+    torch.cuda.synchronize()
+    torch.testing.assert_close(a2, F.gelu(a), rtol=2e-6, atol=2e-6)
