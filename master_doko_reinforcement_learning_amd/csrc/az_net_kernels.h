@@ -989,6 +989,28 @@ __device__ __forceinline__ f32x2_t gelu_erf2_pk(f32x2_t v) {
     return __builtin_elementwise_fma(-ha, c, __builtin_elementwise_fma(v, f32x2_t{0.5f, 0.5f}, ha));
 }
 
+// GELU with erfc from one exp2 and no reciprocal (round 4): with a = min(|v|, 5.5),
+// log2 erfc(a / sqrt2) ~= a (c0 + c1 a + ... + c6 a^6) (weighted least-squares fit on
+// [0, 5.5]), GELU(v) = max(v, 0) - 0.5 |v| erfc(|v| / sqrt2).  |error| <= 2.5e-7 over all v
+// (f32 evaluation, checked against the f64 erf form on a 4M-point grid of [-12, 12]); a third
+// of the bf16 rounding flips of the A&S 7.1.26 form above.  9 VALU + 1 transcendental per
+// value against 13 + 2.
+#ifndef DK_GELU_POLY
+#define DK_GELU_POLY 1
+#endif
+__device__ __forceinline__ float gelu_poly(float v) {
+    const float a = fminf(fabsf(v), 5.5f);
+    float q = -3.68217712320984e-07f;
+    q = fmaf(q, a, 3.816817479673773e-05f);
+    q = fmaf(q, a, -0.0007888087420724332f);
+    q = fmaf(q, a, 0.008100297302007675f);
+    q = fmaf(q, a, -0.05338268727064133f);
+    q = fmaf(q, a, -0.45883968472480774f);
+    q = fmaf(q, a, -1.1511608362197876f);
+    q *= a;
+    return fmaf(-0.5f * fabsf(v), __builtin_amdgcn_exp2f(q), fmaxf(v, 0.0f));
+}
+
 // f32 pair -> two bf16 (round to nearest even, NaN kept), one v_cvt_pk_bf16_f32
 constexpr uint32_t MLP_MAX_HIDDEN = 1024;
 #ifndef DK_MLP_SKEW
@@ -1003,8 +1025,20 @@ constexpr uint32_t MLP_MAX_HIDDEN = 1024;
 #ifndef DK_MLP_P2
 #define DK_MLP_P2 1
 #endif
-template <int D, int NC>
-__global__ void __launch_bounds__(512, 1) mlp_ln_kernel(const uint16_t* __restrict__ h, uint16_t* __restrict__ x_io,
+#ifndef DK_MLP_WAVES160
+#define DK_MLP_WAVES160 8
+#endif
+#ifndef DK_MLP_NC160
+#define DK_MLP_NC160 64
+#endif
+#ifndef DK_MLP_WAVES256
+#define DK_MLP_WAVES256 8
+#endif
+#ifndef DK_MLP_MINB
+#define DK_MLP_MINB 2
+#endif
+template <int D, int NC, int WAVES = 8>
+__global__ void __launch_bounds__(64 * WAVES, WAVES == 8 ? 1 : DK_MLP_MINB) mlp_ln_kernel(const uint16_t* __restrict__ h, uint16_t* __restrict__ x_io,
                                                         const uint16_t* __restrict__ w1, const uint16_t* __restrict__ b1,
                                                         const uint16_t* __restrict__ w2, const uint16_t* __restrict__ b2,
                                                         uint32_t rows, uint32_t n_hidden, const uint16_t* __restrict__ gamma,
@@ -1016,13 +1050,14 @@ __global__ void __launch_bounds__(512, 1) mlp_ln_kernel(const uint16_t* __restri
     constexpr int KS = D / 16, OT = D / 32, LDW1 = D + 8, LDW2 = NC + DK_MLP_W2PAD, HT = NC / 32, GS = NC / 16;
     // LDS: the chunk's W1 / W2, in NB buffers: 3 when the waves 4..7 run half a chunk behind
     // (below), 2 otherwise
-    constexpr bool SKEW = DK_MLP_SKEW && D <= 160;   // d = 256 has no registers to spare
+    constexpr int T = 64 * WAVES;                    // threads of the workgroup
+    constexpr bool SKEW = DK_MLP_SKEW && D <= 160 && WAVES == 8;   // d = 256 has no registers to spare
     constexpr int NB = SKEW ? 3 : 2;
     constexpr int W1E = NC * LDW1, W2E = D * LDW2;
     __shared__ __attribute__((aligned(16))) uint16_t lds[NB * (W1E + W2E)];
     __shared__ float b1s[MLP_MAX_HIDDEN];           // the hidden units' biases
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
-    const uint32_t row = blockIdx.x * 256u + (uint32_t)wave * 32u + (uint32_t)r;
+    const uint32_t row = blockIdx.x * (32u * WAVES) + (uint32_t)wave * 32u + (uint32_t)r;
     const bool ok = row < rows;
     bf16x8_t hf[KS];
     {
@@ -1037,28 +1072,32 @@ __global__ void __launch_bounds__(512, 1) mlp_ln_kernel(const uint16_t* __restri
     // indexed in a loop is an alloca that the compiler promoted to LDS here, which serialised
     // every global load behind its LDS store.
     constexpr int P1 = NC * (D / 8), P2 = D * (NC / 8);
-    static_assert(P1 <= 3 * 512 && P2 <= 3 * 512, "three pieces per thread and matrix");
-    uint4 pa0{}, pa1{}, pa2{}, pb0{}, pb1{}, pb2{};
+    static_assert(P1 <= 5 * T && P2 <= 5 * T, "at most five pieces per thread and matrix");
+    uint4 pa0{}, pa1{}, pa2{}, pa3{}, pa4{}, pb0{}, pb1{}, pb2{}, pb3{}, pb4{};
 #define DK_MLP_LD(U, R1, R2, c)                                                                                \
     {                                                                                                          \
-        const int v = threadIdx.x + 512 * (U);                                                                 \
+        const int v = threadIdx.x + T * (U);                                                                    \
         if (v < P1) { const int i = v / (D / 8), p = v - i * (D / 8); R1 = *(const uint4*)(w1 + ((size_t)(c) * NC + i) * D + 8 * p); } \
         if (v < P2) { const int o = v / (NC / 8), p = v - o * (NC / 8); R2 = *(const uint4*)(w2 + (size_t)o * n_hidden + (size_t)(c) * NC + 8 * p); } \
     }
 #define DK_MLP_ST(U, R1, R2, buf)                                                                              \
     {                                                                                                          \
-        const int v = threadIdx.x + 512 * (U);                                                                 \
+        const int v = threadIdx.x + T * (U);                                                                    \
         if (v < P1) { const int i = v / (D / 8), p = v - i * (D / 8); *(uint4*)&lds[(buf) * W1E + i * LDW1 + 8 * p] = R1; } \
         if (v < P2) { const int o = v / (NC / 8), p = v - o * (NC / 8); uint2* d_ = (uint2*)&lds[NB * W1E + (buf) * W2E + o * LDW2 + 8 * p]; \
                       d_[0] = make_uint2(R2.x, R2.y); d_[1] = make_uint2(R2.z, R2.w); } \
     }
-#define DK_MLP_LOAD_CHUNK(c) { DK_MLP_LD(0, pa0, pb0, c) DK_MLP_LD(1, pa1, pb1, c) DK_MLP_LD(2, pa2, pb2, c) }
-#define DK_MLP_STORE_CHUNK(buf) { DK_MLP_ST(0, pa0, pb0, buf) DK_MLP_ST(1, pa1, pb1, buf) DK_MLP_ST(2, pa2, pb2, buf) }
+#define DK_MLP_LOAD_CHUNK(c) { DK_MLP_LD(0, pa0, pb0, c) DK_MLP_LD(1, pa1, pb1, c) DK_MLP_LD(2, pa2, pb2, c)          \
+    if constexpr (3 * T < P1 || 3 * T < P2) DK_MLP_LD(3, pa3, pb3, c)                                          \
+    if constexpr (4 * T < P1 || 4 * T < P2) DK_MLP_LD(4, pa4, pb4, c) }
+#define DK_MLP_STORE_CHUNK(buf) { DK_MLP_ST(0, pa0, pb0, buf) DK_MLP_ST(1, pa1, pb1, buf) DK_MLP_ST(2, pa2, pb2, buf) \
+    if constexpr (3 * T < P1 || 3 * T < P2) DK_MLP_ST(3, pa3, pb3, buf)                                        \
+    if constexpr (4 * T < P1 || 4 * T < P2) DK_MLP_ST(4, pa4, pb4, buf) }
     f32x16_t acc2[OT];
 #pragma unroll
     for (int t = 0; t < OT; ++t) acc2[t] = f32x16_t{0};
     const uint32_t chunks = n_hidden / NC;
-    for (uint32_t i = threadIdx.x; i < n_hidden; i += 512) b1s[i] = bf2f(b1[i]);
+    for (uint32_t i = threadIdx.x; i < n_hidden; i += T) b1s[i] = bf2f(b1[i]);
     DK_MLP_LOAD_CHUNK(0u)
     DK_MLP_STORE_CHUNK(0)
     __syncthreads();
@@ -1124,8 +1163,12 @@ __global__ void __launch_bounds__(512, 1) mlp_ln_kernel(const uint16_t* __restri
             union { uint32_t u[4]; bf16x8_t v; } pk;
 #pragma unroll
             for (int t = 0; t < 8; t += 2) {
+#if DK_GELU_POLY
+                pk.u[t / 2] = pack_bf16x2(gelu_poly(acc1[j][8 * half + t] + bb[t]), gelu_poly(acc1[j][8 * half + t + 1] + bb[t + 1]));
+#else
                 const f32x2_t g = gelu_erf2_pk(f32x2_t{acc1[j][8 * half + t] + bb[t], acc1[j][8 * half + t + 1] + bb[t + 1]});
                 pk.u[t / 2] = pack_bf16x2(g.x, g.y);
+#endif
             }
             af[s] = pk.v;
         }

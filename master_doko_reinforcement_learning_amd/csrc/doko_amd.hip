@@ -283,7 +283,7 @@ __global__ void __launch_bounds__(WAVE, H::MIN_WAVES) search_kernel(const dk_sta
         mem.ovf_st = ovf_st + wr * dk::MAX_DEPTH;
         mem.cap_slots = cap_slots; mem.cap_states = T;
 #ifdef DK_PHASE_PROF
-        mem.prof = prof + (size_t)root * 16;
+        mem.prof = prof + (size_t)root * dk::PROF_SLOTS;
 #else
         (void)prof;
 #endif
@@ -1301,8 +1301,8 @@ dk_ctx* dk_create(const dk_config* cfg) {
          hipMemset(ctx->slot_err, 0, dk_ctx::MAX_INFLIGHT * sizeof(int)) == hipSuccess;
     ok = ok && hipEventCreateWithFlags(&ctx->fb_done, hipEventDisableTiming) == hipSuccess;
 #ifdef DK_PHASE_PROF
-    ok = ok && hipMalloc(&ctx->prof, (size_t)cfg->max_roots * 16 * sizeof(uint64_t)) == hipSuccess;
-    ok = ok && hipMemset(ctx->prof, 0, (size_t)cfg->max_roots * 16 * sizeof(uint64_t)) == hipSuccess;
+    ok = ok && hipMalloc(&ctx->prof, (size_t)cfg->max_roots * dk::PROF_SLOTS * sizeof(uint64_t)) == hipSuccess;
+    ok = ok && hipMemset(ctx->prof, 0, (size_t)cfg->max_roots * dk::PROF_SLOTS * sizeof(uint64_t)) == hipSuccess;
 #endif
     if (ok) {
         // ln(N) exactly as glibc `log` computes it — what Rust's f64::ln calls (node.rs:253).
@@ -1368,8 +1368,8 @@ int dk_last_error(const dk_ctx* ctx) { return ctx ? ctx->last_error : DK_E_INVAL
 int dk_phase_profile(dk_ctx* ctx, uint64_t* out, uint32_t n) {
     if (!ctx || !ctx->prof || n > ctx->max_roots) return DK_E_INVALID;
     DK_HIP(hipDeviceSynchronize());
-    DK_HIP(hipMemcpy(out, ctx->prof, (size_t)n * 16 * sizeof(uint64_t), hipMemcpyDeviceToHost));
-    DK_HIP(hipMemset(ctx->prof, 0, (size_t)ctx->max_roots * 16 * sizeof(uint64_t)));
+    DK_HIP(hipMemcpy(out, ctx->prof, (size_t)n * dk::PROF_SLOTS * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    DK_HIP(hipMemset(ctx->prof, 0, (size_t)ctx->max_roots * dk::PROF_SLOTS * sizeof(uint64_t)));
     return DK_OK;
 }
 #endif
@@ -2028,16 +2028,17 @@ int dk_net_mlp_ln_bf16_async(const void* h, void* x_io, const void* w1, const vo
                              uint32_t rows, uint32_t d, uint32_t n_hidden, const void* gamma, const void* beta, float eps,
                              void* h_out, void* stream) {
     if (!h || !x_io || !w1 || !b1 || !w2 || !b2 || !gamma || !beta || !h_out || (d != 160u && d != 256u) ||
-        n_hidden == 0 || n_hidden > dk::net::MLP_MAX_HIDDEN || n_hidden % (d == 160u ? 64u : 32u))
+        n_hidden == 0 || n_hidden > dk::net::MLP_MAX_HIDDEN || n_hidden % (d == 160u ? DK_MLP_NC160 : 32u))
         return DK_E_INVALID;
     if (rows == 0) return DK_OK;
-    const dim3 grid((rows + 255u) / 256u), block(512);
+    const uint32_t W = d == 160u ? DK_MLP_WAVES160 : DK_MLP_WAVES256;   // waves per workgroup, 32 rows each
+    const dim3 grid((rows + 32u * W - 1u) / (32u * W)), block(64u * W);
     if (d == 160u)
-        hipLaunchKernelGGL((dk::net::mlp_ln_kernel<160, 64>), grid, block, 0, (hipStream_t)stream, (const uint16_t*)h,
+        hipLaunchKernelGGL((dk::net::mlp_ln_kernel<160, DK_MLP_NC160, DK_MLP_WAVES160>), grid, block, 0, (hipStream_t)stream, (const uint16_t*)h,
                            (uint16_t*)x_io, (const uint16_t*)w1, (const uint16_t*)b1, (const uint16_t*)w2, (const uint16_t*)b2,
                            rows, n_hidden, (const uint16_t*)gamma, (const uint16_t*)beta, eps, (uint16_t*)h_out);
     else
-        hipLaunchKernelGGL((dk::net::mlp_ln_kernel<256, 32>), grid, block, 0, (hipStream_t)stream, (const uint16_t*)h,
+        hipLaunchKernelGGL((dk::net::mlp_ln_kernel<256, 32, DK_MLP_WAVES256>), grid, block, 0, (hipStream_t)stream, (const uint16_t*)h,
                            (uint16_t*)x_io, (const uint16_t*)w1, (const uint16_t*)b1, (const uint16_t*)w2, (const uint16_t*)b2,
                            rows, n_hidden, (const uint16_t*)gamma, (const uint16_t*)beta, eps, (uint16_t*)h_out);
     DK_HIP(hipGetLastError());

@@ -49,8 +49,8 @@ namespace dk {
 #if defined(DK_PHASE_PROF) && defined(__HIP_DEVICE_COMPILE__)
 #define DK_STAMP(t) const uint64_t t = __builtin_amdgcn_s_memtime()
 #define DK_PROF(mem, k, v) prof_acc[k] += (v)
-#define DK_PROF_DECL uint64_t prof_acc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}
-#define DK_PROF_FLUSH(mem) for (int k_ = 0; k_ < 16; ++k_) mem.prof_add(k_, prof_acc[k_])
+#define DK_PROF_DECL uint64_t prof_acc[PROF_SLOTS] = {}
+#define DK_PROF_FLUSH(mem) for (int k_ = 0; k_ < PROF_SLOTS; ++k_) mem.prof_add(k_, prof_acc[k_])
 #define DK_STAMP_DRAINED(t) __builtin_amdgcn_s_waitcnt(0); const uint64_t t = __builtin_amdgcn_s_memtime()
 #define DK_PROF_WAVEMAX(k, v) do { int m_ = (v); for (int o_ = 32; o_ >= 1; o_ >>= 1) { const int t_ = __shfl_xor(m_, o_); m_ = t_ > m_ ? t_ : m_; } prof_acc[k] += (uint64_t)m_; } while (0)
 #else
@@ -177,6 +177,7 @@ DK_HD uint32_t ni_make(uint32_t nchild, uint32_t player, bool open, bool head, u
     return nchild | (player << 6) | (open ? 1u << 8 : 0u) | (head ? 1u << 9 : 0u) | (state << 10);
 }
 static constexpr uint32_t NI_MAX_STATES = 1u << 22;
+static constexpr int PROF_SLOTS = 24;   // per-root counters of the profiling build (DK_PHASE_PROF)
 static constexpr int MAX_DEPTH = 512;   // selection path bound (LDS part + global overflow)
 
 DK_HD int sel4i(const int r[4], int p) { return p == 0 ? r[0] : (p == 1 ? r[1] : (p == 2 ? r[2] : r[3])); }
@@ -886,8 +887,16 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
             const bool first = nch == 0 && slot != 0;
             NodeCold cd;
             if (!first) cd = mem.load_cold(slot);
-            w = E::unpack_node(mem.load_state(ni_state(x.info)));
+            const auto packed = mem.load_state(ni_state(x.info));
+            DK_STAMP_DRAINED(tx0);
+            w = E::unpack_node(packed);
+            DK_STAMP_DRAINED(tx1);
             if (first) cd.unexpanded = E::allowed(w, false);
+            DK_STAMP_DRAINED(tx2);
+            DK_PROF(mem, 14, tx0 - t1);   // cold record + state loads
+            DK_PROF(mem, 15, tx1 - tx0);  // unpack
+            DK_PROF(mem, 16, tx2 - tx1);  // first-expansion action set
+            DK_PROF(mem, 17, first ? 1 : 0);
             const uint64_t bit = random_single(cd.unexpanded, rng);
             const int a = ctz64(bit);
             const uint32_t block = nch + (uint32_t)popc64(cd.unexpanded);
@@ -941,6 +950,8 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
             DK_STAMP_DRAINED(te2);
             DK_PROF(mem, 13, te2 - te1);
             mem.store_state(next_state, E::pack_node(w));
+            DK_STAMP_DRAINED(te3);
+            DK_PROF(mem, 18, te3 - te2);  // pack + state store
             next_state += 1;
             if (!child_end) {
                 depth += 1;

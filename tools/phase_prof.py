@@ -34,7 +34,7 @@ def main():
     prof = getattr(L, "dk_phase_profile", None)
     if prof is not None:
         prof.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]
-        out = np.zeros((n_roots, 16), dtype=np.uint64)
+        out = np.zeros((n_roots, 24), dtype=np.uint64)
         prof(eng.ctx, out.ctypes.data, n_roots)  # clear
     step()
     torch.cuda.synchronize(dev)
@@ -55,7 +55,12 @@ def main():
                     "rollout_plies": float(out[:, 10].astype(np.float64).sum() / sims),
                     "rollout_plies_wave_max": float(out[:, 11].astype(np.float64).sum() / sims),
                     "expand_step_cyc": float(out[:, 12].astype(np.float64).sum() / sims),
-                    "expand_allowed_cyc": float(out[:, 13].astype(np.float64).sum() / sims)})
+                    "expand_allowed_cyc": float(out[:, 13].astype(np.float64).sum() / sims),
+                    "expand_load_cyc": float(out[:, 14].astype(np.float64).sum() / sims),
+                    "expand_unpack_cyc": float(out[:, 15].astype(np.float64).sum() / sims),
+                    "expand_first_allowed_cyc": float(out[:, 16].astype(np.float64).sum() / sims),
+                    "expand_first_fraction": float(out[:, 17].astype(np.float64).sum() / sims),
+                    "expand_pack_store_cyc": float(out[:, 18].astype(np.float64).sum() / sims)})
         tot = out[:, :4].astype(np.float64).sum(axis=1)   # per-root wave-clock cycles over the whole search
         if args.workload == "c3":
             k = np.array([[0, 8, 20, 32][(r // args.samples) % 4] for r in range(n_roots)])
