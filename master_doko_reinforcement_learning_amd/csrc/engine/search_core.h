@@ -177,6 +177,9 @@ DK_HD uint32_t ni_make(uint32_t nchild, uint32_t player, bool open, bool head, u
     return nchild | (player << 6) | (open ? 1u << 8 : 0u) | (head ? 1u << 9 : 0u) | (state << 10);
 }
 static constexpr uint32_t NI_MAX_STATES = 1u << 22;
+#ifndef DK_DEFER_BACKUP
+#define DK_DEFER_BACKUP 1
+#endif
 static constexpr int PROF_SLOTS = 24;   // per-root counters of the profiling build (DK_PHASE_PROF)
 static constexpr int MAX_DEPTH = 512;   // selection path bound (LDS part + global overflow)
 
@@ -685,9 +688,45 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
     int status = SR_OK;
     uint64_t scanned = 0;
     DK_PROF_DECL;
+    // Deferred backup (8-B records, DK_DEFER_BACKUP): a simulation's backup writes the updated
+    // statistics into its LDS path entries only; the global stores are issued by the NEXT
+    // simulation's selection, entry k right before the load of the block that holds it (the
+    // block of entry k - 1's node), the rest after the selection.  Every VMEM wait counts the
+    // wave's earlier stores (vmcnt on gfx9), so stores issued right before the selection's
+    // first load put their completion latency on every simulation's critical path; issued one
+    // level ahead, each completes under the previous level's load.  A lane's loads see its own
+    // earlier stores (program order), so every read is the value the immediate stores gave.
+    // (8-B records and lane pairs; the 16- / 32-B three-wave kernels would spill the extra state)
+    constexpr bool DEFER = DK_DEFER_BACKUP && (P8 || Mem::Rec::PAIR);
+    uint32_t pend = 0;                      // pending entries: n | kc << 8 | kx << 16 (0xFF: none)
+    uint32_t pend_ci = 0, pend_xi = 0;      // structure words of the new leaf / the expanded node
+    uint32_t pend_xcb = 0;                  // (16- / 32-B records: the expanded node's child base)
+    auto flush = [&](int k) {
+        uint64_t ns;
+        const uint32_t e = mem.path_get_lds(k, &ns);
+        const uint32_t s = e & 0x3FFFFFFFu;
+        const int kc_ = (int)((pend >> 8) & 0xFFu), kx_ = (int)((pend >> 16) & 0xFFu);
+        if constexpr (P8) {
+            if (k == kc_ || k == kx_) mem.store_rec8(s, p8_w0(ns), k == kc_ ? pend_ci : pend_xi);
+            else mem.store_backup(s, ns, 0.0, 0.0f);
+        } else {
+            if (k == kc_) mem.store_hot(s, make_hot<NodeHot>(ns, 0, pend_ci));
+            else if (k == kx_) mem.store_hot(s, make_hot<NodeHot>(ns, pend_xcb, pend_xi));
+            else mem.store_backup(s, ns, mean_of(ns), rsqrt_approx((float)(uint32_t)ns));
+        }
+    };
+    int fl = 1;                             // next pending entry to store
+    auto flush_upto = [&](int k) {
+        if constexpr (DEFER) {
+            const int pn = (int)(pend & 0xFFu);
+            const int hi = k < pn ? k : pn;
+            for (; fl <= hi; ++fl) flush(fl);
+        }
+    };
 
     for (uint32_t it = 0; it < iters; ++it) {
         DK_STAMP(t0);
+        fl = 1;
         // ---------------- selection
         uint32_t slot = 0;
         NodeHot x;
@@ -704,7 +743,9 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
         // (a chain head jumps to its chain end), then picks among its children.  A wave
         // whose lanes sit at forced and branching levels at the same time thus pays one
         // pick per trip, not one trip per tree level.
+        [[maybe_unused]] int hops = 0;   // dependent chain loads of this simulation (profiling)
         for (;;) {
+            DK_STAMP_DRAINED(tf0);
             while (ni_nchild(x.info) == 1 && !ni_open(x.info)) {
                 chain_head = ni_head(x.info) ? slot : 0xFFFFFFFFu;
                 chain_info = x.info;
@@ -719,9 +760,13 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
                     slot = 0xFFFFFFFFu;
                     break;
                 }
+                flush_upto(depth + 1);
                 const NodeHot y = mem.load_hot(x.child_base);
                 scanned += 1;
                 DK_PROF(mem, 5, 1);
+#ifdef DK_PHASE_PROF
+                hops += 1;
+#endif
                 if (slot == 0) {
                     // the root's only child: a root child, whose stats are the result
                     depth += 1;
@@ -738,6 +783,8 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
                 slot = x.child_base;
                 x = y;
             }
+            DK_STAMP_DRAINED(tf1);
+            DK_PROF(mem, 19, tf1 - tf0);   // forced-chain hops
             if (status != SR_OK || ni_nchild(x.info) == 0 || ni_open(x.info)) break;
             const uint32_t n = ni_nchild(x.info);
             uint32_t pick;
@@ -746,6 +793,7 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
             if (n <= (uint32_t)SCAN_REG) {
                 if constexpr (P8) {
                     // blocks start at even slots: one 16-B load per pair of children
+                    flush_upto(depth + 1);
                     DK_STAMP_DRAINED(tl0);
                     const double lnN = x_visits == N_FROM_BLOCK ? 0.0 : mem.ln(x_visits);
                     Block8 blk;
@@ -773,6 +821,7 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
                     DK_PROF(mem, 9, tl2 - tl1);
                 } else if constexpr (Mem::Rec::PAIR) {
                     // lane pairs: this lane loads and scans its half of the block
+                    flush_upto(depth + 1);
                     DK_STAMP_DRAINED(tl0);
                     const double lnN = mem.ln(x_visits);
                     const uint32_t j0 = mem.half ? (uint32_t)SCAN_HALF : 0u;
@@ -792,6 +841,7 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
                     DK_STAMP_DRAINED(tl2);
                     DK_PROF(mem, 9, tl2 - tl1);
                 } else {
+                    flush_upto(depth + 1);
                     DK_STAMP_DRAINED(tl0);
                     const double lnN = mem.ln(x_visits);
                     Block blk;
@@ -815,6 +865,7 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
                 }
             } else {
                 // generic block (never produced by the doko engines, whose nodes offer <= 12 actions)
+                flush_upto(depth + 1);
                 const double lnN = mem.ln(x_visits);
                 double min_q = INFINITY, max_q = -INFINITY;
                 for (uint32_t j = 0; j < n; ++j) {
@@ -868,10 +919,12 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
             }
         }
         if (status != SR_OK) break;
+        flush_upto(1 << 30);
         DK_STAMP(t1);
         DK_PROF(mem, 0, t1 - t0);
         DK_PROF(mem, 4, (uint64_t)depth);
         DK_PROF_WAVEMAX(7, depth);
+        DK_PROF_WAVEMAX(20, hops);
         // ---------------- expansion
         // path entries whose whole record the backup writes: the new leaf (kc = depth) and the
         // expanded node (kx); 8-B records carry their structure words pre-encoded
@@ -992,15 +1045,33 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
             const uint32_t e = mem.path_get_ovf(k, &st);
             put(k, e, st + (((uint64_t)(uint32_t)sel4i(r, (int)(e >> 30)) << 32) | 1ULL));
         }
-        for (int k = k_lds; k >= 1; --k) {
-            uint64_t st;
-            const uint32_t e = mem.path_get_lds(k, &st);
-            put(k, e, st + (((uint64_t)(uint32_t)sel4i(r, (int)(e >> 30)) << 32) | 1ULL));
+        if constexpr (DEFER) {
+            for (int k = k_lds; k >= 1; --k) {
+                uint64_t st;
+                const uint32_t e = mem.path_get_lds(k, &st);
+                mem.path_set(k, e, st + (((uint64_t)(uint32_t)sel4i(r, (int)(e >> 30)) << 32) | 1ULL));
+            }
+            const uint32_t pkc = kc >= 1 && kc <= k_lds ? (uint32_t)kc : 0xFFu;
+            const uint32_t pkx = kx >= 1 && kx <= k_lds ? (uint32_t)kx : 0xFFu;
+            pend = (uint32_t)(k_lds > 0 ? k_lds : 0) | pkc << 8 | pkx << 16;
+            pend_ci = c_info; pend_xi = x_info; pend_xcb = x_cb;
+        } else {
+            for (int k = k_lds; k >= 1; --k) {
+                uint64_t st;
+                const uint32_t e = mem.path_get_lds(k, &st);
+                put(k, e, st + (((uint64_t)(uint32_t)sel4i(r, (int)(e >> 30)) << 32) | 1ULL));
+            }
         }
-        if constexpr (!P8) mem.store_stats(0, (uint64_t)(it + 1));
+        // (the root's own record is read by nothing but the result: deferred, once at the end)
+        if constexpr (!P8 && !DEFER) mem.store_stats(0, (uint64_t)(it + 1));
         if (it + 1 == iters) (void)rng.next_u64();  // random_bool((1f32/1000f32) as f64)
-        DK_STAMP(t4);
+        DK_STAMP_DRAINED(t4);   // (drained: the backup owns its store completion)
         DK_PROF(mem, 3, t4 - t3);
+    }
+    if (status == SR_OK) {   // the last simulation's statistics
+        fl = 1;
+        flush_upto(1 << 30);
+        if constexpr (!P8 && DEFER) mem.store_stats(0, (uint64_t)iters);
     }
     if (ctr_scanned) *ctr_scanned = scanned;
     if (used) { used[0] = next_slot; used[1] = next_state; }   // pool high-water of this root

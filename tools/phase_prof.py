@@ -60,7 +60,9 @@ def main():
                     "expand_unpack_cyc": float(out[:, 15].astype(np.float64).sum() / sims),
                     "expand_first_allowed_cyc": float(out[:, 16].astype(np.float64).sum() / sims),
                     "expand_first_fraction": float(out[:, 17].astype(np.float64).sum() / sims),
-                    "expand_pack_store_cyc": float(out[:, 18].astype(np.float64).sum() / sims)})
+                    "expand_pack_store_cyc": float(out[:, 18].astype(np.float64).sum() / sims),
+                    "select_forced_cyc": float(out[:, 19].astype(np.float64).sum() / sims),
+                    "select_forced_loads_wave_max": float(out[:, 20].astype(np.float64).sum() / sims)})
         tot = out[:, :4].astype(np.float64).sum(axis=1)   # per-root wave-clock cycles over the whole search
         if args.workload == "c3":
             k = np.array([[0, 8, 20, 32][(r // args.samples) % 4] for r in range(n_roots)])
