@@ -178,7 +178,7 @@ DK_HD uint32_t ni_make(uint32_t nchild, uint32_t player, bool open, bool head, u
 }
 static constexpr uint32_t NI_MAX_STATES = 1u << 22;
 #ifndef DK_DEFER_BACKUP
-#define DK_DEFER_BACKUP 1
+#define DK_DEFER_BACKUP 0
 #endif
 static constexpr int PROF_SLOTS = 24;   // per-root counters of the profiling build (DK_PHASE_PROF)
 static constexpr int MAX_DEPTH = 512;   // selection path bound (LDS part + global overflow)
