@@ -533,7 +533,7 @@ def main():
                                "%.0f%%" % (100 * valu["mem_wait_frac"]) if valu else "n/a"),
                 "note": "achieved = the SURVEY 8(d) algorithmic bytes (oracle counters, profiles/alg_bytes_<w>.json) / "
                         "event-timed search kernel; traffic = calibrated DRAM bytes per launch (128 B per read "
-                        "request of the 128-B kind, WRITE_SIZE for writes: profiles/r03/pmc_calib.json) from "
+                        "request of the 128-B kind, WRITE_SIZE for writes: profiles/r04/pmc_calib.json) from "
                         "profiles/pmc_search.json, scaled to this launch",
             },
             "node_pools": pools,

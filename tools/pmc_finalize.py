@@ -1,7 +1,7 @@
 """Turn tools/pmc_passes.sh output into the committed PMC summaries.
 
   calib:  python tools/pmc_finalize.py calib <pmc_dir> <calib.jsonl>        -> profiles/r03/pmc_calib.json
-  search: python tools/pmc_finalize.py search <pmc_dir> <kernel> <roots> <iterations> <out.json> [calib.json]
+  search: python tools/pmc_finalize.py search <pmc_dir> <kernel> <roots> <iterations> <out.json> [calib.json] [main|max]
 
 Calibration (tools/pmc_calib.hip, known work per launch) fixes how the gfx950 counters read:
   * DRAM read bytes = 32 x TCC_EA0_RDREQ_32B + 64 x TCC_EA0_RDREQ_64B + 128 x TCC_EA0_RDREQ_128B
@@ -70,8 +70,8 @@ def calib(pmc_dir, jsonl):
     return out
 
 
-def search(pmc_dir, kernel, roots, iters, calib_path=None):
-    c = collect(pmc_dir, [kernel], "main")[kernel]
+def search(pmc_dir, kernel, roots, iters, calib_path=None, mode="main"):
+    c = collect(pmc_dir, [kernel], mode)[kernel]
     trace_ns = []
     import csv
     import glob
@@ -80,7 +80,10 @@ def search(pmc_dir, kernel, roots, iters, calib_path=None):
             for r in csv.DictReader(fh):
                 if kernel in r["Kernel_Name"]:
                     trace_ns.append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
-    main = [t for t in trace_ns if t >= 0.05 * max(trace_ns)] if trace_ns else []
+    if mode == "max":
+        main = [t for t in trace_ns if t >= 0.95 * max(trace_ns)] if trace_ns else []
+    else:
+        main = [t for t in trace_ns if t >= 0.05 * max(trace_ns)] if trace_ns else []
     ms = sum(main) / len(main) / 1e6 if main else None
     d = derived(c, ms)
     sims = roots * iters
@@ -112,7 +115,7 @@ def main():
         path = sys.argv[4] if len(sys.argv) > 4 else "profiles/r03/pmc_calib.json"
     else:
         res = search(sys.argv[2], sys.argv[3], int(sys.argv[4]), int(sys.argv[5]),
-                     sys.argv[7] if len(sys.argv) > 7 else None)
+                     sys.argv[7] if len(sys.argv) > 7 else None, sys.argv[8] if len(sys.argv) > 8 else "main")
         path = sys.argv[6]
     with open(path, "w") as fh:
         json.dump(res, fh, indent=1)

@@ -28,6 +28,9 @@ def collect(d, subs, mode):
             ids = sorted(per[s])
             if mode == "last":
                 pick = [ids[-1]]
+            elif mode == "max":   # the single heaviest dispatch (the headline launch of a bench run)
+                w = {k: sum(per[s][k].values()) for k in ids}
+                pick = [max(ids, key=lambda k: w[k])]
             else:
                 w = {k: sum(per[s][k].values()) for k in ids}
                 top = max(w.values())
