@@ -1037,6 +1037,28 @@ constexpr uint32_t MLP_MAX_HIDDEN = 1024;
 #ifndef DK_MLP_MINB
 #define DK_MLP_MINB 2
 #endif
+// Epilogue stores 16 B per lane (DK_MLP_WIDE_STORE): lane (r, hh) holds columns
+// 32 t + 8 q + 4 hh .. + 3 of row r, 8 B per (t, q).  For the q pair (2m, 2m + 1) one
+// v_permlane32_swap per word trades the half-wave's pieces -- the lower lane gives its q = 2m + 1
+// piece for the upper lane's q = 2m piece -- so the lower lane holds columns 16 m .. + 7 and the
+// upper 16 m + 8 .. + 15: ten 16-B stores per row and tensor instead of twenty 8-B ones (the
+// epilogue's store issue, not its bytes, is what it costs).
+#ifndef DK_MLP_WIDE_STORE
+#define DK_MLP_WIDE_STORE 1
+#endif
+template <int OT>
+__device__ __forceinline__ void mlp_store_row16(const uint2 (&v)[OT][4], uint16_t* row, int hh, bool ok) {
+#pragma unroll
+    for (int t = 0; t < OT; ++t)
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+            const auto a = __builtin_amdgcn_permlane32_swap(v[t][2 * m].x, v[t][2 * m + 1].x, false, false);
+            const auto b = __builtin_amdgcn_permlane32_swap(v[t][2 * m].y, v[t][2 * m + 1].y, false, false);
+            // lower lanes: (own q = 2m piece, partner's q = 2m piece); upper: (partner's 2m + 1, own 2m + 1)
+            if (ok) *(uint4*)(row + 32 * t + 16 * m + 8 * hh) = make_uint4(a[0], b[0], a[1], b[1]);
+        }
+}
+
 template <int D, int NC, int WAVES = 8>
 __global__ void __launch_bounds__(64 * WAVES, WAVES == 8 ? 1 : DK_MLP_MINB) mlp_ln_kernel(const uint16_t* __restrict__ h, uint16_t* __restrict__ x_io,
                                                         const uint16_t* __restrict__ w1, const uint16_t* __restrict__ b1,
@@ -1052,6 +1074,7 @@ __global__ void __launch_bounds__(64 * WAVES, WAVES == 8 ? 1 : DK_MLP_MINB) mlp_
     // (below), 2 otherwise
     constexpr int T = 64 * WAVES;                    // threads of the workgroup
     constexpr bool SKEW = DK_MLP_SKEW && D <= 160 && WAVES == 8;   // d = 256 has no registers to spare
+    constexpr bool WIDE = DK_MLP_WIDE_STORE && D <= 160;           // (d = 256: spills)
     constexpr int NB = SKEW ? 3 : 2;
     constexpr int W1E = NC * LDW1, W2E = D * LDW2;
     __shared__ __attribute__((aligned(16))) uint16_t lds[NB * (W1E + W2E)];
@@ -1269,8 +1292,10 @@ __global__ void __launch_bounds__(64 * WAVES, WAVES == 8 ? 1 : DK_MLP_MINB) mlp_
                 acc2[t][4 * q + e] = xn[e];
                 s1 += xn[e];
             }
-            if (ok) *(uint2*)(xr + col) = make_uint2(pack_bf16x2(xn[0], xn[1]), pack_bf16x2(xn[2], xn[3]));
+            if constexpr (WIDE) xv[t][q] = make_uint2(pack_bf16x2(xn[0], xn[1]), pack_bf16x2(xn[2], xn[3]));   // (x read above)
+            else if (ok) *(uint2*)(xr + col) = make_uint2(pack_bf16x2(xn[0], xn[1]), pack_bf16x2(xn[2], xn[3]));
         }
+    if constexpr (WIDE) mlp_store_row16<OT>(xv, xr, hh, ok);
     s1 += __shfl_xor(s1, 32);
     const float mean = s1 / (float)D;
     float s2 = 0.0f;
@@ -1295,8 +1320,10 @@ __global__ void __launch_bounds__(64 * WAVES, WAVES == 8 ? 1 : DK_MLP_MINB) mlp_
             float o[4];
 #pragma unroll
             for (int e = 0; e < 4; ++e) o[e] = (acc2[t][4 * q + e] - mean) * rstd * bf2f(gs[e]) + bf2f(bs[e]);
-            if (ok) *(uint2*)(hr + col) = make_uint2(pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]));
+            if constexpr (WIDE) xv[t][q] = make_uint2(pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]));
+            else if (ok) *(uint2*)(hr + col) = make_uint2(pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]));
         }
+    if constexpr (WIDE) mlp_store_row16<OT>(xv, hr, hh, ok);
 }
 #undef DK_MLP_LD
 #undef DK_MLP_ST
