@@ -923,6 +923,12 @@ struct dk_ctx {
     bool az_root_done = false;
     std::vector<void*> scratch;
     std::vector<size_t> scratch_size;
+    // results of the synchronous (host-pointer) entry points: DMA into this page-locked buffer,
+    // copied into the caller's memory by the CPU once the stream is drained (copy_out / finish)
+    char* pinned = nullptr;
+    size_t pinned_size = 0, pinned_used = 0;
+    struct OutCopy { void* dst; size_t off, bytes; };
+    std::vector<OutCopy> outs;
     std::mutex mu;                  // host-pointer calls (scratch buffers, ctx->stream)
     std::mutex slot_mu;             // search slots and lane ranges
 };
@@ -953,10 +959,49 @@ void* scratch(dk_ctx* ctx, int k, size_t bytes) {
     return ctx->scratch[k];
 }
 
+// The queued result copies of a synchronous entry point, after its stream is drained.
+void flush_outs(dk_ctx* ctx) {
+    for (const dk_ctx::OutCopy& o : ctx->outs) memcpy(o.dst, ctx->pinned + o.off, o.bytes);
+    ctx->outs.clear();
+    ctx->pinned_used = 0;
+}
+
+// A device-to-host result copy of a synchronous entry point (round 4, the review's pageable-copy
+// concern): the DMA lands in the context's page-locked staging buffer on ctx->stream, and
+// finish() copies it into the caller's (possibly pageable) buffer with the CPU after the stream
+// is drained, so nothing depends on how the runtime stages a copy into pageable memory.
+hipError_t copy_out(dk_ctx* ctx, void* dst, const void* src, size_t bytes) {
+    hipError_t e = hipSuccess;
+    const size_t off = (ctx->pinned_used + 255) & ~(size_t)255;
+    if (off + bytes > ctx->pinned_size) {
+        // drain what is queued, then grow
+        if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) { ctx->outs.clear(); ctx->pinned_used = 0; return e; }
+        flush_outs(ctx);
+        if (bytes > ctx->pinned_size) {
+            if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+            ctx->pinned = nullptr;
+            ctx->pinned_size = 0;
+            const size_t sz = bytes < ((size_t)1 << 20) ? ((size_t)1 << 20) : bytes;
+            if ((e = hipHostMalloc((void**)&ctx->pinned, sz, hipHostMallocDefault)) != hipSuccess) { ctx->pinned = nullptr; return e; }
+            ctx->pinned_size = sz;
+        }
+        return copy_out(ctx, dst, src, bytes);
+    }
+    if ((e = hipMemcpyAsync(ctx->pinned + off, src, bytes, hipMemcpyDeviceToHost, ctx->stream)) != hipSuccess) {
+        ctx->outs.clear();
+        ctx->pinned_used = 0;
+        return e;
+    }
+    ctx->outs.push_back({dst, off, bytes});
+    ctx->pinned_used = off + bytes;
+    return hipSuccess;
+}
+
 // Wait for stream `st`, then collect the error flags: the context's (env, sampler, AlphaZero
 // kernels) and those of the search launches issued on `st` since its last sync.
 int finish(dk_ctx* ctx, hipStream_t st) {
-    if (hipStreamSynchronize(st) != hipSuccess) return ctx->last_error = DK_E_LAUNCH;
+    if (hipStreamSynchronize(st) != hipSuccess) { ctx->outs.clear(); ctx->pinned_used = 0; return ctx->last_error = DK_E_LAUNCH; }
+    if (st == ctx->stream) flush_outs(ctx);
     int flag = 0;
     if (hipMemcpy(&flag, ctx->err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return ctx->last_error = DK_E_LAUNCH;
     (void)hipMemset(ctx->err, 0, sizeof(int));
@@ -1333,6 +1378,7 @@ void dk_destroy(dk_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     for (void* p : ctx->scratch) if (p) (void)hipFree(p);
+    if (ctx->pinned) (void)hipHostFree(ctx->pinned);
     if (ctx->hot) (void)hipFree(ctx->hot);
     if (ctx->cold) (void)hipFree(ctx->cold);
     if (ctx->ovf) (void)hipFree(ctx->ovf);
@@ -1457,7 +1503,7 @@ int dk_new_game_batch(dk_ctx* ctx, int game, const uint64_t* seeds, uint32_t n, 
     DK_HIP(hipMemcpyAsync(d_seeds, seeds, n * sizeof(uint64_t), hipMemcpyHostToDevice, ctx->stream));
     int rc = dk_new_game_batch_async(ctx, game, d_seeds, n, d_out, ctx->stream);
     if (rc) return rc;
-    DK_HIP(hipMemcpyAsync(out, d_out, n * sizeof(dk_state), hipMemcpyDeviceToHost, ctx->stream));
+    DK_HIP(copy_out(ctx, out, d_out, n * sizeof(dk_state)));
     return finish(ctx, ctx->stream);
 }
 
@@ -1472,7 +1518,7 @@ int dk_env_allowed_batch(dk_ctx* ctx, const dk_state* states, uint32_t n, int fi
     DK_HIP(hipMemcpyAsync(d_s, states, n * sizeof(dk_state), hipMemcpyHostToDevice, ctx->stream));
     hipLaunchKernelGGL(env_allowed_kernel, dim3(grid_for(n, 64)), dim3(64), 0, ctx->stream, d_s, n, first_expansion, d_m, ctx->err);
     DK_HIP(hipGetLastError());
-    DK_HIP(hipMemcpyAsync(masks, d_m, n * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream));
+    DK_HIP(copy_out(ctx, masks, d_m, n * sizeof(uint64_t)));
     return finish(ctx, ctx->stream);
 }
 
@@ -1487,7 +1533,7 @@ int dk_env_step_batch(dk_ctx* ctx, dk_state* states, const uint64_t* action_bits
     DK_HIP(hipMemcpyAsync(d_a, action_bits, n * sizeof(uint64_t), hipMemcpyHostToDevice, ctx->stream));
     hipLaunchKernelGGL(env_step_kernel, dim3(grid_for(n, 64)), dim3(64), 0, ctx->stream, d_s, d_a, n, ctx->err);
     DK_HIP(hipGetLastError());
-    DK_HIP(hipMemcpyAsync(states, d_s, n * sizeof(dk_state), hipMemcpyDeviceToHost, ctx->stream));
+    DK_HIP(copy_out(ctx, states, d_s, n * sizeof(dk_state)));
     return finish(ctx, ctx->stream);
 }
 
@@ -1502,8 +1548,8 @@ int dk_env_rewards_batch(dk_ctx* ctx, const dk_state* states, uint32_t n, int32_
     DK_HIP(hipMemcpyAsync(d_s, states, n * sizeof(dk_state), hipMemcpyHostToDevice, ctx->stream));
     hipLaunchKernelGGL(env_rewards_kernel, dim3(grid_for(n, 64)), dim3(64), 0, ctx->stream, d_s, n, d_h, d_r);
     DK_HIP(hipGetLastError());
-    DK_HIP(hipMemcpyAsync(has_rewards, d_h, n * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
-    DK_HIP(hipMemcpyAsync(rewards, d_r, 4 * n * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    DK_HIP(copy_out(ctx, has_rewards, d_h, n * sizeof(int32_t)));
+    DK_HIP(copy_out(ctx, rewards, d_r, 4 * n * sizeof(double)));
     return finish(ctx, ctx->stream);
 }
 
@@ -1527,8 +1573,8 @@ int dk_env_rollout_batch(dk_ctx* ctx, const dk_state* states, uint64_t* rng_stat
     DK_HIP(hipMemcpyAsync(d_g, rng_states, 4 * n * sizeof(uint64_t), hipMemcpyHostToDevice, ctx->stream));
     int rc = dk_env_rollout_batch_async(ctx, d_s, d_g, n, d_r, ctx->stream);
     if (rc) return rc;
-    DK_HIP(hipMemcpyAsync(rewards, d_r, 4 * n * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
-    DK_HIP(hipMemcpyAsync(rng_states, d_g, 4 * n * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream));
+    DK_HIP(copy_out(ctx, rewards, d_r, 4 * n * sizeof(double)));
+    DK_HIP(copy_out(ctx, rng_states, d_g, 4 * n * sizeof(uint64_t)));
     return finish(ctx, ctx->stream);
 }
 
@@ -1545,8 +1591,8 @@ int dk_env_random_plies_batch(dk_ctx* ctx, dk_state* states, uint64_t* rng_state
     DK_HIP(hipMemcpyAsync(d_p, plies, n * sizeof(uint32_t), hipMemcpyHostToDevice, ctx->stream));
     hipLaunchKernelGGL(random_plies_kernel, dim3(grid_for(n, 64)), dim3(64), 0, ctx->stream, d_s, d_g, d_p, n);
     DK_HIP(hipGetLastError());
-    DK_HIP(hipMemcpyAsync(states, d_s, n * sizeof(dk_state), hipMemcpyDeviceToHost, ctx->stream));
-    DK_HIP(hipMemcpyAsync(rng_states, d_g, 4 * n * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream));
+    DK_HIP(copy_out(ctx, states, d_s, n * sizeof(dk_state)));
+    DK_HIP(copy_out(ctx, rng_states, d_g, 4 * n * sizeof(uint64_t)));
     return finish(ctx, ctx->stream);
 }
 
@@ -1612,11 +1658,11 @@ int search_host(dk_ctx* ctx, int game, const dk_state* roots, const uint64_t* se
     int rc = search_async(ctx, game, d_r, rng_states ? nullptr : d_s, rng_states ? d_s : nullptr, n, iterations, c, d_v,
                           d_val, d_b, ctx->stream);
     if (rc) return rc;
-    DK_HIP(hipMemcpyAsync(visits, d_v, (size_t)n * 39 * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
-    DK_HIP(hipMemcpyAsync(values, d_val, (size_t)n * 39 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
-    DK_HIP(hipMemcpyAsync(best, d_b, n, hipMemcpyDeviceToHost, ctx->stream));
+    DK_HIP(copy_out(ctx, visits, d_v, (size_t)n * 39 * sizeof(uint32_t)));
+    DK_HIP(copy_out(ctx, values, d_val, (size_t)n * 39 * sizeof(double)));
+    DK_HIP(copy_out(ctx, best, d_b, n));
     if (rng_states)
-        DK_HIP(hipMemcpyAsync(rng_states, d_s, 4 * (size_t)n * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream));
+        DK_HIP(copy_out(ctx, rng_states, d_s, 4 * (size_t)n * sizeof(uint64_t)));
     return finish(ctx, ctx->stream);
 }
 }  // namespace
@@ -1673,7 +1719,7 @@ int dk_determinize_batch(dk_ctx* ctx, const dk_state* infostates, uint32_t n_inf
     DK_HIP(hipMemcpyAsync(d_s, seeds, n * sizeof(uint64_t), hipMemcpyHostToDevice, ctx->stream));
     int rc = dk_determinize_batch_async(ctx, d_i, n_info, samples, d_s, d_o, ctx->stream);
     if (rc) return rc;
-    DK_HIP(hipMemcpyAsync(out, d_o, n * sizeof(dk_state), hipMemcpyDeviceToHost, ctx->stream));
+    DK_HIP(copy_out(ctx, out, d_o, n * sizeof(dk_state)));
     return finish(ctx, ctx->stream);
 }
 
@@ -1727,7 +1773,7 @@ int dk_fuse(dk_ctx* ctx, const uint32_t* visits, uint32_t n_info, uint32_t sampl
     if (rc) return rc;
     rc = dk_fuse_select_async(ctx, n_info, mode, d_a, d_u, d_f, d_out, ctx->stream);
     if (rc) return rc;
-    DK_HIP(hipMemcpyAsync(action, d_out, n_info, hipMemcpyDeviceToHost, ctx->stream));
+    DK_HIP(copy_out(ctx, action, d_out, n_info));
     return finish(ctx, ctx->stream);
 }
 
@@ -1746,7 +1792,7 @@ int dk_is_consistent_batch(dk_ctx* ctx, const dk_az_state* infostates, const uin
     DK_HIP(hipMemcpyAsync(d_r, reservations, 4 * (size_t)n, hipMemcpyHostToDevice, ctx->stream));
     hipLaunchKernelGGL(is_consistent_kernel, dim3(grid_for(n, 64)), dim3(64), 0, ctx->stream, d_i, d_h, d_r, n, d_o);
     DK_HIP(hipGetLastError());
-    DK_HIP(hipMemcpyAsync(reasons, d_o, n, hipMemcpyDeviceToHost, ctx->stream));
+    DK_HIP(copy_out(ctx, reasons, d_o, n));
     return finish(ctx, ctx->stream);
 }
 
@@ -1810,8 +1856,8 @@ int dk_decide_batch(dk_ctx* ctx, const dk_state* infostates, uint32_t n_info, ui
     if (rc) return rc;
     rc = dk_fuse_select_async(ctx, n_info, fuse_mode, d_allowed, d_u, d_f, d_b + n, ctx->stream);
     if (rc) return rc;
-    DK_HIP(hipMemcpyAsync(actions, d_b + n, n_info, hipMemcpyDeviceToHost, ctx->stream));
-    if (visits) DK_HIP(hipMemcpyAsync(visits, d_v, n * 39 * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+    DK_HIP(copy_out(ctx, actions, d_b + n, n_info));
+    if (visits) DK_HIP(copy_out(ctx, visits, d_v, n * 39 * sizeof(uint32_t)));
     return finish(ctx, ctx->stream);
 }
 
