@@ -210,5 +210,128 @@ __global__ void __launch_bounds__(64) attn62_f32_kernel(const float* __restrict_
         *(float4*)(yr + 4 * e4) = make_float4(acc[e4].x * inv, acc[e4].y * inv, acc[e4].z * inv, acc[e4].w * inv);
 }
 
+// The same attention core on the f32 matrix cores (v_mfma_f32_32x32x2_f32: f32 products, f32
+// accumulation -- no narrowing), one wave per (sample, head):
+//   S^T = K Q^T  : A = K (rows = keys), B = Q^T (columns = queries), k = the head dimension in
+//                  steps of 2 (lane half hh supplies dimension hh HD/2 + s), scores pre-scaled by
+//                  scale * log2 e in Q; lane (i, hh) then holds query i's scores of keys
+//                  32b + (g & 3) + 8 (g >> 2) + 4 hh, so the softmax is the lane's own registers
+//                  plus one exchange with lane i ^ 32;
+//   O^T = V^T P^T: the k order of a step only has to agree between the operands, so step
+//                  (b, g) pairs key j = 32b + (g & 3) + 8 (g >> 2) + 4 hh of each lane half: the
+//                  probabilities never leave their registers, V^T comes from LDS;
+//   y = O / l    : lane (i, hh) holds dimensions 32t + (g & 3) + 8 (g >> 2) + 4 hh of query i.
+// Query tiles one at a time (32 queries; the K fragments stay in registers).  Keys 62, 63 score
+// -inf; V rows 62, 63 are zero in LDS.
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+// waves per SIMD: 3 at HD = 40 (0.447 against 0.470 ms at 8,192 samples, two spilled registers),
+// 2 at HD = 64 (3 spills more there and measured slower)
+#ifndef DK_ATTNF32_WAVES40
+#define DK_ATTNF32_WAVES40 3
+#endif
+template <int HD>
+__global__ void __launch_bounds__(64, HD == 40 ? DK_ATTNF32_WAVES40 : 2) attn62_f32_mfma_kernel(const float* __restrict__ qkv, float* __restrict__ y,
+                                                             uint32_t batch, uint32_t heads, float scale) {
+    static_assert(HD % 8 == 0 && HD <= 64, "head dimension: a multiple of 8, at most 64");
+    constexpr int KS = HD / 2, DT = (HD + 31) / 32;
+    constexpr int LDV = (4 * HD) % 64 == 32 ? HD : HD + 8;   // V rows j and j + 4 in disjoint bank halves
+    __shared__ float vs[64 * LDV];
+    const uint32_t sample = blockIdx.x / heads, head = blockIdx.x % heads;
+    const int lane = threadIdx.x, r = lane & 31, hh = lane >> 5;
+    const uint32_t d = heads * HD;
+    const float* base = qkv + (size_t)sample * 62 * 3 * d;
+    for (int i = lane; i < 64 * (HD / 4); i += 64) {
+        const int t = i / (HD / 4), e4 = i % (HD / 4);
+        const float4 v = t < 62 ? *(const float4*)(base + (size_t)t * 3 * d + 2 * d + head * HD + 4 * e4)
+                                : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        *(float4*)&vs[t * LDV + 4 * e4] = v;
+    }
+    // K fragments of both key tiles: kf[b][s] = K[32b + r][hh KS + s] (step s pairs dimensions s
+    // and KS + s: any pairing works if Q uses the same, and this one is two contiguous runs)
+    float kf[2][KS];
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+        const int j = 32 * b + r;
+        const float4* kr = (const float4*)(base + (size_t)(j < 62 ? j : 0) * 3 * d + d + head * HD + hh * KS);
+#pragma unroll
+        for (int s4 = 0; s4 < KS / 4; ++s4) {
+            const float4 v = j < 62 ? kr[s4] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            kf[b][4 * s4] = v.x; kf[b][4 * s4 + 1] = v.y; kf[b][4 * s4 + 2] = v.z; kf[b][4 * s4 + 3] = v.w;
+        }
+    }
+    __syncthreads();
+    const float sl = scale * 1.4426950408889634f;
+#pragma unroll 1
+    for (int a = 0; a < 2; ++a) {
+        const int i = 32 * a + r;                      // this lane's query
+        float qf[KS];
+        {
+            const float4* qr = (const float4*)(base + (size_t)(i < 62 ? i : 0) * 3 * d + head * HD + hh * KS);
+#pragma unroll
+            for (int s4 = 0; s4 < KS / 4; ++s4) {
+                const float4 v = i < 62 ? qr[s4] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                qf[4 * s4] = v.x * sl; qf[4 * s4 + 1] = v.y * sl; qf[4 * s4 + 2] = v.z * sl; qf[4 * s4 + 3] = v.w * sl;
+            }
+        }
+        f32x16_t st[2] = {f32x16_t{0}, f32x16_t{0}};
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+#pragma unroll
+            for (int b = 0; b < 2; ++b) st[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(kf[b][s], qf[s], st[b], 0, 0, 0);
+        // keys 62, 63 (tile 1, rows 30, 31: g = 14, 15 of the upper half) take no weight
+        if (hh) { st[1][14] = -INFINITY; st[1][15] = -INFINITY; }
+        float m = -INFINITY;
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int g = 0; g < 16; ++g) m = fmaxf(m, st[b][g]);
+        m = fmaxf(m, __shfl_xor(m, 32));
+        float l = 0.0f;
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int g = 0; g < 16; ++g) {
+                const float pv = exp2f(st[b][g] - m);
+                st[b][g] = pv;
+                l += pv;
+            }
+        l += __shfl_xor(l, 32);
+        f32x16_t ot[DT];
+#pragma unroll
+        for (int t = 0; t < DT; ++t) ot[t] = f32x16_t{0};
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            // the key tile's V^T fragments, all read before its MFMAs
+            float vf[16][DT];
+#pragma unroll
+            for (int g = 0; g < 16; ++g) {
+                const int j = 32 * b + (g & 3) + 8 * (g >> 2) + 4 * hh;
+#pragma unroll
+                for (int t = 0; t < DT; ++t) {
+                    const int e = 32 * t + r;
+                    vf[g][t] = e < HD ? vs[j * LDV + e] : 0.0f;
+                }
+            }
+#pragma unroll
+            for (int g = 0; g < 16; ++g)
+#pragma unroll
+                for (int t = 0; t < DT; ++t) ot[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(vf[g][t], st[b][g], ot[t], 0, 0, 0);
+        }
+        if (i < 62) {
+            const float inv = 1.0f / l;
+            float* yr = y + ((size_t)sample * 62 + i) * d + head * HD;
+#pragma unroll
+            for (int t = 0; t < DT; ++t)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int e = 32 * t + 8 * q + 4 * hh;
+                    if (e < HD)
+                        *(float4*)(yr + e) = make_float4(ot[t][4 * q] * inv, ot[t][4 * q + 1] * inv, ot[t][4 * q + 2] * inv,
+                                                         ot[t][4 * q + 3] * inv);
+                }
+        }
+    }
+}
+
 }  // namespace net
 }  // namespace dk

@@ -2217,17 +2217,29 @@ int dk_net_gelu_f32_async(void* y, uint64_t n, void* stream) {
     return DK_OK;
 }
 
+#ifndef DK_ATTN_F32_MFMA
+#define DK_ATTN_F32_MFMA 1
+#endif
 int dk_net_attn62_f32_async(const void* qkv, void* y, uint32_t batch, uint32_t heads, uint32_t head_dim, void* stream) {
     if (!qkv || !y || heads == 0 || (head_dim != 40u && head_dim != 64u)) return DK_E_INVALID;
     if (batch == 0) return DK_OK;
     if ((uint64_t)batch * heads > 0x7FFFFFFFull) return DK_E_INVALID;
     const float scale = 1.0f / sqrtf((float)head_dim);
+#if DK_ATTN_F32_MFMA   // f32 matrix cores (default); 0: the VALU kernel
+    if (head_dim == 40u)
+        hipLaunchKernelGGL((dk::net::attn62_f32_mfma_kernel<40>), dim3(batch * heads), dim3(64), 0, (hipStream_t)stream,
+                           (const float*)qkv, (float*)y, batch, heads, scale);
+    else
+        hipLaunchKernelGGL((dk::net::attn62_f32_mfma_kernel<64>), dim3(batch * heads), dim3(64), 0, (hipStream_t)stream,
+                           (const float*)qkv, (float*)y, batch, heads, scale);
+#else
     if (head_dim == 40u)
         hipLaunchKernelGGL((dk::net::attn62_f32_kernel<40>), dim3(batch * heads), dim3(64), 0, (hipStream_t)stream,
                            (const float*)qkv, (float*)y, batch, heads, scale);
     else
         hipLaunchKernelGGL((dk::net::attn62_f32_kernel<64>), dim3(batch * heads), dim3(64), 0, (hipStream_t)stream,
                            (const float*)qkv, (float*)y, batch, heads, scale);
+#endif
     DK_HIP(hipGetLastError());
     return DK_OK;
 }
