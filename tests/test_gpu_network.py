@@ -285,7 +285,8 @@ def test_class_pool_ln_matches_torch(d, C):
 
 @pytest.mark.parametrize("hd", [40, 64])
 def test_attn62_f32_matches_torch(hd):
-    """f32 attention core (one wave per sample and head, online softmax over chunks of 8 keys)
+    """f32 attention core (one wave per sample and head on the f32 matrix cores; -DDK_ATTN_F32_MFMA=0:
+    the VALU kernel with an online softmax over chunks of 8 keys)
     against torch f32 softmax(q k^T / sqrt(hd)) v at full f32 precision."""
     dev = torch.device("cuda", 0)
     torch.manual_seed(13)
