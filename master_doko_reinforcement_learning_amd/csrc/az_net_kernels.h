@@ -680,11 +680,21 @@ __global__ void __launch_bounds__(256, 2) class_pool_ln_kernel(const uint16_t* _
     const uint16_t* xg = xin + (size_t)b * S * D;
     for (int p = threadIdx.x; p < 64 * (D / 8); p += 256) {
         const int t = p / (D / 8), d0 = 8 * (p - t * (D / 8));
-        union { uint4 u; uint16_t s[8]; } v;
-        v.u = t < S ? *(const uint4*)(xg + (size_t)t * D + d0) : make_uint4(0u, 0u, 0u, 0u);
-        *(uint4*)&xs[t * LDX + d0] = v.u;
+        *(uint4*)&xs[t * LDX + d0] = t < S ? *(const uint4*)(xg + (size_t)t * D + d0) : make_uint4(0u, 0u, 0u, 0u);
+    }
+    __syncthreads();
+    // x^T from the rows in LDS: thread (d, t0) gathers 8 tokens of one dimension (2-B reads, a
+    // half-wave on 32 consecutive dimensions of a row) and writes them as two 8-B pieces.  The
+    // direct 2-B scatter of the loaded pieces put 16 lanes on two banks (67 % of LDS cycles
+    // were bank conflicts, profiles/r04/net/pmc_c5net.json).
+    for (int p = threadIdx.x; p < D * 8; p += 256) {
+        const int dd = p % D, t0 = 8 * (p / D);
+        union { uint2 u[2]; uint16_t s[8]; } v;
 #pragma unroll
-        for (int m = 0; m < 8; ++m) xt[(d0 + m) * LDT + t] = v.s[m];
+        for (int m = 0; m < 8; ++m) v.s[m] = xs[(t0 + m) * LDX + dd];
+        uint2* o = (uint2*)&xt[dd * LDT + t0];   // (rows of 136 B: 8-B aligned)
+        o[0] = v.u[0];
+        o[1] = v.u[1];
     }
     __syncthreads();
     const int CT = C > 32 ? 2 : 1, WPC = 4 / CT;       // class tiles, waves per class tile
