@@ -366,8 +366,22 @@ __device__ __forceinline__ void proj_res_ln(const uint16_t* ys, uint16_t* lds_a,
     for (int m = 0; m < 4; ++m)
 #pragma unroll
         for (int j = 0; j < NJ; ++j) acc[m][j] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
+    // Wp fragments one k-step ahead (a two-deep register ring): loaded inside the k-step that
+    // used them, each L2 round trip sat between its load and its four MFMAs, KS x NJ times in a
+    // row (the phase clocks of profiles/r04/net/attn_prof.log: the tail was the longest phase)
+    auto wfrag = [&](int ks, int j) {
+        const int t = wave + 4 * j;
+        return load_frag8(wp + (size_t)(16 * (t < NT ? t : 0) + rl) * D + 32 * ks + 8 * kg, t < NT);
+    };
+    bf16x8_t wr[2][NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) wr[0][j] = wfrag(0, j);
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
+        if (ks + 1 < KS) {
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) wr[(ks + 1) & 1][j] = wfrag(ks + 1, j);
+        }
         bf16x8_t a[4];
 #pragma unroll
         for (int m = 0; m < 4; ++m) a[m] = *(const bf16x8_t*)&ys[(16 * m + rl) * LDY + 32 * ks + 8 * kg];
@@ -375,9 +389,8 @@ __device__ __forceinline__ void proj_res_ln(const uint16_t* ys, uint16_t* lds_a,
         for (int j = 0; j < NJ; ++j) {
             const int t = wave + 4 * j;
             if (t < NT) {
-                const bf16x8_t w = load_frag8(wp + (size_t)(16 * t + rl) * D + 32 * ks + 8 * kg, true);
 #pragma unroll
-                for (int m = 0; m < 4; ++m) acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[m], w, acc[m][j], 0, 0, 0);
+                for (int m = 0; m < 4; ++m) acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[m], wr[ks & 1][j], acc[m][j], 0, 0, 0);
             }
         }
     }
@@ -603,6 +616,15 @@ __device__ __forceinline__ void pack_head(const f32x16_t (&acc)[2][2], bf16x8_t 
         }
 }
 
+// Phase clocks of qkv_attn_ln_kernel (profiling builds, -DDK_NET_PROF): wave 0 of each
+// workgroup stamps the shader clock after each phase; dk_net_prof_read sums them.
+#ifdef DK_NET_PROF
+__device__ unsigned long long dk_net_prof_acc[8];
+#define DK_NSTAMP(k) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    if (threadIdx.x == 0) atomicAdd(&dk_net_prof_acc[k], t_ - t_prev); t_prev = t_; } while (0)
+#else
+#define DK_NSTAMP(k) ((void)0)
+#endif
 template <int HD>
 __global__ void __launch_bounds__(256, HD == 40 ? DK_QKV_WPE : 2) qkv_attn_ln_kernel(const uint16_t* __restrict__ h_in, uint16_t* __restrict__ x_io,
                                                              const uint16_t* __restrict__ wqkv, const uint16_t* __restrict__ bqkv,
@@ -617,12 +639,16 @@ __global__ void __launch_bounds__(256, HD == 40 ? DK_QKV_WPE : 2) qkv_attn_ln_ke
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t b = blockIdx.x;                                                // one sample per workgroup
     (void)batch;
+#ifdef DK_NET_PROF
+    unsigned long long t_prev = __builtin_amdgcn_s_memtime();
+#endif
     const uint16_t* hg = h_in + (size_t)b * S * D;
     for (int p = threadIdx.x; p < 64 * (D / 8); p += 256) {
         const int rr = p / (D / 8), kp = p - rr * (D / 8);
         *(uint4*)&ys[rr * LDY + 8 * kp] = rr < S ? *(const uint4*)(hg + 8 * p) : make_uint4(0u, 0u, 0u, 0u);
     }
     __syncthreads();
+    DK_NSTAMP(0);
     const int hh = lane >> 5, r = lane & 31;
     const uint16_t* wh = wqkv + (size_t)wave * HD * D;   // the head's q rows; k, v rows d and 2 d further
     const uint16_t* bh = bqkv + wave * HD;
@@ -641,15 +667,21 @@ __global__ void __launch_bounds__(256, HD == 40 ? DK_QKV_WPE : 2) qkv_attn_ln_ke
                     vt[m * LDT + 32 + r] = f2bf(acc[dt][1][g]);
                 }
             }
+        DK_NSTAMP(1);
         head_tiles<HD, D>(ys, wh + (size_t)D * D, bh + D, acc);            // K^T
         pack_head<HD>(acc, kf);
+        DK_NSTAMP(2);
         head_tiles<HD, D>(ys, wh, bh, acc);                                // Q^T
         pack_head<HD>(acc, qf);
+        DK_NSTAMP(3);
     }
     // attn62_core's barrier also ends every wave's reads of the h rows: y may then overwrite them
     attn62_core<HD>(qf, kf, vt, scale, true, [&](int s, int e, float v) { ys[s * LDY + wave * HD + e] = f2bf(v); });
+    DK_NSTAMP(4);
     __syncthreads();   // y complete (rows 62, 63 still the zero h padding); the V^T tiles are dead
+    DK_NSTAMP(5);
     proj_res_ln<HD>(ys, lds_a, x_io, wp, bp, b, gamma, beta, eps, h_out);
+    DK_NSTAMP(6);
 }
 
 // ---------------------------------------------------------------------------

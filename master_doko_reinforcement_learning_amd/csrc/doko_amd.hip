@@ -2091,6 +2091,15 @@ int dk_net_mlp_ln_bf16_async(const void* h, void* x_io, const void* w1, const vo
     return DK_OK;
 }
 
+#ifdef DK_NET_PROF
+// profiling builds: the summed phase clocks of qkv_attn_ln_kernel since the last read (then cleared)
+extern "C" int dk_net_prof_read(uint64_t* out8) {
+    DK_HIP(hipMemcpyFromSymbol(out8, HIP_SYMBOL(dk::net::dk_net_prof_acc), 8 * sizeof(uint64_t)));
+    const uint64_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    DK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(dk::net::dk_net_prof_acc), z, sizeof(z)));
+    return DK_OK;
+}
+#endif
 int dk_net_class_pool_ln_bf16_async(const void* x, uint32_t batch, uint32_t d, const void* queries, uint32_t classes,
                                     float scale, const void* ln_w, const void* ln_b, float eps, void* out, void* stream) {
     if (!x || !queries || !ln_w || !ln_b || !out || classes == 0 || classes > 64u || (d != 160u && d != 256u))
