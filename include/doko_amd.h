@@ -520,7 +520,8 @@ int dk_net_attn62_bf16_async(const void* qkv, void* y, uint32_t batch, uint32_t 
  * az_doko.py:379-400, 539-541).  d % 4 == 0, d <= 512; f32 tables / gamma / beta / activations.
  * dk_net_embed_ln_f32_async: x = e0[t0] + e1[t1] + ... + e5[t5] (f32, left to right), h = LN(x).
  * dk_net_add_ln_f32_async:   x += delta (delta may be NULL), h = LN(x).
- * dk_net_attn62_f32_async:   softmax(q k^T / sqrt(head_dim)) v, 62 tokens, q/k/v read from qkv[batch*62][3d]
+ * dk_net_attn62_f32_async:   softmax(q k^T / sqrt(head_dim)) v on the f32 matrix cores (f32 products and sums),
+ *                            62 tokens, q/k/v read from qkv[batch*62][3d]
  *                            (heads contiguous), y[batch*62][d]; head_dim 40 or 64.
  * dk_net_gelu_f32_async:     y = GELU(y) in place (exact erf form), n elements, n % 4 == 0. */
 int dk_net_embed_ln_f32_async(const int32_t* d_tokens, uint32_t batch, const void* const* tables, uint32_t d,
