@@ -620,6 +620,7 @@ __device__ __forceinline__ void pack_head(const f32x16_t (&acc)[2][2], bf16x8_t 
 // workgroup stamps the shader clock after each phase; dk_net_prof_read sums them.
 #ifdef DK_NET_PROF
 __device__ unsigned long long dk_net_prof_acc[8];
+__device__ unsigned long long dk_mlp_prof_acc[16];   // mlp_ln_kernel: [wave 0 | wave 4][phase]
 #define DK_NSTAMP(k) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
     if (threadIdx.x == 0) atomicAdd(&dk_net_prof_acc[k], t_ - t_prev); t_prev = t_; } while (0)
 #else
@@ -1123,6 +1124,13 @@ __global__ void __launch_bounds__(64 * WAVES, WAVES == 8 ? 1 : DK_MLP_MINB) mlp_
     __shared__ float b1s[MLP_MAX_HIDDEN];           // the hidden units' biases
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
     const uint32_t row = blockIdx.x * (32u * WAVES) + (uint32_t)wave * 32u + (uint32_t)r;
+#ifdef DK_NET_PROF
+    unsigned long long m_prev = __builtin_amdgcn_s_memtime();
+#define DK_MSTAMP(k) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    if (lane == 0 && (wave == 0 || wave == 4)) atomicAdd(&dk_mlp_prof_acc[(wave ? 8 : 0) + (k)], t_ - m_prev); m_prev = t_; } while (0)
+#else
+#define DK_MSTAMP(k) ((void)0)
+#endif
     const bool ok = row < rows;
     bf16x8_t hf[KS];
     {
@@ -1283,21 +1291,28 @@ __global__ void __launch_bounds__(64 * WAVES, WAVES == 8 ? 1 : DK_MLP_MINB) mlp_
             return;
         }
         if (c > 0) gelu_gemm2(c - 1);
+        DK_MSTAMP(1);
         if constexpr (!L) {
             if (early) {
                 DK_MLP_STORE_CHUNK((c + 1) % NB)
+                DK_MSTAMP(2);
                 sync();
+                DK_MSTAMP(3);
             }
         }
         gemm1(c);
         if constexpr (L) prefetch_x();
+        DK_MSTAMP(4);
         if constexpr (!L) {
             if (!early) {
                 DK_MLP_STORE_CHUNK((c + 1) % NB)
+                DK_MSTAMP(2);
                 sync();
+                DK_MSTAMP(3);
             }
         }
     };
+    DK_MSTAMP(0);
     for (uint32_t c = 0; c + 1 < chunks; ++c) iteration(c, std::false_type{});
     iteration(chunks - 1, std::true_type{});
     if constexpr (SKEW) gelu_gemm2(chunks - 1);
@@ -1366,7 +1381,9 @@ __global__ void __launch_bounds__(64 * WAVES, WAVES == 8 ? 1 : DK_MLP_MINB) mlp_
             else if (ok) *(uint2*)(hr + col) = make_uint2(pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]));
         }
     if constexpr (WIDE) mlp_store_row16<OT>(xv, hr, hh, ok);
+    DK_MSTAMP(5);
 }
+#undef DK_MSTAMP
 #undef DK_MLP_LD
 #undef DK_MLP_ST
 #undef DK_MLP_LOAD_CHUNK

@@ -2099,6 +2099,13 @@ extern "C" int dk_net_prof_read(uint64_t* out8) {
     DK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(dk::net::dk_net_prof_acc), z, sizeof(z)));
     return DK_OK;
 }
+// the same for mlp_ln_kernel: [wave 0 (early group) | wave 4 (late group)][phase], 16 words
+extern "C" int dk_net_mlp_prof_read(uint64_t* out16) {
+    DK_HIP(hipMemcpyFromSymbol(out16, HIP_SYMBOL(dk::net::dk_mlp_prof_acc), 16 * sizeof(uint64_t)));
+    const uint64_t z[16] = {};
+    DK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(dk::net::dk_mlp_prof_acc), z, sizeof(z)));
+    return DK_OK;
+}
 #endif
 int dk_net_class_pool_ln_bf16_async(const void* x, uint32_t batch, uint32_t d, const void* queries, uint32_t classes,
                                     float scale, const void* ln_w, const void* ln_b, float eps, void* out, void* stream) {
