@@ -1125,9 +1125,10 @@ __global__ void __launch_bounds__(64 * WAVES, WAVES == 8 ? 1 : DK_MLP_MINB) mlp_
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
     const uint32_t row = blockIdx.x * (32u * WAVES) + (uint32_t)wave * 32u + (uint32_t)r;
 #ifdef DK_NET_PROF
-    unsigned long long m_prev = __builtin_amdgcn_s_memtime();
-#define DK_MSTAMP(k) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
-    if (lane == 0 && (wave == 0 || wave == 4)) atomicAdd(&dk_mlp_prof_acc[(wave ? 8 : 0) + (k)], t_ - m_prev); m_prev = t_; } while (0)
+    // phase sums in registers, one atomic per phase at the end (mid-kernel atomics would sit in
+    // vmcnt in front of the very loads being timed)
+    unsigned long long m_prev = __builtin_amdgcn_s_memtime(), macc[6] = {0, 0, 0, 0, 0, 0};
+#define DK_MSTAMP(k) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); macc[k] += t_ - m_prev; m_prev = t_; } while (0)
 #else
 #define DK_MSTAMP(k) ((void)0)
 #endif
@@ -1382,6 +1383,10 @@ __global__ void __launch_bounds__(64 * WAVES, WAVES == 8 ? 1 : DK_MLP_MINB) mlp_
         }
     if constexpr (WIDE) mlp_store_row16<OT>(xv, hr, hh, ok);
     DK_MSTAMP(5);
+#ifdef DK_NET_PROF
+    if (lane == 0 && (wave == 0 || wave == 4))
+        for (int k = 0; k < 6; ++k) atomicAdd(&dk_mlp_prof_acc[(wave ? 8 : 0) + k], macc[k]);
+#endif
 }
 #undef DK_MSTAMP
 #undef DK_MLP_LD
