@@ -1037,7 +1037,7 @@ __device__ __forceinline__ f32x2_t gelu_erf2_pk(f32x2_t v) {
 // [0, 5.5]), GELU(v) = max(v, 0) - 0.5 |v| erfc(|v| / sqrt2).  |error| <= 2.5e-7 over all v
 // (f32 evaluation, checked against the f64 erf form on a 4M-point grid of [-12, 12]); a third
 // of the bf16 rounding flips of the A&S 7.1.26 form above.  9 VALU + 1 transcendental per
-// value against 13 + 2.
+// value against 13 + 2 (the abs values are source modifiers).
 #ifndef DK_GELU_POLY
 #define DK_GELU_POLY 1
 #endif
@@ -1050,8 +1050,8 @@ __device__ __forceinline__ float gelu_poly(float v) {
     q = fmaf(q, a, -0.05338268727064133f);
     q = fmaf(q, a, -0.45883968472480774f);
     q = fmaf(q, a, -1.1511608362197876f);
-    q *= a;
-    return fmaf(-0.5f * fabsf(v), __builtin_amdgcn_exp2f(q), fmaxf(v, 0.0f));
+    // 0.5 erfc = exp2(a P(a) - 1): the halving rides in the last fma, not in a multiply of |v|
+    return fmaf(-fabsf(v), __builtin_amdgcn_exp2f(fmaf(q, a, -1.0f)), fmaxf(v, 0.0f));
 }
 
 // f32 pair -> two bf16 (round to nearest even, NaN kept), one v_cvt_pk_bf16_f32
