@@ -974,14 +974,17 @@ hipError_t copy_out(dk_ctx* ctx, void* dst, const void* src, size_t bytes) {
     hipError_t e = hipSuccess;
     const size_t off = (ctx->pinned_used + 255) & ~(size_t)255;
     if (off + bytes > ctx->pinned_size) {
-        // drain what is queued, then grow
+        // drain what is queued, then grow to hold everything this call has queued so far (the
+        // next call with the same sizes then fits without a mid-call drain)
+        const size_t want = off + bytes;
         if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) { ctx->outs.clear(); ctx->pinned_used = 0; return e; }
         flush_outs(ctx);
-        if (bytes > ctx->pinned_size) {
+        if (want > ctx->pinned_size) {
             if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+            const size_t grown = 2 * ctx->pinned_size > want ? 2 * ctx->pinned_size : want;
             ctx->pinned = nullptr;
             ctx->pinned_size = 0;
-            const size_t sz = bytes < ((size_t)1 << 20) ? ((size_t)1 << 20) : bytes;
+            const size_t sz = grown < ((size_t)1 << 20) ? ((size_t)1 << 20) : grown;
             if ((e = hipHostMalloc((void**)&ctx->pinned, sz, hipHostMallocDefault)) != hipSuccess) { ctx->pinned = nullptr; return e; }
             ctx->pinned_size = sz;
         }
