@@ -530,6 +530,17 @@ int dk_net_add_ln_f32_async(void* x_io, const void* delta, uint32_t rows, uint32
                             float eps, void* h_out, void* stream);
 int dk_net_attn62_f32_async(const void* qkv, void* y, uint32_t batch, uint32_t heads, uint32_t head_dim, void* stream);
 int dk_net_gelu_f32_async(void* y, uint64_t n, void* stream);
+/* The same with the producing GEMM's bias applied first (so the GEMM itself runs without its bias
+ * epilogue: hipBLASLt's f32 GEMMs at matmul precision "medium" take ~2x longer with it,
+ * profiles/r04/fp32_bias_probe.log).  bias may be NULL.
+ * dk_net_add_bias_ln_f32_async: x += (delta + bias[col]), h = LN(x)   (torch: delta = F.linear(.., b))
+ * dk_net_gelu_bias_f32_async:   y = GELU(y + bias[i % width]), width % 4 == 0, n % width == 0
+ * dk_net_attn62_bias_f32_async: q, k, v = qkv + bqkv[3d] as they load, then as dk_net_attn62_f32_async */
+int dk_net_add_bias_ln_f32_async(void* x_io, const void* delta, const void* bias, uint32_t rows, uint32_t d,
+                                 const void* gamma, const void* beta, float eps, void* h_out, void* stream);
+int dk_net_gelu_bias_f32_async(void* y, const void* bias, uint64_t n, uint32_t width, void* stream);
+int dk_net_attn62_bias_f32_async(const void* qkv, const void* bqkv, void* y, uint32_t batch, uint32_t heads,
+                                 uint32_t head_dim, void* stream);
 
 /* ---- completion / errors / timing of *_async work -------------------------------
  * dk_sync: waits for the stream and returns the first device-side error

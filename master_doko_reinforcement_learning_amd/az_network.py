@@ -233,26 +233,35 @@ class FusedTrunkF32(FusedTrunk):
         self.ck(self.L.dk_net_embed_ln_f32_async(tok.data_ptr(), B, tables, d, ln0.weight.data_ptr(), ln0.bias.data_ptr(),
                                                  ln0.eps, self.x.data_ptr(), self.h.data_ptr(), self.st))
 
-    def add_ln(self, x, delta, ln):
+    # The GEMMs run without their bias (hipBLASLt's f32 GEMMs at "medium" take about twice as long
+    # with the bias epilogue, profiles/r04/fp32_bias_probe.log); each bias is added, in the
+    # epilogue's order (GEMM output + bias, then the next op), by the f32 kernel that reads the
+    # GEMM's output.
+    def add_ln(self, x, delta, ln, bias=None):
         h = torch.empty_like(x)
-        self.ck(self.L.dk_net_add_ln_f32_async(x.data_ptr(), delta.data_ptr() if delta is not None else None, self.rows,
-                                               self.d, ln.weight.data_ptr(), ln.bias.data_ptr(), ln.eps, h.data_ptr(), self.st))
+        self.ck(self.L.dk_net_add_bias_ln_f32_async(x.data_ptr(), delta.data_ptr() if delta is not None else None,
+                                                    bias.data_ptr() if bias is not None else None, self.rows, self.d,
+                                                    ln.weight.data_ptr(), ln.bias.data_ptr(), ln.eps, h.data_ptr(),
+                                                    self.st))
         return h
 
     def attn_ln(self, x, blk, h, ln):
         if not (self.d % blk.heads == 0 and self.d // blk.heads in (40, 64)):
             return self.add_ln(x, blk.attn_delta(h), ln)
-        qkv = F.linear(h, blk.qkv.weight, blk.qkv.bias).contiguous()     # [B, 62, 3d]: q | k | v, heads contiguous
+        qkv = F.linear(h, blk.qkv.weight).contiguous()                   # [B, 62, 3d]: q | k | v, heads contiguous
         y = torch.empty_like(h)
-        self.ck(self.L.dk_net_attn62_f32_async(qkv.data_ptr(), y.data_ptr(), h.shape[0], blk.heads, self.d // blk.heads,
-                                               self.st))
+        bq = blk.qkv.bias.contiguous() if blk.qkv.bias is not None else None
+        self.ck(self.L.dk_net_attn62_bias_f32_async(qkv.data_ptr(), bq.data_ptr() if bq is not None else None,
+                                                    y.data_ptr(), h.shape[0], blk.heads, self.d // blk.heads, self.st))
         w, b = blk.folded_proj()
-        return self.add_ln(x, F.linear(y, w, b), ln)
+        return self.add_ln(x, F.linear(y, w), ln, b)
 
     def mlp_ln(self, x, blk, h, ln):
-        a = F.linear(h, blk.fc.weight, blk.fc.bias).contiguous()
-        self.ck(self.L.dk_net_gelu_f32_async(a.data_ptr(), a.numel(), self.st))
-        return self.add_ln(x, blk.proj(a), ln)
+        a = F.linear(h, blk.fc.weight).contiguous()
+        b1 = blk.fc.bias.contiguous() if blk.fc.bias is not None else None
+        self.ck(self.L.dk_net_gelu_bias_f32_async(a.data_ptr(), b1.data_ptr() if b1 is not None else None, a.numel(),
+                                                  a.shape[-1], self.st))
+        return self.add_ln(x, F.linear(a, blk.proj.weight), ln, blk.proj.bias)
 
 
 class DokoAzNet(nn.Module):

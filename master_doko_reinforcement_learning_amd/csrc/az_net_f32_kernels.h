@@ -90,7 +90,8 @@ __global__ void embed_ln_f32_kernel(const int32_t* __restrict__ tokens, uint32_t
 
 template <int P4>
 __global__ void add_ln_f32_kernel(float* __restrict__ x_io, const float* __restrict__ delta, uint32_t rows, int d,
-                                  const float* gamma, const float* beta, float eps, float* __restrict__ h_out) {
+                                  const float* gamma, const float* beta, float eps, float* __restrict__ h_out,
+                                  const float* __restrict__ bias = nullptr) {
     const uint32_t row = blockIdx.x * (blockDim.x / 32) + threadIdx.x / 32;
     const int lane = threadIdx.x & 31, n4 = d / 4;
     if (row >= rows) return;
@@ -104,7 +105,11 @@ __global__ void add_ln_f32_kernel(float* __restrict__ x_io, const float* __restr
         if (j < n4) {
             float4 v = xr[j];
             if (dr) {
-                const float4 e = dr[j];
+                float4 e = dr[j];
+                if (bias) {   // the GEMM's bias, added to its output first (torch's F.linear epilogue order)
+                    const float4 b = ((const float4*)bias)[j];
+                    e.x += b.x; e.y += b.y; e.z += b.z; e.w += b.w;
+                }
                 v.x += e.x; v.y += e.y; v.z += e.z; v.w += e.w;
                 xr[j] = v;
             }
@@ -114,11 +119,16 @@ __global__ void add_ln_f32_kernel(float* __restrict__ x_io, const float* __restr
     ln_row_f32<P4>(x, d, lane, (const float4*)gamma, (const float4*)beta, eps, (float4*)(h_out + (size_t)row * d));
 }
 
-// GELU(v) = 0.5 v (1 + erf(v / sqrt 2)), the exact form (libm erff)
-__global__ void gelu_f32_kernel(float* __restrict__ y, size_t n4) {
+// GELU(v) = 0.5 v (1 + erf(v / sqrt 2)), the exact form (libm erff); bias (may be NULL): the
+// producing GEMM's bias over rows of w4 float4 groups, added first
+__global__ void gelu_f32_kernel(float* __restrict__ y, size_t n4, const float* __restrict__ bias = nullptr, uint32_t w4 = 1) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n4) return;
     float4 v = ((float4*)y)[i];
+    if (bias) {
+        const float4 b = ((const float4*)bias)[i % w4];
+        v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
+    }
     v.x = 0.5f * v.x * (1.0f + erff(v.x * 0.70710678118654752f));
     v.y = 0.5f * v.y * (1.0f + erff(v.y * 0.70710678118654752f));
     v.z = 0.5f * v.z * (1.0f + erff(v.z * 0.70710678118654752f));
@@ -231,7 +241,8 @@ typedef float f32x16_t __attribute__((ext_vector_type(16)));
 #endif
 template <int HD>
 __global__ void __launch_bounds__(64, HD == 40 ? DK_ATTNF32_WAVES40 : 2) attn62_f32_mfma_kernel(const float* __restrict__ qkv, float* __restrict__ y,
-                                                             uint32_t batch, uint32_t heads, float scale) {
+                                                             uint32_t batch, uint32_t heads, float scale,
+                                                             const float* __restrict__ bqkv = nullptr) {
     static_assert(HD % 8 == 0 && HD <= 64, "head dimension: a multiple of 8, at most 64");
     constexpr int KS = HD / 2, DT = (HD + 31) / 32;
     constexpr int LDV = (4 * HD) % 64 == 32 ? HD : HD + 8;   // V rows j and j + 4 in disjoint bank halves
@@ -240,10 +251,17 @@ __global__ void __launch_bounds__(64, HD == 40 ? DK_ATTNF32_WAVES40 : 2) attn62_
     const int lane = threadIdx.x, r = lane & 31, hh = lane >> 5;
     const uint32_t d = heads * HD;
     const float* base = qkv + (size_t)sample * 62 * 3 * d;
+    // the qkv GEMM's bias (may be NULL; q | k | v segments of 3d) is added as the operands load
+    const float4 zero4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    auto badd = [&](float4 v, int off) {
+        if (bqkv) { const float4 b = *(const float4*)(bqkv + off); v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w; }
+        return v;
+    };
     for (int i = lane; i < 64 * (HD / 4); i += 64) {
         const int t = i / (HD / 4), e4 = i % (HD / 4);
-        const float4 v = t < 62 ? *(const float4*)(base + (size_t)t * 3 * d + 2 * d + head * HD + 4 * e4)
-                                : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        const float4 v = t < 62 ? badd(*(const float4*)(base + (size_t)t * 3 * d + 2 * d + head * HD + 4 * e4),
+                                       2 * (int)d + (int)head * HD + 4 * e4)
+                                : zero4;
         *(float4*)&vs[t * LDV + 4 * e4] = v;
     }
     // K fragments of both key tiles: kf[b][s] = K[32b + r][hh KS + s] (step s pairs dimensions s
@@ -255,7 +273,7 @@ __global__ void __launch_bounds__(64, HD == 40 ? DK_ATTNF32_WAVES40 : 2) attn62_
         const float4* kr = (const float4*)(base + (size_t)(j < 62 ? j : 0) * 3 * d + d + head * HD + hh * KS);
 #pragma unroll
         for (int s4 = 0; s4 < KS / 4; ++s4) {
-            const float4 v = j < 62 ? kr[s4] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            const float4 v = j < 62 ? badd(kr[s4], (int)d + (int)head * HD + hh * KS + 4 * s4) : zero4;
             kf[b][4 * s4] = v.x; kf[b][4 * s4 + 1] = v.y; kf[b][4 * s4 + 2] = v.z; kf[b][4 * s4 + 3] = v.w;
         }
     }
@@ -269,7 +287,7 @@ __global__ void __launch_bounds__(64, HD == 40 ? DK_ATTNF32_WAVES40 : 2) attn62_
             const float4* qr = (const float4*)(base + (size_t)(i < 62 ? i : 0) * 3 * d + head * HD + hh * KS);
 #pragma unroll
             for (int s4 = 0; s4 < KS / 4; ++s4) {
-                const float4 v = i < 62 ? qr[s4] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                const float4 v = i < 62 ? badd(qr[s4], (int)head * HD + hh * KS + 4 * s4) : zero4;
                 qf[4 * s4] = v.x * sl; qf[4 * s4 + 1] = v.y * sl; qf[4 * s4 + 2] = v.z * sl; qf[4 * s4 + 3] = v.w * sl;
             }
         }

@@ -2211,6 +2211,10 @@ int dk_net_embed_ln_f32_async(const int32_t* d_tokens, uint32_t batch, const voi
 
 int dk_net_add_ln_f32_async(void* x_io, const void* delta, uint32_t rows, uint32_t d, const void* gamma, const void* beta,
                             float eps, void* h_out, void* stream) {
+    return dk_net_add_bias_ln_f32_async(x_io, delta, nullptr, rows, d, gamma, beta, eps, h_out, stream);
+}
+int dk_net_add_bias_ln_f32_async(void* x_io, const void* delta, const void* bias, uint32_t rows, uint32_t d,
+                                 const void* gamma, const void* beta, float eps, void* h_out, void* stream) {
     const int p4 = p4_of(d);
     if (!x_io || !h_out || !gamma || !beta || p4 == 0) return DK_E_INVALID;
     if (rows == 0) return DK_OK;
@@ -2218,7 +2222,8 @@ int dk_net_add_ln_f32_async(void* x_io, const void* delta, uint32_t rows, uint32
     hipStream_t st = (hipStream_t)stream;
     switch (p4) {
 #define M(P) case P: hipLaunchKernelGGL(dk::net::add_ln_f32_kernel<P>, grid, block, 0, st, (float*)x_io, (const float*)delta, \
-                                        rows, (int)d, (const float*)gamma, (const float*)beta, eps, (float*)h_out); break;
+                                        rows, (int)d, (const float*)gamma, (const float*)beta, eps, (float*)h_out,          \
+                                        (const float*)bias); break;
         DK_P4_CASES(M)
 #undef M
     }
@@ -2226,12 +2231,13 @@ int dk_net_add_ln_f32_async(void* x_io, const void* delta, uint32_t rows, uint32
     return DK_OK;
 }
 
-int dk_net_gelu_f32_async(void* y, uint64_t n, void* stream) {
-    if (!y || n % 4u) return DK_E_INVALID;
+int dk_net_gelu_f32_async(void* y, uint64_t n, void* stream) { return dk_net_gelu_bias_f32_async(y, nullptr, n, 4u, stream); }
+int dk_net_gelu_bias_f32_async(void* y, const void* bias, uint64_t n, uint32_t width, void* stream) {
+    if (!y || n % 4u || width == 0 || width % 4u || n % width) return DK_E_INVALID;
     if (n == 0) return DK_OK;
     const uint64_t n4 = n / 4u;
     hipLaunchKernelGGL(dk::net::gelu_f32_kernel, dim3((unsigned)((n4 + 255u) / 256u)), dim3(256), 0, (hipStream_t)stream,
-                       (float*)y, (size_t)n4);
+                       (float*)y, (size_t)n4, (const float*)bias, width / 4u);
     DK_HIP(hipGetLastError());
     return DK_OK;
 }
@@ -2240,6 +2246,10 @@ int dk_net_gelu_f32_async(void* y, uint64_t n, void* stream) {
 #define DK_ATTN_F32_MFMA 1
 #endif
 int dk_net_attn62_f32_async(const void* qkv, void* y, uint32_t batch, uint32_t heads, uint32_t head_dim, void* stream) {
+    return dk_net_attn62_bias_f32_async(qkv, nullptr, y, batch, heads, head_dim, stream);
+}
+int dk_net_attn62_bias_f32_async(const void* qkv, const void* bqkv, void* y, uint32_t batch, uint32_t heads, uint32_t head_dim,
+                                 void* stream) {
     if (!qkv || !y || heads == 0 || (head_dim != 40u && head_dim != 64u)) return DK_E_INVALID;
     if (batch == 0) return DK_OK;
     if ((uint64_t)batch * heads > 0x7FFFFFFFull) return DK_E_INVALID;
@@ -2247,11 +2257,12 @@ int dk_net_attn62_f32_async(const void* qkv, void* y, uint32_t batch, uint32_t h
 #if DK_ATTN_F32_MFMA   // f32 matrix cores (default); 0: the VALU kernel
     if (head_dim == 40u)
         hipLaunchKernelGGL((dk::net::attn62_f32_mfma_kernel<40>), dim3(batch * heads), dim3(64), 0, (hipStream_t)stream,
-                           (const float*)qkv, (float*)y, batch, heads, scale);
+                           (const float*)qkv, (float*)y, batch, heads, scale, (const float*)bqkv);
     else
         hipLaunchKernelGGL((dk::net::attn62_f32_mfma_kernel<64>), dim3(batch * heads), dim3(64), 0, (hipStream_t)stream,
-                           (const float*)qkv, (float*)y, batch, heads, scale);
+                           (const float*)qkv, (float*)y, batch, heads, scale, (const float*)bqkv);
 #else
+    if (bqkv) return DK_E_INVALID;   // (the VALU kernel takes the biased qkv only)
     if (head_dim == 40u)
         hipLaunchKernelGGL((dk::net::attn62_f32_kernel<40>), dim3(batch * heads), dim3(64), 0, (hipStream_t)stream,
                            (const float*)qkv, (float*)y, batch, heads, scale);
