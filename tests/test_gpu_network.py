@@ -338,3 +338,42 @@ def test_f32_row_kernels_match_torch(d):
     assert _lib().dk_net_gelu_f32_async(a2.data_ptr(), a2.numel(), st) == 0
     torch.cuda.synchronize()
     torch.testing.assert_close(a2, F.gelu(a), rtol=2e-6, atol=2e-6)
+
+
+@pytest.mark.parametrize("d", [160, 256])
+def test_f32_bias_kernels_match_torch(d):
+    """The f32 kernels that take the producing GEMM's bias (the GEMMs then run without their
+    bias epilogue): GELU(y + b) and x += (delta + b), h = LN(x), and the attention core with the
+    qkv bias added as q / k / v load -- against torch f32 in the epilogue's order."""
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(d + 7)
+    B = 29
+    st = torch.cuda.current_stream(dev).cuda_stream
+    n = 4 * d
+    y = torch.randn(B * 62, n, device=dev)
+    b = torch.randn(n, device=dev)
+    ref = F.gelu(y + b)
+    assert _lib().dk_net_gelu_bias_f32_async(y.data_ptr(), b.data_ptr(), y.numel(), n, st) == 0
+    torch.cuda.synchronize()
+    torch.testing.assert_close(y, ref, rtol=1e-6, atol=1e-6)
+    x = torch.randn(B * 62, d, device=dev)
+    delta = torch.randn(B * 62, d, device=dev)
+    bd = torch.randn(d, device=dev)
+    g, be = 1 + 0.1 * torch.randn(d, device=dev), 0.1 * torch.randn(d, device=dev)
+    x_ref = x + (delta + bd)
+    h_ref = F.layer_norm(x_ref, (d,), g, be, 1e-5)
+    h = torch.empty_like(x)
+    assert _lib().dk_net_add_bias_ln_f32_async(x.data_ptr(), delta.data_ptr(), bd.data_ptr(), B * 62, d, g.data_ptr(),
+                                               be.data_ptr(), 1e-5, h.data_ptr(), st) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(x, x_ref)
+    torch.testing.assert_close(h, h_ref, rtol=1e-5, atol=1e-5)
+    hd = d // 4
+    qkv = torch.randn(B, 62, 3 * d, device=dev) * 1.5
+    bq = torch.randn(3 * d, device=dev)
+    out = torch.empty(B, 62, d, device=dev)
+    assert _lib().dk_net_attn62_bias_f32_async(qkv.data_ptr(), bq.data_ptr(), out.data_ptr(), B, 4, hd, st) == 0
+    torch.cuda.synchronize()
+    q, k, v = (qkv + bq).double().view(B, 62, 3, 4, hd).permute(2, 0, 3, 1, 4)
+    ref = (torch.softmax(q @ k.transpose(-1, -2) / hd ** 0.5, dim=-1) @ v).transpose(1, 2).reshape(B, 62, d)
+    torch.testing.assert_close(out.double(), ref, rtol=2e-5, atol=2e-5)
