@@ -1033,23 +1033,23 @@ __device__ __forceinline__ f32x2_t gelu_erf2_pk(f32x2_t v) {
 }
 
 // GELU with erfc from one exp2 and no reciprocal (round 4): with a = min(|v|, 5.5),
-// log2 erfc(a / sqrt2) ~= a (c0 + c1 a + ... + c6 a^6) (weighted least-squares fit on
-// [0, 5.5]), GELU(v) = max(v, 0) - 0.5 |v| erfc(|v| / sqrt2).  |error| <= 2.5e-7 over all v
-// (f32 evaluation, checked against the f64 erf form on a 4M-point grid of [-12, 12]); a third
-// of the bf16 rounding flips of the A&S 7.1.26 form above.  9 VALU + 1 transcendental per
-// value against 13 + 2 (the abs values are source modifiers).
+// log2 erfc(a / sqrt2) ~= a (c0 + c1 a + ... + c5 a^5) (least squares on [0, 5.5] weighted by
+// 0.5 a erfc, the GELU error it causes), GELU(v) = max(v, 0) - 0.5 |v| erfc(|v| / sqrt2).
+// |error| <= 2.9e-7 over all v (f32 evaluation in the kernel's fma order against the f64 erf
+// form, tests/test_cpu_gelu_poly.py); a third of the bf16 rounding flips of the A&S 7.1.26 form
+// above.  8 VALU + 1 transcendental per value against 13 + 2 (the abs values are source
+// modifiers).
 #ifndef DK_GELU_POLY
 #define DK_GELU_POLY 1
 #endif
 __device__ __forceinline__ float gelu_poly(float v) {
     const float a = fminf(fabsf(v), 5.5f);
-    float q = -3.68217712320984e-07f;
-    q = fmaf(q, a, 3.816817479673773e-05f);
-    q = fmaf(q, a, -0.0007888087420724332f);
-    q = fmaf(q, a, 0.008100297302007675f);
-    q = fmaf(q, a, -0.05338268727064133f);
-    q = fmaf(q, a, -0.45883968472480774f);
-    q = fmaf(q, a, -1.1511608362197876f);
+    float q = 3.236920019844547e-05f;
+    q = fmaf(q, a, -0.0007541869999840856f);
+    q = fmaf(q, a, 0.008001405745744705f);
+    q = fmaf(q, a, -0.05324144661426544f);
+    q = fmaf(q, a, -0.45893436670303345f);
+    q = fmaf(q, a, -1.1511378288269043f);
     // 0.5 erfc = exp2(a P(a) - 1): the halving rides in the last fma, not in a multiply of |v|
     return fmaf(-fabsf(v), __builtin_amdgcn_exp2f(fmaf(q, a, -1.0f)), fmaxf(v, 0.0f));
 }

@@ -1,7 +1,7 @@
-"""The bf16 network's GELU (az_net_kernels.h gelu_poly): log2 erfc(a / sqrt2) as a P6(a) on
-a = min(|v|, 5.5), GELU(v) = max(v, 0) - |v| exp2(a P6(a) - 1).  Its coefficients are read from
+"""The bf16 network's GELU (az_net_kernels.h gelu_poly): log2 erfc(a / sqrt2) as a P5(a) on
+a = min(|v|, 5.5), GELU(v) = max(v, 0) - |v| exp2(a P5(a) - 1).  Its coefficients are read from
 the kernel header and evaluated in f32 step by step (the kernel's fma order) over a dense grid:
-the absolute error against the f64 erf form stays under 2.5e-7 (the A&S 7.1.26 form it
+the absolute error against the f64 erf form stays under 2.9e-7 (the A&S 7.1.26 form it
 replaced: 3.3e-7)."""
 import os
 import re
@@ -28,7 +28,7 @@ def _fma32(a, b, c):
 
 def test_gelu_poly_error_bound():
     c = _coefficients()
-    assert len(c) == 7
+    assert len(c) == 6
     v = np.linspace(-12.0, 12.0, 2_000_001).astype(np.float32)
     a = np.minimum(np.abs(v), np.float32(5.5))
     q = np.full_like(a, c[0])
@@ -37,4 +37,4 @@ def test_gelu_poly_error_bound():
     e = np.exp2(_fma32(q, a, np.full_like(a, -1.0))).astype(np.float32)
     g = _fma32(-np.abs(v), e, np.maximum(v, np.float32(0.0)))
     ref = 0.5 * v.astype(np.float64) * (1.0 + erf(v.astype(np.float64) / np.sqrt(2.0)))
-    assert np.abs(g - ref).max() < 2.5e-7
+    assert np.abs(g - ref).max() < 2.9e-7
