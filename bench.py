@@ -609,15 +609,17 @@ def run_c5(args, dk, L, dev, stream, rank, world, local_rank, dist):
 
     ndt, nlabel, npeak, nnote = net_precision(args, torch)
     evaluator = TimedEval(eng, net, dtype=ndt)
-    search = dk.AlphaZeroSearch(eng, 4.0, 0.3, 10, 0.5)
-    dirichlet = torch.distributions.Dirichlet(torch.full((39,), 0.8, device=dev))
+    search = dk.AlphaZeroSearch(eng, 4.0, 0.3, 10, 0.5, dirichlet_alpha=0.8)
     next_seed = [int(seeds[-1]) + 1]
     moves = [0, 0]
+    # one SmallRng per game slot, carried across its searches (the reference's `rng: &mut SmallRng`);
+    # each search draws its root's Dirichlet([0.8; 39]) noise from it (async_mcts.rs:111-113)
+    rng_states = torch.from_numpy(dk.splitmix_rng_states(np.asarray(seeds, dtype=np.uint64) ^ np.uint64(0xA2))
+                                  .view(np.int64).copy()).to(dev)
 
     def step():
-        noise = dirichlet.sample((G,)).float()
         srch = np.arange(G, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15) + np.uint64(next_seed[0])
-        actions, _ = search.mcts_search(records, evaluator, noise, iters, srch)
+        actions, _ = search.mcts_search(records, evaluator, None, iters, srch, rng_states=rng_states)
         dk.az_step(eng, records, actions)
         fin = (records[:, 99] == 3).nonzero().flatten()      # phase byte: Finished -> a fresh deal
         moves[0] += int((actions != 255).sum().item())
@@ -667,8 +669,8 @@ def run_c5(args, dk, L, dev, stream, rank, world, local_rank, dist):
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": nlabel + ", f32 tree statistics",
-            "data": "synthetic: seeded full-doko deals, random-initialised DokoAzNet (d 160, 6 blocks); Dirichlet "
-                    "noise from torch",
+            "data": "synthetic: seeded full-doko deals, random-initialised DokoAzNet (d 160, 6 blocks); root "
+                    "Dirichlet noise drawn on the device from each game's SmallRng (rand_distr 0.5.1)",
             "config": {"workload": "C5 AlphaZero self-play: %d concurrent games x %d PUCT iterations per move per GPU"
                                    % (G, iters),
                        "c_puct": 4.0, "dirichlet": [0.8, 0.3], "temperature": 0.5,

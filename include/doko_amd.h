@@ -373,9 +373,12 @@ int dk_decide_batch(dk_ctx* ctx, const dk_state* infostates, uint32_t n_info, ui
  *
  *   dk_az_begin_async   roots (dk_az_state records) -> d_eval[g] = root  (new_root_node, node.rs:209-244)
  *   network(d_eval)     -> value[n][4] (POV of each state's current player), logits[n][39]
- *   dk_az_root_async    priors = softmax(logits) mixed with the Dirichlet noise d_noise[n][39]
- *                       (1 - eps, eps), restricted to the root's allowed actions and renormalised;
- *                       announcements are offered at the root iff epoch >= 10
+ *   dk_az_root_async    priors = softmax(logits) mixed with the root's Dirichlet noise (1 - eps, eps),
+ *                       restricted to the root's allowed actions and renormalised; announcements are
+ *                       offered at the root iff epoch >= 10.  d_noise == NULL (the reference's way):
+ *                       each game draws Dirichlet([dirichlet_alpha; 39]) from its own SmallRng
+ *                       (rand_distr 0.5.1, async_mcts.rs:111-113; alpha must be > 0.1, the crate's
+ *                       Gamma construction); otherwise d_noise[n][39] is used and nothing is drawn
  *                                                                        (expand_root_node, async_mcts.rs:71-196)
  *   repeat `iterations` times:
  *     dk_az_select_async  PUCT descent, leaf expansion; d_eval[g] = leaf state,
@@ -388,15 +391,19 @@ int dk_decide_batch(dk_ctx* ctx, const dk_state* infostates, uint32_t n_info, ui
  *                       (greedy, last maximum), 1 = infinite (uniform), 2 = finite `temperature`
  *                       (visits^(1/T) WeightedIndex); d_visits[n][39] = root child visits
  *                                                                        (async_mcts.rs:347-405, mcts.rs:185-248)
- * seeds[g] seeds game g's SmallRng (used by the final draws).  The Dirichlet noise is an input:
- * the reference samples it from the search's SmallRng (rand_distr 0.5.1), which is not restated.
+ * seeds[g] seeds game g's SmallRng: the root noise first, then the final draws.
+ *   dk_az_rng_async     set = 1 (between begin and root): game g continues the SmallRng state
+ *                       d_rng[g][4] (Xoshiro256++ words) instead of seeds[g], like the reference's
+ *                       `rng: &mut SmallRng` carried across searches; set = 0 (any time after begin):
+ *                       d_rng[g][4] = game g's current state (after finish: the stream's end state)
  * One AZ search batch per context at a time; node/state pools grow on demand (48 B per node,
  * 1 + 12 (iterations + 1) + 39 nodes and iterations + 2 packed states per game).
  */
 int dk_az_begin_async(dk_ctx* ctx, const dk_az_state* d_roots, const uint64_t* d_seeds, uint32_t n_games,
                       uint32_t iterations, int epoch, dk_az_state* d_eval, void* stream);
-int dk_az_root_async(dk_ctx* ctx, const float* d_value, const float* d_logits, const float* d_noise,
+int dk_az_root_async(dk_ctx* ctx, const float* d_value, const float* d_logits, const float* d_noise, float dirichlet_alpha,
                      float dirichlet_epsilon, void* stream);
+int dk_az_rng_async(dk_ctx* ctx, uint64_t* d_rng, int set, void* stream);
 int dk_az_select_async(dk_ctx* ctx, float c, dk_az_state* d_eval, uint8_t* d_need_eval, void* stream);
 int dk_az_backup_async(dk_ctx* ctx, const float* d_value, const float* d_logits, void* stream);
 int dk_az_finish_async(dk_ctx* ctx, int temperature_mode, float temperature, uint32_t* d_visits, uint8_t* d_action,

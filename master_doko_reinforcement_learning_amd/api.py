@@ -575,21 +575,28 @@ class AlphaZeroSearch:
     temperature: None (greedy), float('inf') (uniform) or a finite T (select_action,
     mcts.rs:185-248)."""
 
-    def __init__(self, engine, puct_exploration_constant=1.0, dirichlet_epsilon=0.25, epoch=10, temperature=None):
+    def __init__(self, engine, puct_exploration_constant=1.0, dirichlet_epsilon=0.25, epoch=10, temperature=None,
+                 dirichlet_alpha=0.8):
         self.engine = engine
         self.c = float(puct_exploration_constant)
         self.eps = float(dirichlet_epsilon)
+        self.alpha = float(dirichlet_alpha)   # AlphaZeroTrainOptions::dirichlet_alpha (az_doko.py:592: 0.8)
         self.epoch = int(epoch)
         self.temperature = temperature
 
-    def mcts_search(self, roots, network, noise, iterations, seeds):
-        """roots: uint8 [n, 160] dk_az_state records (GPU); noise: float32 [n, 39] Dirichlet samples (GPU);
-        seeds: uint64 [n] (SmallRng per game).  Returns (actions uint8 [n], visits int32 [n, 39])."""
+    def mcts_search(self, roots, network, noise, iterations, seeds, rng_states=None):
+        """roots: uint8 [n, 160] dk_az_state records (GPU); seeds: uint64 [n] (SmallRng per game).
+        noise: None (the reference's way: each game draws Dirichlet([dirichlet_alpha; 39]) from its own
+        SmallRng at the root, async_mcts.rs:111-113) or float32 [n, 39] samples (GPU) used instead.
+        rng_states: None, or int64 [n, 4] (GPU) SmallRng states (Xoshiro256++ words) that game g
+        continues instead of seeds[g] and that receive the end states (the reference's
+        `rng: &mut SmallRng`, async_mcts.rs:224-406).
+        Returns (actions uint8 [n], visits int32 [n, 39])."""
         # the launches need a real stream handle shared with torch (handle 0 would
         # select the library's own stream, unordered with the network's kernels)
-        return _run_on_stream(roots.device, self._search, roots, network, noise, iterations, seeds)
+        return _run_on_stream(roots.device, self._search, roots, network, noise, iterations, seeds, rng_states)
 
-    def _search(self, roots, network, noise, iterations, seeds, st):
+    def _search(self, roots, network, noise, iterations, seeds, rng_states, st):
         import torch
         L = _native.lib()
         ctx = self.engine.ctx
@@ -597,14 +604,19 @@ class AlphaZeroSearch:
         dev = roots.device
         seeds_t = torch.as_tensor(np.ascontiguousarray(seeds, dtype=np.uint64).view(np.int64), device=dev)
         roots = roots.contiguous()
-        noise = noise.contiguous().float()
+        noise = None if noise is None else noise.contiguous().float()
         ev = torch.empty((n, AZ_STATE_BYTES), dtype=torch.uint8, device=dev)
         need = torch.empty(n, dtype=torch.uint8, device=dev)
         _check(L.dk_az_begin_async(ctx, roots.data_ptr(), seeds_t.data_ptr(), n, iterations, self.epoch,
                                    ev.data_ptr(), st))
+        if rng_states is not None:
+            if rng_states.dtype != torch.int64 or tuple(rng_states.shape) != (n, 4) or not rng_states.is_contiguous():
+                raise ValueError("rng_states: contiguous int64 [n, 4] expected")
+            _check(L.dk_az_rng_async(ctx, rng_states.data_ptr(), 1, st))
         value, logits = network(ev)
         value, logits = value.float().contiguous(), logits.float().contiguous()
-        _check(L.dk_az_root_async(ctx, value.data_ptr(), logits.data_ptr(), noise.data_ptr(), self.eps, st))
+        _check(L.dk_az_root_async(ctx, value.data_ptr(), logits.data_ptr(), None if noise is None else noise.data_ptr(),
+                                  self.alpha, self.eps, st))
         for _ in range(iterations):
             _check(L.dk_az_select_async(ctx, self.c, ev.data_ptr(), need.data_ptr(), st))
             value, logits = network(ev)
@@ -615,6 +627,8 @@ class AlphaZeroSearch:
         t = self.temperature
         mode, temp = (0, 1.0) if t is None else ((1, 1.0) if np.isinf(t) else (2, float(t)))
         _check(L.dk_az_finish_async(ctx, mode, temp, visits.data_ptr(), actions.data_ptr(), st))
+        if rng_states is not None:
+            _check(L.dk_az_rng_async(ctx, rng_states.data_ptr(), 0, st))
         _check(L.dk_sync(ctx, st))
         return actions, visits
 

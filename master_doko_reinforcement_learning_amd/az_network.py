@@ -11,14 +11,19 @@ with TransformerBlock.py / SelfAttention.py), default config n_embd 160, 4 heads
             then a per-class LN -> Linear(d, d) -> GELU -> Linear(d, 1)
     value [B, 4], policy logits [B, 39]
 
-Re-expressed for MI355X rather than translated:
-  * the attention core is torch's fused scaled_dot_product_attention over a fused
-    qkv projection (the reference's nn.MultiheadAttention in_proj has the same
-    [q; k; v] weight layout, see load_reference_state_dict);
+Re-expressed for MI355X rather than translated (forward_fused):
+  * bf16 inference runs on hand-written gfx950 kernels (csrc/az_net_kernels.h): the
+    embedding sum + first LayerNorm, the whole attention half of a block (qkv projection,
+    MFMA attention core, folded out/c projection, residual add + LayerNorm) in
+    qkv_attn_ln_kernel, the whole MLP half (GEMM + GELU + GEMM + residual + LayerNorm) in
+    mlp_ln_kernel, and the heads' class pooling + LayerNorm in class_pool_ln_kernel;
+  * the reference's f32 precision (FusedTrunkF32, csrc/az_net_f32_kernels.h) for
+    `--net-precision f32`;
   * the 4 + 39 per-class MLPs of the heads run as ONE batched GEMM per layer
     (class-stacked weights [C, d, d]) instead of 43 small launches;
-  * inference runs in bf16 (hipBLASLt GEMMs on the matrix cores); the tokens come
-    straight from the device encoder, no host round trip.
+  * the tokens come straight from the device encoder, no host round trip.
+  forward_torch keeps the reference structure (the qkv projection has the
+  nn.MultiheadAttention in_proj [q; k; v] layout, see load_reference_state_dict).
 Weights are random-initialised here (no checkpoint ships with the reference);
 load_reference_state_dict maps a reference state_dict onto this module.
 """
@@ -212,6 +217,29 @@ class FusedTrunk:
         return h
 
 
+def autocast_on(dev_type="cuda"):
+    """True when torch autocast would change F.linear's output dtype on `dev_type`."""
+    try:
+        return torch.is_autocast_enabled(dev_type)
+    except TypeError:   # (older torch: no per-device query)
+        return torch.is_autocast_enabled()
+
+
+def f32_fused_ok(tokens, weight):
+    """The f32 fused forward reads every GEMM output through raw pointers as float32: take it
+    only for f32 weights on the GPU, without autograd, and with autocast off (under autocast
+    F.linear returns bf16 / f16 buffers half the size)."""
+    return (tokens.is_cuda and weight.dtype == torch.float32 and not torch.is_grad_enabled()
+            and not autocast_on(tokens.device.type))
+
+
+def _f32c(t):
+    """A GEMM output handed to an f32 kernel: float32 and contiguous, or raise (never reinterpret)."""
+    if t.dtype != torch.float32:
+        raise RuntimeError("f32 fused trunk: expected a float32 activation, got %s (autocast?)" % t.dtype)
+    return t.contiguous()
+
+
 class FusedTrunkF32(FusedTrunk):
     """The f32 GPU forward of a token trunk: the reference's precision (f32 activations; the
     GEMMs as torch F.linear, i.e. hipBLASLt at the caller's matmul precision -- the reference
@@ -247,21 +275,21 @@ class FusedTrunkF32(FusedTrunk):
 
     def attn_ln(self, x, blk, h, ln):
         if not (self.d % blk.heads == 0 and self.d // blk.heads in (40, 64)):
-            return self.add_ln(x, blk.attn_delta(h), ln)
-        qkv = F.linear(h, blk.qkv.weight).contiguous()                   # [B, 62, 3d]: q | k | v, heads contiguous
+            return self.add_ln(x, _f32c(blk.attn_delta(h)), ln)
+        qkv = _f32c(F.linear(h, blk.qkv.weight))                         # [B, 62, 3d]: q | k | v, heads contiguous
         y = torch.empty_like(h)
         bq = blk.qkv.bias.contiguous() if blk.qkv.bias is not None else None
         self.ck(self.L.dk_net_attn62_bias_f32_async(qkv.data_ptr(), bq.data_ptr() if bq is not None else None,
                                                     y.data_ptr(), h.shape[0], blk.heads, self.d // blk.heads, self.st))
         w, b = blk.folded_proj()
-        return self.add_ln(x, F.linear(y, w), ln, b)
+        return self.add_ln(x, _f32c(F.linear(y, w)), ln, b)
 
     def mlp_ln(self, x, blk, h, ln):
-        a = F.linear(h, blk.fc.weight).contiguous()
+        a = _f32c(F.linear(h, blk.fc.weight))
         b1 = blk.fc.bias.contiguous() if blk.fc.bias is not None else None
         self.ck(self.L.dk_net_gelu_bias_f32_async(a.data_ptr(), b1.data_ptr() if b1 is not None else None, a.numel(),
                                                   a.shape[-1], self.st))
-        return self.add_ln(x, F.linear(a, blk.proj.weight), ln, blk.proj.bias)
+        return self.add_ln(x, _f32c(F.linear(a, blk.proj.weight)), ln, blk.proj.bias)
 
 
 class DokoAzNet(nn.Module):
@@ -279,7 +307,7 @@ class DokoAzNet(nn.Module):
     def forward(self, tokens):                                   # int32/int64 [B, 311]
         if tokens.is_cuda and self.emb[0].weight.dtype == torch.bfloat16:
             return self.forward_fused(tokens)
-        if tokens.is_cuda and self.emb[0].weight.dtype == torch.float32 and not torch.is_grad_enabled():
+        if f32_fused_ok(tokens, self.emb[0].weight):
             return self.forward_fused(tokens, FusedTrunkF32)
         return self.forward_torch(tokens)
 

@@ -20,6 +20,7 @@
 #include "engine/assign_engine.h"
 #include "engine/ar_engine.h"
 #include "engine/az_core.h"
+#include "engine/rand_distr.h"
 #include "engine/encode_pi.h"
 #include "az_net_kernels.h"
 #include "az_net_f32_kernels.h"
@@ -525,14 +526,25 @@ __global__ void az_init_kernel(const dk_az_state* roots, const uint64_t* seeds, 
     eval[g] = r;
 }
 
-__global__ void az_root_kernel(const float* value, const float* logits, const float* noise, float eps, int epoch,
-                               uint32_t n, dk::az::Node* nodes, dk_az_state* states, dk::az::Game* games,
-                               uint32_t cap_nodes, uint32_t cap_states, int* err) {
+// noise == nullptr: the root's Dirichlet([alpha; 39]) noise is drawn from the game's own SmallRng
+// (async_mcts.rs:111-113, rand_distr.h) before any other draw of the search.
+__global__ void az_root_kernel(const float* value, const float* logits, const float* noise, float alpha, dk::rd::Open01Tab tab,
+                               float eps, int epoch, uint32_t n, dk::az::Node* nodes, dk_az_state* states,
+                               dk::az::Game* games, uint32_t cap_nodes, uint32_t cap_states, int* err) {
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= n) return;
     dk::az::Mem m = az_mem(nodes, states, g, cap_nodes, cap_states);
     dk::az::Game gm = games[g];
-    dk::az::root_expand(gm, m, value + 4 * (size_t)g, logits + 39 * (size_t)g, noise + 39 * (size_t)g, eps, epoch);
+    float drawn[39];
+    const float* nz = noise + 39 * (size_t)g;
+    if (!noise) {
+        dk::Rng r;
+        r.s0 = gm.rng[0]; r.s1 = gm.rng[1]; r.s2 = gm.rng[2]; r.s3 = gm.rng[3];
+        dk::rd::dirichlet39(alpha, r, tab, drawn);
+        gm.rng[0] = r.s0; gm.rng[1] = r.s1; gm.rng[2] = r.s2; gm.rng[3] = r.s3;
+        nz = drawn;
+    }
+    dk::az::root_expand(gm, m, value + 4 * (size_t)g, logits + 39 * (size_t)g, nz, eps, epoch);
     if (gm.status) atomicOr(err, 1);
     games[g] = gm;
 }
@@ -572,6 +584,17 @@ __global__ void az_finish_kernel(int temp_mode, float temperature, uint32_t n, d
     for (int k = 0; k < 39; ++k) visits[39 * (size_t)g + k] = v[k];
     action[g] = a < 0 ? (uint8_t)DK_NONE : (uint8_t)a;
     games[g] = gm;
+}
+
+// the games' SmallRng states: dir 0 reads them into rng[g][4], dir 1 sets them (a caller's
+// &mut SmallRng carried across searches, async_mcts.rs:224-406 takes `rng: &mut SmallRng`)
+__global__ void az_rng_kernel(dk::az::Game* games, uint32_t n, uint64_t* rng, int dir) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n) return;
+    for (int i = 0; i < 4; ++i) {
+        if (dir) games[g].rng[i] = rng[4 * (size_t)g + i];
+        else rng[4 * (size_t)g + i] = games[g].rng[i];
+    }
 }
 
 // records of packed states that have no announcements yet
@@ -921,6 +944,10 @@ struct dk_ctx {
     float ar_log_chance = 0.0f;
     int az_epoch = 0;
     bool az_root_done = false;
+    // glibc logf / powf(., 1 / shape) of the 2^23 Open01<f32> values (rand_distr.h), built on first use
+    float* rd_ln = nullptr;
+    float* rd_pw = nullptr;
+    float rd_inv_shape = 0.0f;
     std::vector<void*> scratch;
     std::vector<size_t> scratch_size;
     // results of the synchronous (host-pointer) entry points: DMA into this page-locked buffer,
@@ -1001,10 +1028,16 @@ hipError_t copy_out(dk_ctx* ctx, void* dst, const void* src, size_t bytes) {
 }
 
 // Wait for stream `st`, then collect the error flags: the context's (env, sampler, AlphaZero
-// kernels) and those of the search launches issued on `st` since its last sync.
-int finish(dk_ctx* ctx, hipStream_t st) {
-    if (hipStreamSynchronize(st) != hipSuccess) { ctx->outs.clear(); ctx->pinned_used = 0; return ctx->last_error = DK_E_LAUNCH; }
-    if (st == ctx->stream) flush_outs(ctx);
+// kernels) and those of the search launches issued on `st` since its last sync.  host_copies:
+// the caller is a synchronous host-pointer entry point holding ctx->mu, whose queued result
+// copies (ctx->outs, the staging buffer) are flushed here.  dk_sync passes false: it never
+// touches another thread's staging state (a dk_sync racing a host-pointer call).
+int finish(dk_ctx* ctx, hipStream_t st, bool host_copies = true) {
+    if (hipStreamSynchronize(st) != hipSuccess) {
+        if (host_copies) { ctx->outs.clear(); ctx->pinned_used = 0; }
+        return ctx->last_error = DK_E_LAUNCH;
+    }
+    if (host_copies && st == ctx->stream) flush_outs(ctx);
     int flag = 0;
     if (hipMemcpy(&flag, ctx->err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return ctx->last_error = DK_E_LAUNCH;
     (void)hipMemset(ctx->err, 0, sizeof(int));
@@ -1406,6 +1439,8 @@ void dk_destroy(dk_ctx* ctx) {
     if (ctx->ar_lanes) (void)hipFree(ctx->ar_lanes);
     if (ctx->az_states) (void)hipFree(ctx->az_states);
     if (ctx->az_games) (void)hipFree(ctx->az_games);
+    if (ctx->rd_ln) (void)hipFree(ctx->rd_ln);
+    if (ctx->rd_pw) (void)hipFree(ctx->rd_pw);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -1470,7 +1505,7 @@ int dk_last_search_waves(dk_ctx* ctx, double* out) {
 
 int dk_sync(dk_ctx* ctx, void* stream) {
     if (!ctx) return DK_E_INVALID;
-    return finish(ctx, pick(ctx, stream));
+    return finish(ctx, pick(ctx, stream), false);
 }
 
 int dk_last_search_ms(dk_ctx* ctx, float* ms) {
@@ -1893,14 +1928,56 @@ int dk_az_begin_async(dk_ctx* ctx, const dk_az_state* d_roots, const uint64_t* d
     return DK_OK;
 }
 
-int dk_az_root_async(dk_ctx* ctx, const float* d_value, const float* d_logits, const float* d_noise,
+// The Open01<f32> tables of rand_distr.h: u_k = (1 + k 2^-23) - (1 - 2^-24), k < 2^23, and glibc's
+// logf(u_k) / powf(u_k, inv_shape) -- what Rust's f32::ln / f32::powf call.  Built on the host like
+// the ln(N) table of the UCT search (64 MB at most; rebuilt when the shape changes).
+static int rd_tables(dk_ctx* ctx, float alpha, hipStream_t st) {
+    constexpr uint32_t K = 1u << 23;
+    const bool small = alpha < 1.0f;
+    const float inv_shape = 1.0f / alpha;
+    if (ctx->rd_ln && (!small || (ctx->rd_pw && ctx->rd_inv_shape == inv_shape))) return DK_OK;
+    std::vector<float> h(K);
+    auto u_of = [](uint32_t k) { return __builtin_bit_cast(float, k | 0x3F800000u) - (1.0f - FLT_EPSILON / 2.0f); };
+    if (hipStreamSynchronize(st) != hipSuccess) return DK_E_LAUNCH;   // (a running root kernel may read the table)
+    if (!ctx->rd_ln) {
+        for (uint32_t k = 0; k < K; ++k) h[k] = logf(u_of(k));
+        if (hipMalloc(&ctx->rd_ln, K * sizeof(float)) != hipSuccess) { ctx->rd_ln = nullptr; return DK_E_CAPACITY; }
+        if (hipMemcpy(ctx->rd_ln, h.data(), K * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) return DK_E_LAUNCH;
+    }
+    if (small && !(ctx->rd_pw && ctx->rd_inv_shape == inv_shape)) {
+        for (uint32_t k = 0; k < K; ++k) h[k] = powf(u_of(k), inv_shape);
+        if (!ctx->rd_pw && hipMalloc(&ctx->rd_pw, K * sizeof(float)) != hipSuccess) { ctx->rd_pw = nullptr; return DK_E_CAPACITY; }
+        if (hipMemcpy(ctx->rd_pw, h.data(), K * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) return DK_E_LAUNCH;
+        ctx->rd_inv_shape = inv_shape;
+    }
+    return DK_OK;
+}
+
+int dk_az_root_async(dk_ctx* ctx, const float* d_value, const float* d_logits, const float* d_noise, float dirichlet_alpha,
                      float dirichlet_epsilon, void* stream) {
-    if (!ctx || !ctx->az_n || !d_value || !d_logits || !d_noise) return DK_E_INVALID;
+    if (!ctx || !ctx->az_n || !d_value || !d_logits) return DK_E_INVALID;
+    dk::rd::Open01Tab tab{nullptr, nullptr};
+    if (!d_noise) {
+        if (!dk::rd::dirichlet_alpha_ok(dirichlet_alpha)) return DK_E_INVALID;
+        const int rc = rd_tables(ctx, dirichlet_alpha, pick(ctx, stream));
+        if (rc) return ctx->last_error = rc;
+        tab.ln = ctx->rd_ln;
+        tab.pw = ctx->rd_pw;
+    }
     hipLaunchKernelGGL(az_root_kernel, dim3(grid_for(ctx->az_n, 64)), dim3(64), 0, pick(ctx, stream), d_value, d_logits,
-                       d_noise, dirichlet_epsilon, ctx->az_epoch, ctx->az_n, ctx->az_nodes, ctx->az_states,
-                       ctx->az_games, ctx->az_cap_nodes, ctx->az_cap_states, ctx->err);
+                       d_noise, dirichlet_alpha, tab, dirichlet_epsilon, ctx->az_epoch, ctx->az_n, ctx->az_nodes,
+                       ctx->az_states, ctx->az_games, ctx->az_cap_nodes, ctx->az_cap_states, ctx->err);
     DK_HIP(hipGetLastError());
     ctx->az_root_done = true;
+    return DK_OK;
+}
+
+int dk_az_rng_async(dk_ctx* ctx, uint64_t* d_rng, int set, void* stream) {
+    if (!ctx || !ctx->az_n || !d_rng || (set != 0 && set != 1)) return DK_E_INVALID;
+    if (set && ctx->az_root_done) return DK_E_INVALID;   // the root has drawn from the old streams
+    hipLaunchKernelGGL(az_rng_kernel, dim3(grid_for(ctx->az_n, 64)), dim3(64), 0, pick(ctx, stream), ctx->az_games,
+                       ctx->az_n, d_rng, set);
+    DK_HIP(hipGetLastError());
     return DK_OK;
 }
 

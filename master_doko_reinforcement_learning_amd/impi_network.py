@@ -18,7 +18,7 @@ load_reference_state_dict maps a reference state_dict onto this module.
 import torch
 from torch import nn
 
-from .az_network import SEQ, Block, ClassHead, FusedTrunk, FusedTrunkF32
+from .az_network import SEQ, Block, ClassHead, FusedTrunk, FusedTrunkF32, f32_fused_ok
 
 VOCAB_IPI = (43, 57, 5, 13, 3, 5)   # object, position, player, subposition, team, player to guess (main.py:91-96)
 IPI_CLASSES = 33
@@ -35,7 +35,7 @@ class DokoImpiNet(nn.Module):
     def forward(self, tokens):                                   # int32/int64 [B, 311] -> [B, 33]
         if tokens.is_cuda and self.emb[0].weight.dtype == torch.bfloat16:
             return self.forward_fused(tokens)
-        if tokens.is_cuda and self.emb[0].weight.dtype == torch.float32 and not torch.is_grad_enabled():
+        if f32_fused_ok(tokens, self.emb[0].weight):
             return self.forward_fused(tokens, FusedTrunkF32)
         return self.forward_torch(tokens)
 

@@ -16,11 +16,12 @@
 //                                    every RotArr read/write goes through get_for_i / index_for_i)
 // The network is a callback (the batch processor's `process`): it returns the
 // value vector from the evaluated state's current player's point of view and
-// 39 policy logits.  The Dirichlet noise of the root is an INPUT here: the
-// reference draws it from the search's SmallRng through rand_distr 0.5.1
-// (Dirichlet::new([alpha; 39]).sample(rng)), an algorithm this restatement does
-// not reproduce (parity unpinned).  The search's own draws (random_bool(1/5000)
-// at the end, then the temperature pick) follow the reference's order.
+// 39 policy logits.  The Dirichlet noise of the root is drawn from the search's
+// SmallRng as the reference draws it (Dirichlet::new([alpha; 39]).sample(rng),
+// async_mcts.rs:111-113, rand_distr 0.5.1: rand_distr05.hpp, parity unpinned), after
+// the root's network call and before every other draw of the search: random_bool(1/5000)
+// at the end (async_mcts.rs:347), then the temperature pick (mcts.rs:235).  A caller may
+// pass the noise instead (the search then draws none).
 #pragma once
 #include <cmath>
 #include <cstdint>
@@ -30,6 +31,7 @@
 
 #include "full_doko.hpp"
 #include "rand09.hpp"
+#include "rand_distr05.hpp"
 
 namespace oracle {
 namespace az {
@@ -89,6 +91,7 @@ struct Node {
 struct Options {
     float c = 1.0f;                 // puct_exploration_constant
     float dirichlet_epsilon = 0.25f;
+    float dirichlet_alpha = 0.8f;   // used when the caller passes no noise
     int epoch = MIN_EPOCH;          // >= MIN_EPOCH: announcements offered at the root
     bool has_temperature = false;   // None -> greedy (max_by_key visits)
     float temperature = 1.0f;       // +inf -> uniform choose
@@ -174,6 +177,13 @@ struct Search {
             float value[4], probs[39];
             eval(root_state, value, probs);
             softmax(probs, 39);
+            float drawn[39];
+            if (!noise) {   // Dirichlet::new([dirichlet_alpha; 39]).unwrap().sample(rng)
+                float al[39];
+                for (float& a : al) a = o.dirichlet_alpha;
+                if (!rdist::dirichlet(al, 39, rng, drawn)) return -2;   // (the reference's unwrap panics)
+                noise = drawn;
+            }
             float nz[39];
             for (int i = 0; i < 39; ++i) probs[i] *= (1.0f - o.dirichlet_epsilon);
             for (int i = 0; i < 39; ++i) nz[i] = noise[i] * o.dirichlet_epsilon;

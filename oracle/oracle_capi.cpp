@@ -356,11 +356,12 @@ void* or_do_sample_full(void* sp, uint64_t* rng_state) {
 
 // ---------------------------------------------------------------- AlphaZero PUCT (synthetic network)
 void or_az_hash_eval(const uint8_t* packed, float* value, float* logits) { az::hash_eval(packed, value, logits); }
-// temp_mode: 0 None, 1 infinite, 2 finite `temp`.  Returns the chosen action.
-int or_az_search(void* sp, const float* noise, uint32_t iters, float c, float eps, int epoch, int temp_mode, float temp,
-                 uint64_t* rng_state, uint32_t* visits, float* root_priors) {
+// temp_mode: 0 None, 1 infinite, 2 finite `temp`.  noise NULL: the search draws
+// Dirichlet([alpha; 39]) from its own SmallRng.  Returns the chosen action (-2: alpha refused).
+int or_az_search(void* sp, const float* noise, float alpha, uint32_t iters, float c, float eps, int epoch, int temp_mode,
+                 float temp, uint64_t* rng_state, uint32_t* visits, float* root_priors) {
     az::Env e; e.doko = *(fdo::State*)sp;
-    az::Options o; o.c = c; o.dirichlet_epsilon = eps; o.epoch = epoch;
+    az::Options o; o.c = c; o.dirichlet_epsilon = eps; o.epoch = epoch; o.dirichlet_alpha = alpha;
     o.has_temperature = temp_mode != 0; o.temperature = temp_mode == 1 ? INFINITY : temp;
     auto eval = [](const az::Env& st, float v[4], float l[39]) {
         uint8_t b[128]; or_fdo_pack((void*)&st.doko, b); az::hash_eval(b, v, l);
@@ -385,6 +386,40 @@ void or_fdo_pack_az(void* sp, uint8_t* out) {
     r->ann_n = (uint8_t)s.announcements.n;
 }
 void or_az_take_action(void* sp, int a) { az::Env e; e.doko = *(fdo::State*)sp; *(fdo::State*)sp = e.take_action(a, true).doko; }
+
+// rand_distr 0.5.1 draws (rand_distr05.hpp) for the moment tests and the host harness.
+// Dirichlet([alpha; n]) n_draws times from one stream; returns 0 if alpha is refused.
+int or_dirichlet(float alpha, int n, uint32_t n_draws, uint64_t* rng_state, float* out) {
+    std::vector<float> al((size_t)n, alpha);
+    SmallRng r = rng_from(rng_state);
+    for (uint32_t d = 0; d < n_draws; ++d)
+        if (!rdist::dirichlet(al.data(), n, r, out + (size_t)d * n)) return 0;
+    rng_to(r, rng_state);
+    return 1;
+}
+void or_gamma(float shape, uint32_t n, uint64_t* rng_state, float* out) {
+    SmallRng r = rng_from(rng_state);
+    const rdist::Gamma g(shape);
+    for (uint32_t i = 0; i < n; ++i) out[i] = g.sample(r);
+    rng_to(r, rng_state);
+}
+void or_normal_f64(uint32_t n, uint64_t* rng_state, double* out) {
+    SmallRng r = rng_from(rng_state);
+    for (uint32_t i = 0; i < n; ++i) out[i] = rdist::normal_f64(r);
+    rng_to(r, rng_state);
+}
+void or_exp1_f64(uint32_t n, uint64_t* rng_state, double* out) {
+    SmallRng r = rng_from(rng_state);
+    for (uint32_t i = 0; i < n; ++i) out[i] = rdist::exp1_f64(r);
+    rng_to(r, rng_state);
+}
+// the ziggurat tables as the oracle computed them: [NORM_X, NORM_F, EXP_X, EXP_F] x 257, R_norm, R_exp
+void or_ziggurat_tables(double* out) {
+    const rdist::Zig& z = rdist::zig();
+    memcpy(out, z.nx, sizeof z.nx); memcpy(out + 257, z.nf, sizeof z.nf);
+    memcpy(out + 514, z.ex, sizeof z.ex); memcpy(out + 771, z.ef, sizeof z.ef);
+    out[1028] = z.norm_r; out[1029] = z.exp_r;
+}
 
 // ---------------------------------------------------------------- encode_state_pi
 void or_encode_pi(void* sp, int64_t* out) { enc::encode_state_pi(*(fdo::State*)sp, out); }

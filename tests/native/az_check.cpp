@@ -2,7 +2,9 @@
 // checked against the ORACLE mcts_search restatement (oracle/az_mcts.hpp) with
 // the synthetic hash network: root priors, visit counts, the chosen action and
 // the RNG stream position must be identical, for greedy, infinite and T = 1
-// temperatures.  The batch is driven exactly as the GPU drives it: init ->
+// temperatures, with caller-supplied root noise and with the noise the search draws
+// from its own SmallRng (rand_distr.h as az_root_kernel runs it; alphas 0.8 / 1.0 / 0.5:
+// the three Gamma paths).  The batch is driven exactly as the GPU drives it: init ->
 // network(root) -> root_expand -> iterations x {select -> network(leaves) ->
 // backup} -> finish, over all games at once.
 // Usage: az_check <positions> <iterations> <seed>
@@ -15,6 +17,7 @@
 
 #include "../../master_doko_reinforcement_learning_amd/csrc/engine/az_core.h"
 #include "../../master_doko_reinforcement_learning_amd/csrc/engine/encode_pi.h"
+#include "../../master_doko_reinforcement_learning_amd/csrc/engine/rand_distr.h"
 #include "../../oracle/encode_pi.hpp"
 #include "../../oracle/az_eval.hpp"
 #include "../../oracle/full_doko.hpp"
@@ -22,8 +25,8 @@
 using namespace oracle;
 extern "C" void or_fdo_pack(void* sp, uint8_t* out);
 extern "C" void or_fdo_pack_az(void* sp, uint8_t* out);
-extern "C" int or_az_search(void* sp, const float* noise, uint32_t iters, float c, float eps, int epoch, int temp_mode,
-                            float temp, uint64_t* rng_state, uint32_t* visits, float* root_priors);
+extern "C" int or_az_search(void* sp, const float* noise, float alpha, uint32_t iters, float c, float eps, int epoch,
+                            int temp_mode, float temp, uint64_t* rng_state, uint32_t* visits, float* root_priors);
 
 int main(int argc, char** argv) {
     const int npos = argc > 1 ? atoi(argv[1]) : 40;
@@ -68,7 +71,18 @@ int main(int argc, char** argv) {
     const int G = (int)pos.size();
     const float c = 2.5f, eps = 0.25f;
     long checked = 0;
-    for (int mode = 0; mode < 3; ++mode) {
+    // the Open01 tables of the context (doko_amd.hip rd_tables)
+    constexpr uint32_t K = 1u << 23;
+    std::vector<float> ln01(K), pw01(K);
+    auto u_of = [](uint32_t k) { return __builtin_bit_cast(float, k | 0x3F800000u) - (1.0f - FLT_EPSILON / 2.0f); };
+    for (uint32_t k = 0; k < K; ++k) ln01[k] = logf(u_of(k));
+    for (int run = 0; run < 6; ++run) {
+        const int mode = run % 3;
+        const bool drawn = run >= 3;
+        const float alpha = mode == 0 ? 0.8f : (mode == 1 ? 1.0f : 0.5f);
+        if (drawn && alpha < 1.0f)
+            for (uint32_t k = 0; k < K; ++k) pw01[k] = powf(u_of(k), 1.0f / alpha);
+        const dk::rd::Open01Tab tab{pw01.data(), ln01.data()};
         const int epoch = mode == 1 ? 3 : 12;
         const float temp = 1.0f;
         std::vector<float> noise((size_t)G * 39);
@@ -91,7 +105,15 @@ int main(int argc, char** argv) {
             dk::az::init(r, games[g], m, seeds[g]);
             eval[g] = r;
             network(g);
-            dk::az::root_expand(games[g], m, &val[4 * g], &logit[39 * g], &noise[39 * (size_t)g], eps, epoch);
+            const float* nz = &noise[39 * (size_t)g];
+            float dn[39];
+            if (drawn) {   // az_root_kernel with d_noise == NULL
+                dk::Rng r; r.s0 = games[g].rng[0]; r.s1 = games[g].rng[1]; r.s2 = games[g].rng[2]; r.s3 = games[g].rng[3];
+                dk::rd::dirichlet39(alpha, r, tab, dn);
+                games[g].rng[0] = r.s0; games[g].rng[1] = r.s1; games[g].rng[2] = r.s2; games[g].rng[3] = r.s3;
+                nz = dn;
+            }
+            dk::az::root_expand(games[g], m, &val[4 * g], &logit[39 * g], nz, eps, epoch);
         }
         for (uint32_t it = 0; it < iters; ++it) {
             for (int g = 0; g < G; ++g) { dk::az::Mem m = mem(g); dk::az::select(games[g], m, c, epoch, &eval[g]); }
@@ -108,16 +130,17 @@ int main(int argc, char** argv) {
             { const SmallRng r = SmallRng::seed_from_u64(seeds[g]); for (int i = 0; i < 4; ++i) rs[i] = r.s[i]; }
             uint32_t ov[39]; float op[39];
             for (int a = 0; a < 39; ++a) op[a] = -1.0f;
-            const int oa = or_az_search(&pos[g], &noise[39 * (size_t)g], iters, c, eps, epoch, mode, temp, rs, ov, op);
+            const int oa = or_az_search(&pos[g], drawn ? nullptr : &noise[39 * (size_t)g], alpha, iters, c, eps, epoch, mode,
+                                        temp, rs, ov, op);
             for (int a = 0; a < 39; ++a)
-                if (dv[a] != ov[a]) { printf("MISMATCH visits mode %d game %d action %d: %u vs %u\n", mode, g, a, dv[a], ov[a]); return 1; }
+                if (dv[a] != ov[a]) { printf("MISMATCH visits run %d game %d action %d: %u vs %u\n", run, g, a, dv[a], ov[a]); return 1; }
             const dk::az::Node root = m.nodes[0];
             for (uint32_t j = 0; j < root.nchild; ++j) {
                 const dk::az::Node ch = m.nodes[root.child_base + j];
-                if (memcmp(&ch.prior, &op[ch.action], 4) != 0) { printf("MISMATCH root prior mode %d game %d\n", mode, g); return 1; }
+                if (memcmp(&ch.prior, &op[ch.action], 4) != 0) { printf("MISMATCH root prior run %d game %d\n", run, g); return 1; }
             }
-            if (da != oa) { printf("MISMATCH action mode %d game %d: %d vs %d\n", mode, g, da, oa); return 1; }
-            for (int i = 0; i < 4; ++i) if (games[g].rng[i] != rs[i]) { printf("MISMATCH rng mode %d game %d\n", mode, g); return 1; }
+            if (da != oa) { printf("MISMATCH action run %d game %d: %d vs %d\n", run, g, da, oa); return 1; }
+            for (int i = 0; i < 4; ++i) if (games[g].rng[i] != rs[i]) { printf("MISMATCH rng run %d game %d\n", run, g); return 1; }
             checked++;
         }
     }

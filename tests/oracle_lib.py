@@ -82,8 +82,13 @@ def lib():
                                                        u64p, u64p]),
             "or_do_sample_full": (vp, [vp, u64p]),
             "or_az_hash_eval": (None, [u8p, f32p, f32p]),
-            "or_az_search": (ctypes.c_int, [vp, f32p, ctypes.c_uint32, ctypes.c_float, ctypes.c_float, ctypes.c_int,
-                                            ctypes.c_int, ctypes.c_float, u64p, u32p, f32p]),
+            "or_az_search": (ctypes.c_int, [vp, f32p, ctypes.c_float, ctypes.c_uint32, ctypes.c_float, ctypes.c_float,
+                                            ctypes.c_int, ctypes.c_int, ctypes.c_float, u64p, u32p, f32p]),
+            "or_dirichlet": (ctypes.c_int, [ctypes.c_float, ctypes.c_int, ctypes.c_uint32, u64p, f32p]),
+            "or_gamma": (None, [ctypes.c_float, ctypes.c_uint32, u64p, f32p]),
+            "or_normal_f64": (None, [ctypes.c_uint32, u64p, f64p]),
+            "or_exp1_f64": (None, [ctypes.c_uint32, u64p, f64p]),
+            "or_ziggurat_tables": (None, [f64p]),
             "or_az_take_action": (None, [vp, ctypes.c_int]),
             "or_encode_pi": (None, [vp, ctypes.POINTER(ctypes.c_int64)]),
             "or_fdo_pack_az": (None, [vp, u8p]),
@@ -195,12 +200,14 @@ class FdoState:
     def card_matching(self, rng):
         return FdoState(lib().or_fdo_card_matching(self.h, rng))
 
-    def az_search(self, noise, iters, c, eps, epoch, temp_mode, temp, rng):
+    def az_search(self, noise, iters, c, eps, epoch, temp_mode, temp, rng, alpha=0.8):
         """AlphaZero mcts_search (async_mcts.rs:224-406) with the synthetic hash
-        network of oracle/az_eval.hpp -> (action, visits[39], root priors[39])."""
+        network of oracle/az_eval.hpp -> (action, visits[39], root priors[39]).
+        noise None: the search draws Dirichlet([alpha; 39]) from rng (rand_distr05.hpp)."""
         v = arr(ctypes.c_uint32, 39)
         pr = arr(ctypes.c_float, 39, [-1.0] * 39)
-        a = lib().or_az_search(self.h, arr(ctypes.c_float, 39, noise), iters, c, eps, epoch, temp_mode, temp, rng, v, pr)
+        nz = None if noise is None else arr(ctypes.c_float, 39, noise)
+        a = lib().or_az_search(self.h, nz, ctypes.c_float(alpha), iters, c, eps, epoch, temp_mode, temp, rng, v, pr)
         return a, list(v), list(pr)
 
     def pack_az(self):

@@ -81,10 +81,19 @@ def test_engine_assignment_vs_oracle(native_bins):
     assert _run("assign_check", 200, 3) > 40000
 
 
+def test_dirichlet_vs_oracle(native_bins):
+    """engine/rand_distr.h (the root noise the GPU draws, host build) = the oracle's rand_distr
+    0.5.1 restatement: ziggurat tables, StandardNormal / Exp1 streams, Gamma on all three paths
+    and Dirichlet<f32, 39>, value for value with the RNG stream position (parity unpinned:
+    no reference vector exists for these draws)."""
+    assert _run("dirichlet_check", 20000, 3) == 2120000
+
+
 def test_az_core_vs_oracle(native_bins):
     """az_core.h (host build, driven batch-wise like the GPU) = oracle AlphaZero
-    mcts_search: root priors, visits, chosen action and RNG position, three temperature modes."""
-    assert _run("az_check", 120, 300, 5) == 360
+    mcts_search: root priors, visits, chosen action and RNG position, three temperature modes,
+    with caller-supplied noise and with the Dirichlet noise the search draws itself."""
+    assert _run("az_check", 120, 300, 5) == 720
 
 
 def test_fusion_kats():

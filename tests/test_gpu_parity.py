@@ -635,11 +635,17 @@ def test_decide_end_to_end_doko(eng):
 
 
 # ---------------------------------------------------------------- AlphaZero PUCT search
+@pytest.mark.parametrize("drawn", [False, True])
 @pytest.mark.parametrize("temp_mode", [0, 1, 2])
-def test_az_search_parity(eng, temp_mode):
+def test_az_search_parity(eng, temp_mode, drawn):
     """AlphaZero mcts_search (rs-doko-alpha-zero async_mcts.rs:224-406) on the GPU ==
     the oracle restatement, with the synthetic hash network (oracle/az_eval.hpp) on both
-    sides: root child visits, chosen action (greedy / uniform / T = 1) for every game."""
+    sides: root child visits, chosen action (greedy / uniform / T = 1) and the SmallRng end
+    state for every game.  drawn: the root's Dirichlet([alpha; 39]) noise is drawn by each game
+    from its own SmallRng, as the reference draws it (async_mcts.rs:111-113; rand_distr 0.5.1,
+    parity unpinned: no reference vector), with alpha 0.8 / 1.0 / 0.5 (the three Gamma paths);
+    otherwise the caller's noise.  The drawn runs start from caller-held RNG states
+    (dk_az_rng_async, the reference's &mut SmallRng) and read the end states back."""
     import torch
     import master_doko_reinforcement_learning_amd as dk
     pool = [s for s in fdo_states(24, 31) if s.info()["phase"] != 3]
@@ -656,13 +662,23 @@ def test_az_search_parity(eng, temp_mode):
         return torch.from_numpy(v).to(dev), torch.from_numpy(l).to(dev)
 
     roots = torch.from_numpy(np.frombuffer(b"".join(s.pack_az() for s in info), dtype=np.uint8).reshape(-1, 160).copy()).to(dev)
-    az = dk.AlphaZeroSearch(eng, c, eps, epoch, [None, float("inf"), 1.0][temp_mode])
-    actions, visits = az.mcts_search(roots, network, torch.from_numpy(noise).to(dev), iters, seeds)
+    alpha = [0.8, 1.0, 0.5][temp_mode]
+    az = dk.AlphaZeroSearch(eng, c, eps, epoch, [None, float("inf"), 1.0][temp_mode], dirichlet_alpha=alpha)
+    rs = None
+    if drawn:
+        start = np.array([list(ol.rng_seed(int(x) ^ 0x5EED)) for x in seeds], dtype=np.uint64)
+        rs = torch.from_numpy(start.view(np.int64).copy()).to(dev)
+    actions, visits = az.mcts_search(roots, network, None if drawn else torch.from_numpy(noise).to(dev), iters, seeds,
+                                     rng_states=rs)
     actions, visits = actions.cpu().numpy(), visits.cpu().numpy()
+    ends = rs.cpu().numpy().view(np.uint64) if drawn else None
     for g, s in enumerate(info):
-        a, v, _ = s.az_search(list(noise[g]), iters, c, eps, epoch, temp_mode, 1.0, ol.rng_seed(int(seeds[g])))
+        r = ol.rng_seed(int(seeds[g]) ^ 0x5EED) if drawn else ol.rng_seed(int(seeds[g]))
+        a, v, _ = s.az_search(None if drawn else list(noise[g]), iters, c, eps, epoch, temp_mode, 1.0, r, alpha=alpha)
         assert list(visits[g]) == v
         assert int(actions[g]) == a
+        if drawn:
+            assert [int(x) for x in ends[g]] == list(r)
 
 
 def test_az_encode_and_step_parity(eng):
@@ -709,8 +725,8 @@ def test_az_selfplay_with_network(eng):
     st = torch.from_numpy(eng.new_games(dk.GAME_FULL_DOKO, np.arange(G, dtype=np.uint64) + 900)).to(dev)
     recs = dk.az_records(eng, st)
     ev = AzEvaluator(eng, DokoAzNet().to(dev))
-    search = dk.AlphaZeroSearch(eng, 4.0, 0.3, 10, 0.5)
-    noise = torch.distributions.Dirichlet(torch.full((39,), 0.8, device=dev)).sample((G,))
+    search = dk.AlphaZeroSearch(eng, 4.0, 0.3, 10, 0.5, dirichlet_alpha=0.8)
+    noise = None   # drawn by every game from its own SmallRng (async_mcts.rs:111-113)
     for move in range(6):
         tok = dk.az_encode(eng, recs).cpu().numpy()
         for i, v in enumerate(VOCAB):
