@@ -53,6 +53,12 @@ def parse():
     p.add_argument("--prod-iterations", type=int, default=200000, help="prod: iterations per sample (run.rs:270-291)")
     p.add_argument("--prod-samples", default="5,10,50", help="prod: samples per decision, one leg each")
     p.add_argument("--prod-inflight", type=int, default=16, help="prod: decisions in flight in the batched leg")
+    p.add_argument("--prod-capacity", type=int, default=-1,
+                   help="prod: decisions of max(samples) samples in flight at the pools' capacity in one pass "
+                        "(-1: as many as fit in the free device memory; 0: skip)")
+    p.add_argument("--prod-slots-per-iter", type=float, default=2.5,
+                   help="prod capacity leg: node slots per iteration and root (measured demand 1.95 at 200,000; a "
+                        "root that outgrows them is searched again in the fallback pool, results unchanged)")
     p.add_argument("--games", type=int, default=8192, help="concurrent self-play games per GPU (c5)")
     p.add_argument("--az-iterations", type=int, default=200, help="PUCT iterations per move (c5)")
     p.add_argument("--ar-samples", type=int, default=4, help="AR samples per infostate (impi)")
@@ -829,9 +835,7 @@ def run_prod(args, dk, L, dev, stream, rank, world, local_rank, dist):
         pol = dk.DefaultImpiPolicy(eng, args.c, iters, S, dk.FUSE_MAXN)
 
         def seeds_for(j):
-            base = np.uint64(0xC3200000 + j * 4096)
-            sd = np.concatenate([np.arange(S, dtype=np.uint64) + base, np.arange(S, dtype=np.uint64) + base + np.uint64(2048)])
-            return torch.tensor(sd.view(np.int64), device=dev)
+            return torch.tensor(seeds_for_prod(j, S).view(np.int64), device=dev)
 
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
@@ -855,6 +859,12 @@ def run_prod(args, dk, L, dev, stream, rank, world, local_rank, dist):
                "one_decision_rollouts_per_s": S * iters / lat}
         legs.append(leg)
     hw, cap, overflowed = eng.pool_high_water(sp)
+    pool_small = eng.pool_bytes()
+    inflight_visits0 = res[0][1].cpu().numpy()   # decision 0 of the last S's in-flight leg
+    eng.close()
+    capleg = None
+    if args.prod_capacity != 0:
+        capleg = prod_capacity_leg(args, dk, L, dev, sp, Ss[-1], iters, local_rank, inflight_visits0, seeds_for_prod)
     result = None
     if rank == 0:
         if not args.no_cpu_baseline:
@@ -881,19 +891,28 @@ def run_prod(args, dk, L, dev, stream, rank, world, local_rank, dist):
                 leg["cpu"] = {"decision_latency_s": secs, "threads": thr, "kind": "port",
                               "rollouts_per_s": S * iters / secs, "visits_equal_gpu": same}
                 leg["gpu_over_cpu_latency"] = leg["decision_latency_s"] / secs
+            if capleg is not None:
+                capleg["oracle_check"] = prod_oracle_check(args, dk, iters, Ss[-1], capleg.pop("_check_rows"))
+        if capleg is not None:
+            capleg.pop("_check_rows", None)
+        top = capleg if capleg is not None else {"rollouts_per_s": legs[-1]["inflight_rollouts_per_s"],
+                                                 "s": legs[-1]["inflight_s"]}
         result = {
             "metric": "determinized decision latency and throughput at the production search shape "
                       "(S CAP samples x %d UCT iterations, MaxN)" % iters,
-            "value": legs[-1]["inflight_rollouts_per_s"],
+            "value": top["rollouts_per_s"],
             "unit": "rollouts/s",
             "n_gpus": world, "steps": 1, "warmup": 0,
-            "ms_per_step": legs[-1]["inflight_s"] * 1e3,
+            "ms_per_step": top["s"] * 1e3,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64+f64",
             "data": "synthetic: C3-style seeded deals (4x Healthy, k in {0,8,20,32} random plies), CAP samples",
-            "config": {"workload": "prod: S in %s samples x %d iterations; one decision, and %d decisions in flight "
-                                   "(execute_many)" % (Ss, iters, K), "parallelism": "replicas x%d" % world},
+            "config": {"workload": "prod: S in %s samples x %d iterations; one decision, %d decisions in flight "
+                                   "(execute_many), and %s decisions of %d samples at the pools' capacity"
+                                   % (Ss, iters, K, capleg["decisions"] if capleg else 0, Ss[-1]),
+                       "parallelism": "replicas x%d" % world},
             "legs": legs,
-            "node_pools": {"bytes": eng.pool_bytes(), "slot_capacity": cap, "slot_high_water": hw,
+            "capacity": capleg,
+            "node_pools": {"bytes": pool_small, "slot_capacity": cap, "slot_high_water": hw,
                            "overflowed_roots": overflowed},
             "roofline": None,
             "note": "a root's simulations are sequential (bit-exact reference semantics), so one decision's "
@@ -902,8 +921,99 @@ def run_prod(args, dk, L, dev, stream, rank, world, local_rank, dist):
         print(json.dumps(result))
     if world > 1:
         dist.destroy_process_group()
-    eng.close()
     return result
+
+
+def seeds_for_prod(j, S):
+    """Sampler and search seeds of prod decision j (S samples): [S sampler seeds | S search seeds]."""
+    base = np.uint64(0xC3200000 + j * 4096)
+    return np.concatenate([np.arange(S, dtype=np.uint64) + base, np.arange(S, dtype=np.uint64) + base + np.uint64(2048)])
+
+
+def prod_infostates(dk, L, eng, dev, sp, K):
+    """K C3-style infostates: seeded deals, 4x Healthy, k in {0, 8, 20, 32} random plies (round robin)."""
+    import torch
+    info_seeds = torch.tensor((np.arange(K, dtype=np.uint64) + np.uint64(0xC3000000)).view(np.int64), device=dev)
+    info = torch.zeros((K, 128), dtype=torch.uint8, device=dev)
+    assert L.dk_new_game_batch_async(eng.ctx, dk.GAME_FULL_DOKO, info_seeds.data_ptr(), K, info.data_ptr(), sp) == 0
+    a = torch.full((K,), 1 << 24, dtype=torch.int64, device=dev)
+    for _ in range(4):
+        assert L.dk_env_step_batch_async(eng.ctx, info.data_ptr(), a.data_ptr(), K, sp) == 0
+    plies = torch.tensor(np.array([[0, 8, 20, 32][j % 4] for j in range(K)], dtype=np.uint32).view(np.int32), device=dev)
+    ply_rng = torch.tensor(dk.splitmix_rng_states(np.arange(K, dtype=np.uint64) + np.uint64(0xC3100000)).view(np.int64),
+                           device=dev)
+    assert L.dk_env_random_plies_batch_async(eng.ctx, info.data_ptr(), ply_rng.data_ptr(), plies.data_ptr(), K, sp) == 0
+    assert L.dk_sync(eng.ctx, sp) == 0
+    return info
+
+
+def prod_capacity_leg(args, dk, L, dev, sp, S, iters, local_rank, visits0, seeds_for):
+    """As many decisions of S samples x `iters` iterations in flight as the device memory holds, in
+    one pass (DefaultImpiPolicy.execute_many): the evaluator's regime (2 x available_parallelism
+    concurrent games, run.rs:775) at this GPU's capacity.  Per root: the slots (16-B hot + 16-B cold
+    records, --prod-slots-per-iter x iterations), the 64-B node states and the path overflow."""
+    import torch
+    slots = int(64 + args.prod_slots_per_iter * iters + 255) // 256 * 256
+    per_root = slots * 32 + (iters + 1) * 64 + 512 * 12
+    torch.cuda.empty_cache()
+    free_b, _ = torch.cuda.mem_get_info(dev)
+    reserve = (12 << 30) + (6 << 30)          # the fallback pool (<= 16 GB of 32-B records; ~11.5 GB here) + headroom
+    K = args.prod_capacity
+    if K < 0:
+        K = max(1, int((free_b - reserve) * 0.95 // (per_root * S)))
+    eng = dk.Engine(device=local_rank, max_roots=K * S, max_iterations=iters, slot_capacity=slots)
+    try:
+        info = prod_infostates(dk, L, eng, dev, sp, K)
+        pol = dk.DefaultImpiPolicy(eng, args.c, iters, S, dk.FUSE_MAXN)
+        batches = [(info[j:j + 1], torch.tensor(seeds_for(j, S).view(np.int64), device=dev)) for j in range(K)]
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        res = pol.execute_many(batches, game=dk.GAME_FULL_DOKO)
+        torch.cuda.synchronize(dev)
+        el = time.perf_counter() - t0
+        kms = eng.last_search_ms()
+        vis = torch.cat([v for _, v in res]).cpu().numpy()
+        assert np.all(vis.sum(axis=1) == iters), "prod capacity: a root without exactly %d simulations" % iters
+        # decision 0 equals its in-flight-leg result (a different batch, engine and pool placement)
+        assert np.array_equal(vis[:S], visits0), "prod capacity: decision 0 differs from the 16-decision leg"
+        hw, cap, overflowed = eng.pool_high_water(sp)
+        last = K - 1
+        rows = {"decisions": [last], "samples": list(range(min(S, 8))),
+                "visits": {last: vis[last * S:last * S + min(S, 8)].tolist()}}
+        return {"samples": S, "decisions": K, "roots": K * S, "s": el, "search_kernel_ms": kms,
+                "decisions_per_s": K / el, "rollouts_per_s": K * S * iters / el,
+                "pool_bytes": eng.pool_bytes(), "pool_bytes_per_root": eng.pool_bytes() / (K * S),
+                "slot_capacity": cap, "slot_high_water": hw, "overflowed_roots": overflowed,
+                "actions_of_decision_0_equal_inflight_leg": True, "_check_rows": rows}
+    finally:
+        eng.close()
+
+
+def prod_oracle_check(args, dk, iters, S, rows):
+    """The oracle (CPU restatement) on roots of the capacity leg's last decision: visits equal."""
+    import ctypes
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as ol
+    out = []
+    for j in rows["decisions"]:
+        st = ol.FdoState.new_game(0xC3000000 + j)
+        for _ in range(4):
+            st.play(24)
+        rng = ol.arr(ctypes.c_uint64, 4, [int(x) for x in dk.splitmix_rng_states(np.array([0xC3100000 + j], dtype=np.uint64))[0]])
+        st.random_plies(rng, [0, 8, 20, 32][j % 4], True)
+        sd = seeds_for_prod(j, S)
+        ks = rows["samples"]
+        roots = [st.card_matching(ol.rng_seed(int(sd[k]))) for k in ks]
+        handles = (ctypes.c_void_p * len(ks))(*[r.h for r in roots])
+        vis = (ctypes.c_uint32 * (39 * len(ks)))()
+        seeds = ol.arr(ctypes.c_uint64, len(ks), [int(sd[S + k]) for k in ks])
+        cores, quota = cpu_quota_cores()
+        thr = min(len(ks), int(np.ceil(quota)) if quota else cores)
+        secs = ol.lib().or_fdo_search_many(None, handles, seeds, len(ks), iters, args.c, vis, thr)
+        same = all(list(vis[39 * i:39 * i + 39]) == [int(x) for x in rows["visits"][j][i]] for i in range(len(ks)))
+        out.append({"decision": j, "roots": len(ks), "visits_equal_gpu": same, "oracle_s": secs})
+        assert same, "prod capacity: oracle visits differ on decision %d" % j
+    return out
 
 
 def impi_flop_per_eval(d=256, seq=62, blocks=4, classes=33):

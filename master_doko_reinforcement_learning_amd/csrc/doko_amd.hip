@@ -923,6 +923,7 @@ struct dk_ctx {
     int pair = -1;                  // DK_PAIR=0 / 1: lane pairs off / on for launches of <= 32 roots per wave
     bool p8_ok = false;             // the pools' slot capacities suit the 8-B records (even-aligned blocks)
     bool wide = false;              // a wave's pool region reaches 4 GiB: NodeHot32W (64-bit offsets) only
+    size_t hot_rec = 16;            // bytes per hot-record slot in the pools (16, or 32: forced / wide)
     bool ln_in_lds = false;         // DK_LN_LDS=1: ln(N) table copied into every workgroup's LDS (8 KB at
                                     // 1000 iterations); by default it is read through the L1/L2 caches
     int lds_path = 16;              // path entries kept in LDS (deeper ones spill to global): at most
@@ -1138,8 +1139,8 @@ hipError_t launch_search_t(dk_ctx* ctx, const dk_state* roots, const uint64_t* s
     sl.lanes = lanes;
     if (ctx->verbose)
         fprintf(stderr, "doko_amd: search n=%u rpw=%u hot=%dB lds_path=%d lds=%zuB resident/CU=%d grid=%u root_window=%u "
-                "wide=%d lanes=%u+%u pair=%d\n", n, rpw, (int)sizeof(H), lp, lds_bytes, per_cu, grid, ctx->root_window,
-                (int)H::WIDE, base, lanes, (int)H::PAIR);
+                "wide=%d lanes=%u+%u pair=%d long=%d\n", n, rpw, (int)sizeof(H), lp, lds_bytes, per_cu, grid, ctx->root_window,
+                (int)H::WIDE, base, lanes, (int)H::PAIR, (int)H::LONG);
     e = hipMemsetAsync(sl.queue, 0, sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
     // group order only matters when waves take several groups each
@@ -1206,9 +1207,12 @@ hipError_t launch_search(dk_ctx* ctx, const dk_state* roots, const uint64_t* see
     // contexts: C2 33.0 ms against 33.8 ms for the 32-B records and 35.3 ms for 8 B, the
     // 512-infostate batch 41.6 / 42.8 / 43.6 ms; profiles/r04/layout_single_wave.log), 32 B
     // (cached exact means) beyond the 16-B records' 24-bit cross products (P24_MAX_ITERS)
+    // beyond P24_MAX_ITERS the 16-B records compare by 64-bit cross products (NodeHot16L /
+    // NodeHot16PL, round 5); the 32-B records remain for DK_HOT_RECORD=32 and the wide pools
     const uint32_t simds = 4u * (uint32_t)ctx->cu_count;
     const bool multi = grid_for(n, rpw) >= 2u * simds;
-    const bool h16 = iters <= dk::P24_MAX_ITERS && (ctx->hot_layout ? ctx->hot_layout <= 16 : true);
+    const bool lng = iters > dk::P24_MAX_ITERS;
+    const bool h16 = ctx->hot_layout ? ctx->hot_layout <= 16 : true;
     // 8-B records where their fields hold the search (visits, state index, slots: P8_MAX_ITERS)
     const bool h8 = h16 && iters <= dk::P8_MAX_ITERS && ctx->hot_layout != 16 && ctx->p8_ok &&
                     (ctx->hot_layout == 8 || multi);
@@ -1216,9 +1220,13 @@ hipError_t launch_search(dk_ctx* ctx, const dk_state* roots, const uint64_t* see
         return launch_search_t<E, false, dk::NodeHot32W>(ctx, roots, seeds, n, iters, c, visits, values, best, st, 0, rpw, sl, err, rng_io);
     // lane pairs where a single wave per SIMD holds at most 32 roots (DK_PAIR=0 / 1 forces)
     const bool pair = h16 && !h8 && rpw <= 32u && (ctx->pair < 0 ? !multi : ctx->pair == 1);
+    if (pair && lng)   // (iterations > 4095: never the LDS ln table)
+        return launch_search_t<E, false, dk::NodeHot16PL>(ctx, roots, seeds, n, iters, c, visits, values, best, st, 0, rpw, sl, err, rng_io);
     if (pair)
         return ln ? launch_search_t<E, true, dk::NodeHot16P>(ctx, roots, seeds, n, iters, c, visits, values, best, st, ln_bytes, rpw, sl, err, rng_io)
                   : launch_search_t<E, false, dk::NodeHot16P>(ctx, roots, seeds, n, iters, c, visits, values, best, st, ln_bytes, rpw, sl, err, rng_io);
+    if (h16 && lng)
+        return launch_search_t<E, false, dk::NodeHot16L>(ctx, roots, seeds, n, iters, c, visits, values, best, st, 0, rpw, sl, err, rng_io);
     if (h8)
         return ln ? launch_search_t<E, true, dk::NodeHot8>(ctx, roots, seeds, n, iters, c, visits, values, best, st, ln_bytes, rpw, sl, err, rng_io)
                   : launch_search_t<E, false, dk::NodeHot8>(ctx, roots, seeds, n, iters, c, visits, values, best, st, ln_bytes, rpw, sl, err, rng_io);
@@ -1322,7 +1330,9 @@ dk_ctx* dk_create(const dk_config* cfg) {
         size_t free_b = 0, total_b = 0;
         if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
             const uint32_t floor_cap = ((64u + 4u * cfg->max_iterations) + 255u) & ~255u;
-            const size_t per_slot = sizeof(dk::NodeHot32) + sizeof(dk::NodeCold);
+            const size_t per_slot = (getenv("DK_HOT_RECORD") && atoi(getenv("DK_HOT_RECORD")) == 32 ? sizeof(dk::NodeHot32)
+                                                                                                  : sizeof(dk::NodeHot16)) +
+                                    sizeof(dk::NodeCold);
             while (ctx->cap_slots > floor_cap && (size_t)ctx->pool_roots * ctx->cap_slots * per_slot > free_b / 2)
                 ctx->cap_slots = (ctx->cap_slots / 2 + 255u) & ~255u;
             if (ctx->cap_slots < floor_cap) ctx->cap_slots = floor_cap < proven ? floor_cap : proven;
@@ -1337,8 +1347,25 @@ dk_ctx* dk_create(const dk_config* cfg) {
         if (v >= (long long)T) ST = (size_t)v;
     }
     ctx->state_stride = (uint32_t)ST;
+    // Hot records per slot: 16 B (the 8-B, 16-B and long 16-B layouts all fit; rounds 1-4 always
+    // allocated 32 B), 32 B only when DK_HOT_RECORD=32 forces the cached-mean layout or a wave's
+    // regions reach 4 GiB (NodeHot32W, 64-bit offsets).  32-bit pool offsets (GpuMem::at) cover a
+    // wave's region only below 4 GiB: 64 lanes x the capacity x the record, in the main and the
+    // fallback pools, and the node states.
+    {
+        const uint64_t lim = 1ULL << 32, lanes = WAVE;
+        const uint64_t slots = with_fallback ? std::max<uint64_t>(S, proven) : S;
+        auto wide_at = [&](uint64_t rec) {
+            return lanes * slots * rec >= lim || lanes * slots * sizeof(dk::NodeCold) >= lim ||
+                   lanes * ST * STATE_SLOT_BYTES >= lim;
+        };
+        ctx->hot_rec = ctx->hot_layout == 32 ? sizeof(dk::NodeHot32) : sizeof(dk::NodeHot16);
+        ctx->wide = wide_at(ctx->hot_rec);
+        if (ctx->wide) ctx->hot_rec = sizeof(dk::NodeHot32);
+    }
+    const size_t HR = ctx->hot_rec;
     bool ok = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) == hipSuccess;
-    ok = ok && hipMalloc(&ctx->hot, R * S * sizeof(dk::NodeHot32)) == hipSuccess;
+    ok = ok && hipMalloc(&ctx->hot, R * S * HR) == hipSuccess;
     ok = ok && hipMalloc(&ctx->cold, R * S * sizeof(dk::NodeCold)) == hipSuccess;
     ok = ok && hipMalloc(&ctx->ovf, R * dk::MAX_DEPTH * sizeof(uint32_t)) == hipSuccess;
     ok = ok && hipMalloc(&ctx->ovf_st, R * dk::MAX_DEPTH * sizeof(uint64_t)) == hipSuccess;
@@ -1354,18 +1381,18 @@ dk_ctx* dk_create(const dk_config* cfg) {
         // pass only has to finish the few roots that need it
         // (long searches: at most FALLBACK_BYTES, in whole 64-root regions; 64 roots at 200,000
         // iterations are 8 GB)
-        const size_t FS = proven, per_root = FS * (sizeof(dk::NodeHot32) + sizeof(dk::NodeCold)) + ST * STATE_SLOT_BYTES;
+        const size_t FS = proven, per_root = FS * (HR + sizeof(dk::NodeCold)) + ST * STATE_SLOT_BYTES;
         size_t FR = R < FALLBACK_ROOTS ? R : FALLBACK_ROOTS;
         const size_t by_bytes = std::max<size_t>(64, FALLBACK_BYTES / per_root / 64 * 64);
         FR = FR < by_bytes ? FR : by_bytes;
         ctx->fb_roots = (uint32_t)FR;
         ctx->fb_slots = proven;
-        ok = hipMalloc(&ctx->fb_hot, FR * FS * sizeof(dk::NodeHot32)) == hipSuccess;
+        ok = hipMalloc(&ctx->fb_hot, FR * FS * HR) == hipSuccess;
         ok = ok && hipMalloc(&ctx->fb_cold, FR * FS * sizeof(dk::NodeCold)) == hipSuccess;
         ok = ok && hipMalloc(&ctx->fb_ovf, FR * dk::MAX_DEPTH * sizeof(uint32_t)) == hipSuccess;
         ok = ok && hipMalloc(&ctx->fb_ovf_st, FR * dk::MAX_DEPTH * sizeof(uint64_t)) == hipSuccess;
         ok = ok && hipMalloc(&ctx->fb_states, FR * ST * STATE_SLOT_BYTES) == hipSuccess;
-        ctx->fb_bytes = FR * FS * (sizeof(dk::NodeHot32) + sizeof(dk::NodeCold)) + FR * ST * STATE_SLOT_BYTES;
+        ctx->fb_bytes = FR * FS * (HR + sizeof(dk::NodeCold)) + FR * ST * STATE_SLOT_BYTES;
     }
     // search slots (in-flight launches); the slot's lists are sized for max_roots
     ctx->slots.resize(dk_ctx::MAX_INFLIGHT);
@@ -1396,15 +1423,7 @@ dk_ctx* dk_create(const dk_config* cfg) {
     // root, whatever the pools' capacity (sized for max_iterations), so the 8-B records' 13-bit
     // child_base/2 field always holds its slots: only the even block alignment is a condition.
     ctx->p8_ok = ctx->cap_slots % 2 == 0 && ctx->fb_slots % 2 == 0;
-    // 32-bit pool offsets (GpuMem::at) cover a wave's region only below 4 GiB: 64 lanes x the
-    // capacity x the widest record, in the main and the fallback pools, and the node states
-    {
-        const uint64_t lim = 1ULL << 32, lanes = WAVE;
-        const uint64_t slots = std::max<uint64_t>(ctx->cap_slots, ctx->fb_slots);
-        ctx->wide = lanes * slots * sizeof(dk::NodeHot32) >= lim || lanes * slots * sizeof(dk::NodeCold) >= lim ||
-                    lanes * ST * STATE_SLOT_BYTES >= lim;
-    }
-    ctx->pool_bytes = R * S * (sizeof(dk::NodeHot32) + sizeof(dk::NodeCold)) + R * ST * STATE_SLOT_BYTES + ctx->fb_bytes;
+    ctx->pool_bytes = R * S * (HR + sizeof(dk::NodeCold)) + R * ST * STATE_SLOT_BYTES + ctx->fb_bytes;
     if (!ok) { dk_destroy(ctx); return nullptr; }
     return ctx;
 }

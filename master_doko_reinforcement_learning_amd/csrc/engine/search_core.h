@@ -39,6 +39,7 @@
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <type_traits>
 #include "common.h"
 #include "rng.h"
 
@@ -81,6 +82,7 @@ struct alignas(16) NodeHot16 {
     static constexpr int MIN_WAVES = DK_HOT16_WAVES;   // search-kernel register budget (3 waves per SIMD: <= 168 VGPRs)
     static constexpr bool WIDE = false;                // pool offsets: 32-bit (a wave's regions < 4 GiB)
     static constexpr bool PAIR = false;                // two lanes per root (NodeHot16P)
+    static constexpr bool LONG = false;                // 64-bit cross products (NodeHot16L)
 };
 // 16-B records searched by lane PAIRS: launches of at most 32 roots per wave (a single wave per
 // SIMD, half of its lanes otherwise idle) give every root two lanes, lane l and l + 32.  Both
@@ -91,6 +93,17 @@ struct alignas(16) NodeHot16 {
 struct alignas(16) NodeHot16P : NodeHot16 {
     static constexpr int MIN_WAVES = 1;
     static constexpr bool PAIR = true;
+};
+// 16-B records for searches beyond P24_MAX_ITERS iterations (the production shape: 200,000
+// iterations per sample, compare_impi/run.rs:270-291): the same record and pick, with the sibling
+// means compared by 64-bit cross products (|w| <= 123 v, v < 2^22: products < 2^53).  Until round
+// 4 such searches took the 32-B records (NodeHot32); these halve the hot pool per slot.
+struct alignas(16) NodeHot16L : NodeHot16 {
+    static constexpr int MIN_WAVES = 2;
+    static constexpr bool LONG = true;
+};
+struct alignas(16) NodeHot16PL : NodeHot16P {
+    static constexpr bool LONG = true;
 };
 struct alignas(32) NodeHot32 {
     uint64_t stats;
@@ -103,6 +116,7 @@ struct alignas(32) NodeHot32 {
     static constexpr int MIN_WAVES = 1;   // no budget (its launches have one wave per SIMD)
     static constexpr bool WIDE = false;
     static constexpr bool PAIR = false;
+    static constexpr bool LONG = false;   // (its pick compares the cached exact means)
 };
 // NodeHot32 addressed with 64-bit offsets: contexts whose per-wave pool regions reach 4 GiB
 // (very long searches: the fallback pool's 32-B records at >= ~175 K iterations, node states
@@ -124,6 +138,7 @@ struct alignas(8) NodeHot8 {
     static constexpr int MIN_WAVES = DK_HOT16_WAVES;
     static constexpr bool WIDE = false;
     static constexpr bool PAIR = false;
+    static constexpr bool LONG = false;
 };
 // visits < 2^11, slots < 2^14, state indices < 2^10 (bit 10 of the state field marks a
 // resolved chain head, below)
@@ -157,7 +172,9 @@ template <> struct is_p8<NodeHot8> { static constexpr bool value = true; };
 #ifndef DK_HOT16
 #define DK_HOT16 1
 #endif
-#if DK_HOT16
+#if defined(DK_HOT16L) && DK_HOT16L
+using NodeHot = NodeHot16L;   // (host builds of the long 16-B records: 64-bit cross products)
+#elif DK_HOT16
 using NodeHot = NodeHot16;
 #else
 using NodeHot = NodeHot32;
@@ -353,6 +370,29 @@ DK_HD int mul24(int a, int b) {
 #endif
 }
 DK_HD bool mean_lt(int32_t wa, uint32_t va, int32_t wb, uint32_t vb) { return mul24(wa, (int)vb) < mul24(wb, (int)va); }
+// the comparison of the long records (NodeHot16L): 64-bit cross products, exact for |w| <= 123 v and
+// v < NI_MAX_STATES (iterations are bounded by the state index field): |w| v < 123 * 2^44 < 2^51
+template <bool LONG>
+DK_HD bool mean_lt_t(int32_t wa, uint32_t va, int32_t wb, uint32_t vb) {
+    if constexpr (LONG) return (int64_t)wa * (int64_t)vb < (int64_t)wb * (int64_t)va;
+    else return mean_lt(wa, va, wb, vb);
+}
+// The spread of the sibling means as D = wmax vmin - wmin vmax >= 0 (exact), returned as f32
+// (D == 0 <=> the reference's `range < f64::EPSILON`: distinct fractions with denominators below
+// 2^22 differ by more than 2^-44, which their f64 quotients keep).
+template <bool LONG>
+DK_HD float spread_d(int32_t wmax, uint32_t vmax, int32_t wmin, uint32_t vmin, bool* flat) {
+    if constexpr (LONG) {
+        const int64_t D = (int64_t)wmax * (int64_t)vmin - (int64_t)wmin * (int64_t)vmax;
+        *flat = D == 0;
+        return (float)D;
+    } else {
+        // >= 0 and < 2^32: exact in u32 arithmetic (each product is < 2^31 in magnitude, mean_lt)
+        const uint32_t D = (uint32_t)mul24(wmax, (int)vmin) - (uint32_t)mul24(wmin, (int)vmax);
+        *flat = D == 0;
+        return (float)D;
+    }
+}
 
 // Blocks of 8-B records held as raw words.
 struct Block8 {
@@ -362,6 +402,7 @@ struct Block8 {
 // Record accessors of the shared pick (pick_child_x): a child's raw fields as the block
 // holds them, its visits / win_score, and the in-register decode of the picked child.
 struct Raw16 {
+    static constexpr bool LONG = false;
     uint64_t st; uint32_t cb, inf;
     DK_HD static Raw16 at(const Block& b, int j) { return Raw16{b.st[j], b.cb[j], b.inf[j]}; }
     DK_HD uint32_t vis() const { return (uint32_t)st; }
@@ -372,7 +413,12 @@ struct Raw16 {
     DK_HD uint32_t info() const { return inf; }
     DK_HD bool forced() const { return ni_nchild(inf) == 1 && !ni_open(inf); }
 };
+struct Raw16L : Raw16 {   // (NodeHot16L: 64-bit cross products)
+    static constexpr bool LONG = true;
+    DK_HD static Raw16L at(const Block& b, int j) { Raw16L r; r.st = b.st[j]; r.cb = b.cb[j]; r.inf = b.inf[j]; return r; }
+};
 struct Raw8 {
+    static constexpr bool LONG = false;
     uint32_t w0, w1;
     DK_HD static Raw8 at(const Block8& b, int j) { return Raw8{b.w0[j], b.w1[j]}; }
     DK_HD uint32_t vis() const { return p8_visits(w0); }
@@ -389,6 +435,10 @@ template <>
 DK_HD Raw16 sel_raw(bool p, const Raw16& a, const Raw16& b) { return Raw16{p ? a.st : b.st, p ? a.cb : b.cb, p ? a.inf : b.inf}; }
 template <>
 DK_HD Raw8 sel_raw(bool p, const Raw8& a, const Raw8& b) { return Raw8{p ? a.w0 : b.w0, p ? a.w1 : b.w1}; }
+template <>
+DK_HD Raw16L sel_raw(bool p, const Raw16L& a, const Raw16L& b) {
+    Raw16L r; r.st = p ? a.st : b.st; r.cb = p ? a.cb : b.cb; r.inf = p ? a.inf : b.inf; return r;
+}
 
 
 // The pick for 8-B and 16-B records (no stored mean), bit-exact with the reference's first
@@ -430,17 +480,16 @@ DK_HD uint32_t pick_child_x(const B& b, uint32_t n, double lnN, double c, Mem& m
             const R r = R::at(b, j);
             const int32_t w = r.win();
             const uint32_t v = r.vis();
-            const bool lt = mean_lt(w, v, wmin, vmin);
-            const bool gt = mean_lt(wmax, vmax, w, v);
+            const bool lt = mean_lt_t<R::LONG>(w, v, wmin, vmin);
+            const bool gt = mean_lt_t<R::LONG>(wmax, vmax, w, v);
             wmin = lt ? w : wmin; vmin = lt ? v : vmin;
             wmax = gt ? w : wmax; vmax = gt ? v : vmax;
         }
     }
-    // >= 0 and < 2^32: exact in u32 arithmetic (each product is < 2^31 in magnitude, mean_lt)
-    const uint32_t D = (uint32_t)mul24(wmax, (int)vmin) - (uint32_t)mul24(wmin, (int)vmax);
-    const bool flat = D == 0;
-    const float vv = (float)vmin * (float)vmax;                           // exact: < 2^24
-    const float A = flat ? 0.0f : 2.0f * vv * rcp_approx((float)D);
+    bool flat;
+    const float Df = spread_d<R::LONG>(wmax, vmax, wmin, vmin, &flat);
+    const float vv = (float)vmin * (float)vmax;                           // exact below 2^24 (LONG: one rounding)
+    const float A = flat ? 0.0f : 2.0f * vv * rcp_approx(Df);
     const float minf = (float)wmin * rcp_approx((float)vmin);
     const float maxf = (float)wmax * rcp_approx((float)vmax);
     const float Bc = flat ? 1.0f : -(minf * A + 1.0f);
@@ -542,7 +591,7 @@ DK_HD double pair_xd(double v) { union { double d; uint64_t u; } a; a.d = v; a.u
 // the lower half's only when it is STRICTLY smaller (sibling minimum), strictly larger (sibling
 // maximum, first estimate maximum, first exact maximum), so both lanes end with the reference's
 // first strict maximum (node.rs:258-277) and the same record.
-template <class Mem>
+template <bool LONG, class Mem>
 DK_HD uint32_t pick_child_pair(const BlockH& b, uint32_t n, uint32_t j0, double lnN, double c, Mem& mem,
                                uint64_t* p_st, uint32_t* p_cb, uint32_t* p_inf, NodeHot16* end, bool* end_ok,
                                uint32_t cbx) {
@@ -556,8 +605,8 @@ DK_HD uint32_t pick_child_pair(const BlockH& b, uint32_t n, uint32_t j0, double 
         if (j0 + (uint32_t)k < n) {
             const int32_t w = (int32_t)(b.st[k] >> 32);
             const uint32_t v = (uint32_t)b.st[k];
-            const bool lt = mean_lt(w, v, wmin, vmin);
-            const bool gt = mean_lt(wmax, vmax, w, v);
+            const bool lt = mean_lt_t<LONG>(w, v, wmin, vmin);
+            const bool gt = mean_lt_t<LONG>(wmax, vmax, w, v);
             wmin = lt ? w : wmin; vmin = lt ? v : vmin;
             wmax = gt ? w : wmax; vmax = gt ? v : vmax;
         }
@@ -572,15 +621,15 @@ DK_HD uint32_t pick_child_pair(const BlockH& b, uint32_t n, uint32_t j0, double 
         const int32_t bwmin = upper ? wmin : pwmin, bwmax = upper ? wmax : pwmax;
         const uint32_t bvmin = upper ? vmin : pvmin, bvmax = upper ? vmax : pvmax;
         const bool bh = upper ? have : phave;
-        const bool bmin = bh && mean_lt(bwmin, bvmin, awmin, avmin);
-        const bool bmax = bh && mean_lt(awmax, avmax, bwmax, bvmax);
+        const bool bmin = bh && mean_lt_t<LONG>(bwmin, bvmin, awmin, avmin);
+        const bool bmax = bh && mean_lt_t<LONG>(awmax, avmax, bwmax, bvmax);
         wmin = bmin ? bwmin : awmin; vmin = bmin ? bvmin : avmin;
         wmax = bmax ? bwmax : awmax; vmax = bmax ? bvmax : avmax;
     }
-    const uint32_t D = (uint32_t)mul24(wmax, (int)vmin) - (uint32_t)mul24(wmin, (int)vmax);
-    const bool flat = D == 0;
+    bool flat;
+    const float Df = spread_d<LONG>(wmax, vmax, wmin, vmin, &flat);
     const float vv = (float)vmin * (float)vmax;
-    const float A = flat ? 0.0f : 2.0f * vv * rcp_approx((float)D);
+    const float A = flat ? 0.0f : 2.0f * vv * rcp_approx(Df);
     const float minf = (float)wmin * rcp_approx((float)vmin);
     const float maxf = (float)wmax * rcp_approx((float)vmax);
     const float Bc = flat ? 1.0f : -(minf * A + 1.0f);
@@ -837,7 +886,7 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
                     }
                     DK_STAMP_DRAINED(tl1);
                     DK_PROF(mem, 8, tl1 - tl0);
-                    pick = pick_child_pair(blk, n, j0, lnN, c, mem, &y.stats, &y.child_base, &y.info, &end, &end_ok, x.child_base);
+                    pick = pick_child_pair<Mem::Rec::LONG>(blk, n, j0, lnN, c, mem, &y.stats, &y.child_base, &y.info, &end, &end_ok, x.child_base);
                     DK_STAMP_DRAINED(tl2);
                     DK_PROF(mem, 9, tl2 - tl1);
                 } else {
@@ -859,7 +908,8 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
                     if constexpr (NodeHot::CACHED_MEAN)
                         pick = pick_child_reg(blk, n, lnN, c, mem, &y.stats, &y.child_base, &y.info, &end, &end_ok);
                     else
-                        pick = pick_child_x<Raw16>(blk, n, lnN, c, mem, &y.stats, &y.child_base, &y.info, &end, &end_ok, x.child_base);
+                        pick = pick_child_x<typename std::conditional<Mem::Rec::LONG, Raw16L, Raw16>::type>(
+                            blk, n, lnN, c, mem, &y.stats, &y.child_base, &y.info, &end, &end_ok, x.child_base);
                     DK_STAMP_DRAINED(tl2);
                     DK_PROF(mem, 9, tl2 - tl1);
                 }

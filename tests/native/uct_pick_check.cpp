@@ -1,5 +1,6 @@
 // TEST INFRASTRUCTURE: the search's UCT picks (pick_child_x over 16-B or, with
-// -DDK_PICK8, 8-B records; pick_child_reg over 32-B records in DK_HOT16=0 builds) against the plain
+// -DDK_PICK8, 8-B records, with -DDK_HOT16L the long 16-B records whose means compare by 64-bit
+// cross products; pick_child_reg over 32-B records in DK_HOT16=0 builds) against the plain
 // two-pass f64 UCT of the reference (node.rs:202-277) on random and near-tied
 // child blocks, with the f32 reciprocal / sqrt perturbed by up to 4 ulp (the
 // GPU's v_rcp_f32 / v_sqrt_f32 are within 1 ulp).  Prints "OK <n>".
@@ -58,6 +59,8 @@ int main(int argc, char** argv) {
         // and |mean| <= 123 (search_core.h); mode 5 probes large visit counts within that
 #if DK_PICK8
         const uint32_t VBOUND = dk::P8_MAX_ITERS;
+#elif defined(DK_HOT16L) && DK_HOT16L
+        const uint32_t VBOUND = dk::NI_MAX_STATES - 1;   // the long records: any search length
 #else
         const uint32_t VBOUND = dk::P24_MAX_ITERS;
 #endif
@@ -119,7 +122,9 @@ int main(int argc, char** argv) {
             blk.st[j] = rec[j].stats; blk.cb[j] = cb_of((uint32_t)j); blk.inf[j] = info_of((uint32_t)j);
             blk.q[j] = dk::hot_q(rec[j]); blk.isv[j] = dk::hot_isv(rec[j]);
         }
-#if DK_HOT16
+#if defined(DK_HOT16L) && DK_HOT16L
+        const uint32_t a = dk::pick_child_x<dk::Raw16L>(blk, n, lnN, c, nm, &gs, &gc, &gi, &end, &end_ok, 0u);
+#elif DK_HOT16
         const uint32_t a = dk::pick_child_x<dk::Raw16>(blk, n, lnN, c, nm, &gs, &gc, &gi, &end, &end_ok, 0u);
 #else
         const uint32_t a = dk::pick_child_reg(blk, n, lnN, c, nm, &gs, &gc, &gi, &end, &end_ok);

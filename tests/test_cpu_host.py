@@ -62,6 +62,16 @@ def test_hot32_variant_exact(native_bins):
     assert _run("search_check32", 6, 400, 5) > 10
 
 
+def test_hot16l_variant_exact(native_bins):
+    """The long 16-B records (NodeHot16L / NodeHot16PL: searches beyond 4,095 iterations, the
+    production shape's 200,000) compare sibling means by 64-bit cross products: the filtered pick
+    equals the plain f64 UCT for visit counts up to 2^22, and whole searches past the 24-bit
+    limit equal the oracle's."""
+    assert _run("uct_pick_check16l", 1000000, 6) == 1000000
+    assert _run("search_check16l", 3, 5000, 21) > 2
+    assert _run("search_check16l", 1, 12000, 31) >= 1
+
+
 def test_hot8_variant_exact(native_bins):
     """The 8-B packed hot records (DK_HOT8: even-aligned child blocks, pair loads, the root
     in registers) give the oracle's searches exactly."""

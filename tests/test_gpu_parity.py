@@ -742,13 +742,17 @@ def test_az_selfplay_with_network(eng):
         dk.az_step(eng, recs, actions)
 
 
-@pytest.mark.parametrize("iters,env,hot", [(1023, {"DK_HOT_RECORD": "8"}, "8B"), (1024, {"DK_HOT_RECORD": "8"}, "16B"),
-                                           (4095, {"DK_HOT_RECORD": "16"}, "16B"), (4096, {"DK_HOT_RECORD": "16"}, "32B")])
+@pytest.mark.parametrize("iters,env,hot", [(1023, {"DK_HOT_RECORD": "8"}, "8B long=0"), (1024, {"DK_HOT_RECORD": "8"}, "16B"),
+                                           (4095, {"DK_HOT_RECORD": "16"}, "16B long=0"),
+                                           (4096, {"DK_HOT_RECORD": "16"}, "16B long=1"),
+                                           (4096, {"DK_HOT_RECORD": "32"}, "32B long=0")])
 def test_search_record_width_limits(iters, env, hot, monkeypatch, capfd):
     """The iteration limits of the packed hot records (search_core.h): 8-B records hold
-    <= 1023 iterations (11-bit visits, 10-bit state indices), 16-B records <= 4095 (24-bit
-    cross products); one iteration more takes the next wider layout even when a narrower
-    one is forced.  Roots at the limit equal oracle searches bitwise."""
+    <= 1023 iterations (11-bit visits, 10-bit state indices), 16-B records compare means by
+    24-bit cross products up to 4095 iterations and by 64-bit ones beyond (NodeHot16L, round 5);
+    one iteration more takes the next layout even when a narrower one is forced, and the 32-B
+    cached-mean records stay available (DK_HOT_RECORD=32).  Roots at the limit equal oracle
+    searches bitwise."""
     import master_doko_reinforcement_learning_amd as dk
     for k, v in env.items():
         monkeypatch.setenv(k, v)
@@ -762,7 +766,8 @@ def test_search_record_width_limits(iters, env, hot, monkeypatch, capfd):
         visits, values, best = dk.CachedMCTS(e, dk.GAME_FULL_DOKO).monte_carlo_tree_search(pack_all(pick), 2.5, iters, seeds)
         err = capfd.readouterr().err
         lines = [l for l in err.splitlines() if l.startswith("doko_amd: search")]
-        assert lines and ("hot=%s" % hot) in lines[0], err[-1000:]
+        h, _, lg = hot.partition(" ")
+        assert lines and ("hot=%s" % h) in lines[0] and lg in lines[0], err[-1000:]
         for i, (b, v, val) in enumerate(_oracle_search(pick, seeds, iters, 2.5, "fdo")):
             assert sum(v) == iters and list(visits[i]) == v, i
             assert values[i].tobytes() == np.array(val, dtype=np.float64).tobytes(), i
@@ -771,14 +776,16 @@ def test_search_record_width_limits(iters, env, hot, monkeypatch, capfd):
         e.close()
 
 
-@pytest.mark.parametrize("iters,n", [(12000, 6), (50000, 2), (200000, 1)])
-def test_search_parity_production_shape(iters, n):
+@pytest.mark.parametrize("iters,n,hot32", [(12000, 6, False), (50000, 2, False), (200000, 1, False), (200000, 1, True)])
+def test_search_parity_production_shape(iters, n, hot32, monkeypatch):
     """Searches of the thesis's production length (run.rs:270-291 runs 200,000 iterations per
-    sample; its grid goes to 2,000,000, run.rs:107-118): 32-B records with cached means
-    (iterations > 4095), deep LDS-path overflow, and at 200,000 iterations 64-bit pool offsets
-    (a wave's fallback region passes 4 GiB).  Visits, values (bitwise) and the best move
-    equal the oracle's."""
+    sample; its grid goes to 2,000,000, run.rs:107-118): the long 16-B records (64-bit cross
+    products, iterations > 4095) and deep LDS-path overflow; with DK_HOT_RECORD=32 the 32-B
+    records with cached means, which at 200,000 iterations take 64-bit pool offsets (a wave's
+    fallback region passes 4 GiB).  Visits, values (bitwise) and the best move equal the oracle's."""
     import master_doko_reinforcement_learning_amd as dk
+    if hot32:
+        monkeypatch.setenv("DK_HOT_RECORD", "32")
     pool = [s for s in fdo_states(8, 53) if s.info()["phase"] != 3 and s.info()["card_index"] < 24]
     rng = np.random.default_rng(iters)
     pick = [pool[i] for i in rng.choice(len(pool), size=n, replace=False)]
