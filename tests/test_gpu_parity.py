@@ -263,13 +263,18 @@ def test_search_capacity_fallback(cap, env, monkeypatch):
         e.close()
 
 
-def test_search_wide_pools(monkeypatch, capfd):
-    """A context sized for 200,000 iterations (compare_impi's setting): its fallback pool's
-    per-wave region (64 lanes x 2.4 M slots x 32 B) passes 4 GiB, so every launch takes the
-    64-bit-offset records (NodeHot32W, launch line wide=1).  With a 256-slot main pool the
-    roots overflow into that fallback pool; results equal the oracle's."""
+@pytest.mark.parametrize("hot32", [True, False])
+def test_search_wide_pools(hot32, monkeypatch, capfd):
+    """A context sized for 200,000 iterations (compare_impi's setting).  With the 32-B records
+    (DK_HOT_RECORD=32) its fallback pool's per-wave region (64 lanes x 2.4 M slots x 32 B) passes
+    4 GiB, so every launch takes the 64-bit-offset records (NodeHot32W, launch line wide=1); with
+    the default 16-B records (round 5) the region stays below 4 GiB and the 32-bit offsets hold
+    (wide=0).  With a 256-slot main pool the roots overflow into the fallback pool; results
+    equal the oracle's either way."""
     import master_doko_reinforcement_learning_amd as dk
     monkeypatch.setenv("DK_VERBOSE", "1")
+    if hot32:
+        monkeypatch.setenv("DK_HOT_RECORD", "32")
     e = dk.Engine(device=0, max_roots=64, max_iterations=200000, slot_capacity=256)
     try:
         pool = [s for s in fdo_states(8, 31) if s.info()["phase"] != 3]
@@ -281,7 +286,10 @@ def test_search_wide_pools(monkeypatch, capfd):
     finally:
         e.close()
     err = capfd.readouterr().err
-    assert "wide=1" in err and "hot=32B" in err, err[-800:]
+    if hot32:
+        assert "wide=1" in err and "hot=32B" in err, err[-800:]
+    else:
+        assert "wide=0" in err and "hot=16B" in err, err[-800:]
     for i, (b, v, val) in enumerate(_oracle_search(pick, seeds, 1500, 2.5, "fdo")):
         assert list(visits[i]) == v, i
         assert values[i].tobytes() == np.array(val, dtype=np.float64).tobytes(), i
