@@ -47,7 +47,7 @@ def _bench(tmp_path, gpus, infostates, fusion, tag, partition="samples", backend
            "--no-cpu-baseline", "--small-infostates", "0", "--infostates", str(infostates),
            "--iterations", str(ITERS), "--fusion", fusion, "--dump-actions", act, "--dump-acc", acc,
            "--partition", partition] + list(extra)
-    out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=110)
+    out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=110 + 20 * gpus)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
     line = [l for l in out.stdout.splitlines() if l.startswith("{")][-1]
     return json.loads(line), np.load(act), np.load(acc)
@@ -99,21 +99,23 @@ def test_bench_rccl_one_rank(tmp_path, partition):
     assert np.array_equal(acc, acc0) and np.array_equal(a, a0)
 
 
+@pytest.mark.parametrize("ranks", [4, 8])
 @pytest.mark.parametrize("partition", ["infostates", "samples"])
-def test_bench_four_ranks(tmp_path, partition):
-    """Four ranks on one GPU (gloo): the all-gather of the actions (infostates) and the
-    all-reduce of the accumulators (samples, the shape config 4 names: "RCCL visit
-    all-reduce") at the width of a 4-GPU run.  MaxN decisions and accumulators equal the
+def test_bench_many_ranks(tmp_path, partition, ranks):
+    """Four and eight ranks on one GPU (gloo): the all-gather of the actions (infostates) and
+    the all-reduce of the accumulators (samples, the shape config 4 names: "RCCL visit
+    all-reduce") at the width of a 4- and an 8-GPU run (C4's full width: 8 samples per
+    infostate and rank with the sample split).  MaxN decisions and accumulators equal the
     1-rank run over the same global workload bit for bit, and the line attributes each rank's
     step: search-kernel and collective milliseconds per rank (compare_impi.rs:217-291)."""
-    per = INFO_PER_RANK // 2          # --infostates: per rank (infostates) / global = 4 x per (samples)
-    r4, a4, acc4 = _bench(tmp_path, 4, per, "maxn", "q4" + partition, partition)
-    assert r4["n_gpus"] == 4 and r4["ranks"] == 4
-    assert len(r4["search_kernel_ms_per_rank"]) == 4 and len(r4["collective_ms_per_rank"]) == 4
-    assert all(ms > 0 for ms in r4["search_kernel_ms_per_rank"]) and r4["collective_ms"] >= 0
-    assert r4["collective"].startswith("all_gather" if partition == "infostates" else "all_reduce")
-    total = 4 * per
-    assert r4["config"]["roots_per_gpu"] == per * 64        # infostates: per x 64; samples: 4 per x 16
-    r1, a1, acc1 = _bench(tmp_path, 1, total, "maxn", "q1" + partition, partition)
-    assert a4.shape == (total,)
-    assert np.array_equal(acc4, acc1) and np.array_equal(a4, a1)
+    per = INFO_PER_RANK // 2          # --infostates: per rank (infostates) / global = ranks x per (samples)
+    rN, aN, accN = _bench(tmp_path, ranks, per, "maxn", "q%d%s" % (ranks, partition), partition)
+    assert rN["n_gpus"] == ranks and rN["ranks"] == ranks
+    assert len(rN["search_kernel_ms_per_rank"]) == ranks and len(rN["collective_ms_per_rank"]) == ranks
+    assert all(ms > 0 for ms in rN["search_kernel_ms_per_rank"]) and rN["collective_ms"] >= 0
+    assert rN["collective"].startswith("all_gather" if partition == "infostates" else "all_reduce")
+    total = ranks * per
+    assert rN["config"]["roots_per_gpu"] == per * 64        # infostates: per x 64; samples: ranks per x 64/ranks
+    r1, a1, acc1 = _bench(tmp_path, 1, total, "maxn", "q1%d%s" % (ranks, partition), partition)
+    assert aN.shape == (total,)
+    assert np.array_equal(accN, acc1) and np.array_equal(aN, a1)
