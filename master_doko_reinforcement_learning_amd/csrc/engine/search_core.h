@@ -54,12 +54,19 @@ namespace dk {
 #define DK_PROF_FLUSH(mem) for (int k_ = 0; k_ < PROF_SLOTS; ++k_) mem.prof_add(k_, prof_acc[k_])
 #define DK_STAMP_DRAINED(t) __builtin_amdgcn_s_waitcnt(0); const uint64_t t = __builtin_amdgcn_s_memtime()
 #define DK_PROF_WAVEMAX(k, v) do { int m_ = (v); for (int o_ = 32; o_ >= 1; o_ >>= 1) { const int t_ = __shfl_xor(m_, o_); m_ = t_ > m_ ? t_ : m_; } prof_acc[k] += (uint64_t)m_; } while (0)
+// a wave-level event counted once (by the lowest active lane): the trip of a loop, with a histogram
+// of its active lanes (slots k+1 .. k+5: <= 8, <= 16, <= 32, <= 48, <= 64) and their sum (k+6)
+#define DK_PROF_TRIP(k) do { const uint64_t b_ = __builtin_amdgcn_ballot_w64(true); const int na_ = popc64(b_); \
+    if ((int)__lane_id() == ctz64(b_)) { prof_acc[k] += 1; \
+        prof_acc[(k) + 1 + (na_ <= 8 ? 0 : na_ <= 16 ? 1 : na_ <= 32 ? 2 : na_ <= 48 ? 3 : 4)] += 1; \
+        prof_acc[(k) + 6] += (uint64_t)na_; } } while (0)
 #else
 #define DK_STAMP(t) [[maybe_unused]] const uint64_t t = 0
 #define DK_PROF(mem, k, v) ((void)0)
 #define DK_PROF_DECL
 #define DK_PROF_FLUSH(mem) ((void)0)
 #define DK_PROF_WAVEMAX(k, v) ((void)0)
+#define DK_PROF_TRIP(k) ((void)0)
 #define DK_STAMP_DRAINED(t) [[maybe_unused]] const uint64_t t = 0
 #endif
 
@@ -197,7 +204,7 @@ static constexpr uint32_t NI_MAX_STATES = 1u << 22;
 #ifndef DK_DEFER_BACKUP
 #define DK_DEFER_BACKUP 0
 #endif
-static constexpr int PROF_SLOTS = 24;   // per-root counters of the profiling build (DK_PHASE_PROF)
+static constexpr int PROF_SLOTS = 40;   // per-root counters of the profiling build (DK_PHASE_PROF)
 static constexpr int MAX_DEPTH = 512;   // selection path bound (LDS part + global overflow)
 
 DK_HD int sel4i(const int r[4], int p) { return p == 0 ? r[0] : (p == 1 ? r[1] : (p == 2 ? r[2] : r[3])); }
@@ -836,6 +843,7 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
             DK_PROF(mem, 19, tf1 - tf0);   // forced-chain hops
             if (status != SR_OK || ni_nchild(x.info) == 0 || ni_open(x.info)) break;
             const uint32_t n = ni_nchild(x.info);
+            DK_PROF_TRIP(21);   // branching-level trips of the wave (slots 21-27)
             uint32_t pick;
             NodeHot y, end;
             bool end_ok = false;

@@ -34,7 +34,7 @@ def main():
     prof = getattr(L, "dk_phase_profile", None)
     if prof is not None:
         prof.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]
-        out = np.zeros((n_roots, 24), dtype=np.uint64)
+        out = np.zeros((n_roots, 40), dtype=np.uint64)
         prof(eng.ctx, out.ctypes.data, n_roots)  # clear
     step()
     torch.cuda.synchronize(dev)
@@ -63,6 +63,16 @@ def main():
                     "expand_pack_store_cyc": float(out[:, 18].astype(np.float64).sum() / sims),
                     "select_forced_cyc": float(out[:, 19].astype(np.float64).sum() / sims),
                     "select_forced_loads_wave_max": float(out[:, 20].astype(np.float64).sum() / sims)})
+        # wave-level branching trips (counted once per wave): per wave-simulation, the histogram of
+        # their active lanes and the mean active lanes of a trip
+        # roots per wave of the launch (DK_PROF_RPW: 64 for C3, 32 for single-wave launches like C2)
+        res["rpw_eff"] = int(os.environ.get("DK_PROF_RPW", "64"))
+        wsims = sims / float(res["rpw_eff"])
+        trips = float(out[:, 21].astype(np.float64).sum())
+        res["select_trips_per_wave_sim"] = trips / wsims
+        res["select_trip_active_hist_per_wave_sim"] = {
+            b: float(out[:, 22 + i].astype(np.float64).sum()) / wsims for i, b in enumerate(["<=8", "<=16", "<=32", "<=48", "<=64"])}
+        res["select_trip_mean_active_lanes"] = float(out[:, 27].astype(np.float64).sum()) / max(trips, 1.0)
         tot = out[:, :4].astype(np.float64).sum(axis=1)   # per-root wave-clock cycles over the whole search
         if args.workload == "c3":
             k = np.array([[0, 8, 20, 32][(r // args.samples) % 4] for r in range(n_roots)])
