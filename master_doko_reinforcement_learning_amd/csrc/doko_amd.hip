@@ -100,6 +100,7 @@ struct GpuMem {
     int lds_n;            // path entries held in LDS
     const double* ln_glob;
     uint32_t cap_slots, cap_states;
+    uint32_t balign;      // child blocks start at multiples of this many slots (a power of two)
 #ifdef DK_PHASE_PROF
     uint64_t* prof;
 #endif
@@ -219,7 +220,8 @@ __global__ void __launch_bounds__(WAVE, H::MIN_WAVES) search_kernel(const dk_sta
                                                       uint32_t iters, double c, const double* __restrict__ ln_table,
                                                       void* hot_pool, dk::NodeCold* cold, typename E::Node* states,
                                                       uint32_t* ovf, uint64_t* ovf_st,
-                                                      uint32_t cap_slots, uint32_t st_stride, uint32_t rpw, int lds_n,
+                                                      uint32_t cap_slots, uint32_t st_stride, uint32_t balign,
+                                                      uint32_t rpw, int lds_n,
                                                       uint32_t* visits, double* values,
                                                       uint8_t* best, int* err, uint32_t* queue, uint64_t* prof,
                                                       const uint32_t* __restrict__ order, uint32_t* retry,
@@ -282,7 +284,7 @@ __global__ void __launch_bounds__(WAVE, H::MIN_WAVES) search_kernel(const dk_sta
         mem.half = PAIR ? lane >> 5 : 0u;
         mem.ovf = ovf + wr * dk::MAX_DEPTH;
         mem.ovf_st = ovf_st + wr * dk::MAX_DEPTH;
-        mem.cap_slots = cap_slots; mem.cap_states = T;
+        mem.cap_slots = cap_slots; mem.cap_states = T; mem.balign = balign;
 #ifdef DK_PHASE_PROF
         mem.prof = prof + (size_t)root * dk::PROF_SLOTS;
 #else
@@ -924,6 +926,8 @@ struct dk_ctx {
     bool p8_ok = false;             // the pools' slot capacities suit the 8-B records (even-aligned blocks)
     bool wide = false;              // a wave's pool region reaches 4 GiB: NodeHot32W (64-bit offsets) only
     size_t hot_rec = 16;            // bytes per hot-record slot in the pools (16, or 32: forced / wide)
+    uint32_t block_align = 1;       // DK_BLOCK_ALIGN: child blocks of the main pass start at multiples of
+                                    // this many slots (8-B records: at least 2); the fallback pass packs
     bool ln_in_lds = false;         // DK_LN_LDS=1: ln(N) table copied into every workgroup's LDS (8 KB at
                                     // 1000 iterations); by default it is read through the L1/L2 caches
     int lds_path = 16;              // path entries kept in LDS (deeper ones spill to global): at most
@@ -1168,7 +1172,7 @@ hipError_t launch_search_t(dk_ctx* ctx, const dk_state* roots, const uint64_t* s
     }
     hipLaunchKernelGGL(kern, dim3(grid), dim3(WAVE), lds_bytes, st, roots, seeds, n, iters, c, ctx->ln_table,
                        ctx->hot, ctx->cold, (typename E::Node*)ctx->states, ctx->ovf, ctx->ovf_st, ctx->cap_slots,
-                       ctx->state_stride,
+                       ctx->state_stride, ctx->block_align,
                        rpw, lp, visits, values, best, err, sl.queue, ctx->prof,
                        ordered ? (const uint32_t*)sl.order : (const uint32_t*)nullptr,
                        fallback ? sl.retry : (uint32_t*)nullptr, (const uint32_t*)nullptr, ctx->high_water, perm, base,
@@ -1186,7 +1190,7 @@ hipError_t launch_search_t(dk_ctx* ctx, const dk_state* roots, const uint64_t* s
     const uint32_t fb_grid = ctx->fb_roots / rpw;
     hipLaunchKernelGGL(kern, dim3(fb_grid), dim3(WAVE), lds_bytes, st, roots, seeds, n, iters, c, ctx->ln_table,
                        ctx->fb_hot, ctx->fb_cold, (typename E::Node*)ctx->fb_states, ctx->fb_ovf, ctx->fb_ovf_st,
-                       ctx->fb_slots, ctx->state_stride, rpw, lp, visits, values, best, err, sl.queue_fb, ctx->prof,
+                       ctx->fb_slots, ctx->state_stride, 1u, rpw, lp, visits, values, best, err, sl.queue_fb, ctx->prof,
                        (const uint32_t*)nullptr, (uint32_t*)nullptr, (const uint32_t*)sl.retry, ctx->high_water + 2,
                        (const uint32_t*)nullptr, 0u, (uint64_t*)nullptr, rng_io);
     if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -1310,6 +1314,10 @@ dk_ctx* dk_create(const dk_config* cfg) {
         if (v == 8 || v == 16 || v == 32) ctx->hot_layout = v;
     }
     if (const char* e = getenv("DK_VERBOSE")) ctx->verbose = atoi(e) != 0;
+    if (const char* e = getenv("DK_BLOCK_ALIGN")) {
+        const int v = atoi(e);
+        if (v >= 1 && v <= 64 && (v & (v - 1)) == 0) ctx->block_align = (uint32_t)v;
+    }
     if (const char* e = getenv("DK_PAIR")) ctx->pair = atoi(e) != 0 ? 1 : 0;
     if (const char* e = getenv("DK_LN_LDS")) ctx->ln_in_lds = atoi(e) != 0;
     if (const char* e = getenv("DK_LDS_PATH")) {

@@ -1012,12 +1012,15 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
             const int a = ctz64(bit);
             const uint32_t block = nch + (uint32_t)popc64(cd.unexpanded);
             if (nch == 0) {
-                if (next_slot + block > mem.cap_slots || next_state >= mem.cap_states || next_state >= NI_MAX_STATES) {
+                // (8-B records: blocks start at even slots, next_slot stays even; mem.balign >= 1 may
+                // align them further, e.g. to whole 128-B lines)
+                const uint32_t base = (next_slot + mem.balign - 1u) & ~(mem.balign - 1u);
+                if (base + block > mem.cap_slots || next_state >= mem.cap_states || next_state >= NI_MAX_STATES) {
                     status = SR_CAPACITY;
                     break;
                 }
-                x.child_base = next_slot;
-                next_slot += P8 ? (block + 1u) & ~1u : block;
+                x.child_base = base;
+                next_slot = base + (P8 ? (block + 1u) & ~1u : block);
             }
             cd.unexpanded &= ~bit;
             const uint32_t child = x.child_base + nch;

@@ -10,6 +10,7 @@ template <class W, class R>
 struct HostMemBase {
     using Rec = R;               // the stored layout
     uint32_t cap_slots, cap_states, max_path;
+    uint32_t balign = 1;         // child-block alignment in slots (GpuMem::balign)
     std::vector<R> hot;
     std::vector<dk::NodeCold> cold;
     std::vector<W> states;
