@@ -498,6 +498,17 @@ int dk_net_fc_gelu_bf16_async(const void* x, const void* w, const void* bias, ui
 int dk_net_mlp_ln_bf16_async(const void* h, void* x_io, const void* w1, const void* b1, const void* w2, const void* b2,
                              uint32_t rows, uint32_t d, uint32_t n_hidden, const void* gamma, const void* beta, float eps,
                              void* h_out, void* stream);
+/* dk_net_mlp_ln_f32x3_async: the same MLP half at the reference's precision (round 5): f32
+ * activations and biases, bf16x3 products (each f32 operand split into bf16 hi + lo; three MFMAs
+ * per k-step, ~16-bit product accuracy as hipBLASLt's f32 GEMMs at matmul precision "medium"
+ * on gfx950).  w1_hi / w1_lo [n_hidden][d] and w2_hi / w2_lo [d][n_hidden] are the weights'
+ * bf16 hi / lo parts; x += (a W2^T + b2); h_out = LN(x).  d = 160 or 256, n_hidden % 32 == 0,
+ * n_hidden <= 1024.  Replaces F.linear + GELU + F.linear + add + LayerNorm of
+ * rs-doko-py-bridge/python/az_doko.py:87-145 at f32. */
+int dk_net_mlp_ln_f32x3_async(const float* h, float* x_io, const void* w1_hi, const void* w1_lo, const float* b1,
+                              const void* w2_hi, const void* w2_lo, const float* b2, uint32_t rows, uint32_t d,
+                              uint32_t n_hidden, const float* gamma, const float* beta, float eps, float* h_out,
+                              void* stream);
 /* dk_net_class_pool_ln_bf16_async: PerClassAttentionMLPHead's attention pooling and each class
  * MLP's opening LayerNorm (az_doko.py:42-50): x [batch][62][d], queries [classes][d] (classes
  * <= 64), w = softmax(queries x^T * scale) over the 62 tokens, a = w x, out[c][b][:] =

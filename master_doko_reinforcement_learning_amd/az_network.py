@@ -240,12 +240,29 @@ def _f32c(t):
     return t.contiguous()
 
 
+def split_bf16x3(blk):
+    """The MLP weights of a block as bf16 hi / lo pairs (w = hi + lo to ~16 bits), cached on the
+    block and rebuilt when a weight changes (version counter): the operands of the bf16x3 products
+    of mlp_ln_f32x3_kernel."""
+    key = (blk.fc.weight.data_ptr(), blk.fc.weight._version, blk.proj.weight.data_ptr(), blk.proj.weight._version)
+    c = getattr(blk, "_bf16x3", None)
+    if c is None or c[0] != key:
+        parts = []
+        for w in (blk.fc.weight.detach(), blk.proj.weight.detach()):
+            hi = w.float().bfloat16().contiguous()
+            parts += [hi, (w.float() - hi.float()).bfloat16().contiguous()]
+        c = (key, tuple(parts))
+        blk._bf16x3 = c
+    return c[1]
+
+
 class FusedTrunkF32(FusedTrunk):
-    """The f32 GPU forward of a token trunk: the reference's precision (f32 activations; the
-    GEMMs as torch F.linear, i.e. hipBLASLt at the caller's matmul precision -- the reference
-    sets "medium", az_doko.py:539-541) with HIP kernels (csrc/az_net_f32_kernels.h) for the
-    embedding sum + first LayerNorm, every residual add fused with the LayerNorm after it, the
-    attention core (f32, one wave per sample and head) and the GELU in place.  The attention
+    """The f32 GPU forward of a token trunk: the reference's precision (f32 activations; GEMM
+    products at least as fine as the reference's matmul precision "medium", az_doko.py:539-541)
+    with HIP kernels (csrc/az_net_f32_kernels.h): the embedding sum + first LayerNorm; at d = 160
+    the whole MLP half in one kernel with bf16x3 products (mlp_ln_f32x3_kernel, round 5); the
+    attention core (f32 MFMA), residual adds fused with the LayerNorm after them, and the GEMMs
+    left on hipBLASLt at "medium" (the attention projections, the d = 256 MLP).  The attention
     half's out_proj and c_proj run folded into one GEMM (Block.folded_proj, f32)."""
 
     def __init__(self, tokens, emb, ln0):
@@ -285,6 +302,16 @@ class FusedTrunkF32(FusedTrunk):
         return self.add_ln(x, _f32c(F.linear(y, w)), ln, b)
 
     def mlp_ln(self, x, blk, h, ln):
+        n = blk.fc.weight.shape[0]
+        if self.d == 160 and n % 32 == 0 and n <= 1024 and blk.fc.bias is not None and blk.proj.bias is not None:
+            # the whole MLP half in one kernel, bf16x3 products (mlp_ln_f32x3_kernel)
+            w1h, w1l, w2h, w2l = split_bf16x3(blk)
+            ho = torch.empty_like(x)
+            self.ck(self.L.dk_net_mlp_ln_f32x3_async(h.data_ptr(), x.data_ptr(), w1h.data_ptr(), w1l.data_ptr(),
+                                                     blk.fc.bias.data_ptr(), w2h.data_ptr(), w2l.data_ptr(),
+                                                     blk.proj.bias.data_ptr(), self.rows, self.d, n, ln.weight.data_ptr(),
+                                                     ln.bias.data_ptr(), ln.eps, ho.data_ptr(), self.st))
+            return ho
         a = _f32c(F.linear(h, blk.fc.weight))
         b1 = blk.fc.bias.contiguous() if blk.fc.bias is not None else None
         self.ck(self.L.dk_net_gelu_bias_f32_async(a.data_ptr(), b1.data_ptr() if b1 is not None else None, a.numel(),

@@ -351,5 +351,205 @@ __global__ void __launch_bounds__(64, HD == 40 ? DK_ATTNF32_WAVES40 : 2) attn62_
     }
 }
 
+// ---------------------------------------------------------------------------
+// The whole MLP half of a block at the reference's precision (round 5), in one pass:
+//   a = GELU(h W1^T + b1);  delta = a W2^T;  x += delta + b2;  h' = LN'(x)        (all f32)
+// The products are bf16x3: every f32 operand v is split into v_hi = bf16(v) and
+// v_lo = bf16(v - v_hi), and each k-step takes three v_mfma_f32_32x32x16_bf16 --
+// A_lo B_hi + A_hi B_lo + A_hi B_hi into one f32 accumulator -- so a product carries
+// ~16 mantissa bits (the dropped A_lo B_lo is below 2^-16 of it), the accuracy hipBLASLt
+// gives f32 GEMMs at matmul precision "medium" on gfx950 (profiles/r04/fp32_gemm_probe.json:
+// ~5e-6 relative) and finer than the TF32 products the reference's setting selects on its
+// CUDA hardware (az_doko.py:539-541, main.py:508).  The weights come pre-split (w1_hi / w1_lo,
+// w2_hi / w2_lo: bf16 copies made once per module, az_network.FusedTrunkF32); activations
+// are split in registers.  Accumulation, bias, GELU, residual and LayerNorm stay f32.
+// Layout as mlp_ln_kernel: 8 waves x 32 rows; h fragments (hi and lo) of all K = d in
+// registers; chunks of NC = 32 hidden units with W1 rows and W2 columns (hi and lo) staged in
+// LDS, double-buffered; GEMM1 D1 = W1_c h^T puts a row's hidden units in the lane's registers,
+// whose bias + GELU + split ARE the B operand of GEMM2 (D2 = W2_c a^T) without lane movement.
+// Unfused (hipBLASLt GEMMs + GELU pass + add / LN pass) the 4d-wide f32 activation went to HBM
+// and back three times per block; here a row costs its h and x reads and its x and h' writes.
+__device__ __forceinline__ void split_bf16x8(const float (&v)[8], bf16x8_t& hi, bf16x8_t& lo) {
+    union { uint32_t u[4]; bf16x8_t v; } a, b;
+#pragma unroll
+    for (int t = 0; t < 8; t += 2) {
+        a.u[t / 2] = pack_bf16x2(v[t], v[t + 1]);
+        b.u[t / 2] = pack_bf16x2(v[t] - bf2f((uint16_t)a.u[t / 2]), v[t + 1] - bf2f((uint16_t)(a.u[t / 2] >> 16)));
+    }
+    hi = a.v;
+    lo = b.v;
+}
+
+template <int D, int NC>
+__global__ void __launch_bounds__(512, 1) mlp_ln_f32x3_kernel(const float* __restrict__ h, float* __restrict__ x_io,
+                                                                const uint16_t* __restrict__ w1h, const uint16_t* __restrict__ w1l,
+                                                                const float* __restrict__ b1,
+                                                                const uint16_t* __restrict__ w2h, const uint16_t* __restrict__ w2l,
+                                                                const float* __restrict__ b2, uint32_t rows, uint32_t n_hidden,
+                                                                const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                                float eps, float* __restrict__ h_out) {
+    static_assert(D % 32 == 0 && NC == 32, "d: multiple of 32; chunks of 32 hidden units");
+    constexpr int WAVES = 8, T = 64 * WAVES;
+    constexpr int KS = D / 16, OT = D / 32, LDW1 = D + 8, LDW2 = NC + 4, GS = NC / 16;
+    constexpr int W1E = NC * LDW1, W2E = D * LDW2, BUF = 2 * (W1E + W2E);   // one buffer: W1 hi, W1 lo, W2 hi, W2 lo
+    __shared__ __attribute__((aligned(16))) uint16_t lds[2 * BUF];
+    __shared__ float b1s[MLP_MAX_HIDDEN];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
+    const uint32_t row = blockIdx.x * (32u * WAVES) + (uint32_t)wave * 32u + (uint32_t)r;
+    const bool ok = row < rows;
+    // the row's h, split: lane (r, hh) holds k = 16 kk + 8 hh .. + 7 of row r
+    bf16x8_t hfh[KS], hfl[KS];
+    {
+        const float* hr = h + (size_t)(ok ? row : 0u) * D + 8 * hh;
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk) {
+            float v[8];
+            const float4 a = ok ? *(const float4*)(hr + 16 * kk) : make_float4(0.f, 0.f, 0.f, 0.f);
+            const float4 b = ok ? *(const float4*)(hr + 16 * kk + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+            v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+            split_bf16x8(v, hfh[kk], hfl[kk]);
+        }
+    }
+    // chunk staging: 16-B pieces of W1 (NC rows x D) and W2 (D rows x NC), hi and lo
+    constexpr int P1 = NC * (D / 8), P2 = D * (NC / 8), PT = 2 * (P1 + P2), PER = (PT + T - 1) / T;
+    uint4 pc[PER];
+    auto load_chunk = [&](uint32_t c) {
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            int v = threadIdx.x + T * u;
+            if (v < 2 * P1) {
+                const uint16_t* w = v < P1 ? w1h : w1l;
+                v = v < P1 ? v : v - P1;
+                const int i = v / (D / 8), p = v - i * (D / 8);
+                pc[u] = *(const uint4*)(w + ((size_t)c * NC + i) * D + 8 * p);
+            } else if (v < PT) {
+                v -= 2 * P1;
+                const uint16_t* w = v < P2 ? w2h : w2l;
+                v = v < P2 ? v : v - P2;
+                const int o = v / (NC / 8), p = v - o * (NC / 8);
+                pc[u] = *(const uint4*)(w + (size_t)o * n_hidden + (size_t)c * NC + 8 * p);
+            }
+        }
+    };
+    auto store_chunk = [&](int buf) {
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            int v = threadIdx.x + T * u;
+            if (v < 2 * P1) {
+                const int lo = v < P1 ? 0 : 1;
+                v = lo ? v - P1 : v;
+                const int i = v / (D / 8), p = v - i * (D / 8);
+                *(uint4*)&lds[buf * BUF + lo * W1E + i * LDW1 + 8 * p] = pc[u];
+            } else if (v < PT) {
+                v -= 2 * P1;
+                const int lo = v < P2 ? 0 : 1;
+                v = lo ? v - P2 : v;
+                const int o = v / (NC / 8), p = v - o * (NC / 8);
+                uint2* d_ = (uint2*)&lds[buf * BUF + 2 * W1E + lo * W2E + o * LDW2 + 8 * p];
+                d_[0] = make_uint2(pc[u].x, pc[u].y);
+                d_[1] = make_uint2(pc[u].z, pc[u].w);
+            }
+        }
+    };
+    f32x16_t acc2[OT];
+#pragma unroll
+    for (int t = 0; t < OT; ++t) acc2[t] = f32x16_t{0};
+    const uint32_t chunks = n_hidden / NC;
+    for (uint32_t i = threadIdx.x; i < n_hidden; i += T) b1s[i] = b1[i];
+    load_chunk(0u);
+    store_chunk(0);
+    __syncthreads();
+    for (uint32_t c = 0; c < chunks; ++c) {
+        const int buf = (int)(c & 1u);
+        if (c + 1 < chunks) load_chunk(c + 1);
+        // GEMM1: D1 = W1_c h^T (one 32 x 32 tile), three products per k-step
+        f32x16_t acc1 = f32x16_t{0};
+        const uint16_t* a1h = &lds[buf * BUF + r * LDW1 + 8 * hh];
+        const uint16_t* a1l = a1h + W1E;
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk) {
+            const bf16x8_t ah = *(const bf16x8_t*)(a1h + 16 * kk), al = *(const bf16x8_t*)(a1l + 16 * kk);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, hfh[kk], acc1, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, hfl[kk], acc1, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, hfh[kk], acc1, 0, 0, 0);
+        }
+        // bias + GELU (f32) -> split B fragments of GEMM2 (k-step s = half: registers 8 s .. 8 s + 7,
+        // hidden units 16 s + 4 hh + (g & 3) + 8 ((g >> 2) & 1))
+        bf16x8_t afh[GS], afl[GS];
+#pragma unroll
+        for (int s2 = 0; s2 < GS; ++s2) {
+            const int h0 = 16 * s2 + 4 * hh;
+            const float4 bl = *(const float4*)&b1s[c * NC + h0], bh = *(const float4*)&b1s[c * NC + h0 + 8];
+            const float bb[8] = {bl.x, bl.y, bl.z, bl.w, bh.x, bh.y, bh.z, bh.w};
+            float g[8];
+#pragma unroll
+            for (int t = 0; t < 8; ++t) g[t] = gelu_poly(acc1[8 * s2 + t] + bb[t]);
+            split_bf16x8(g, afh[s2], afl[s2]);
+        }
+        // GEMM2: D2 += W2_c a^T, OT tiles of 32 output columns, three products per k-step
+        const uint16_t* a2h = &lds[buf * BUF + 2 * W1E + r * LDW2 + 4 * hh];
+        const uint16_t* a2l = a2h + W2E;
+#pragma unroll
+        for (int s2 = 0; s2 < GS; ++s2)
+#pragma unroll
+            for (int t = 0; t < OT; ++t) {
+                const int off = (32 * t) * LDW2 + 16 * s2;
+                union { uint2 u[2]; bf16x8_t v; } wh, wl;
+                wh.u[0] = *(const uint2*)(a2h + off); wh.u[1] = *(const uint2*)(a2h + off + 8);
+                wl.u[0] = *(const uint2*)(a2l + off); wl.u[1] = *(const uint2*)(a2l + off + 8);
+                acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl.v, afh[s2], acc2[t], 0, 0, 0);
+                acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh.v, afl[s2], acc2[t], 0, 0, 0);
+                acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh.v, afh[s2], acc2[t], 0, 0, 0);
+            }
+        if (c + 1 < chunks) {
+            store_chunk(buf ^ 1);
+            __syncthreads();
+        }
+    }
+    // epilogue: acc2[t][g] = delta of row `row`, column 32 t + 8 (g >> 2) + 4 hh + (g & 3);
+    // x += (delta + b2) (the GEMM's bias first: F.linear's epilogue order), then LN
+    float* xr = x_io + (size_t)(ok ? row : 0u) * D;
+    float s1 = 0.0f;
+#pragma unroll
+    for (int t = 0; t < OT; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int col = 32 * t + 8 * q + 4 * hh;
+            const float4 xv = ok ? *(const float4*)(xr + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+            const float4 bv = *(const float4*)(b2 + col);
+            const float xn[4] = {xv.x + (acc2[t][4 * q] + bv.x), xv.y + (acc2[t][4 * q + 1] + bv.y),
+                                 xv.z + (acc2[t][4 * q + 2] + bv.z), xv.w + (acc2[t][4 * q + 3] + bv.w)};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc2[t][4 * q + e] = xn[e];
+            s1 += (xn[0] + xn[1]) + (xn[2] + xn[3]);
+            if (ok) *(float4*)(xr + col) = make_float4(xn[0], xn[1], xn[2], xn[3]);
+        }
+    s1 += __shfl_xor(s1, 32);
+    const float mean = s1 / (float)D;
+    float s2 = 0.0f;
+#pragma unroll
+    for (int t = 0; t < OT; ++t)
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+            const float dv = acc2[t][g] - mean;
+            s2 += dv * dv;
+        }
+    s2 += __shfl_xor(s2, 32);
+    const float rstd = rsqrtf(s2 / (float)D + eps);
+    float* hr = h_out + (size_t)(ok ? row : 0u) * D;
+#pragma unroll
+    for (int t = 0; t < OT; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int col = 32 * t + 8 * q + 4 * hh;
+            const float4 gv = *(const float4*)(gamma + col), bv = *(const float4*)(beta + col);
+            if (ok)
+                *(float4*)(hr + col) = make_float4((acc2[t][4 * q] - mean) * rstd * gv.x + bv.x,
+                                                   (acc2[t][4 * q + 1] - mean) * rstd * gv.y + bv.y,
+                                                   (acc2[t][4 * q + 2] - mean) * rstd * gv.z + bv.z,
+                                                   (acc2[t][4 * q + 3] - mean) * rstd * gv.w + bv.w);
+        }
+}
+
 }  // namespace net
 }  // namespace dk

@@ -2198,6 +2198,28 @@ int dk_net_mlp_ln_bf16_async(const void* h, void* x_io, const void* w1, const vo
     return DK_OK;
 }
 
+// The MLP half at the reference's precision: f32 activations, bf16x3 products (mlp_ln_f32x3_kernel).
+int dk_net_mlp_ln_f32x3_async(const float* h, float* x_io, const void* w1_hi, const void* w1_lo, const float* b1,
+                              const void* w2_hi, const void* w2_lo, const float* b2, uint32_t rows, uint32_t d,
+                              uint32_t n_hidden, const float* gamma, const float* beta, float eps, float* h_out,
+                              void* stream) {
+    if (!h || !x_io || !w1_hi || !w1_lo || !b1 || !w2_hi || !w2_lo || !b2 || !gamma || !beta || !h_out ||
+        (d != 160u && d != 256u) || n_hidden == 0 || n_hidden > dk::net::MLP_MAX_HIDDEN || n_hidden % 32u)
+        return DK_E_INVALID;
+    if (rows == 0) return DK_OK;
+    const dim3 grid((rows + 255u) / 256u), block(512u);
+    if (d == 160u)
+        hipLaunchKernelGGL((dk::net::mlp_ln_f32x3_kernel<160, 32>), grid, block, 0, (hipStream_t)stream, h, x_io,
+                           (const uint16_t*)w1_hi, (const uint16_t*)w1_lo, b1, (const uint16_t*)w2_hi, (const uint16_t*)w2_lo,
+                           b2, rows, n_hidden, gamma, beta, eps, h_out);
+    else
+        hipLaunchKernelGGL((dk::net::mlp_ln_f32x3_kernel<256, 32>), grid, block, 0, (hipStream_t)stream, h, x_io,
+                           (const uint16_t*)w1_hi, (const uint16_t*)w1_lo, b1, (const uint16_t*)w2_hi, (const uint16_t*)w2_lo,
+                           b2, rows, n_hidden, gamma, beta, eps, h_out);
+    DK_HIP(hipGetLastError());
+    return DK_OK;
+}
+
 #ifdef DK_NET_PROF
 // profiling builds: the summed phase clocks of qkv_attn_ln_kernel since the last read (then cleared)
 extern "C" int dk_net_prof_read(uint64_t* out8) {

@@ -36,6 +36,49 @@ def test_add_ln_matches_torch(d):
     torch.testing.assert_close(h.float(), h_ref, rtol=1e-2, atol=2e-2)   # bf16 output of an f32 LayerNorm
 
 
+@pytest.mark.parametrize("d,n", [(160, 640), (256, 1024)])
+def test_mlp_ln_f32x3_matches_torch(d, n):
+    """The f32 MLP half with bf16x3 products (mlp_ln_f32x3_kernel): x += proj(GELU(fc(h))) + b,
+    h' = LN'(x), against exact f32 torch (matmul precision "highest") on f32 inputs: within 2e-5
+    of the output scale (bf16x3 products carry ~16 bits; hipBLASLt at "medium" measured ~5e-6
+    relative per GEMM, profiles/r04/fp32_gemm_probe.json)."""
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(11)
+    rows = 62 * 41 + 3                                   # not a multiple of the 256-row workgroup tile
+    h = torch.randn(rows, d, device=dev)
+    x = torch.randn(rows, d, device=dev) * 2
+    w1 = torch.randn(n, d, device=dev) / d ** 0.5
+    b1 = torch.randn(n, device=dev) * 0.1
+    w2 = torch.randn(d, n, device=dev) / n ** 0.5
+    b2 = torch.randn(d, device=dev) * 0.1
+    g = 1 + 0.1 * torch.randn(d, device=dev)
+    be = 0.1 * torch.randn(d, device=dev)
+    prev = torch.get_float32_matmul_precision()
+    torch.set_float32_matmul_precision("highest")
+    try:
+        delta_ref = F.linear(F.gelu(F.linear(h, w1, b1)), w2, b2)
+    finally:
+        torch.set_float32_matmul_precision(prev)
+    x_ref = x + delta_ref
+    h_ref = F.layer_norm(x_ref, (d,), g, be, 1e-5)
+    split = []
+    for w in (w1, w2):
+        hi = w.bfloat16().contiguous()
+        split += [hi, (w - hi.float()).bfloat16().contiguous()]
+    xo = x.clone()
+    out = torch.full((rows, d), float("nan"), device=dev)
+    rc = _lib().dk_net_mlp_ln_f32x3_async(h.data_ptr(), xo.data_ptr(), split[0].data_ptr(), split[1].data_ptr(),
+                                          b1.data_ptr(), split[2].data_ptr(), split[3].data_ptr(), b2.data_ptr(), rows,
+                                          d, n, g.data_ptr(), be.data_ptr(), 1e-5, out.data_ptr(),
+                                          torch.cuda.current_stream(dev).cuda_stream)
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert torch.isfinite(out).all() and torch.isfinite(xo).all()
+    ex = (xo - x_ref).abs().max().item() / delta_ref.abs().max().item()
+    eh = (out - h_ref).abs().max().item() / h_ref.abs().max().item()
+    assert ex < 2e-5 and eh < 2e-5, (ex, eh)
+
+
 @pytest.mark.parametrize("hd", [40, 64])
 def test_attn62_matches_torch(hd):
     """MFMA attention core (62 tokens, 4 heads x hd) against fp32 softmax(q k^T / sqrt(hd)) v."""
