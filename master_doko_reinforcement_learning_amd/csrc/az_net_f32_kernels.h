@@ -380,8 +380,8 @@ __device__ __forceinline__ void split_bf16x8(const float (&v)[8], bf16x8_t& hi, 
     lo = b.v;
 }
 
-template <int D, int NC>
-__global__ void __launch_bounds__(512, 1) mlp_ln_f32x3_kernel(const float* __restrict__ h, float* __restrict__ x_io,
+template <int D, int NC, int WAVES = 8, int NB = 2>
+__global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) mlp_ln_f32x3_kernel(const float* __restrict__ h, float* __restrict__ x_io,
                                                                 const uint16_t* __restrict__ w1h, const uint16_t* __restrict__ w1l,
                                                                 const float* __restrict__ b1,
                                                                 const uint16_t* __restrict__ w2h, const uint16_t* __restrict__ w2l,
@@ -389,10 +389,17 @@ __global__ void __launch_bounds__(512, 1) mlp_ln_f32x3_kernel(const float* __res
                                                                 const float* __restrict__ gamma, const float* __restrict__ beta,
                                                                 float eps, float* __restrict__ h_out) {
     static_assert(D % 32 == 0 && NC == 32, "d: multiple of 32; chunks of 32 hidden units");
-    constexpr int WAVES = 8, T = 64 * WAVES;
-    constexpr int KS = D / 16, OT = D / 32, LDW1 = D + 8, LDW2 = NC + 4, GS = NC / 16;
+    // WAVES x 32 rows per workgroup; NB = 2: the chunks' weights double-buffered (one barrier per
+    // chunk), NB = 1: one buffer (two barriers per chunk, half the LDS)
+    constexpr int T = 64 * WAVES;
+    // LDS rows padded by one 16-B piece (W1: d + 8 elements; W2: NC + 8), so that a chunk is staged
+    // by direct global -> LDS loads (global_load_lds_dwordx4: no staging registers), each wave
+    // instruction filling 64 consecutive 16-B pieces of the buffer
+    constexpr int KS = D / 16, OT = D / 32, LDW1 = D + 8, LDW2 = NC + 8, GS = NC / 16;
     constexpr int W1E = NC * LDW1, W2E = D * LDW2, BUF = 2 * (W1E + W2E);   // one buffer: W1 hi, W1 lo, W2 hi, W2 lo
-    __shared__ __attribute__((aligned(16))) uint16_t lds[2 * BUF];
+    constexpr int Q1 = LDW1 / 8, Q2 = LDW2 / 8;                             // pieces per row
+    constexpr int NP = BUF / 8, NI = (NP + 63) / 64;                        // pieces per buffer, wave instructions
+    __shared__ __attribute__((aligned(16))) uint16_t lds[NB * BUF];
     __shared__ float b1s[MLP_MAX_HIDDEN];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
     const uint32_t row = blockIdx.x * (32u * WAVES) + (uint32_t)wave * 32u + (uint32_t)r;
@@ -410,45 +417,19 @@ __global__ void __launch_bounds__(512, 1) mlp_ln_f32x3_kernel(const float* __res
             split_bf16x8(v, hfh[kk], hfl[kk]);
         }
     }
-    // chunk staging: 16-B pieces of W1 (NC rows x D) and W2 (D rows x NC), hi and lo
-    constexpr int P1 = NC * (D / 8), P2 = D * (NC / 8), PT = 2 * (P1 + P2), PER = (PT + T - 1) / T;
-    uint4 pc[PER];
-    auto load_chunk = [&](uint32_t c) {
-#pragma unroll
-        for (int u = 0; u < PER; ++u) {
-            int v = threadIdx.x + T * u;
-            if (v < 2 * P1) {
-                const uint16_t* w = v < P1 ? w1h : w1l;
-                v = v < P1 ? v : v - P1;
-                const int i = v / (D / 8), p = v - i * (D / 8);
-                pc[u] = *(const uint4*)(w + ((size_t)c * NC + i) * D + 8 * p);
-            } else if (v < PT) {
-                v -= 2 * P1;
-                const uint16_t* w = v < P2 ? w2h : w2l;
-                v = v < P2 ? v : v - P2;
-                const int o = v / (NC / 8), p = v - o * (NC / 8);
-                pc[u] = *(const uint4*)(w + (size_t)o * n_hidden + (size_t)c * NC + 8 * p);
+    typedef __attribute__((address_space(3))) void lds_void;
+    auto stage = [&](uint32_t c, int buf) {
+        for (int u = wave; u < NI; u += WAVES) {
+            const int k = 64 * u + lane;   // this lane's piece of the buffer
+            const uint16_t* g = w1h;       // (padding pieces read a valid piece and are never used)
+            if (k < 2 * NC * Q1) {
+                const int lo = k >= NC * Q1, kk = lo ? k - NC * Q1 : k, i = kk / Q1, p = kk - i * Q1;
+                g = (lo ? w1l : w1h) + ((size_t)c * NC + i) * D + 8 * (p < D / 8 ? p : 0);
+            } else if (k < NP) {
+                const int k2 = k - 2 * NC * Q1, lo = k2 >= D * Q2, kk = lo ? k2 - D * Q2 : k2, o = kk / Q2, p = kk - o * Q2;
+                g = (lo ? w2l : w2h) + (size_t)o * n_hidden + (size_t)c * NC + 8 * (p < NC / 8 ? p : 0);
             }
-        }
-    };
-    auto store_chunk = [&](int buf) {
-#pragma unroll
-        for (int u = 0; u < PER; ++u) {
-            int v = threadIdx.x + T * u;
-            if (v < 2 * P1) {
-                const int lo = v < P1 ? 0 : 1;
-                v = lo ? v - P1 : v;
-                const int i = v / (D / 8), p = v - i * (D / 8);
-                *(uint4*)&lds[buf * BUF + lo * W1E + i * LDW1 + 8 * p] = pc[u];
-            } else if (v < PT) {
-                v -= 2 * P1;
-                const int lo = v < P2 ? 0 : 1;
-                v = lo ? v - P2 : v;
-                const int o = v / (NC / 8), p = v - o * (NC / 8);
-                uint2* d_ = (uint2*)&lds[buf * BUF + 2 * W1E + lo * W2E + o * LDW2 + 8 * p];
-                d_[0] = make_uint2(pc[u].x, pc[u].y);
-                d_[1] = make_uint2(pc[u].z, pc[u].w);
-            }
+            if (k < NP) __builtin_amdgcn_global_load_lds(g, (lds_void*)&lds[buf * BUF + 512 * u], 16, 0, 0);
         }
     };
     f32x16_t acc2[OT];
@@ -456,12 +437,12 @@ __global__ void __launch_bounds__(512, 1) mlp_ln_f32x3_kernel(const float* __res
     for (int t = 0; t < OT; ++t) acc2[t] = f32x16_t{0};
     const uint32_t chunks = n_hidden / NC;
     for (uint32_t i = threadIdx.x; i < n_hidden; i += T) b1s[i] = b1[i];
-    load_chunk(0u);
-    store_chunk(0);
+    stage(0u, 0);
+    __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
     for (uint32_t c = 0; c < chunks; ++c) {
-        const int buf = (int)(c & 1u);
-        if (c + 1 < chunks) load_chunk(c + 1);
+        const int buf = NB == 2 ? (int)(c & 1u) : 0;
+        if (NB == 2 && c + 1 < chunks) stage(c + 1, buf ^ 1);
         // GEMM1: D1 = W1_c h^T (one 32 x 32 tile), three products per k-step
         f32x16_t acc1 = f32x16_t{0};
         const uint16_t* a1h = &lds[buf * BUF + r * LDW1 + 8 * hh];
@@ -502,7 +483,11 @@ __global__ void __launch_bounds__(512, 1) mlp_ln_f32x3_kernel(const float* __res
                 acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh.v, afh[s2], acc2[t], 0, 0, 0);
             }
         if (c + 1 < chunks) {
-            store_chunk(buf ^ 1);
+            if constexpr (NB == 1) {
+                __syncthreads();   // every wave is done with the buffer
+                stage(c + 1, 0);
+            }
+            __builtin_amdgcn_s_waitcnt(0);   // this wave's pieces have landed
             __syncthreads();
         }
     }
