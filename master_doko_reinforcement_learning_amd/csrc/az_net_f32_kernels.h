@@ -404,6 +404,13 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) mlp_ln_f32x3_kernel(con
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
     const uint32_t row = blockIdx.x * (32u * WAVES) + (uint32_t)wave * 32u + (uint32_t)r;
     const bool ok = row < rows;
+#ifdef DK_NET_PROF
+    // phase clocks of wave 0 (profiling builds): drained stamps, sums in registers, atomics at the end
+    unsigned long long f_prev = __builtin_amdgcn_s_memtime(), facc[6] = {0, 0, 0, 0, 0, 0};
+#define DK_FSTAMP(k) do { __builtin_amdgcn_s_waitcnt(0); const unsigned long long t_ = __builtin_amdgcn_s_memtime(); facc[k] += t_ - f_prev; f_prev = t_; } while (0)
+#else
+#define DK_FSTAMP(k) ((void)0)
+#endif
     // the row's h, split: lane (r, hh) holds k = 16 kk + 8 hh .. + 7 of row r
     bf16x8_t hfh[KS], hfl[KS];
     {
@@ -440,6 +447,7 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) mlp_ln_f32x3_kernel(con
     stage(0u, 0);
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
+    DK_FSTAMP(0);
     for (uint32_t c = 0; c < chunks; ++c) {
         const int buf = NB == 2 ? (int)(c & 1u) : 0;
         if (NB == 2 && c + 1 < chunks) stage(c + 1, buf ^ 1);
@@ -447,13 +455,17 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) mlp_ln_f32x3_kernel(con
         f32x16_t acc1 = f32x16_t{0};
         const uint16_t* a1h = &lds[buf * BUF + r * LDW1 + 8 * hh];
         const uint16_t* a1l = a1h + W1E;
+        // W1 fragments read one k-step ahead (the LDS latency under the previous k-step's MFMAs)
+        bf16x8_t nh = *(const bf16x8_t*)a1h, nl = *(const bf16x8_t*)a1l;
 #pragma unroll
         for (int kk = 0; kk < KS; ++kk) {
-            const bf16x8_t ah = *(const bf16x8_t*)(a1h + 16 * kk), al = *(const bf16x8_t*)(a1l + 16 * kk);
+            const bf16x8_t ah = nh, al = nl;
+            if (kk + 1 < KS) { nh = *(const bf16x8_t*)(a1h + 16 * (kk + 1)); nl = *(const bf16x8_t*)(a1l + 16 * (kk + 1)); }
             acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, hfh[kk], acc1, 0, 0, 0);
             acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, hfl[kk], acc1, 0, 0, 0);
             acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, hfh[kk], acc1, 0, 0, 0);
         }
+        DK_FSTAMP(1);
         // bias + GELU (f32) -> split B fragments of GEMM2 (k-step s = half: registers 8 s .. 8 s + 7,
         // hidden units 16 s + 4 hh + (g & 3) + 8 ((g >> 2) & 1))
         bf16x8_t afh[GS], afl[GS];
@@ -467,21 +479,29 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) mlp_ln_f32x3_kernel(con
             for (int t = 0; t < 8; ++t) g[t] = gelu_poly(acc1[8 * s2 + t] + bb[t]);
             split_bf16x8(g, afh[s2], afl[s2]);
         }
+        DK_FSTAMP(2);
         // GEMM2: D2 += W2_c a^T, OT tiles of 32 output columns, three products per k-step
         const uint16_t* a2h = &lds[buf * BUF + 2 * W1E + r * LDW2 + 4 * hh];
         const uint16_t* a2l = a2h + W2E;
+        // W2 fragments read one (k-step, tile) ahead
+        union F8 { uint2 u[2]; bf16x8_t v; };
+        auto w2f = [&](const uint16_t* base, int q) {
+            const int off = (32 * (q % OT)) * LDW2 + 16 * (q / OT);
+            F8 f;
+            f.u[0] = *(const uint2*)(base + off); f.u[1] = *(const uint2*)(base + off + 8);
+            return f.v;
+        };
+        bf16x8_t ph = w2f(a2h, 0), pl = w2f(a2l, 0);
 #pragma unroll
-        for (int s2 = 0; s2 < GS; ++s2)
-#pragma unroll
-            for (int t = 0; t < OT; ++t) {
-                const int off = (32 * t) * LDW2 + 16 * s2;
-                union { uint2 u[2]; bf16x8_t v; } wh, wl;
-                wh.u[0] = *(const uint2*)(a2h + off); wh.u[1] = *(const uint2*)(a2h + off + 8);
-                wl.u[0] = *(const uint2*)(a2l + off); wl.u[1] = *(const uint2*)(a2l + off + 8);
-                acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl.v, afh[s2], acc2[t], 0, 0, 0);
-                acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh.v, afl[s2], acc2[t], 0, 0, 0);
-                acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh.v, afh[s2], acc2[t], 0, 0, 0);
-            }
+        for (int q = 0; q < GS * OT; ++q) {
+            const int s2 = q / OT, t = q % OT;
+            const bf16x8_t wh = ph, wl = pl;
+            if (q + 1 < GS * OT) { ph = w2f(a2h, q + 1); pl = w2f(a2l, q + 1); }
+            acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl, afh[s2], acc2[t], 0, 0, 0);
+            acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, afl[s2], acc2[t], 0, 0, 0);
+            acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, afh[s2], acc2[t], 0, 0, 0);
+        }
+        DK_FSTAMP(3);
         if (c + 1 < chunks) {
             if constexpr (NB == 1) {
                 __syncthreads();   // every wave is done with the buffer
@@ -490,6 +510,7 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) mlp_ln_f32x3_kernel(con
             __builtin_amdgcn_s_waitcnt(0);   // this wave's pieces have landed
             __syncthreads();
         }
+        DK_FSTAMP(4);
     }
     // epilogue: acc2[t][g] = delta of row `row`, column 32 t + 8 (g >> 2) + 4 hh + (g & 3);
     // x += (delta + b2) (the GEMM's bias first: F.linear's epilogue order), then LN
@@ -534,6 +555,12 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) mlp_ln_f32x3_kernel(con
                                                    (acc2[t][4 * q + 2] - mean) * rstd * gv.z + bv.z,
                                                    (acc2[t][4 * q + 3] - mean) * rstd * gv.w + bv.w);
         }
+    DK_FSTAMP(5);
+#ifdef DK_NET_PROF
+    if (lane == 0 && wave == 0)
+        for (int q = 0; q < 6; ++q) atomicAdd(&dk_mlp_prof_acc[q], facc[q]);
+#endif
+#undef DK_FSTAMP
 }
 
 }  // namespace net
