@@ -874,6 +874,15 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
                         lnN_x = mem.ln(N);
                     }
                     pick = pick_child_x<Raw8>(blk, n, lnN_x, c, mem, &y.stats, &y.child_base, &y.info, &end, &end_ok, x.child_base);
+#if defined(DK_PICK_DOUBLE) && defined(__HIP_DEVICE_COMPILE__)
+                    // measurement builds: the pick computed a second time (result discarded) in the trips
+                    // with at most DK_PICK_DOUBLE active lanes: the time it adds is those picks' cost
+                    if (popc64(__builtin_amdgcn_ballot_w64(true)) <= DK_PICK_DOUBLE) {
+                        uint64_t s2; uint32_t c2, i2; NodeHot e2; bool o2 = false;
+                        const uint32_t p2 = pick_child_x<Raw8>(blk, n, lnN_x * 1.0000000001, c, mem, &s2, &c2, &i2, &e2, &o2, x.child_base);
+                        if ((p2 ^ (uint32_t)s2 ^ c2 ^ i2) == 0xDEADBEEFu && o2) status = SR_STATE;
+                    }
+#endif
                     DK_STAMP_DRAINED(tl2);
                     DK_PROF(mem, 9, tl2 - tl1);
                 } else if constexpr (Mem::Rec::PAIR) {
