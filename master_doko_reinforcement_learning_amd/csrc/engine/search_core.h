@@ -880,7 +880,7 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
                     if (popc64(__builtin_amdgcn_ballot_w64(true)) <= DK_PICK_DOUBLE) {
                         uint64_t s2; uint32_t c2, i2; NodeHot e2; bool o2 = false;
                         const uint32_t p2 = pick_child_x<Raw8>(blk, n, lnN_x * 1.0000000001, c, mem, &s2, &c2, &i2, &e2, &o2, x.child_base);
-                        if ((p2 ^ (uint32_t)s2 ^ c2 ^ i2) == 0xDEADBEEFu && o2) status = SR_STATE;
+                        asm volatile("" :: "v"(p2), "v"((uint32_t)s2), "v"(c2), "v"(i2), "v"((uint32_t)o2));   // keep it
                     }
 #endif
                     DK_STAMP_DRAINED(tl2);
