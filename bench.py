@@ -518,10 +518,12 @@ def main():
                              "note": "each wave of the persistent grid stamps the 100 MHz counter at start and once "
                                      "the group queue is dry for it; 1 - busy_frac = drain tail + launch ramp"},
             "roofline": {
-                # achieved/peak/frac: the north-star's HBM figures, algorithmic bytes / event-timed
-                # kernel vs 8 TB/s; traffic: calibrated DRAM bytes per launch (PMC); neither VALU nor
-                # DRAM is saturated (valu below): the launch is latency-bound at 3 waves per SIMD
-                "bound": "hbm",
+                # bound: what binds the launch, measured (round-4 review): latency of the per-lane tree
+                # walks -- neither VALU nor DRAM is saturated (valu below).  achieved/peak/frac stay the
+                # north-star's HBM figures (algorithmic bytes / event-timed kernel vs 8 TB/s, the
+                # resource it is priced against); traffic: calibrated DRAM bytes per launch (PMC)
+                "bound": "latency",
+                "priced_against": "hbm",
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -572,7 +574,8 @@ def net_precision(args, torch):
         torch.set_float32_matmul_precision("medium")
         torch.backends.cuda.matmul.allow_tf32 = True
         return (torch.float32, "f32 network (reference precision: f32 activations, matmul precision 'medium')", 2500.0 / 3,
-                "f32 activations; hipBLASLt computes the f32 GEMMs of precision 'medium' from bf16 products "
+                "f32 activations; GEMM products from bf16 pieces: the MLP half in one HIP kernel with bf16x3 "
+                "MFMA products (mlp_ln_f32x3_kernel, d = 160), the other GEMMs on hipBLASLt at precision 'medium' "
                 "(max relative error ~5e-6 against f64, profiles/r04/fp32_gemm_probe.json): peak = bf16 dense / 3")
     return torch.bfloat16, "bf16 network", 2500.0, "bf16 dense peak"
 
