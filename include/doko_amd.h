@@ -509,6 +509,17 @@ int dk_net_mlp_ln_f32x3_async(const float* h, float* x_io, const void* w1_hi, co
                               const void* w2_hi, const void* w2_lo, const float* b2, uint32_t rows, uint32_t d,
                               uint32_t n_hidden, const float* gamma, const float* beta, float eps, float* h_out,
                               void* stream);
+/* dk_net_qkv_attn_ln_f32x3_async: the attention half at the reference's precision (round 5), one
+ * workgroup per sample: Q, K, V = W h^T + b, softmax(K Q^T / sqrt(hd)), y = P V, x += y Wp^T + bp,
+ * h_out = LN(x) -- f32 activations, bf16x3 products everywhere (operands split into bf16 hi + lo).
+ * wqkv_hi / _lo [3d][d] (q | k | v rows, heads contiguous), wp_hi / _lo [d][d] the folded
+ * out_proj / c_proj (Block.folded_proj), bp f32 [d].  d = 160 (4 heads of 40).  Replaces the qkv
+ * F.linear, the attention core, the projection F.linear and add + LayerNorm of
+ * rs-doko-py-bridge/python/az_doko.py:87-145 at f32. */
+int dk_net_qkv_attn_ln_f32x3_async(const float* h, float* x_io, const void* wqkv_hi, const void* wqkv_lo, const float* bqkv,
+                                   const void* wp_hi, const void* wp_lo, const float* bp, uint32_t batch, uint32_t heads,
+                                   uint32_t head_dim, const float* gamma, const float* beta, float eps, float* h_out,
+                                   void* stream);
 /* dk_net_class_pool_ln_bf16_async: PerClassAttentionMLPHead's attention pooling and each class
  * MLP's opening LayerNorm (az_doko.py:42-50): x [batch][62][d], queries [classes][d] (classes
  * <= 64), w = softmax(queries x^T * scale) over the 62 tokens, a = w x, out[c][b][:] =

@@ -256,6 +256,23 @@ def split_bf16x3(blk):
     return c[1]
 
 
+def split_attn_bf16x3(blk):
+    """The attention half's weights as bf16 hi / lo pairs: Wqkv and the folded projection
+    (Block.folded_proj, f32), cached on the block until a weight changes; with the folded f32 bias."""
+    key = (blk.qkv.weight.data_ptr(), blk.qkv.weight._version, blk.out.weight._version, blk.c_proj.weight._version,
+           blk.out.bias._version, blk.c_proj.bias._version)
+    c = getattr(blk, "_attn_bf16x3", None)
+    if c is None or c[0] != key:
+        wp, bp = blk.folded_proj()
+        parts = []
+        for w in (blk.qkv.weight.detach(), wp.detach()):
+            hi = w.float().bfloat16().contiguous()
+            parts += [hi, (w.float() - hi.float()).bfloat16().contiguous()]
+        c = (key, tuple(parts) + (bp.detach().float().contiguous(),))
+        blk._attn_bf16x3 = c
+    return c[1]
+
+
 class FusedTrunkF32(FusedTrunk):
     """The f32 GPU forward of a token trunk: the reference's precision (f32 activations; GEMM
     products at least as fine as the reference's matmul precision "medium", az_doko.py:539-541)
@@ -293,6 +310,15 @@ class FusedTrunkF32(FusedTrunk):
     def attn_ln(self, x, blk, h, ln):
         if not (self.d % blk.heads == 0 and self.d // blk.heads in (40, 64)):
             return self.add_ln(x, _f32c(blk.attn_delta(h)), ln)
+        if self.d == 160 and blk.heads == 4 and blk.qkv.bias is not None:
+            # the whole attention half in one kernel per sample, bf16x3 products (qkv_attn_ln_f32x3_kernel)
+            wqh, wql, wph, wpl, bpf = split_attn_bf16x3(blk)
+            ho = torch.empty_like(x)
+            self.ck(self.L.dk_net_qkv_attn_ln_f32x3_async(h.data_ptr(), x.data_ptr(), wqh.data_ptr(), wql.data_ptr(),
+                                                          blk.qkv.bias.data_ptr(), wph.data_ptr(), wpl.data_ptr(),
+                                                          bpf.data_ptr(), h.shape[0], 4, self.d // 4, ln.weight.data_ptr(),
+                                                          ln.bias.data_ptr(), ln.eps, ho.data_ptr(), self.st))
+            return ho
         qkv = _f32c(F.linear(h, blk.qkv.weight))                         # [B, 62, 3d]: q | k | v, heads contiguous
         y = torch.empty_like(h)
         bq = blk.qkv.bias.contiguous() if blk.qkv.bias is not None else None

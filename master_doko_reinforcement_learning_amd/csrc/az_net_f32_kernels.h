@@ -563,5 +563,357 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) mlp_ln_f32x3_kernel(con
 #undef DK_FSTAMP
 }
 
+// ---------------------------------------------------------------------------
+// The whole attention half of a block at the reference's precision (round 5), one 256-thread
+// workgroup per sample (as qkv_attn_ln_kernel at bf16):
+//   Q, K, V = W h^T + b            (head w on wave w; bf16x3 products, f32 accumulators)
+//   P = softmax(K Q^T * scale)      (bf16x3 products; softmax in f32)
+//   y = P V                         (bf16x3 products)
+//   delta = y Wp^T;  x += delta + bp;  h' = LN(x)        (bf16x3 products; f32 residual and LN)
+// with the folded out / c projection (Block.folded_proj).  Every operand is split into bf16
+// hi + lo and each k-step takes three MFMAs (A_lo B_hi + A_hi B_lo + A_hi B_hi), as
+// mlp_ln_f32x3_kernel.  The weights come pre-split (wq_hi / wq_lo [3d][d], wp_hi / wp_lo [d][d]).
+// Unfused (hipBLASLt qkv GEMM, the f32 attention kernel, the projection GEMM, add + LN), q, k, v
+// (12 d bytes per token), y and delta went to HBM and back.
+// LDS, one region reused in turn: the sample's h rows (hi, lo) -> the heads' V^T tiles (hi, lo)
+// -> y rows (hi, lo) -> the residual rows (f32).
+template <int HD, int D>
+__device__ __forceinline__ void head_tiles_x3(const uint16_t* hsh, const uint16_t* hsl, const uint16_t* __restrict__ wh,
+                                              const uint16_t* __restrict__ wl, const float* __restrict__ bias,
+                                              f32x16_t (&acc)[2][2]) {
+    constexpr int LDY = D + 8, NKS = D / 16;
+    const int lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int si = 0; si < 2; ++si) acc[dt][si] = f32x16_t{0};
+    const bool ok1 = 32 + r < HD;
+    const size_t o0 = (size_t)r * D, o1 = (size_t)(ok1 ? 32 + r : 0) * D;
+    // W fragments one k-step ahead
+    bf16x8_t nw[2][2];
+    auto wfr = [&](int ks) {
+        const int k0 = 16 * ks + 8 * hh;
+        nw[0][0] = load_frag8(wh + o0 + k0, true);
+        nw[0][1] = load_frag8(wl + o0 + k0, true);
+        nw[1][0] = load_frag8(wh + o1 + k0, ok1);
+        nw[1][1] = load_frag8(wl + o1 + k0, ok1);
+    };
+    wfr(0);
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+        const bf16x8_t a0h = nw[0][0], a0l = nw[0][1], a1h = nw[1][0], a1l = nw[1][1];
+        if (ks + 1 < NKS) wfr(ks + 1);
+        bf16x8_t bhf[2], blf[2];
+#pragma unroll
+        for (int si = 0; si < 2; ++si) {
+            bhf[si] = *(const bf16x8_t*)&hsh[(32 * si + r) * LDY + 16 * ks + 8 * hh];
+            blf[si] = *(const bf16x8_t*)&hsl[(32 * si + r) * LDY + 16 * ks + 8 * hh];
+        }
+#pragma unroll
+        for (int si = 0; si < 2; ++si) {
+            acc[0][si] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0l, bhf[si], acc[0][si], 0, 0, 0);
+            acc[0][si] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0h, blf[si], acc[0][si], 0, 0, 0);
+            acc[0][si] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0h, bhf[si], acc[0][si], 0, 0, 0);
+            if (HD > 32) {
+                acc[1][si] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1l, bhf[si], acc[1][si], 0, 0, 0);
+                acc[1][si] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1h, blf[si], acc[1][si], 0, 0, 0);
+                acc[1][si] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1h, bhf[si], acc[1][si], 0, 0, 0);
+            }
+        }
+        // (keeps the compiler from hoisting every k-step's W loads to the top: registers)
+        __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+            const int m = 32 * dt + (g & 3) + 8 * (g >> 2) + 4 * hh;
+            const float bv = m < HD ? bias[m] : 0.0f;
+            acc[dt][0][g] += bv;
+            acc[dt][1][g] += bv;
+        }
+}
+
+// Q^T / K^T accumulators -> hi / lo fragments of the attention's k-steps (pack_head's order)
+template <int HD>
+__device__ __forceinline__ void split_head(const f32x16_t (&acc)[2][2], bf16x8_t (&fh)[2][(HD + 15) / 16],
+                                           bf16x8_t (&fl)[2][(HD + 15) / 16]) {
+#pragma unroll
+    for (int si = 0; si < 2; ++si)
+#pragma unroll
+        for (int kk = 0; kk < (HD + 15) / 16; ++kk) {
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = acc[kk >> 1][si][8 * (kk & 1) + j];
+            split_bf16x8(v, fh[si][kk], fl[si][kk]);
+        }
+}
+
+template <int HD>
+__global__ void __launch_bounds__(256, 2) qkv_attn_ln_f32x3_kernel(const float* __restrict__ h_in, float* __restrict__ x_io,
+                                                                   const uint16_t* __restrict__ wqh, const uint16_t* __restrict__ wql,
+                                                                   const float* __restrict__ bqkv,
+                                                                   const uint16_t* __restrict__ wph, const uint16_t* __restrict__ wpl,
+                                                                   const float* __restrict__ bp, float scale,
+                                                                   const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                                   float eps, float* __restrict__ h_out) {
+    constexpr int S = 62, D = HD * 4, LDY = D + 8, LDT = 64 + 4, KS = (HD + 15) / 16, LDX = D + 4;
+    constexpr int RH = 2 * 64 * LDY;                       // h rows / y rows: hi then lo (bf16 elements)
+    constexpr int RV = 2 * 4 * HD * LDT;                   // the V^T tiles: hi then lo
+    constexpr int RX = 2 * 64 * LDX;                       // the residual rows (f32, in bf16 elements)
+    constexpr int R = RH > RV ? (RH > RX ? RH : RX) : (RV > RX ? RV : RX);
+    __shared__ __attribute__((aligned(16))) uint16_t lds[R];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
+    const uint32_t b = blockIdx.x;
+    uint16_t* hsh = lds;
+    uint16_t* hsl = lds + 64 * LDY;
+    // the sample's h rows, split; rows 62, 63 zero
+    const float* hg = h_in + (size_t)b * S * D;
+    for (int p = threadIdx.x; p < 64 * (D / 8); p += 256) {
+        const int rr = p / (D / 8), kp = p - rr * (D / 8);
+        float v[8];
+        if (rr < S) {
+            const float4 a = *(const float4*)(hg + 8 * p), c = *(const float4*)(hg + 8 * p + 4);
+            v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = c.x; v[5] = c.y; v[6] = c.z; v[7] = c.w;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = 0.0f;
+        }
+        bf16x8_t fh, fl;
+        split_bf16x8(v, fh, fl);
+        *(bf16x8_t*)&hsh[rr * LDY + 8 * kp] = fh;
+        *(bf16x8_t*)&hsl[rr * LDY + 8 * kp] = fl;
+    }
+    __syncthreads();
+    // Register budget: Q^T and K^T into split fragments, then X = K Q^T and the softmax (Q / K
+    // dead), then the V^T projection while only P is live; V^T goes to LDS once every wave is
+    // done with the h rows.
+    const size_t hq = (size_t)wave * HD * D;
+    bf16x8_t pfh[2][4], pfl[2][4];
+    {
+        bf16x8_t qfh[2][KS], qfl[2][KS], kfh[2][KS], kfl[2][KS];
+        {
+            f32x16_t acc[2][2];
+            head_tiles_x3<HD, D>(hsh, hsl, wqh + hq, wql + hq, bqkv + wave * HD, acc);                          // Q^T
+            split_head<HD>(acc, qfh, qfl);
+            head_tiles_x3<HD, D>(hsh, hsl, wqh + hq + (size_t)D * D, wql + hq + (size_t)D * D, bqkv + D + wave * HD, acc);   // K^T
+            split_head<HD>(acc, kfh, kfl);
+        }
+        // X[ti][si] = K_ti Q_si^T, three products per k-step
+        f32x16_t x[2][2];
+#pragma unroll
+        for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+            for (int si = 0; si < 2; ++si) {
+                f32x16_t acc = {0};
+#pragma unroll
+                for (int kk = 0; kk < KS; ++kk) {
+                    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kfl[ti][kk], qfh[si][kk], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kfh[ti][kk], qfl[si][kk], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kfh[ti][kk], qfh[si][kk], acc, 0, 0, 0);
+                }
+                x[ti][si] = acc;
+            }
+        // softmax over the keys t of every query column s (f32), P split
+#pragma unroll
+        for (int si = 0; si < 2; ++si) {
+            float m = -INFINITY;
+#pragma unroll
+            for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+                for (int g = 0; g < 16; ++g) {
+                    const int t = 32 * ti + (g & 3) + 8 * (g >> 2) + 4 * hh;
+                    x[ti][si][g] *= scale;
+                    if (t < S) m = fmaxf(m, x[ti][si][g]);
+                }
+            m = fmaxf(m, __shfl_xor(m, 32));
+            float l = 0.0f;
+#pragma unroll
+            for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+                for (int g = 0; g < 16; ++g) {
+                    const int t = 32 * ti + (g & 3) + 8 * (g >> 2) + 4 * hh;
+                    const float pv = t < S ? expf(x[ti][si][g] - m) : 0.0f;
+                    x[ti][si][g] = pv;
+                    l += pv;
+                }
+            l += __shfl_xor(l, 32);
+            const float inv = 1.0f / l;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                float v[8];
+#pragma unroll
+                for (int jj = 0; jj < 8; ++jj) v[jj] = x[q >> 1][si][8 * (q & 1) + jj] * inv;
+                split_bf16x8(v, pfh[si][q], pfl[si][q]);
+            }
+        }
+    }
+    f32x16_t vacc[2][2];
+    head_tiles_x3<HD, D>(hsh, hsl, wqh + hq + (size_t)2 * D * D, wql + hq + (size_t)2 * D * D, bqkv + 2 * D + wave * HD,
+                         vacc);                                                                           // V^T
+    __syncthreads();   // every wave is done with the h rows
+    uint16_t* vth = lds + wave * HD * LDT;
+    uint16_t* vtl = lds + 4 * HD * LDT + wave * HD * LDT;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+            const int m = 32 * dt + (g & 3) + 8 * (g >> 2) + 4 * hh;
+            if (m < HD) {
+#pragma unroll
+                for (int si = 0; si < 2; ++si) {
+                    const float v = vacc[dt][si][g];
+                    const uint16_t hi = f2bf(v);
+                    vth[m * LDT + 32 * si + r] = hi;
+                    vtl[m * LDT + 32 * si + r] = f2bf(v - bf2f(hi));
+                }
+            }
+        }
+    __syncthreads();   // V^T tiles complete
+    // O[si][et] = P_si V_et, three products per k-step; y kept in registers until the V^T tiles
+    // are dead
+    f32x16_t yo[2][2];
+#pragma unroll
+    for (int et = 0; et < 2; ++et) {
+        const int e = 32 * et + r, er = e < HD ? e : HD - 1;
+        bf16x8_t vfh[4], vfl[4];
+        if (32 * et < HD) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int t0 = 16 * q + 4 * hh;
+                union { uint2 u[2]; bf16x8_t v; } fh, fl;
+                fh.u[0] = *(const uint2*)&vth[er * LDT + t0]; fh.u[1] = *(const uint2*)&vth[er * LDT + t0 + 8];
+                fl.u[0] = *(const uint2*)&vtl[er * LDT + t0]; fl.u[1] = *(const uint2*)&vtl[er * LDT + t0 + 8];
+                vfh[q] = fh.v; vfl[q] = fl.v;
+            }
+        }
+#pragma unroll
+        for (int si = 0; si < 2; ++si) {
+            f32x16_t acc = {0};
+            if (32 * et < HD) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pfl[si][q], vfh[q], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pfh[si][q], vfl[q], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pfh[si][q], vfh[q], acc, 0, 0, 0);
+                }
+            }
+            yo[si][et] = acc;
+        }
+    }
+    __syncthreads();   // every wave is done with the V^T tiles
+    // y rows (hi, lo) into LDS: y[s][wave HD + e]; rows 62, 63 stay zero (A operand padding)
+    uint16_t* ysh = lds;
+    uint16_t* ysl = lds + 64 * LDY;
+#pragma unroll
+    for (int si = 0; si < 2; ++si)
+#pragma unroll
+        for (int et = 0; et < 2; ++et) {
+            const int e = 32 * et + r;
+            if (e < HD) {
+#pragma unroll
+                for (int g = 0; g < 16; ++g) {
+                    const int sidx = 32 * si + (g & 3) + 8 * (g >> 2) + 4 * hh;
+                    const float v = sidx < S ? yo[si][et][g] : 0.0f;
+                    const uint16_t hi = f2bf(v);
+                    ysh[sidx * LDY + wave * HD + e] = hi;
+                    ysl[sidx * LDY + wave * HD + e] = f2bf(v - bf2f(hi));
+                }
+            }
+        }
+    __syncthreads();   // y complete
+    // delta = y Wp^T (v_mfma_f32_16x16x32_bf16; the wave's column tiles wave + 4 j over all 64 rows)
+    constexpr int NT = D / 16, KP = D / 32, NJ = (NT + 3) / 4;
+    const int rl = lane & 15, kg = lane >> 4;
+    f32x4_t acc[4][NJ];
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[m][j] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int ks = 0; ks < KP; ++ks) {
+        bf16x8_t ah[4], al[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            ah[m] = *(const bf16x8_t*)&ysh[(16 * m + rl) * LDY + 32 * ks + 8 * kg];
+            al[m] = *(const bf16x8_t*)&ysl[(16 * m + rl) * LDY + 32 * ks + 8 * kg];
+        }
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int t = wave + 4 * j;
+            if (t < NT) {
+                const size_t wo = (size_t)(16 * t + rl) * D + 32 * ks + 8 * kg;
+                const bf16x8_t bh = load_frag8(wph + wo, true), bl = load_frag8(wpl + wo, true);
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[m], bh, acc[m][j], 0, 0, 0);
+                    acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[m], bl, acc[m][j], 0, 0, 0);
+                    acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[m], bh, acc[m][j], 0, 0, 0);
+                }
+            }
+        }
+    }
+    __syncthreads();   // every wave is done with the y rows
+    // the residual rows (f32) into LDS, x' = x + (delta + bp) in place
+    float* xs = reinterpret_cast<float*>(lds);
+    const float* xg = x_io + (size_t)b * S * D;
+    for (int p = threadIdx.x; p < S * (D / 4); p += 256) {
+        const int rr = p / (D / 4), kp = p - rr * (D / 4);
+        *(float4*)&xs[rr * LDX + 4 * kp] = *(const float4*)(xg + 4 * p);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        const int t = wave + 4 * j;
+        if (t < NT) {
+            const int col = 16 * t + rl;
+            const float bias = bp[col];
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    const int row = 16 * m + 4 * kg + v;
+                    if (row < S) xs[row * LDX + col] += acc[m][j][v] + bias;
+                }
+        }
+    }
+    __syncthreads();
+    // LayerNorm: 4 threads per row, two-pass mean / biased variance; x' and h' written as float4
+    {
+        constexpr int LP = D / 16;     // float4 pieces per thread
+        const int row = threadIdx.x >> 2, q = threadIdx.x & 3;
+        float4 xv[LP];
+        float s1 = 0.0f;
+#pragma unroll
+        for (int i = 0; i < LP; ++i) {
+            xv[i] = *(const float4*)&xs[row * LDX + 4 * (q + 4 * i)];
+            s1 += (xv[i].x + xv[i].y) + (xv[i].z + xv[i].w);
+        }
+        s1 += __shfl_xor(s1, 1);
+        s1 += __shfl_xor(s1, 2);
+        const float mean = s1 / (float)D;
+        float s2 = 0.0f;
+#pragma unroll
+        for (int i = 0; i < LP; ++i) {
+            const float a = xv[i].x - mean, c = xv[i].y - mean, e = xv[i].z - mean, f = xv[i].w - mean;
+            s2 += (a * a + c * c) + (e * e + f * f);
+        }
+        s2 += __shfl_xor(s2, 1);
+        s2 += __shfl_xor(s2, 2);
+        const float rstd = rsqrtf(s2 / (float)D + eps);
+        if (row < S) {
+            const size_t o = ((size_t)b * S + row) * D;
+#pragma unroll
+            for (int i = 0; i < LP; ++i) {
+                const int c0 = 4 * (q + 4 * i);
+                const float4 g = *(const float4*)(gamma + c0), be = *(const float4*)(beta + c0);
+                *(float4*)(x_io + o + c0) = xv[i];
+                *(float4*)(h_out + o + c0) = make_float4((xv[i].x - mean) * rstd * g.x + be.x, (xv[i].y - mean) * rstd * g.y + be.y,
+                                                         (xv[i].z - mean) * rstd * g.z + be.z, (xv[i].w - mean) * rstd * g.w + be.w);
+            }
+        }
+    }
+}
+
 }  // namespace net
 }  // namespace dk

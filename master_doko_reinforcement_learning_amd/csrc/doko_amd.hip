@@ -2231,6 +2231,24 @@ int dk_net_mlp_ln_f32x3_async(const float* h, float* x_io, const void* w1_hi, co
     return DK_OK;
 }
 
+// The attention half at the reference's precision: f32 activations, bf16x3 products
+// (qkv_attn_ln_f32x3_kernel; d = 160, four heads of 40).
+int dk_net_qkv_attn_ln_f32x3_async(const float* h, float* x_io, const void* wqkv_hi, const void* wqkv_lo, const float* bqkv,
+                                   const void* wp_hi, const void* wp_lo, const float* bp, uint32_t batch, uint32_t heads,
+                                   uint32_t head_dim, const float* gamma, const float* beta, float eps, float* h_out,
+                                   void* stream) {
+    if (!h || !x_io || !wqkv_hi || !wqkv_lo || !bqkv || !wp_hi || !wp_lo || !bp || !gamma || !beta || !h_out ||
+        h == h_out || heads != 4u || head_dim != 40u)
+        return DK_E_INVALID;
+    if (batch == 0) return DK_OK;
+    const float scale = 1.0f / sqrtf((float)head_dim);
+    hipLaunchKernelGGL((dk::net::qkv_attn_ln_f32x3_kernel<40>), dim3(batch), dim3(256), 0, (hipStream_t)stream, h, x_io,
+                       (const uint16_t*)wqkv_hi, (const uint16_t*)wqkv_lo, bqkv, (const uint16_t*)wp_hi,
+                       (const uint16_t*)wp_lo, bp, scale, gamma, beta, eps, h_out);
+    DK_HIP(hipGetLastError());
+    return DK_OK;
+}
+
 #ifdef DK_NET_PROF
 // profiling builds: the summed phase clocks of qkv_attn_ln_kernel since the last read (then cleared)
 extern "C" int dk_net_prof_read(uint64_t* out8) {

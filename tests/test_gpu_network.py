@@ -79,6 +79,47 @@ def test_mlp_ln_f32x3_matches_torch(d, n):
     assert ex < 2e-5 and eh < 2e-5, (ex, eh)
 
 
+def test_qkv_attn_ln_f32x3_matches_torch():
+    """The f32 attention half with bf16x3 products (qkv_attn_ln_f32x3_kernel, d = 160, 4 heads of 40):
+    x += (softmax(q k^T / sqrt(40)) v) Wp^T + bp, h' = LN(x), against exact f32 torch (matmul
+    precision "highest"): within 2e-5 of the output scale."""
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(13)
+    B, d, H, hd = 37, 160, 4, 40
+    h = torch.randn(B, 62, d, device=dev)
+    x = torch.randn(B, 62, d, device=dev) * 2
+    wq, bq = torch.randn(3 * d, d, device=dev) / d ** 0.5, torch.randn(3 * d, device=dev) * 0.1
+    wp, bp = torch.randn(d, d, device=dev) / d ** 0.5, torch.randn(d, device=dev) * 0.1
+    g, be = 1 + 0.1 * torch.randn(d, device=dev), 0.1 * torch.randn(d, device=dev)
+    prev = torch.get_float32_matmul_precision()
+    torch.set_float32_matmul_precision("highest")
+    try:
+        qkv = F.linear(h, wq, bq)
+        q, k, v = (qkv[..., i * d:(i + 1) * d].reshape(B, 62, H, hd).transpose(1, 2) for i in range(3))
+        p = torch.softmax((q @ k.transpose(-1, -2)) / hd ** 0.5, dim=-1)
+        y = (p @ v).transpose(1, 2).reshape(B, 62, d)
+        delta = F.linear(y, wp, bp)
+    finally:
+        torch.set_float32_matmul_precision(prev)
+    x_ref = x + delta
+    h_ref = F.layer_norm(x_ref, (d,), g, be, 1e-5)
+    sp = []
+    for w in (wq, wp):
+        hi = w.bfloat16().contiguous()
+        sp += [hi, (w - hi.float()).bfloat16().contiguous()]
+    xo = x.clone()
+    out = torch.full_like(x, float("nan"))
+    rc = _lib().dk_net_qkv_attn_ln_f32x3_async(h.data_ptr(), xo.data_ptr(), sp[0].data_ptr(), sp[1].data_ptr(), bq.data_ptr(),
+                                               sp[2].data_ptr(), sp[3].data_ptr(), bp.data_ptr(), B, H, hd, g.data_ptr(),
+                                               be.data_ptr(), 1e-5, out.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert torch.isfinite(out).all() and torch.isfinite(xo).all()
+    ex = (xo - x_ref).abs().max().item() / delta.abs().max().item()
+    eh = (out - h_ref).abs().max().item() / h_ref.abs().max().item()
+    assert ex < 2e-5 and eh < 2e-5, (ex, eh)
+
+
 @pytest.mark.parametrize("hd", [40, 64])
 def test_attn62_matches_torch(hd):
     """MFMA attention core (62 tokens, 4 heads x hd) against fp32 softmax(q k^T / sqrt(hd)) v."""
