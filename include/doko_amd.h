@@ -520,6 +520,19 @@ int dk_net_qkv_attn_ln_f32x3_async(const float* h, float* x_io, const void* wqkv
                                    const void* wp_hi, const void* wp_lo, const float* bp, uint32_t batch, uint32_t heads,
                                    uint32_t head_dim, const float* gamma, const float* beta, float eps, float* h_out,
                                    void* stream);
+/* The heads at the reference's precision (round 5; PerClassAttentionMLPHead,
+ * rs-doko-py-bridge/python/az_doko.py:28-56), f32 activations, bf16x3 MFMA products:
+ * dk_net_class_pool_ln_f32_async: x [B, 62, d] -> out [C, B, d] (class-major) =
+ *   LN(softmax(q_c x^T * scale) x) * ln_w[c] + ln_b[c]; queries / ln_w / ln_b [C, d] f32;
+ *   C <= 64, d = 160 or 256.  The f32 form of dk_net_class_pool_ln_bf16_async.
+ * dk_net_class_mlp_f32x3_async: pooled [C, B, d] -> out [B, C] = w2[c] . GELU(W1[c] a + b1[c])
+ *   + b2[c] (exact erf GELU); w1_hi / w1_lo [C, d, d] bf16 (the split of W1), b1 / w2 [C, d],
+ *   b2 [C] f32.  The class MLPs of the head's forward in one launch. */
+int dk_net_class_pool_ln_f32_async(const float* x, uint32_t batch, uint32_t d, const float* queries, uint32_t classes,
+                                   float scale, const float* ln_w, const float* ln_b, float eps, float* out, void* stream);
+int dk_net_class_mlp_f32x3_async(const float* pooled, uint32_t batch, uint32_t d, uint32_t classes, const void* w1_hi,
+                                 const void* w1_lo, const float* b1, const float* w2, const float* b2, float* out,
+                                 void* stream);
 /* dk_net_class_pool_ln_bf16_async: PerClassAttentionMLPHead's attention pooling and each class
  * MLP's opening LayerNorm (az_doko.py:42-50): x [batch][62][d], queries [classes][d] (classes
  * <= 64), w = softmax(queries x^T * scale) over the 62 tokens, a = w x, out[c][b][:] =

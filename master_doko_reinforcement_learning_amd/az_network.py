@@ -122,7 +122,39 @@ class ClassHead(nn.Module):
         # faulted on that layout
         return a.transpose(0, 1).contiguous()                    # [C, B, d]
 
-    def forward(self, x):                                        # x [B, S, d]
+    def f32_fused_ok(self, x):
+        B, S, d = x.shape
+        return (x.is_cuda and x.dtype == torch.float32 and S == SEQ and d in (160, 256) and self.queries.shape[0] <= 64
+                and not torch.is_grad_enabled() and not autocast_on(x.device.type)
+                and all(p.dtype == torch.float32 and p.is_contiguous() for p in self.parameters()))
+
+    def forward_f32(self, x):
+        """The f32 forward on two HIP kernels (bf16x3 products): the pooling + class LayerNorms
+        (class_pool_ln_f32x3_kernel) and every class's MLP (class_mlp_f32x3_kernel) -> [B, C]."""
+        from . import _native
+        L = _native.lib()
+        B, S, d = x.shape
+        C = self.queries.shape[0]
+        x = x.contiguous()
+        st = torch.cuda.current_stream(x.device).cuda_stream
+        key = (self.w1.data_ptr(), self.w1._version)
+        if getattr(self, "_w1_split", (None,))[0] != key:
+            hi = self.w1.detach().bfloat16().contiguous()
+            self._w1_split = (key, hi, (self.w1.detach() - hi.float()).bfloat16().contiguous())
+        _, w1h, w1l = self._w1_split
+        ac = torch.empty((C, B, d), dtype=torch.float32, device=x.device)
+        out = torch.empty((B, C), dtype=torch.float32, device=x.device)
+        for rc in (L.dk_net_class_pool_ln_f32_async(x.data_ptr(), B, d, self.queries.data_ptr(), C, self.scale,
+                                                    self.ln_w.data_ptr(), self.ln_b.data_ptr(), 1e-5, ac.data_ptr(), st),
+                   L.dk_net_class_mlp_f32x3_async(ac.data_ptr(), B, d, C, w1h.data_ptr(), w1l.data_ptr(), self.b1.data_ptr(),
+                                                  self.w2.data_ptr(), self.b2.data_ptr(), out.data_ptr(), st)):
+            if rc != 0:
+                raise RuntimeError("doko_amd f32 head kernel error %d" % rc)
+        return out
+
+    def forward(self, x, fused=True):                            # x [B, S, d]
+        if fused and self.f32_fused_ok(x):
+            return self.forward_f32(x)
         ac = self.pooled(x)
         h = F.gelu(torch.bmm(ac, self.w1.transpose(1, 2)) + self.b1[:, None, :])   # [C, B, d]
         return ((h * self.w2[:, None, :]).sum(-1) + self.b2[:, None]).transpose(0, 1)   # [B, C]
@@ -277,10 +309,11 @@ class FusedTrunkF32(FusedTrunk):
     """The f32 GPU forward of a token trunk: the reference's precision (f32 activations; GEMM
     products at least as fine as the reference's matmul precision "medium", az_doko.py:539-541)
     with HIP kernels (csrc/az_net_f32_kernels.h): the embedding sum + first LayerNorm; at d = 160
-    the whole MLP half in one kernel with bf16x3 products (mlp_ln_f32x3_kernel, round 5); the
-    attention core (f32 MFMA), residual adds fused with the LayerNorm after them, and the GEMMs
-    left on hipBLASLt at "medium" (the attention projections, the d = 256 MLP).  The attention
-    half's out_proj and c_proj run folded into one GEMM (Block.folded_proj, f32)."""
+    each block as two kernels with bf16x3 products (round 5): the whole attention half
+    (qkv_attn_ln_f32x3_kernel) and the whole MLP half (mlp_ln_f32x3_kernel); otherwise (d = 256)
+    the attention core (f32 MFMA), residual adds fused with the LayerNorm after them and the
+    GEMMs on hipBLASLt at "medium", the attention half's out_proj and c_proj folded into one GEMM
+    (Block.folded_proj, f32).  The heads: ClassHead.forward_f32."""
 
     def __init__(self, tokens, emb, ln0):
         from . import _native
@@ -375,7 +408,7 @@ class DokoAzNet(nn.Module):
             xp = blk(xp)
         for blk in self.v_blocks:
             xv = blk(xv)
-        return self.value_head(self.v_ln(xv)), self.policy_head(self.p_ln(xp))
+        return self.value_head(self.v_ln(xv), fused=False), self.policy_head(self.p_ln(xp), fused=False)
 
     def forward_fused(self, tokens, trunk=None):
         """bf16 forward on the GPU with HIP kernels (csrc/az_net_kernels.h): the embedding

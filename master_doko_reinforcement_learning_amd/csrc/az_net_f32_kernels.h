@@ -915,5 +915,229 @@ __global__ void __launch_bounds__(256, 2) qkv_attn_ln_f32x3_kernel(const float* 
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// The heads at the reference's precision (round 5): PerClassAttentionMLPHead
+// (az_doko.py:28-56), f32 activations, bf16x3 MFMA products (as mlp_ln_f32x3_kernel).
+// 8 f32 values -> the hi / lo fragments of one k-step
+__device__ __forceinline__ void split_f32x8(const float* p, bool ok, bf16x8_t& hi, bf16x8_t& lo) {
+    float v[8];
+    if (ok) {
+        const float4 a = *(const float4*)p, c = *(const float4*)(p + 4);
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = c.x; v[5] = c.y; v[6] = c.z; v[7] = c.w;
+    } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = 0.0f;
+    }
+    split_bf16x8(v, hi, lo);
+}
+
+// The pooling and each class's LayerNorm, one 256-thread workgroup per sample (the f32 form of
+// class_pool_ln_kernel):
+//   scores^T = X Q^T * scale   (the token in the registers, the class on the lane)
+//   P = softmax over the 62 tokens (f32)
+//   A = P X                    (X^T fragments gathered from the f32 rows in LDS)
+//   out[c][b][:] = LN(A[c]) * w[c] + b[c]   (class-major [C, B, d]: the class MLP's operand)
+// LDS: the sample's x rows (f32, rows padded to d + 8: the two half-waves of a gather 4 rows apart
+// land on disjoint bank halves), then the pooled rows.
+template <int D>
+__global__ void __launch_bounds__(256, 2) class_pool_ln_f32x3_kernel(const float* __restrict__ xin, uint32_t batch,
+                                                                     const float* __restrict__ queries, uint32_t classes,
+                                                                     float scale, const float* __restrict__ lnw,
+                                                                     const float* __restrict__ lnb, float eps,
+                                                                     float* __restrict__ out) {
+    constexpr int S = 62, LDX = D + 8, KD = D / 16, DT = D / 32, LP = D / 32;
+    static_assert(D % 32 == 0, "d: a multiple of 32");
+    __shared__ __attribute__((aligned(16))) float xs[64 * LDX];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
+    const uint32_t b = blockIdx.x;
+    const int C = (int)classes;
+    const float* xg = xin + (size_t)b * S * D;
+    for (int p = threadIdx.x; p < 64 * (D / 4); p += 256) {
+        const int t = p / (D / 4), d0 = 4 * (p - t * (D / 4));
+        *(float4*)&xs[t * LDX + d0] = t < S ? *(const float4*)(xg + (size_t)t * D + d0) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    __syncthreads();
+    const int CT = C > 32 ? 2 : 1, WPC = 4 / CT;       // class tiles, waves per class tile
+    const int ct = wave % CT, part = wave / CT;
+    const int cls = 32 * ct + r;
+    const float* qrow = queries + (size_t)(cls < C ? cls : 0) * D + 8 * hh;
+    f32x16_t sc[2];
+    sc[0] = f32x16_t{0};
+    sc[1] = f32x16_t{0};
+#pragma unroll 2
+    for (int ks = 0; ks < KD; ++ks) {
+        bf16x8_t qh, ql;
+        split_f32x8(qrow + 16 * ks, cls < C, qh, ql);
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+            bf16x8_t xh, xl;
+            split_f32x8(&xs[(32 * mt + r) * LDX + 16 * ks + 8 * hh], true, xh, xl);
+            sc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xl, qh, sc[mt], 0, 0, 0);
+            sc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xh, ql, sc[mt], 0, 0, 0);
+            sc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xh, qh, sc[mt], 0, 0, 0);
+        }
+    }
+    // softmax over the tokens t < 62 of the lane's class (torch: exp(v - max) / sum)
+    bf16x8_t pfh[4], pfl[4];
+    {
+        float mx = -INFINITY;
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+            for (int g = 0; g < 16; ++g) {
+                const int t = 32 * mt + (g & 3) + 8 * (g >> 2) + 4 * hh;
+                sc[mt][g] *= scale;
+                if (t < S) mx = fmaxf(mx, sc[mt][g]);
+            }
+        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        float l = 0.0f;
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+            for (int g = 0; g < 16; ++g) {
+                const int t = 32 * mt + (g & 3) + 8 * (g >> 2) + 4 * hh;
+                const float e = t < S ? expf(sc[mt][g] - mx) : 0.0f;
+                sc[mt][g] = e;
+                l += e;
+            }
+        l += __shfl_xor(l, 32);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = sc[q >> 1][8 * (q & 1) + j] / l;
+            split_bf16x8(v, pfh[q], pfl[q]);
+        }
+    }
+    // A = P X for the wave's d tiles t = part, part + WPC, ...: the B fragment of k-step q holds
+    // the tokens 16 q + 4 hh + {0..3, 8..11} of dimension 32 t + r (P's register order)
+    constexpr int MAXT = (DT + 1) / 2;
+    f32x16_t acc[MAXT];
+#pragma unroll
+    for (int i = 0; i < MAXT; ++i) {
+        const int t = part + WPC * i;
+        acc[i] = f32x16_t{0};
+        if (t < DT) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int t0 = 16 * q + 4 * hh;
+                const float* col = &xs[t0 * LDX + 32 * t + r];
+                float v[8];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    v[j] = col[j * LDX];
+                    v[4 + j] = col[(8 + j) * LDX];
+                }
+                bf16x8_t fh, fl;
+                split_bf16x8(v, fh, fl);
+                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pfl[q], fh, acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pfh[q], fl, acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pfh[q], fh, acc[i], 0, 0, 0);
+            }
+        }
+    }
+    __syncthreads();   // every wave's reads of the x rows done: the pooled rows replace them
+#pragma unroll
+    for (int i = 0; i < MAXT; ++i) {
+        const int t = part + WPC * i;
+        if (t < DT) {
+#pragma unroll
+            for (int g = 0; g < 16; ++g) {
+                const int c = 32 * ct + (g & 3) + 8 * (g >> 2) + 4 * hh;
+                if (c < C) xs[c * LDX + 32 * t + r] = acc[i][g];
+            }
+        }
+    }
+    __syncthreads();
+    // LayerNorm of each class row (F.layer_norm without affine, then * w[c] + b[c]): 4 threads per row
+    {
+        const int c = threadIdx.x >> 2, q = threadIdx.x & 3;
+        float4 xv[2 * LP];
+        float s1 = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 2 * LP; ++i) {
+            xv[i] = *(const float4*)&xs[c * LDX + 4 * (q + 4 * i)];
+            s1 += (xv[i].x + xv[i].y) + (xv[i].z + xv[i].w);
+        }
+        s1 += __shfl_xor(s1, 1);
+        s1 += __shfl_xor(s1, 2);
+        const float mean = s1 / (float)D;
+        float s2 = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 2 * LP; ++i) {
+            const float a = xv[i].x - mean, e = xv[i].y - mean, f = xv[i].z - mean, g = xv[i].w - mean;
+            s2 += (a * a + e * e) + (f * f + g * g);
+        }
+        s2 += __shfl_xor(s2, 1);
+        s2 += __shfl_xor(s2, 2);
+        const float rstd = rsqrtf(s2 / (float)D + eps);
+        if (c < C) {
+            const size_t o = ((size_t)c * batch + b) * D;
+#pragma unroll
+            for (int i = 0; i < 2 * LP; ++i) {
+                const int c0 = 4 * (q + 4 * i);
+                const float4 gv = *(const float4*)(lnw + (size_t)c * D + c0), bv = *(const float4*)(lnb + (size_t)c * D + c0);
+                *(float4*)(out + o + c0) = make_float4((xv[i].x - mean) * rstd * gv.x + bv.x, (xv[i].y - mean) * rstd * gv.y + bv.y,
+                                                       (xv[i].z - mean) * rstd * gv.z + bv.z, (xv[i].w - mean) * rstd * gv.w + bv.w);
+            }
+        }
+    }
+}
+
+// Each class's MLP, out[b][c] = w2[c] . GELU(W1[c] a[c][b] + b1[c]) + b2[c] (the exact erf GELU
+// of nn.GELU), grid (row blocks of 128, classes), 4 waves x 32 rows: the row's pooled vector split
+// in registers, W1[c] hi / lo fragments straight from L2 one k-step ahead (a class's W1 is 2 d^2
+// bf16 pieces, read by every workgroup of the class), the hidden units reduced into the output
+// without leaving the registers.  Replaces the class-batched GEMM, the bias + GELU pass and the
+// w2 product + sum over d of ClassHead.forward.
+template <int D>
+__global__ void __launch_bounds__(256, 2) class_mlp_f32x3_kernel(const float* __restrict__ ac, uint32_t batch, uint32_t classes,
+                                                                 const uint16_t* __restrict__ w1h, const uint16_t* __restrict__ w1l,
+                                                                 const float* __restrict__ b1, const float* __restrict__ w2,
+                                                                 const float* __restrict__ b2, float* __restrict__ out) {
+    constexpr int KS = D / 16, OT = D / 32;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
+    const uint32_t c = blockIdx.y;
+    const uint32_t row = blockIdx.x * 128u + (uint32_t)wave * 32u + (uint32_t)r;
+    const bool ok = row < batch;
+    bf16x8_t afh[KS], afl[KS];
+    const float* ar = ac + ((size_t)c * batch + (ok ? row : 0u)) * D + 8 * hh;
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) split_f32x8(ar + 16 * kk, ok, afh[kk], afl[kk]);
+    const uint16_t* wh = w1h + (size_t)c * D * D + (size_t)r * D + 8 * hh;
+    const uint16_t* wl = w1l + (size_t)c * D * D + (size_t)r * D + 8 * hh;
+    const float* b1c = b1 + (size_t)c * D;
+    const float* w2c = w2 + (size_t)c * D;
+    float part = 0.0f;
+    // W fragments one k-step ahead, across the output tiles too
+    bf16x8_t nh = load_frag8(wh, true), nl = load_frag8(wl, true);
+#pragma unroll 1
+    for (int ot = 0; ot < OT; ++ot) {
+        f32x16_t acc = f32x16_t{0};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            const bf16x8_t ah = nh, al = nl;
+            if (ks + 1 < KS || ot + 1 < OT) {
+                const int o2 = ks + 1 < KS ? 32 * ot * D + 16 * (ks + 1) : 32 * (ot + 1) * D;
+                nh = load_frag8(wh + o2, true);
+                nl = load_frag8(wl + o2, true);
+            }
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, afh[ks], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, afl[ks], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, afh[ks], acc, 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+            const int i = 32 * ot + (g & 3) + 8 * (g >> 2) + 4 * hh;
+            const float v = acc[g] + b1c[i];
+            part += 0.5f * v * (1.0f + erff(v * 0.70710678118654752f)) * w2c[i];
+        }
+    }
+    part += __shfl_xor(part, 32);
+    if (ok && hh == 0) out[(size_t)row * classes + c] = part + b2[c];
+}
+
 }  // namespace net
 }  // namespace dk

@@ -2249,6 +2249,39 @@ int dk_net_qkv_attn_ln_f32x3_async(const float* h, float* x_io, const void* wqkv
     return DK_OK;
 }
 
+int dk_net_class_pool_ln_f32_async(const float* x, uint32_t batch, uint32_t d, const float* queries, uint32_t classes,
+                                   float scale, const float* ln_w, const float* ln_b, float eps, float* out, void* stream) {
+    if (!x || !queries || !ln_w || !ln_b || !out || classes == 0 || classes > 64u || (d != 160u && d != 256u))
+        return DK_E_INVALID;
+    if (batch == 0) return DK_OK;
+    if (d == 160u)
+        hipLaunchKernelGGL((dk::net::class_pool_ln_f32x3_kernel<160>), dim3(batch), dim3(256), 0, (hipStream_t)stream, x,
+                           batch, queries, classes, scale, ln_w, ln_b, eps, out);
+    else
+        hipLaunchKernelGGL((dk::net::class_pool_ln_f32x3_kernel<256>), dim3(batch), dim3(256), 0, (hipStream_t)stream, x,
+                           batch, queries, classes, scale, ln_w, ln_b, eps, out);
+    DK_HIP(hipGetLastError());
+    return DK_OK;
+}
+
+int dk_net_class_mlp_f32x3_async(const float* pooled, uint32_t batch, uint32_t d, uint32_t classes, const void* w1_hi,
+                                 const void* w1_lo, const float* b1, const float* w2, const float* b2, float* out,
+                                 void* stream) {
+    if (!pooled || !w1_hi || !w1_lo || !b1 || !w2 || !b2 || !out || classes == 0 || classes > 65535u ||
+        (d != 160u && d != 256u))
+        return DK_E_INVALID;
+    if (batch == 0) return DK_OK;
+    const dim3 grid((batch + 127u) / 128u, classes);
+    if (d == 160u)
+        hipLaunchKernelGGL((dk::net::class_mlp_f32x3_kernel<160>), grid, dim3(256), 0, (hipStream_t)stream, pooled, batch,
+                           classes, (const uint16_t*)w1_hi, (const uint16_t*)w1_lo, b1, w2, b2, out);
+    else
+        hipLaunchKernelGGL((dk::net::class_mlp_f32x3_kernel<256>), grid, dim3(256), 0, (hipStream_t)stream, pooled, batch,
+                           classes, (const uint16_t*)w1_hi, (const uint16_t*)w1_lo, b1, w2, b2, out);
+    DK_HIP(hipGetLastError());
+    return DK_OK;
+}
+
 #ifdef DK_NET_PROF
 // profiling builds: the summed phase clocks of qkv_attn_ln_kernel since the last read (then cleared)
 extern "C" int dk_net_prof_read(uint64_t* out8) {

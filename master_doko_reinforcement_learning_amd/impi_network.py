@@ -44,7 +44,7 @@ class DokoImpiNet(nn.Module):
         x = sum(self.emb[i](t[:, SEQ * i:SEQ * (i + 1)]) for i in range(5)) + self.emb[5](t[:, 310:311])
         for blk in self.blocks:
             x = blk(x)
-        return self.head(self.ln_f(x))
+        return self.head(self.ln_f(x), fused=False)
 
     def forward_fused(self, tokens, trunk=None):
         f = (trunk or FusedTrunk)(tokens, self.emb, self.blocks[0].ln_1)

@@ -367,6 +367,33 @@ def test_class_pool_ln_matches_torch(d, C):
     torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=4e-2)
 
 
+@pytest.mark.parametrize("d,C", [(160, 39), (160, 4), (256, 33)])
+def test_class_head_f32_matches_torch(d, C):
+    """The f32 heads (class_pool_ln_f32x3_kernel + class_mlp_f32x3_kernel, bf16x3 products)
+    against ClassHead's torch forward at matmul precision "highest": within 2e-5 of the output
+    scale (B = 300: a partial row block of the class MLP grid)."""
+    from master_doko_reinforcement_learning_amd.az_network import ClassHead
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(5)
+    head = ClassHead(d, C).to(dev).eval()
+    with torch.no_grad():
+        head.ln_w.add_(0.1 * torch.randn_like(head.ln_w))
+        head.ln_b.add_(0.1 * torch.randn_like(head.ln_b))
+    x = torch.randn(300, 62, d, device=dev)
+    prev = torch.get_float32_matmul_precision()
+    torch.set_float32_matmul_precision("highest")
+    try:
+        with torch.inference_mode():
+            assert head.f32_fused_ok(x)
+            ref = head(x, fused=False)
+            got = head(x)
+    finally:
+        torch.set_float32_matmul_precision(prev)
+    assert got.shape == ref.shape == (300, C) and torch.isfinite(got).all()
+    e = (got - ref).abs().max().item() / ref.abs().max().item()
+    assert e < 2e-5, e
+
+
 @pytest.mark.parametrize("hd", [40, 64])
 def test_attn62_f32_matches_torch(hd):
     """f32 attention core (one wave per sample and head on the f32 matrix cores; -DDK_ATTN_F32_MFMA=0:
