@@ -272,18 +272,27 @@ def _f32c(t):
     return t.contiguous()
 
 
+def mlp_split_bf16x3(w1, w2):
+    """The MLP weights in mlp_ln_f32x3_kernel's split layout: bf16 hi / lo pairs (w = hi + lo to
+    ~16 bits) of W1 [n, d] and of W2 [d, n] with W2's columns permuted within every group of 16
+    hidden units (units 4-7 and 8-11 swapped: a lane's GEMM2 fragment becomes one 16-B piece)."""
+    w2 = w2.float()
+    n = w2.shape[1]
+    w2 = w2.reshape(-1, n // 16, 4, 4)[:, :, [0, 2, 1, 3], :].reshape(-1, n)
+    parts = []
+    for w in (w1.float(), w2):
+        hi = w.bfloat16().contiguous()
+        parts += [hi, (w - hi.float()).bfloat16().contiguous()]
+    return tuple(parts)
+
+
 def split_bf16x3(blk):
-    """The MLP weights of a block as bf16 hi / lo pairs (w = hi + lo to ~16 bits), cached on the
-    block and rebuilt when a weight changes (version counter): the operands of the bf16x3 products
-    of mlp_ln_f32x3_kernel."""
+    """A block's MLP weights in the split layout (mlp_split_bf16x3), cached on the block and
+    rebuilt when a weight changes (version counter)."""
     key = (blk.fc.weight.data_ptr(), blk.fc.weight._version, blk.proj.weight.data_ptr(), blk.proj.weight._version)
     c = getattr(blk, "_bf16x3", None)
     if c is None or c[0] != key:
-        parts = []
-        for w in (blk.fc.weight.detach(), blk.proj.weight.detach()):
-            hi = w.float().bfloat16().contiguous()
-            parts += [hi, (w.float() - hi.float()).bfloat16().contiguous()]
-        c = (key, tuple(parts))
+        c = (key, mlp_split_bf16x3(blk.fc.weight.detach(), blk.proj.weight.detach()))
         blk._bf16x3 = c
     return c[1]
 
@@ -362,7 +371,7 @@ class FusedTrunkF32(FusedTrunk):
 
     def mlp_ln(self, x, blk, h, ln):
         n = blk.fc.weight.shape[0]
-        if self.d == 160 and n % 32 == 0 and n <= 1024 and blk.fc.bias is not None and blk.proj.bias is not None:
+        if self.d in (160, 256) and n % 32 == 0 and n <= 1024 and blk.fc.bias is not None and blk.proj.bias is not None:
             # the whole MLP half in one kernel, bf16x3 products (mlp_ln_f32x3_kernel)
             w1h, w1l, w2h, w2l = split_bf16x3(blk)
             ho = torch.empty_like(x)

@@ -380,8 +380,8 @@ __device__ __forceinline__ void split_bf16x8(const float (&v)[8], bf16x8_t& hi, 
     lo = b.v;
 }
 
-template <int D, int NC, int WAVES = 8, int NB = 2>
-__global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) mlp_ln_f32x3_kernel(const float* __restrict__ h, float* __restrict__ x_io,
+template <int D, int NC, int WAVES = 4>
+__global__ void __launch_bounds__(64 * WAVES, D <= 160 ? 8 / WAVES : 1) mlp_ln_f32x3_kernel(const float* __restrict__ h, float* __restrict__ x_io,
                                                                 const uint16_t* __restrict__ w1h, const uint16_t* __restrict__ w1l,
                                                                 const float* __restrict__ b1,
                                                                 const uint16_t* __restrict__ w2h, const uint16_t* __restrict__ w2l,
@@ -389,18 +389,29 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) mlp_ln_f32x3_kernel(con
                                                                 const float* __restrict__ gamma, const float* __restrict__ beta,
                                                                 float eps, float* __restrict__ h_out) {
     static_assert(D % 32 == 0 && NC == 32, "d: multiple of 32; chunks of 32 hidden units");
-    // WAVES x 32 rows per workgroup; NB = 2: the chunks' weights double-buffered (one barrier per
-    // chunk), NB = 1: one buffer (two barriers per chunk, half the LDS)
+    // WAVES x 32 rows per workgroup; the chunks' weights double-buffered (one barrier per chunk)
+    // in two LDS arrays: the chunk loop runs in pairs (compute from lds0 while staging into lds1,
+    // then the reverse), so that every LDS access names its array and the compiler's LDS-DMA alias
+    // tracking lets the W reads of one buffer run while the other buffer's DMA is in flight (one
+    // array indexed by the chunk parity made it wait for the DMA before the first MFMA).
+    // LDS unpadded, conflict-free for the ds_read_b128 fragment reads (16 lanes of a group on 16
+    // distinct bank quads) and laid out so that a lane's DMA source address is one per-lane
+    // constant plus a uniform part:
+    //   W1 chunk piece-major: piece p (8 k-values) of hidden row i at (p NC + i) x 16 B -- a
+    //     fragment read is 32 consecutive pieces; DMA instruction u moves pieces 2u, 2u + 1 of
+    //     all 32 rows;
+    //   W2 chunk row-major, pieces XOR-swizzled: piece p of output row o at o NC + 8 (p ^ ((o >> 2) & 3)),
+    //     so that the rows r, r + 12, ... of a read group hit distinct bank quads.
+    // (global_load_lds_dwordx4: the LDS side is 64 consecutive 16-B pieces per wave instruction,
+    // any layout is made on the global side.)  Unpadded, a buffer is 40 KiB at d = 160: two
+    // workgroups of 4 waves with double-buffered chunks fill the CU's 160 KiB.
     constexpr int T = 64 * WAVES;
-    // LDS rows padded by one 16-B piece (W1: d + 8 elements; W2: NC + 8), so that a chunk is staged
-    // by direct global -> LDS loads (global_load_lds_dwordx4: no staging registers), each wave
-    // instruction filling 64 consecutive 16-B pieces of the buffer
-    constexpr int KS = D / 16, OT = D / 32, LDW1 = D + 8, LDW2 = NC + 8, GS = NC / 16;
-    constexpr int W1E = NC * LDW1, W2E = D * LDW2, BUF = 2 * (W1E + W2E);   // one buffer: W1 hi, W1 lo, W2 hi, W2 lo
-    constexpr int Q1 = LDW1 / 8, Q2 = LDW2 / 8;                             // pieces per row
-    constexpr int NP = BUF / 8, NI = (NP + 63) / 64;                        // pieces per buffer, wave instructions
-    __shared__ __attribute__((aligned(16))) uint16_t lds[NB * BUF];
-    __shared__ float b1s[MLP_MAX_HIDDEN];
+    constexpr int KS = D / 16, OT = D / 32, GS = NC / 16;
+    constexpr int W1E = NC * D, W2E = D * NC, BUF = 2 * (W1E + W2E);   // one buffer: W1 hi, W1 lo, W2 hi, W2 lo
+    constexpr int Q1 = D / 8, Q2 = NC / 8;                              // pieces per row
+    constexpr int NP = BUF / 8, NI = (NP + 63) / 64;                    // pieces per buffer, wave instructions
+    __shared__ __attribute__((aligned(16))) uint16_t lds0[BUF];
+    __shared__ __attribute__((aligned(16))) uint16_t lds1[BUF];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
     const uint32_t row = blockIdx.x * (32u * WAVES) + (uint32_t)wave * 32u + (uint32_t)r;
     const bool ok = row < rows;
@@ -418,78 +429,95 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) mlp_ln_f32x3_kernel(con
 #pragma unroll
         for (int kk = 0; kk < KS; ++kk) {
             float v[8];
-            const float4 a = ok ? *(const float4*)(hr + 16 * kk) : make_float4(0.f, 0.f, 0.f, 0.f);
-            const float4 b = ok ? *(const float4*)(hr + 16 * kk + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+            // (rows past the end compute on row 0 and are never stored: unconditional loads, one wait)
+            const float4 a = *(const float4*)(hr + 16 * kk);
+            const float4 b = *(const float4*)(hr + 16 * kk + 4);
             v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
             split_bf16x8(v, hfh[kk], hfl[kk]);
         }
     }
     typedef __attribute__((address_space(3))) void lds_void;
-    auto stage = [&](uint32_t c, int buf) {
-        for (int u = wave; u < NI; u += WAVES) {
-            const int k = 64 * u + lane;   // this lane's piece of the buffer
-            const uint16_t* g = w1h;       // (padding pieces read a valid piece and are never used)
-            if (k < 2 * NC * Q1) {
-                const int lo = k >= NC * Q1, kk = lo ? k - NC * Q1 : k, i = kk / Q1, p = kk - i * Q1;
-                g = (lo ? w1l : w1h) + ((size_t)c * NC + i) * D + 8 * (p < D / 8 ? p : 0);
-            } else if (k < NP) {
-                const int k2 = k - 2 * NC * Q1, lo = k2 >= D * Q2, kk = lo ? k2 - D * Q2 : k2, o = kk / Q2, p = kk - o * Q2;
-                g = (lo ? w2l : w2h) + (size_t)o * n_hidden + (size_t)c * NC + 8 * (p < NC / 8 ? p : 0);
+    // (a compile-time count of DMA instructions per wave: the loads issued before a stage -- the
+    // chunk's biases -- then wait on a counted vmcnt, not on the stage itself)
+    static_assert(NP % 64 == 0 && NI % WAVES == 0 && (NC * Q1) % 64 == 0 && (D * Q2) % 64 == 0,
+                  "whole wave instructions per buffer and region, the same count per wave");
+    // per-lane DMA source offsets (elements): W1 (row lane & 31, piece lane >> 5 of the pair);
+    // W2 (row lane >> 2 of the instruction's 16, swizzled piece); uniform parts added per call
+    const int dma1 = (lane & 31) * D + 8 * (lane >> 5);
+    const int dma2 = (lane >> 2) * (int)n_hidden + 8 * ((lane & 3) ^ ((lane >> 4) & 3));
+    auto stage = [&](uint32_t c, uint16_t* dst) {
+#pragma unroll
+        for (int ui = 0; ui < NI / WAVES; ++ui) {
+            const int u = wave + WAVES * ui;   // wave-uniform
+            const uint16_t* g;
+            if (u < 2 * (NC * Q1 / 64)) {
+                const int lo = u >= NC * Q1 / 64, v = lo ? u - NC * Q1 / 64 : u;
+                g = (lo ? w1l : w1h) + (size_t)c * NC * D + 16 * v + dma1;
+            } else {
+                const int u2 = u - 2 * (NC * Q1 / 64), lo = u2 >= D * Q2 / 64, v = lo ? u2 - D * Q2 / 64 : u2;
+                g = (lo ? w2l : w2h) + (size_t)(16 * v) * n_hidden + (size_t)c * NC + dma2;
             }
-            if (k < NP) __builtin_amdgcn_global_load_lds(g, (lds_void*)&lds[buf * BUF + 512 * u], 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(g, (lds_void*)&dst[512 * u], 16, 0, 0);
         }
     };
+    // the lane's W2 swizzle (rows 32 t + r share (row >> 2) & 3)
+    const int sw = (r >> 2) & 3;
     f32x16_t acc2[OT];
 #pragma unroll
     for (int t = 0; t < OT; ++t) acc2[t] = f32x16_t{0};
     const uint32_t chunks = n_hidden / NC;
-    for (uint32_t i = threadIdx.x; i < n_hidden; i += T) b1s[i] = b1[i];
-    stage(0u, 0);
+    stage(0u, lds0);
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
     DK_FSTAMP(0);
-    for (uint32_t c = 0; c < chunks; ++c) {
-        const int buf = NB == 2 ? (int)(c & 1u) : 0;
-        if (NB == 2 && c + 1 < chunks) stage(c + 1, buf ^ 1);
-        // GEMM1: D1 = W1_c h^T (one 32 x 32 tile), three products per k-step
-        f32x16_t acc1 = f32x16_t{0};
-        const uint16_t* a1h = &lds[buf * BUF + r * LDW1 + 8 * hh];
-        const uint16_t* a1l = a1h + W1E;
-        // W1 fragments read one k-step ahead (the LDS latency under the previous k-step's MFMAs)
-        bf16x8_t nh = *(const bf16x8_t*)a1h, nl = *(const bf16x8_t*)a1l;
+    auto chunk = [&](uint32_t c, const uint16_t* cur, uint16_t* nxt) {
+        // GEMM1 accumulates onto the chunk's biases (acc1[4 j + e] = b1[32 c + 8 j + 4 hh + e]),
+        // read with uniform addresses (scalar loads: counted by lgkmcnt, so that waiting for them
+        // does not wait for the stage's DMA, which vmcnt counts), each lane taking its half
+        float bb[NC];
+#pragma unroll
+        for (int m = 0; m < NC; ++m) bb[m] = b1[c * NC + m];
+        f32x16_t acc1;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc1[4 * j + e] = hh ? bb[8 * j + 4 + e] : bb[8 * j + e];
+        // (unconditional: the last chunk stages itself again into the idle buffer, so that every
+        // path issues the same DMA count and the bias wait stays a counted vmcnt)
+        stage(c + 1 < chunks ? c + 1 : c, nxt);
+        // GEMM1: D1 = W1_c h^T + b1 (one 32 x 32 tile), three products per k-step
+        const uint16_t* a1 = cur + 8 * (NC * hh + r);
+        // W1 fragments read one k-step ahead (the LDS latency under the previous k-step's MFMAs):
+        // k-step kk's piece 2 kk + hh of row r
+        auto w1f = [&](const uint16_t* base, int kk) { return *(const bf16x8_t*)(base + 16 * NC * kk); };
+        bf16x8_t nh = w1f(a1, 0), nl = w1f(a1 + W1E, 0);
 #pragma unroll
         for (int kk = 0; kk < KS; ++kk) {
             const bf16x8_t ah = nh, al = nl;
-            if (kk + 1 < KS) { nh = *(const bf16x8_t*)(a1h + 16 * (kk + 1)); nl = *(const bf16x8_t*)(a1l + 16 * (kk + 1)); }
+            if (kk + 1 < KS) { nh = w1f(a1, kk + 1); nl = w1f(a1 + W1E, kk + 1); }
             acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, hfh[kk], acc1, 0, 0, 0);
             acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, hfl[kk], acc1, 0, 0, 0);
             acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, hfh[kk], acc1, 0, 0, 0);
         }
         DK_FSTAMP(1);
-        // bias + GELU (f32) -> split B fragments of GEMM2 (k-step s = half: registers 8 s .. 8 s + 7,
+        // GELU (f32) -> split B fragments of GEMM2 (k-step s = half: registers 8 s .. 8 s + 7,
         // hidden units 16 s + 4 hh + (g & 3) + 8 ((g >> 2) & 1))
         bf16x8_t afh[GS], afl[GS];
 #pragma unroll
         for (int s2 = 0; s2 < GS; ++s2) {
-            const int h0 = 16 * s2 + 4 * hh;
-            const float4 bl = *(const float4*)&b1s[c * NC + h0], bh = *(const float4*)&b1s[c * NC + h0 + 8];
-            const float bb[8] = {bl.x, bl.y, bl.z, bl.w, bh.x, bh.y, bh.z, bh.w};
             float g[8];
 #pragma unroll
-            for (int t = 0; t < 8; ++t) g[t] = gelu_poly(acc1[8 * s2 + t] + bb[t]);
+            for (int t = 0; t < 8; ++t) g[t] = gelu_poly(acc1[8 * s2 + t]);
             split_bf16x8(g, afh[s2], afl[s2]);
         }
         DK_FSTAMP(2);
         // GEMM2: D2 += W2_c a^T, OT tiles of 32 output columns, three products per k-step
-        const uint16_t* a2h = &lds[buf * BUF + 2 * W1E + r * LDW2 + 4 * hh];
+        const uint16_t* a2h = cur + 2 * W1E + r * NC;
         const uint16_t* a2l = a2h + W2E;
-        // W2 fragments read one (k-step, tile) ahead
-        union F8 { uint2 u[2]; bf16x8_t v; };
+        // W2 fragments read one (k-step, tile) ahead: tile t's row 32 t + r, piece 2 s + hh
+        // (swizzled as GEMM1's pieces: rows 32 t + r and r share (row >> 2) & 3)
         auto w2f = [&](const uint16_t* base, int q) {
-            const int off = (32 * (q % OT)) * LDW2 + 16 * (q / OT);
-            F8 f;
-            f.u[0] = *(const uint2*)(base + off); f.u[1] = *(const uint2*)(base + off + 8);
-            return f.v;
+            return *(const bf16x8_t*)(base + (32 * (q % OT)) * NC + 8 * ((2 * (q / OT) + hh) ^ sw));
         };
         bf16x8_t ph = w2f(a2h, 0), pl = w2f(a2l, 0);
 #pragma unroll
@@ -502,18 +530,18 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) mlp_ln_f32x3_kernel(con
             acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, afh[s2], acc2[t], 0, 0, 0);
         }
         DK_FSTAMP(3);
-        if (c + 1 < chunks) {
-            if constexpr (NB == 1) {
-                __syncthreads();   // every wave is done with the buffer
-                stage(c + 1, 0);
-            }
-            __builtin_amdgcn_s_waitcnt(0);   // this wave's pieces have landed
-            __syncthreads();
-        }
+        __builtin_amdgcn_s_waitcnt(0);   // this wave's pieces of the next chunk have landed
+        __syncthreads();                 // ... and every wave's; every wave is done with `cur`
         DK_FSTAMP(4);
+    };
+    for (uint32_t c = 0; c < chunks; c += 2) {
+        chunk(c, lds0, lds1);
+        if (c + 1 < chunks) chunk(c + 1, lds1, lds0);
     }
     // epilogue: acc2[t][g] = delta of row `row`, column 32 t + 8 (g >> 2) + 4 hh + (g & 3);
     // x += (delta + b2) (the GEMM's bias first: F.linear's epilogue order), then LN
+    // (all loads first, the stores under one branch: per-store branches kept every x load
+    // behind the previous store)
     float* xr = x_io + (size_t)(ok ? row : 0u) * D;
     float s1 = 0.0f;
 #pragma unroll
@@ -521,14 +549,13 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) mlp_ln_f32x3_kernel(con
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int col = 32 * t + 8 * q + 4 * hh;
-            const float4 xv = ok ? *(const float4*)(xr + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+            const float4 xv = *(const float4*)(xr + col);
             const float4 bv = *(const float4*)(b2 + col);
             const float xn[4] = {xv.x + (acc2[t][4 * q] + bv.x), xv.y + (acc2[t][4 * q + 1] + bv.y),
                                  xv.z + (acc2[t][4 * q + 2] + bv.z), xv.w + (acc2[t][4 * q + 3] + bv.w)};
 #pragma unroll
             for (int e = 0; e < 4; ++e) acc2[t][4 * q + e] = xn[e];
             s1 += (xn[0] + xn[1]) + (xn[2] + xn[3]);
-            if (ok) *(float4*)(xr + col) = make_float4(xn[0], xn[1], xn[2], xn[3]);
         }
     s1 += __shfl_xor(s1, 32);
     const float mean = s1 / (float)D;
@@ -543,18 +570,20 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) mlp_ln_f32x3_kernel(con
     s2 += __shfl_xor(s2, 32);
     const float rstd = rsqrtf(s2 / (float)D + eps);
     float* hr = h_out + (size_t)(ok ? row : 0u) * D;
+    if (ok) {
 #pragma unroll
-    for (int t = 0; t < OT; ++t)
+        for (int t = 0; t < OT; ++t)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int col = 32 * t + 8 * q + 4 * hh;
-            const float4 gv = *(const float4*)(gamma + col), bv = *(const float4*)(beta + col);
-            if (ok)
+            for (int q = 0; q < 4; ++q) {
+                const int col = 32 * t + 8 * q + 4 * hh;
+                const float4 gv = *(const float4*)(gamma + col), bv = *(const float4*)(beta + col);
+                *(float4*)(xr + col) = make_float4(acc2[t][4 * q], acc2[t][4 * q + 1], acc2[t][4 * q + 2], acc2[t][4 * q + 3]);
                 *(float4*)(hr + col) = make_float4((acc2[t][4 * q] - mean) * rstd * gv.x + bv.x,
                                                    (acc2[t][4 * q + 1] - mean) * rstd * gv.y + bv.y,
                                                    (acc2[t][4 * q + 2] - mean) * rstd * gv.z + bv.z,
                                                    (acc2[t][4 * q + 3] - mean) * rstd * gv.w + bv.w);
-        }
+            }
+    }
     DK_FSTAMP(5);
 #ifdef DK_NET_PROF
     if (lane == 0 && wave == 0)

@@ -2207,24 +2207,15 @@ int dk_net_mlp_ln_f32x3_async(const float* h, float* x_io, const void* w1_hi, co
         (d != 160u && d != 256u) || n_hidden == 0 || n_hidden > dk::net::MLP_MAX_HIDDEN || n_hidden % 32u)
         return DK_E_INVALID;
     if (rows == 0) return DK_OK;
-    // DK_MLPF32: 0 = 8 waves, double-buffered weights; 1 (default) = 4 waves, one buffer, two
-    // workgroups per CU (tools/mlp_f32_bench.py)
-    static const int variant = getenv("DK_MLPF32") ? atoi(getenv("DK_MLPF32")) : 1;
-    if (d == 160u && variant == 1) {
-        const dim3 grid4((rows + 127u) / 128u), block4(256u);
-        hipLaunchKernelGGL((dk::net::mlp_ln_f32x3_kernel<160, 32, 4, 1>), grid4, block4, 0, (hipStream_t)stream, h, x_io,
-                           (const uint16_t*)w1_hi, (const uint16_t*)w1_lo, b1, (const uint16_t*)w2_hi, (const uint16_t*)w2_lo,
-                           b2, rows, n_hidden, gamma, beta, eps, h_out);
-        DK_HIP(hipGetLastError());
-        return DK_OK;
-    }
-    const dim3 grid((rows + 255u) / 256u), block(512u);
+    // 4 waves x 32 rows per workgroup, double-buffered weight chunks: two workgroups per CU at
+    // d = 160 (80 KiB of LDS each), one at d = 256
+    const dim3 grid((rows + 127u) / 128u), block(256u);
     if (d == 160u)
-        hipLaunchKernelGGL((dk::net::mlp_ln_f32x3_kernel<160, 32>), grid, block, 0, (hipStream_t)stream, h, x_io,
+        hipLaunchKernelGGL((dk::net::mlp_ln_f32x3_kernel<160, 32, 4>), grid, block, 0, (hipStream_t)stream, h, x_io,
                            (const uint16_t*)w1_hi, (const uint16_t*)w1_lo, b1, (const uint16_t*)w2_hi, (const uint16_t*)w2_lo,
                            b2, rows, n_hidden, gamma, beta, eps, h_out);
     else
-        hipLaunchKernelGGL((dk::net::mlp_ln_f32x3_kernel<256, 32>), grid, block, 0, (hipStream_t)stream, h, x_io,
+        hipLaunchKernelGGL((dk::net::mlp_ln_f32x3_kernel<256, 32, 4>), grid, block, 0, (hipStream_t)stream, h, x_io,
                            (const uint16_t*)w1_hi, (const uint16_t*)w1_lo, b1, (const uint16_t*)w2_hi, (const uint16_t*)w2_lo,
                            b2, rows, n_hidden, gamma, beta, eps, h_out);
     DK_HIP(hipGetLastError());

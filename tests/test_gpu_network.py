@@ -44,7 +44,7 @@ def test_mlp_ln_f32x3_matches_torch(d, n):
     relative per GEMM, profiles/r04/fp32_gemm_probe.json)."""
     dev = torch.device("cuda", 0)
     torch.manual_seed(11)
-    rows = 62 * 41 + 3                                   # not a multiple of the 256-row workgroup tile
+    rows = 62 * 41 + 3                                   # not a multiple of the 128-row workgroup tile
     h = torch.randn(rows, d, device=dev)
     x = torch.randn(rows, d, device=dev) * 2
     w1 = torch.randn(n, d, device=dev) / d ** 0.5
@@ -61,10 +61,8 @@ def test_mlp_ln_f32x3_matches_torch(d, n):
         torch.set_float32_matmul_precision(prev)
     x_ref = x + delta_ref
     h_ref = F.layer_norm(x_ref, (d,), g, be, 1e-5)
-    split = []
-    for w in (w1, w2):
-        hi = w.bfloat16().contiguous()
-        split += [hi, (w - hi.float()).bfloat16().contiguous()]
+    from master_doko_reinforcement_learning_amd.az_network import mlp_split_bf16x3
+    split = mlp_split_bf16x3(w1, w2)
     xo = x.clone()
     out = torch.full((rows, d), float("nan"), device=dev)
     rc = _lib().dk_net_mlp_ln_f32x3_async(h.data_ptr(), xo.data_ptr(), split[0].data_ptr(), split[1].data_ptr(),
@@ -248,7 +246,7 @@ def test_mlp_ln_matches_torch(d, n):
     unfused proj GEMM)."""
     dev = torch.device("cuda", 0)
     torch.manual_seed(7)
-    rows = 62 * 41 + 3                                   # not a multiple of the 256-row workgroup tile
+    rows = 62 * 41 + 3                                   # not a multiple of the 128-row workgroup tile
     h = torch.randn(rows, d, device=dev).bfloat16()
     x = (torch.randn(rows, d, device=dev) * 2).bfloat16()
     w1 = (torch.randn(n, d, device=dev) / d ** 0.5).bfloat16()

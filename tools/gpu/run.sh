@@ -18,9 +18,9 @@ for step in "$@"; do
   IFS=: read -r kind name rest more <<< "$step"
   case "$kind" in
     tests)
-      K=${name:+-k "$name"}
+      K=(); [ -n "$name" ] && K=(-k "$name")
       echo "== tests ${name:-all}"
-      eval timeout -k 10 1500 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread $K \
+      timeout -k 10 1500 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread "${K[@]}" \
         > "$OUT/gpu_tests${name:+_sub}.log" 2>&1 || { tail -30 "$OUT/gpu_tests${name:+_sub}.log"; exit 1; } ;;
     smoke)
       echo "== smoke"

@@ -23,10 +23,8 @@ def main(rows=507904, d=160, reps=20):
     w1, b1 = torch.randn(n, d, device=dev) / d ** 0.5, torch.randn(n, device=dev) * 0.1
     w2, b2 = torch.randn(d, n, device=dev) / n ** 0.5, torch.randn(d, device=dev) * 0.1
     g, be = 1 + 0.1 * torch.randn(d, device=dev), 0.1 * torch.randn(d, device=dev)
-    split = []
-    for w in (w1, w2):
-        hi = w.bfloat16().contiguous()
-        split += [hi, (w - hi.float()).bfloat16().contiguous()]
+    from master_doko_reinforcement_learning_amd.az_network import mlp_split_bf16x3
+    split = mlp_split_bf16x3(w1, w2)
     st = torch.cuda.current_stream(dev).cuda_stream
     torch.set_float32_matmul_precision("medium")
     x = x0.clone()

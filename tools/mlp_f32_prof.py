@@ -24,10 +24,8 @@ def main(rows=8192 * 62, reps=10, d=160):
     h = torch.randn(rows, d, device=dev)
     x = torch.randn(rows, d, device=dev)
     w = [torch.randn(n, d, device=dev) / d ** 0.5, torch.randn(d, n, device=dev) / n ** 0.5]
-    sp = []
-    for m in w:
-        hi = m.bfloat16().contiguous()
-        sp += [hi, (m - hi.float()).bfloat16().contiguous()]
+    from master_doko_reinforcement_learning_amd.az_network import mlp_split_bf16x3
+    sp = mlp_split_bf16x3(*w)
     b1, b2 = torch.randn(n, device=dev) * 0.1, torch.randn(d, device=dev) * 0.1
     g, be = torch.ones(d, device=dev), torch.zeros(d, device=dev)
     out = torch.empty(rows, d, device=dev)
@@ -49,7 +47,7 @@ def main(rows=8192 * 62, reps=10, d=160):
     e1.record()
     torch.cuda.synchronize()
     rd(acc.ctypes.data)
-    wpg = 8 if os.environ.get("DK_MLPF32", "1") == "0" else 4
+    wpg = 4
     wgs = (rows + 32 * wpg - 1) // (32 * wpg)
     per = acc.astype(np.float64) / (wgs * reps)
     print(json.dumps({"rows": rows, "ms": e0.elapsed_time(e1) / reps, "waves_per_wg": wpg,
