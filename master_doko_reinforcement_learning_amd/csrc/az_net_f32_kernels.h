@@ -616,22 +616,26 @@ __device__ __forceinline__ void head_tiles_x3(const uint16_t* hsh, const uint16_
     for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
         for (int si = 0; si < 2; ++si) acc[dt][si] = f32x16_t{0};
-    const bool ok1 = 32 + r < HD;
-    const size_t o0 = (size_t)r * D, o1 = (size_t)(ok1 ? 32 + r : 0) * D;
+    const size_t o0 = (size_t)r * D, o1 = (size_t)(32 + r < HD ? 32 + r : 0) * D;
     // W fragments one k-step ahead
     bf16x8_t nw[2][2];
     auto wfr = [&](int ks) {
         const int k0 = 16 * ks + 8 * hh;
         nw[0][0] = load_frag8(wh + o0 + k0, true);
         nw[0][1] = load_frag8(wl + o0 + k0, true);
-        nw[1][0] = load_frag8(wh + o1 + k0, ok1);
-        nw[1][1] = load_frag8(wl + o1 + k0, ok1);
+        // (rows past HD load row 0, unconditionally: a load under a lane condition made the
+        // compiler wait for the next k-step's loads; the rows' outputs are zeroed below)
+        nw[1][0] = load_frag8(wh + o1 + k0, true);
+        nw[1][1] = load_frag8(wl + o1 + k0, true);
     };
     wfr(0);
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
         const bf16x8_t a0h = nw[0][0], a0l = nw[0][1], a1h = nw[1][0], a1l = nw[1][1];
         if (ks + 1 < NKS) wfr(ks + 1);
+        // (the next k-step's loads stay at the top: left to the scheduler they sank to the end of
+        // the step, reusing the current operands' registers, and the next step waited for them)
+        __builtin_amdgcn_sched_barrier(0);
         bf16x8_t bhf[2], blf[2];
 #pragma unroll
         for (int si = 0; si < 2; ++si) {
@@ -657,9 +661,10 @@ __device__ __forceinline__ void head_tiles_x3(const uint16_t* hsh, const uint16_
 #pragma unroll
         for (int g = 0; g < 16; ++g) {
             const int m = 32 * dt + (g & 3) + 8 * (g >> 2) + 4 * hh;
-            const float bv = m < HD ? bias[m] : 0.0f;
-            acc[dt][0][g] += bv;
-            acc[dt][1][g] += bv;
+            const bool real = m < HD;   // (for HD = 40: register g < 4 of tile 1)
+            const float bv = real ? bias[m] : 0.0f;
+            acc[dt][0][g] = real ? acc[dt][0][g] + bv : 0.0f;
+            acc[dt][1][g] = real ? acc[dt][1][g] + bv : 0.0f;
         }
 }
 
@@ -859,8 +864,23 @@ __global__ void __launch_bounds__(256, 2) qkv_attn_ln_f32x3_kernel(const float* 
     for (int m = 0; m < 4; ++m)
 #pragma unroll
         for (int j = 0; j < NJ; ++j) acc[m][j] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
+    // Wp fragments one k-step ahead, issued at the top of the step (each loaded and consumed in
+    // place had every (k-step, tile) wait a full L2 round trip); tiles past NT load tile 0, unused
+    bf16x8_t pcur[NJ][2], pnxt[NJ][2];
+    auto wpf = [&](int ks, bf16x8_t (&dst)[NJ][2]) {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int t = wave + 4 * j;
+            const size_t wo = (size_t)(16 * (t < NT ? t : 0) + rl) * D + 32 * ks + 8 * kg;
+            dst[j][0] = load_frag8(wph + wo, true);
+            dst[j][1] = load_frag8(wpl + wo, true);
+        }
+    };
+    wpf(0, pcur);
 #pragma unroll
     for (int ks = 0; ks < KP; ++ks) {
+        if (ks + 1 < KP) wpf(ks + 1, pnxt);
+        __builtin_amdgcn_sched_barrier(0);
         bf16x8_t ah[4], al[4];
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
@@ -871,8 +891,7 @@ __global__ void __launch_bounds__(256, 2) qkv_attn_ln_f32x3_kernel(const float* 
         for (int j = 0; j < NJ; ++j) {
             const int t = wave + 4 * j;
             if (t < NT) {
-                const size_t wo = (size_t)(16 * t + rl) * D + 32 * ks + 8 * kg;
-                const bf16x8_t bh = load_frag8(wph + wo, true), bl = load_frag8(wpl + wo, true);
+                const bf16x8_t bh = pcur[j][0], bl = pcur[j][1];
 #pragma unroll
                 for (int m = 0; m < 4; ++m) {
                     acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[m], bh, acc[m][j], 0, 0, 0);
@@ -880,6 +899,12 @@ __global__ void __launch_bounds__(256, 2) qkv_attn_ln_f32x3_kernel(const float* 
                     acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[m], bh, acc[m][j], 0, 0, 0);
                 }
             }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            pcur[j][0] = pnxt[j][0];
+            pcur[j][1] = pnxt[j][1];
         }
     }
     __syncthreads();   // every wave is done with the y rows
