@@ -574,9 +574,11 @@ def net_precision(args, torch):
         torch.set_float32_matmul_precision("medium")
         torch.backends.cuda.matmul.allow_tf32 = True
         return (torch.float32, "f32 network (reference precision: f32 activations, matmul precision 'medium')", 2500.0 / 3,
-                "f32 activations; GEMM products from bf16 pieces: the MLP half in one HIP kernel with bf16x3 "
-                "MFMA products (mlp_ln_f32x3_kernel, d = 160), the other GEMMs on hipBLASLt at precision 'medium' "
-                "(max relative error ~5e-6 against f64, profiles/r04/fp32_gemm_probe.json): peak = bf16 dense / 3")
+                "f32 activations; GEMM products from bf16 pieces (bf16x3: three MFMAs per k-step, ~16-bit "
+                "products, as hipBLASLt's 'medium' f32 GEMMs measured, profiles/r04/fp32_gemm_probe.json): at d = 160 "
+                "every block as two HIP kernels (qkv_attn_ln_f32x3_kernel, mlp_ln_f32x3_kernel) and the heads as two "
+                "(class_pool_ln_f32x3_kernel, class_mlp_f32x3_kernel), no hipBLASLt; at d = 256 the MLP half likewise, "
+                "the attention projections on hipBLASLt at 'medium': peak = bf16 dense / 3")
     return torch.bfloat16, "bf16 network", 2500.0, "bf16 dense peak"
 
 
