@@ -606,7 +606,9 @@ __global__ void __launch_bounds__(64 * WAVES, D <= 160 ? 8 / WAVES : 1) mlp_ln_f
 // (12 d bytes per token), y and delta went to HBM and back.
 // LDS, one region reused in turn: the sample's h rows (hi, lo) -> the heads' V^T tiles (hi, lo)
 // -> y rows (hi, lo) -> the residual rows (f32).
-template <int HD, int D>
+// DT1: compute the second 32-row tile (head dims 32 .. HD - 1) here; without it (HD = 40: the
+// tails of Q, K and V come from one shared tile, tail_tiles_x3) acc[1] is left zero.
+template <int HD, int D, bool DT1 = true>
 __device__ __forceinline__ void head_tiles_x3(const uint16_t* hsh, const uint16_t* hsl, const uint16_t* __restrict__ wh,
                                               const uint16_t* __restrict__ wl, const float* __restrict__ bias,
                                               f32x16_t (&acc)[2][2]) {
@@ -625,8 +627,13 @@ __device__ __forceinline__ void head_tiles_x3(const uint16_t* hsh, const uint16_
         nw[0][1] = load_frag8(wl + o0 + k0, true);
         // (rows past HD load row 0, unconditionally: a load under a lane condition made the
         // compiler wait for the next k-step's loads; the rows' outputs are zeroed below)
-        nw[1][0] = load_frag8(wh + o1 + k0, true);
-        nw[1][1] = load_frag8(wl + o1 + k0, true);
+        if (DT1) {
+            nw[1][0] = load_frag8(wh + o1 + k0, true);
+            nw[1][1] = load_frag8(wl + o1 + k0, true);
+        } else {
+            nw[1][0] = nw[0][0];
+            nw[1][1] = nw[0][1];
+        }
     };
     wfr(0);
 #pragma unroll
@@ -647,7 +654,7 @@ __device__ __forceinline__ void head_tiles_x3(const uint16_t* hsh, const uint16_
             acc[0][si] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0l, bhf[si], acc[0][si], 0, 0, 0);
             acc[0][si] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0h, blf[si], acc[0][si], 0, 0, 0);
             acc[0][si] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0h, bhf[si], acc[0][si], 0, 0, 0);
-            if (HD > 32) {
+            if (HD > 32 && DT1) {
                 acc[1][si] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1l, bhf[si], acc[1][si], 0, 0, 0);
                 acc[1][si] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1h, blf[si], acc[1][si], 0, 0, 0);
                 acc[1][si] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1h, bhf[si], acc[1][si], 0, 0, 0);
@@ -661,11 +668,60 @@ __device__ __forceinline__ void head_tiles_x3(const uint16_t* hsh, const uint16_
 #pragma unroll
         for (int g = 0; g < 16; ++g) {
             const int m = 32 * dt + (g & 3) + 8 * (g >> 2) + 4 * hh;
-            const bool real = m < HD;   // (for HD = 40: register g < 4 of tile 1)
+            const bool real = m < HD && (DT1 || dt == 0);   // (for HD = 40: register g < 4 of tile 1)
             const float bv = real ? bias[m] : 0.0f;
             acc[dt][0][g] = real ? acc[dt][0][g] + bv : 0.0f;
             acc[dt][1][g] = real ? acc[dt][1][g] + bv : 0.0f;
         }
+}
+
+// HD = 40: the head dims 32..39 of Q, K and V as ONE 32-row tile -- A row r is row 32 + (r & 7)
+// of projection r >> 3 (Q, K, V; rows 24..31 repeat Q's and are discarded) -- instead of three
+// tiles of which a quarter is real: 60 MFMAs for the three tails instead of 180.  The result:
+// tail[si] register g < 4 (+ 4 p) holds projection p's dim 32 + (g & 3) + 4 hh of token 32 si + r
+// (the register order of tile 1 of head_tiles_x3), bias included.
+template <int HD, int D>
+__device__ __forceinline__ void tail_tiles_x3(const uint16_t* hsh, const uint16_t* hsl, const uint16_t* __restrict__ wh,
+                                              const uint16_t* __restrict__ wl, const float* __restrict__ bias,
+                                              f32x16_t (&tail)[2]) {
+    static_assert(HD > 32 && 3 * (HD - 32) <= 32 && (HD - 32) == 8, "three tails of 8 rows in one tile");
+    constexpr int LDY = D + 8, NKS = D / 16;
+    const int lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
+    const int pr = (r >> 3) < 3 ? (r >> 3) : 0;
+    const size_t o = (size_t)pr * D * D + (size_t)(32 + (r & 7)) * D;
+    tail[0] = f32x16_t{0};
+    tail[1] = f32x16_t{0};
+    bf16x8_t nh = load_frag8(wh + o + 8 * hh, true), nl = load_frag8(wl + o + 8 * hh, true);
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+        const bf16x8_t ah = nh, al = nl;
+        if (ks + 1 < NKS) {
+            nh = load_frag8(wh + o + 16 * (ks + 1) + 8 * hh, true);
+            nl = load_frag8(wl + o + 16 * (ks + 1) + 8 * hh, true);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        bf16x8_t bhf[2], blf[2];
+#pragma unroll
+        for (int si = 0; si < 2; ++si) {
+            bhf[si] = *(const bf16x8_t*)&hsh[(32 * si + r) * LDY + 16 * ks + 8 * hh];
+            blf[si] = *(const bf16x8_t*)&hsl[(32 * si + r) * LDY + 16 * ks + 8 * hh];
+        }
+#pragma unroll
+        for (int si = 0; si < 2; ++si) {
+            tail[si] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bhf[si], tail[si], 0, 0, 0);
+            tail[si] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, blf[si], tail[si], 0, 0, 0);
+            tail[si] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bhf[si], tail[si], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    // bias: register g of projection p = g >> 2 (< 3), dim 32 + (g & 3) + 4 hh; bias points at
+    // the head's Q bias, K's and V's are D and 2 D further
+#pragma unroll
+    for (int g = 0; g < 12; ++g) {
+        const float bv = bias[(g >> 2) * D + 32 + (g & 3) + 4 * hh];
+        tail[0][g] += bv;
+        tail[1][g] += bv;
+    }
 }
 
 // Q^T / K^T accumulators -> hi / lo fragments of the attention's k-steps (pack_head's order)
@@ -684,7 +740,7 @@ __device__ __forceinline__ void split_head(const f32x16_t (&acc)[2][2], bf16x8_t
 }
 
 template <int HD>
-__global__ void __launch_bounds__(256, 2) qkv_attn_ln_f32x3_kernel(const float* __restrict__ h_in, float* __restrict__ x_io,
+__global__ void __launch_bounds__(256, 3) qkv_attn_ln_f32x3_kernel(const float* __restrict__ h_in, float* __restrict__ x_io,
                                                                    const uint16_t* __restrict__ wqh, const uint16_t* __restrict__ wql,
                                                                    const float* __restrict__ bqkv,
                                                                    const uint16_t* __restrict__ wph, const uint16_t* __restrict__ wpl,
@@ -692,6 +748,7 @@ __global__ void __launch_bounds__(256, 2) qkv_attn_ln_f32x3_kernel(const float* 
                                                                    const float* __restrict__ gamma, const float* __restrict__ beta,
                                                                    float eps, float* __restrict__ h_out) {
     constexpr int S = 62, D = HD * 4, LDY = D + 8, LDT = 64 + 4, KS = (HD + 15) / 16, LDX = D + 4;
+    constexpr bool TAIL3 = HD == 40;                       // the three projections' dims 32..39 in one tile
     constexpr int RH = 2 * 64 * LDY;                       // h rows / y rows: hi then lo (bf16 elements)
     constexpr int RV = 2 * 4 * HD * LDT;                   // the V^T tiles: hi then lo
     constexpr int RX = 2 * 64 * LDX;                       // the residual rows (f32, in bf16 elements)
@@ -724,14 +781,38 @@ __global__ void __launch_bounds__(256, 2) qkv_attn_ln_f32x3_kernel(const float* 
     // done with the h rows.
     const size_t hq = (size_t)wave * HD * D;
     bf16x8_t pfh[2][4], pfl[2][4];
+    float vtail[2][4];                                     // V^T dims 32..39 (HD = 40), kept for the V tile
     {
         bf16x8_t qfh[2][KS], qfl[2][KS], kfh[2][KS], kfl[2][KS];
         {
             f32x16_t acc[2][2];
-            head_tiles_x3<HD, D>(hsh, hsl, wqh + hq, wql + hq, bqkv + wave * HD, acc);                          // Q^T
-            split_head<HD>(acc, qfh, qfl);
-            head_tiles_x3<HD, D>(hsh, hsl, wqh + hq + (size_t)D * D, wql + hq + (size_t)D * D, bqkv + D + wave * HD, acc);   // K^T
-            split_head<HD>(acc, kfh, kfl);
+            if constexpr (TAIL3) {
+                // dims 32..39 of Q, K and V from one shared tile, dims 0..31 per projection
+                f32x16_t tl[2];
+                tail_tiles_x3<HD, D>(hsh, hsl, wqh + hq, wql + hq, bqkv + wave * HD, tl);
+#pragma unroll
+                for (int si = 0; si < 2; ++si)
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) vtail[si][g] = tl[si][8 + g];
+                head_tiles_x3<HD, D, false>(hsh, hsl, wqh + hq, wql + hq, bqkv + wave * HD, acc);             // Q^T
+#pragma unroll
+                for (int si = 0; si < 2; ++si)
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) acc[1][si][g] = tl[si][g];
+                split_head<HD>(acc, qfh, qfl);
+                head_tiles_x3<HD, D, false>(hsh, hsl, wqh + hq + (size_t)D * D, wql + hq + (size_t)D * D, bqkv + D + wave * HD,
+                                            acc);                                                            // K^T
+#pragma unroll
+                for (int si = 0; si < 2; ++si)
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) acc[1][si][g] = tl[si][4 + g];
+                split_head<HD>(acc, kfh, kfl);
+            } else {
+                head_tiles_x3<HD, D>(hsh, hsl, wqh + hq, wql + hq, bqkv + wave * HD, acc);                      // Q^T
+                split_head<HD>(acc, qfh, qfl);
+                head_tiles_x3<HD, D>(hsh, hsl, wqh + hq + (size_t)D * D, wql + hq + (size_t)D * D, bqkv + D + wave * HD, acc);   // K^T
+                split_head<HD>(acc, kfh, kfl);
+            }
         }
         // X[ti][si] = K_ti Q_si^T, three products per k-step
         f32x16_t x[2][2];
@@ -783,8 +864,14 @@ __global__ void __launch_bounds__(256, 2) qkv_attn_ln_f32x3_kernel(const float* 
         }
     }
     f32x16_t vacc[2][2];
-    head_tiles_x3<HD, D>(hsh, hsl, wqh + hq + (size_t)2 * D * D, wql + hq + (size_t)2 * D * D, bqkv + 2 * D + wave * HD,
-                         vacc);                                                                           // V^T
+    head_tiles_x3<HD, D, !TAIL3>(hsh, hsl, wqh + hq + (size_t)2 * D * D, wql + hq + (size_t)2 * D * D, bqkv + 2 * D + wave * HD,
+                                 vacc);                                                                   // V^T
+    if constexpr (TAIL3) {
+#pragma unroll
+        for (int si = 0; si < 2; ++si)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) vacc[1][si][g] = vtail[si][g];
+    }
     __syncthreads();   // every wave is done with the h rows
     uint16_t* vth = lds + wave * HD * LDT;
     uint16_t* vtl = lds + 4 * HD * LDT + wave * HD * LDT;
