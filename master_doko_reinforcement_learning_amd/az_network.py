@@ -318,11 +318,11 @@ class FusedTrunkF32(FusedTrunk):
     """The f32 GPU forward of a token trunk: the reference's precision (f32 activations; GEMM
     products at least as fine as the reference's matmul precision "medium", az_doko.py:539-541)
     with HIP kernels (csrc/az_net_f32_kernels.h): the embedding sum + first LayerNorm; at d = 160
-    each block as two kernels with bf16x3 products (round 5): the whole attention half
-    (qkv_attn_ln_f32x3_kernel) and the whole MLP half (mlp_ln_f32x3_kernel); otherwise (d = 256)
-    the attention core (f32 MFMA), residual adds fused with the LayerNorm after them and the
-    GEMMs on hipBLASLt at "medium", the attention half's out_proj and c_proj folded into one GEMM
-    (Block.folded_proj, f32).  The heads: ClassHead.forward_f32."""
+    each block as two kernels with bf16x3 products (round 5; d = 160 or 256, 4 heads): the whole
+    attention half (qkv_attn_ln_f32x3_kernel) and the whole MLP half (mlp_ln_f32x3_kernel);
+    other shapes keep the attention core (f32 MFMA), residual adds fused with the LayerNorm after
+    them and the GEMMs on hipBLASLt at "medium", the attention half's out_proj and c_proj folded
+    into one GEMM (Block.folded_proj, f32).  The heads: ClassHead.forward_f32."""
 
     def __init__(self, tokens, emb, ln0):
         from . import _native
@@ -352,7 +352,7 @@ class FusedTrunkF32(FusedTrunk):
     def attn_ln(self, x, blk, h, ln):
         if not (self.d % blk.heads == 0 and self.d // blk.heads in (40, 64)):
             return self.add_ln(x, _f32c(blk.attn_delta(h)), ln)
-        if self.d == 160 and blk.heads == 4 and blk.qkv.bias is not None:
+        if self.d in (160, 256) and blk.heads == 4 and blk.qkv.bias is not None:
             # the whole attention half in one kernel per sample, bf16x3 products (qkv_attn_ln_f32x3_kernel)
             wqh, wql, wph, wpl, bpf = split_attn_bf16x3(blk)
             ho = torch.empty_like(x)

@@ -740,7 +740,7 @@ __device__ __forceinline__ void split_head(const f32x16_t (&acc)[2][2], bf16x8_t
 }
 
 template <int HD>
-__global__ void __launch_bounds__(256, 3) qkv_attn_ln_f32x3_kernel(const float* __restrict__ h_in, float* __restrict__ x_io,
+__global__ void __launch_bounds__(256, HD == 40 ? 3 : 2) qkv_attn_ln_f32x3_kernel(const float* __restrict__ h_in, float* __restrict__ x_io,
                                                                    const uint16_t* __restrict__ wqh, const uint16_t* __restrict__ wql,
                                                                    const float* __restrict__ bqkv,
                                                                    const uint16_t* __restrict__ wph, const uint16_t* __restrict__ wpl,
@@ -749,6 +749,7 @@ __global__ void __launch_bounds__(256, 3) qkv_attn_ln_f32x3_kernel(const float* 
                                                                    float eps, float* __restrict__ h_out) {
     constexpr int S = 62, D = HD * 4, LDY = D + 8, LDT = 64 + 4, KS = (HD + 15) / 16, LDX = D + 4;
     constexpr bool TAIL3 = HD == 40;                       // the three projections' dims 32..39 in one tile
+    constexpr bool PERDT = HD == 64;                       // Q / K one 32-dim tile at a time
     constexpr int RH = 2 * 64 * LDY;                       // h rows / y rows: hi then lo (bf16 elements)
     constexpr int RV = 2 * 4 * HD * LDT;                   // the V^T tiles: hi then lo
     constexpr int RX = 2 * 64 * LDX;                       // the residual rows (f32, in bf16 elements)
@@ -783,7 +784,8 @@ __global__ void __launch_bounds__(256, 3) qkv_attn_ln_f32x3_kernel(const float* 
     bf16x8_t pfh[2][4], pfl[2][4];
     float vtail[2][4];                                     // V^T dims 32..39 (HD = 40), kept for the V tile
     {
-        bf16x8_t qfh[2][KS], qfl[2][KS], kfh[2][KS], kfl[2][KS];
+        // (PERDT: the fragments of one 32-dim tile, two k-steps)
+        bf16x8_t qfh[2][PERDT ? 2 : KS], qfl[2][PERDT ? 2 : KS], kfh[2][PERDT ? 2 : KS], kfl[2][PERDT ? 2 : KS];
         {
             f32x16_t acc[2][2];
             if constexpr (TAIL3) {
@@ -807,7 +809,7 @@ __global__ void __launch_bounds__(256, 3) qkv_attn_ln_f32x3_kernel(const float* 
 #pragma unroll
                     for (int g = 0; g < 4; ++g) acc[1][si][g] = tl[si][4 + g];
                 split_head<HD>(acc, kfh, kfl);
-            } else {
+            } else if constexpr (!PERDT) {
                 head_tiles_x3<HD, D>(hsh, hsl, wqh + hq, wql + hq, bqkv + wave * HD, acc);                      // Q^T
                 split_head<HD>(acc, qfh, qfl);
                 head_tiles_x3<HD, D>(hsh, hsl, wqh + hq + (size_t)D * D, wql + hq + (size_t)D * D, bqkv + D + wave * HD, acc);   // K^T
@@ -816,6 +818,34 @@ __global__ void __launch_bounds__(256, 3) qkv_attn_ln_f32x3_kernel(const float* 
         }
         // X[ti][si] = K_ti Q_si^T, three products per k-step
         f32x16_t x[2][2];
+        if constexpr (PERDT) {
+            // HD = 64: Q^T and K^T one 32-dim tile at a time, X accumulated over the two (all four
+            // heads' fragments at once would not fit two waves per SIMD)
+#pragma unroll
+            for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+                for (int si = 0; si < 2; ++si) x[ti][si] = f32x16_t{0};
+#pragma unroll
+            for (int dt = 0; dt < 2; ++dt) {
+                const size_t ro = hq + (size_t)32 * dt * D;
+                f32x16_t acc[2][2];
+                head_tiles_x3<HD, D, false>(hsh, hsl, wqh + ro, wql + ro, bqkv + wave * HD + 32 * dt, acc);              // Q^T dims 32 dt ..
+                split_head<32>(acc, qfh, qfl);
+                head_tiles_x3<HD, D, false>(hsh, hsl, wqh + ro + (size_t)D * D, wql + ro + (size_t)D * D,
+                                            bqkv + D + wave * HD + 32 * dt, acc);                                        // K^T
+                split_head<32>(acc, kfh, kfl);
+#pragma unroll
+                for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+                    for (int si = 0; si < 2; ++si)
+#pragma unroll
+                        for (int kk = 0; kk < 2; ++kk) {
+                            x[ti][si] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kfl[ti][kk], qfh[si][kk], x[ti][si], 0, 0, 0);
+                            x[ti][si] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kfh[ti][kk], qfl[si][kk], x[ti][si], 0, 0, 0);
+                            x[ti][si] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kfh[ti][kk], qfh[si][kk], x[ti][si], 0, 0, 0);
+                        }
+            }
+        } else {
 #pragma unroll
         for (int ti = 0; ti < 2; ++ti)
 #pragma unroll
@@ -829,6 +859,7 @@ __global__ void __launch_bounds__(256, 3) qkv_attn_ln_f32x3_kernel(const float* 
                 }
                 x[ti][si] = acc;
             }
+        }
         // softmax over the keys t of every query column s (f32), P split
 #pragma unroll
         for (int si = 0; si < 2; ++si) {

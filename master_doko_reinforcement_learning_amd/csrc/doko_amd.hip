@@ -2229,13 +2229,18 @@ int dk_net_qkv_attn_ln_f32x3_async(const float* h, float* x_io, const void* wqkv
                                    uint32_t head_dim, const float* gamma, const float* beta, float eps, float* h_out,
                                    void* stream) {
     if (!h || !x_io || !wqkv_hi || !wqkv_lo || !bqkv || !wp_hi || !wp_lo || !bp || !gamma || !beta || !h_out ||
-        h == h_out || heads != 4u || head_dim != 40u)
+        h == h_out || heads != 4u || (head_dim != 40u && head_dim != 64u))
         return DK_E_INVALID;
     if (batch == 0) return DK_OK;
     const float scale = 1.0f / sqrtf((float)head_dim);
-    hipLaunchKernelGGL((dk::net::qkv_attn_ln_f32x3_kernel<40>), dim3(batch), dim3(256), 0, (hipStream_t)stream, h, x_io,
-                       (const uint16_t*)wqkv_hi, (const uint16_t*)wqkv_lo, bqkv, (const uint16_t*)wp_hi,
-                       (const uint16_t*)wp_lo, bp, scale, gamma, beta, eps, h_out);
+    if (head_dim == 40u)
+        hipLaunchKernelGGL((dk::net::qkv_attn_ln_f32x3_kernel<40>), dim3(batch), dim3(256), 0, (hipStream_t)stream, h, x_io,
+                           (const uint16_t*)wqkv_hi, (const uint16_t*)wqkv_lo, bqkv, (const uint16_t*)wp_hi,
+                           (const uint16_t*)wp_lo, bp, scale, gamma, beta, eps, h_out);
+    else
+        hipLaunchKernelGGL((dk::net::qkv_attn_ln_f32x3_kernel<64>), dim3(batch), dim3(256), 0, (hipStream_t)stream, h, x_io,
+                           (const uint16_t*)wqkv_hi, (const uint16_t*)wqkv_lo, bqkv, (const uint16_t*)wp_hi,
+                           (const uint16_t*)wp_lo, bp, scale, gamma, beta, eps, h_out);
     DK_HIP(hipGetLastError());
     return DK_OK;
 }

@@ -77,13 +77,15 @@ def test_mlp_ln_f32x3_matches_torch(d, n):
     assert ex < 2e-5 and eh < 2e-5, (ex, eh)
 
 
-def test_qkv_attn_ln_f32x3_matches_torch():
-    """The f32 attention half with bf16x3 products (qkv_attn_ln_f32x3_kernel, d = 160, 4 heads of 40):
+@pytest.mark.parametrize("d", [160, 256])
+def test_qkv_attn_ln_f32x3_matches_torch(d):
+    """The f32 attention half with bf16x3 products (qkv_attn_ln_f32x3_kernel, d = 160 / 256, 4 heads of 40 / 64):
     x += (softmax(q k^T / sqrt(40)) v) Wp^T + bp, h' = LN(x), against exact f32 torch (matmul
     precision "highest"): within 2e-5 of the output scale."""
     dev = torch.device("cuda", 0)
     torch.manual_seed(13)
-    B, d, H, hd = 37, 160, 4, 40
+    B, H = 37, 4
+    hd = d // H
     h = torch.randn(B, 62, d, device=dev)
     x = torch.randn(B, 62, d, device=dev) * 2
     wq, bq = torch.randn(3 * d, d, device=dev) / d ** 0.5, torch.randn(3 * d, device=dev) * 0.1
