@@ -445,9 +445,8 @@ __global__ void __launch_bounds__(64 * WAVES, D <= 160 ? 8 / WAVES : 1) mlp_ln_f
     // W2 (row lane >> 2 of the instruction's 16, swizzled piece); uniform parts added per call
     const int dma1 = (lane & 31) * D + 8 * (lane >> 5);
     const int dma2 = (lane >> 2) * (int)n_hidden + 8 * ((lane & 3) ^ ((lane >> 4) & 3));
-    auto stage = [&](uint32_t c, uint16_t* dst) {
-#pragma unroll
-        for (int ui = 0; ui < NI / WAVES; ++ui) {
+    auto stage_one = [&](uint32_t c, uint16_t* dst, int ui) {
+        {
             const int u = wave + WAVES * ui;   // wave-uniform
             const uint16_t* g;
             if (u < 2 * (NC * Q1 / 64)) {
@@ -460,6 +459,15 @@ __global__ void __launch_bounds__(64 * WAVES, D <= 160 ? 8 / WAVES : 1) mlp_ln_f
             __builtin_amdgcn_global_load_lds(g, (lds_void*)&dst[512 * u], 16, 0, 0);
         }
     };
+    constexpr int NIW = NI / WAVES;   // DMA instructions per wave and chunk
+#ifndef DK_MLPF32_DMA_STEP
+#define DK_MLPF32_DMA_STEP 1
+#endif
+    constexpr int DMA_PER_STEP = DK_MLPF32_DMA_STEP;
+    auto stage = [&](uint32_t c, uint16_t* dst) {
+#pragma unroll
+        for (int ui = 0; ui < NIW; ++ui) stage_one(c, dst, ui);
+    };
     // the lane's W2 swizzle (rows 32 t + r share (row >> 2) & 3)
     const int sw = (r >> 2) & 3;
     f32x16_t acc2[OT];
@@ -467,6 +475,9 @@ __global__ void __launch_bounds__(64 * WAVES, D <= 160 ? 8 / WAVES : 1) mlp_ln_f
     for (int t = 0; t < OT; ++t) acc2[t] = f32x16_t{0};
     const uint32_t chunks = n_hidden / NC;
     stage(0u, lds0);
+#ifdef DK_SOL_NODMA
+    stage(0u, lds1);   // (speed-of-light measurement build: every chunk computes on chunk 0's weights)
+#endif
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
     DK_FSTAMP(0);
@@ -484,7 +495,10 @@ __global__ void __launch_bounds__(64 * WAVES, D <= 160 ? 8 / WAVES : 1) mlp_ln_f
             for (int e = 0; e < 4; ++e) acc1[4 * j + e] = hh ? bb[8 * j + 4 + e] : bb[8 * j + e];
         // (unconditional: the last chunk stages itself again into the idle buffer, so that every
         // path issues the same DMA count and the bias wait stays a counted vmcnt)
-        stage(c + 1 < chunks ? c + 1 : c, nxt);
+        // the next chunk's DMA is spread over GEMM1's k-steps, one wave instruction per k-step
+        // (issued back to back at the top of the chunk, each cost ~100-185 issue cycles of the
+        // wave while its MFMAs waited; MI355X_MICROARCH.md LDS-DMA issue cost)
+        const uint32_t cn = c + 1 < chunks ? c + 1 : c;
         // GEMM1: D1 = W1_c h^T + b1 (one 32 x 32 tile), three products per k-step
         const uint16_t* a1 = cur + 8 * (NC * hh + r);
         // W1 fragments read one k-step ahead (the LDS latency under the previous k-step's MFMAs):
@@ -495,9 +509,28 @@ __global__ void __launch_bounds__(64 * WAVES, D <= 160 ? 8 / WAVES : 1) mlp_ln_f
         for (int kk = 0; kk < KS; ++kk) {
             const bf16x8_t ah = nh, al = nl;
             if (kk + 1 < KS) { nh = w1f(a1, kk + 1); nl = w1f(a1 + W1E, kk + 1); }
+#ifndef DK_SOL_NOGEMM1
             acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, hfh[kk], acc1, 0, 0, 0);
             acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, hfl[kk], acc1, 0, 0, 0);
             acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, hfh[kk], acc1, 0, 0, 0);
+#else
+            asm volatile("" :: "v"(ah), "v"(al));
+#endif
+#ifndef DK_SOL_NODMA
+            // (scheduling barriers keep [next fragments' reads][MFMAs][DMA piece] in that order: the
+            // DMA writes LDS, and the reads the scheduler would not move above it sat one MFMA
+            // before their use)
+            __builtin_amdgcn_sched_barrier(0);
+            // DMA_PER_STEP pieces per k-step from the first: all issued early in GEMM1, so that their
+            // landing latency (~1 us) runs under the rest of the chunk
+#pragma unroll
+            for (int q = 0; q < DMA_PER_STEP; ++q)
+                if (DMA_PER_STEP * kk + q < NIW) stage_one(cn, nxt, DMA_PER_STEP * kk + q);
+            if (kk == KS - 1)
+#pragma unroll
+                for (int ui = DMA_PER_STEP * KS; ui < NIW; ++ui) stage_one(cn, nxt, ui);   // (any rest here)
+            __builtin_amdgcn_sched_barrier(0);
+#endif
         }
         DK_FSTAMP(1);
         // GELU (f32) -> split B fragments of GEMM2 (k-step s = half: registers 8 s .. 8 s + 7,
@@ -525,9 +558,13 @@ __global__ void __launch_bounds__(64 * WAVES, D <= 160 ? 8 / WAVES : 1) mlp_ln_f
             const int s2 = q / OT, t = q % OT;
             const bf16x8_t wh = ph, wl = pl;
             if (q + 1 < GS * OT) { ph = w2f(a2h, q + 1); pl = w2f(a2l, q + 1); }
+#ifndef DK_SOL_NOGEMM2
             acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl, afh[s2], acc2[t], 0, 0, 0);
             acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, afl[s2], acc2[t], 0, 0, 0);
             acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, afh[s2], acc2[t], 0, 0, 0);
+#else
+            asm volatile("" :: "v"(wh), "v"(wl), "v"(afh[s2]), "v"(afl[s2]));
+#endif
         }
         DK_FSTAMP(3);
         __builtin_amdgcn_s_waitcnt(0);   // this wave's pieces of the next chunk have landed

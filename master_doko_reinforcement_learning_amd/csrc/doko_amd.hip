@@ -2209,6 +2209,16 @@ int dk_net_mlp_ln_f32x3_async(const float* h, float* x_io, const void* w1_hi, co
     if (rows == 0) return DK_OK;
     // 4 waves x 32 rows per workgroup, double-buffered weight chunks: two workgroups per CU at
     // d = 160 (80 KiB of LDS each), one at d = 256
+    // (DK_MLPF32_WAVES=8: d = 160 as one 8-wave workgroup of 256 rows per CU, half the weight
+    // staging per row; measurement switch)
+    static const int waves8 = getenv("DK_MLPF32_WAVES") && atoi(getenv("DK_MLPF32_WAVES")) == 8;
+    if (d == 160u && waves8) {
+        hipLaunchKernelGGL((dk::net::mlp_ln_f32x3_kernel<160, 32, 8>), dim3((rows + 255u) / 256u), dim3(512u), 0,
+                           (hipStream_t)stream, h, x_io, (const uint16_t*)w1_hi, (const uint16_t*)w1_lo, b1,
+                           (const uint16_t*)w2_hi, (const uint16_t*)w2_lo, b2, rows, n_hidden, gamma, beta, eps, h_out);
+        DK_HIP(hipGetLastError());
+        return DK_OK;
+    }
     const dim3 grid((rows + 127u) / 128u), block(256u);
     if (d == 160u)
         hipLaunchKernelGGL((dk::net::mlp_ln_f32x3_kernel<160, 32, 4>), grid, block, 0, (hipStream_t)stream, h, x_io,
