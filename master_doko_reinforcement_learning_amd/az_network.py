@@ -60,14 +60,16 @@ class Block(nn.Module):
     def folded_proj(self):
         """c_proj(out(y)) = (Wc Wo) y + (Wc bo + bc): the two back-to-back projections of
         the reference's SelfAttention (MultiheadAttention.out_proj, then c_proj) folded
-        into one GEMM for inference (products in f32, cached until the weights change)."""
+        into one GEMM for inference (products in f64 on the host, cached until the weights change)."""
         key = (self.out.weight.data_ptr(), self.c_proj.weight.data_ptr(), self.out.weight._version,
                self.c_proj.weight._version, self.out.weight.dtype)
         if getattr(self, "_fold_key", None) != key:
-            wo, bo = self.out.weight.float(), self.out.bias.float()
-            wc, bc = self.c_proj.weight.float(), self.c_proj.bias.float()
-            dt = self.out.weight.dtype
-            self._fold = ((wc @ wo).to(dt), (wc @ bo + bc).to(dt))
+            # (in f64 on the host, once per weight version: exact to the storage dtype's rounding,
+            # and no BLAS kernel on the device)
+            wo, bo = self.out.weight.detach().double().cpu(), self.out.bias.detach().double().cpu()
+            wc, bc = self.c_proj.weight.detach().double().cpu(), self.c_proj.bias.detach().double().cpu()
+            dt, dev = self.out.weight.dtype, self.out.weight.device
+            self._fold = ((wc @ wo).to(dev, dt), (wc @ bo + bc).to(dev, dt))
             self._fold_key = key
         return self._fold
 
