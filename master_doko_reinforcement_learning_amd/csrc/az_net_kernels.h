@@ -514,10 +514,15 @@ __global__ void __launch_bounds__(256, 2) attn_ln_kernel(const uint16_t* __restr
 #ifndef DK_QKV_WPE
 #define DK_QKV_WPE 3
 #endif
+#ifndef DK_QKV_TAIL
+#define DK_QKV_TAIL 1   // HD = 40: Q / K / V dims 32..39 from one shared tile (head_tail_tile)
+#endif
 #ifndef DK_QKV_PF
 #define DK_QKV_PF -1   // -1: per head size (below)
 #endif
-template <int HD, int D>
+// DT1 = false: only the first 32-row tile (head dims 0..31); acc[1] stays zero (HD = 40: the
+// dims 32..39 of Q, K and V come from one shared tile, head_tail_tile)
+template <int HD, int D, bool DT1 = true>
 __device__ __forceinline__ void head_tiles(const uint16_t* hs, const uint16_t* __restrict__ w,
                                            const uint16_t* __restrict__ bias, f32x16_t (&acc)[2][2]) {
     constexpr int LDY = D + 8;
@@ -541,7 +546,7 @@ __device__ __forceinline__ void head_tiles(const uint16_t* hs, const uint16_t* _
 #pragma unroll
         for (int st = 0; st < GS; ++st) {
             wa[0][st] = load_frag8(w0 + kb + 8 * st, true);
-            wa[1][st] = load_frag8(w1 + kb + 8 * st, ok1);
+            wa[1][st] = DT1 ? load_frag8(w1 + kb + 8 * st, ok1) : wa[0][st];
         }
 #pragma unroll
         for (int st = 0; st < GS; ++st) {
@@ -549,7 +554,7 @@ __device__ __forceinline__ void head_tiles(const uint16_t* hs, const uint16_t* _
 #pragma unroll
             for (int si = 0; si < 2; ++si) hb[si] = *(const bf16x8_t*)&hs[(32 * si + r) * LDY + kb + 8 * st];
 #pragma unroll
-            for (int dt = 0; dt < 2; ++dt)
+            for (int dt = 0; dt < (DT1 ? 2 : 1); ++dt)
 #pragma unroll
                 for (int si = 0; si < 2; ++si)
                     acc[dt][si] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[dt][st], hb[si], acc[dt][si], 0, 0, 0);
@@ -596,10 +601,47 @@ __device__ __forceinline__ void head_tiles(const uint16_t* hs, const uint16_t* _
 #pragma unroll
         for (int g = 0; g < 16; ++g) {
             const int m = 32 * dt + (g & 3) + 8 * (g >> 2) + 4 * hh;
-            const float bv = m < HD ? bf2f(bias[m]) : 0.0f;
+            const float bv = m < HD && (DT1 || dt == 0) ? bf2f(bias[m]) : 0.0f;
             acc[dt][0][g] += bv;
             acc[dt][1][g] += bv;
         }
+}
+
+// HD = 40: the head dims 32..39 of Q, K and V as ONE 32-row tile -- A row r is row 32 + (r & 7)
+// of projection r >> 3 (Q, K, V; rows 24..31 repeat Q's and are discarded) -- instead of three
+// tiles that are three quarters padding (20 MFMAs for the three tails instead of 60).  Register
+// g < 4 (+ 4 p) of tail[si] holds projection p's dim 32 + (g & 3) + 4 hh of token 32 si + r, bias
+// included (the register order of tile 1 of head_tiles).  w: the head's Q rows; K's and V's are
+// D * D elements further, the biases D further.
+template <int HD, int D>
+__device__ __forceinline__ void head_tail_tile(const uint16_t* hs, const uint16_t* __restrict__ w,
+                                               const uint16_t* __restrict__ bias, f32x16_t (&tail)[2]) {
+    static_assert(HD == 40, "three tails of 8 rows in one tile");
+    constexpr int LDY = D + 8, NKS = D / 16;
+    const int lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
+    const int pr = (r >> 3) < 3 ? (r >> 3) : 0;
+    const uint16_t* wr = w + (size_t)pr * D * D + (size_t)(32 + (r & 7)) * D + 8 * hh;
+    tail[0] = f32x16_t{0};
+    tail[1] = f32x16_t{0};
+    bf16x8_t nw = load_frag8(wr, true);
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+        const bf16x8_t a = nw;
+        if (ks + 1 < NKS) nw = load_frag8(wr + 16 * (ks + 1), true);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int si = 0; si < 2; ++si) {
+            const bf16x8_t hb = *(const bf16x8_t*)&hs[(32 * si + r) * LDY + 16 * ks + 8 * hh];
+            tail[si] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, hb, tail[si], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int g = 0; g < 12; ++g) {
+        const float bv = bf2f(bias[(g >> 2) * D + 32 + (g & 3) + 4 * hh]);
+        tail[0][g] += bv;
+        tail[1][g] += bv;
+    }
 }
 
 template <int HD>
@@ -655,7 +697,40 @@ __global__ void __launch_bounds__(256, HD == 40 ? DK_QKV_WPE : 2) qkv_attn_ln_ke
     const uint16_t* bh = bqkv + wave * HD;
     uint16_t* vt = lds_a + wave * HD * LDT;
     bf16x8_t qf[2][KS], kf[2][KS];
-    {
+    if constexpr (HD == 40 && DK_QKV_TAIL) {
+        // dims 32..39 of V, K and Q from one shared tile (head_tail_tile), dims 0..31 per projection
+        f32x16_t tl[2];
+        head_tail_tile<HD, D>(ys, wh, bh, tl);
+        f32x16_t acc[2][2];
+        head_tiles<HD, D, false>(ys, wh + (size_t)2 * D * D, bh + 2 * D, acc);    // V^T -> [e][t]
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+            const int m = (g & 3) + 8 * (g >> 2) + 4 * hh;
+            vt[m * LDT + r] = f2bf(acc[0][0][g]);
+            vt[m * LDT + 32 + r] = f2bf(acc[0][1][g]);
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int m = 32 + g + 4 * hh;
+            vt[m * LDT + r] = f2bf(tl[0][8 + g]);
+            vt[m * LDT + 32 + r] = f2bf(tl[1][8 + g]);
+        }
+        DK_NSTAMP(1);
+        head_tiles<HD, D, false>(ys, wh + (size_t)D * D, bh + D, acc);            // K^T
+#pragma unroll
+        for (int si = 0; si < 2; ++si)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) acc[1][si][g] = tl[si][4 + g];
+        pack_head<HD>(acc, kf);
+        DK_NSTAMP(2);
+        head_tiles<HD, D, false>(ys, wh, bh, acc);                                // Q^T
+#pragma unroll
+        for (int si = 0; si < 2; ++si)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) acc[1][si][g] = tl[si][g];
+        pack_head<HD>(acc, qf);
+        DK_NSTAMP(3);
+    } else {
         f32x16_t acc[2][2];
         head_tiles<HD, D>(ys, wh + (size_t)2 * D * D, bh + 2 * D, acc);    // V^T -> [e][t]
 #pragma unroll
