@@ -515,7 +515,7 @@ __global__ void __launch_bounds__(256, 2) attn_ln_kernel(const uint16_t* __restr
 #define DK_QKV_WPE 3
 #endif
 #ifndef DK_QKV_TAIL
-#define DK_QKV_TAIL 1   // HD = 40: Q / K / V dims 32..39 from one shared tile (head_tail_tile)
+#define DK_QKV_TAIL 0   // 1: HD = 40 Q / K / V dims 32..39 from one shared tile (head_tail_tile): 0.350 vs 0.343 ms, not kept
 #endif
 #ifndef DK_QKV_PF
 #define DK_QKV_PF -1   // -1: per head size (below)
