@@ -201,6 +201,17 @@ struct GpuMem {
         (void)slot; (void)cb; (void)info;
 #endif
     }
+    // the same request, made before the pick for a lane-pair half's most visited child
+    // (pick_child_pair, -DDK_TOUCH_EARLY=1)
+    __device__ void touch_early(uint32_t slot, uint32_t cb, uint32_t info) const {
+        const uint32_t nch = dk::ni_nchild(info);
+        if (dk::ni_open(info)) {
+            touch(&sr(dk::ni_state(info)));
+            if (nch) touch(&cr(slot));
+        } else if (nch >= 2) {
+            touch(&hr(cb));
+        }
+    }
 #ifdef DK_PHASE_PROF
     __device__ void prof_add(int k, uint64_t v) const { prof[k] += v; }
 #endif

@@ -571,6 +571,9 @@ DK_HD uint32_t pick_child_x(const B& b, uint32_t n, double lnN, double c, Mem& m
     return pick;
 }
 
+#ifndef DK_TOUCH_EARLY
+#define DK_TOUCH_EARLY 0
+#endif
 // ---- lane pairs (NodeHot16P) ----------------------------------------------------------
 static constexpr int SCAN_HALF = SCAN_REG / 2;   // children per lane of a pair
 // Half a child block (16-B records) in registers.
@@ -604,6 +607,21 @@ DK_HD uint32_t pick_child_pair(const BlockH& b, uint32_t n, uint32_t j0, double 
                                uint32_t cbx) {
     const bool upper = j0 != 0;
     const bool have = j0 < n;                 // the lower half always holds child 0
+#if DK_TOUCH_EARLY
+    // 0. before the pick: each lane requests what the next step would load for its half's most
+    // visited child (UCT's pick converges to the most visited), so that the real load of the
+    // picked child's block / state finds it on its way while the pick runs
+    if (have) {
+        uint32_t vb = (uint32_t)b.st[0], jb = 0, cbb = b.cb[0], inb = b.inf[0];
+#pragma unroll
+        for (int k = 1; k < SCAN_HALF; ++k) {
+            const bool better = j0 + (uint32_t)k < n && (uint32_t)b.st[k] > vb;
+            vb = better ? (uint32_t)b.st[k] : vb; jb = better ? (uint32_t)k : jb;
+            cbb = better ? b.cb[k] : cbb; inb = better ? b.inf[k] : inb;
+        }
+        mem.touch_early(cbx + j0 + jb, cbb, inb);
+    }
+#endif
     // 1. sibling min / max (exact, cross products) over this half, then the pair
     int32_t wmin = have ? (int32_t)(b.st[0] >> 32) : 0, wmax = wmin;
     uint32_t vmin = have ? (uint32_t)b.st[0] : 1u, vmax = vmin;
