@@ -185,6 +185,34 @@ def test_fused_network_matches_fp32_module():
 
 
 @pytest.mark.parametrize("net_name", ["az", "impi"])
+@pytest.mark.parametrize("batch", [1, 3])
+def test_f32_network_tiny_batch(net_name, batch):
+    """The f32 network's HIP kernels on 1 and 3 samples (a single, partial row block of the MLP,
+    one workgroup of the attention and head kernels) against the f32 module at full precision."""
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(7)
+    if net_name == "az":
+        from master_doko_reinforcement_learning_amd.az_network import VOCAB, DokoAzNet
+        net = DokoAzNet().to(dev).eval()
+    else:
+        from master_doko_reinforcement_learning_amd.impi_network import VOCAB_IPI as VOCAB, DokoImpiNet
+        net = DokoImpiNet().to(dev).eval()
+    tok = _tokens(dev, batch, VOCAB)
+    try:
+        torch.set_float32_matmul_precision("highest")
+        with torch.inference_mode():
+            ref = net.forward_torch(tok)
+            got = net(tok)
+    finally:
+        torch.set_float32_matmul_precision("highest")
+    ref = ref if isinstance(ref, tuple) else (ref,)
+    got = got if isinstance(got, tuple) else (got,)
+    for r, g in zip(ref, got):
+        assert g.shape == r.shape and torch.isfinite(g).all()
+        assert (g - r).abs().max().item() < F32_REL * r.abs().max().item()
+
+
+@pytest.mark.parametrize("net_name", ["az", "impi"])
 def test_f32_network_reference_precision(net_name):
     """The f32 network path (FusedTrunkF32: f32 embedding + LayerNorm, add + LayerNorm,
     attention-core and GELU kernels, GEMMs at the reference's matmul precision "medium",
