@@ -798,20 +798,31 @@ __global__ void __launch_bounds__(256, HD == 40 ? 3 : 2) qkv_attn_ln_f32x3_kerne
     uint16_t* hsl = lds + 64 * LDY;
     // the sample's h rows, split; rows 62, 63 zero
     const float* hg = h_in + (size_t)b * S * D;
-    for (int p = threadIdx.x; p < 64 * (D / 8); p += 256) {
-        const int rr = p / (D / 8), kp = p - rr * (D / 8);
-        float v[8];
-        if (rr < S) {
-            const float4 a = *(const float4*)(hg + 8 * p), c = *(const float4*)(hg + 8 * p + 4);
-            v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = c.x; v[5] = c.y; v[6] = c.z; v[7] = c.w;
-        } else {
+    {
+        // every load issued before the first split / LDS store (a load -> store loop waited a
+        // memory round trip per iteration); rows 62, 63 zero
+        constexpr int NPC = 64 * (D / 8) / 256;
+        static_assert(64 * (D / 8) % 256 == 0, "whole pieces per thread");
+        float4 va[NPC], vb[NPC];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = 0.0f;
+        for (int i = 0; i < NPC; ++i) {
+            const int p = threadIdx.x + 256 * i, rr = p / (D / 8), kp = p - rr * (D / 8);
+            const float* src = hg + (size_t)(rr < S ? rr : S - 1) * D + 8 * kp;
+            va[i] = *(const float4*)src;
+            vb[i] = *(const float4*)(src + 4);
         }
-        bf16x8_t fh, fl;
-        split_bf16x8(v, fh, fl);
-        *(bf16x8_t*)&hsh[rr * LDY + 8 * kp] = fh;
-        *(bf16x8_t*)&hsl[rr * LDY + 8 * kp] = fl;
+#pragma unroll
+        for (int i = 0; i < NPC; ++i) {
+            const int p = threadIdx.x + 256 * i, rr = p / (D / 8), kp = p - rr * (D / 8);
+            const bool ok = rr < S;
+            float v[8] = {va[i].x, va[i].y, va[i].z, va[i].w, vb[i].x, vb[i].y, vb[i].z, vb[i].w};
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = ok ? v[j] : 0.0f;
+            bf16x8_t fh, fl;
+            split_bf16x8(v, fh, fl);
+            *(bf16x8_t*)&hsh[rr * LDY + 8 * kp] = fh;
+            *(bf16x8_t*)&hsl[rr * LDY + 8 * kp] = fl;
+        }
     }
     __syncthreads();
     // Register budget: Q^T and K^T into split fragments, then X = K Q^T and the softmax (Q / K
@@ -1066,9 +1077,20 @@ __global__ void __launch_bounds__(256, HD == 40 ? 3 : 2) qkv_attn_ln_f32x3_kerne
     // the residual rows (f32) into LDS, x' = x + (delta + bp) in place
     float* xs = reinterpret_cast<float*>(lds);
     const float* xg = x_io + (size_t)b * S * D;
-    for (int p = threadIdx.x; p < S * (D / 4); p += 256) {
-        const int rr = p / (D / 4), kp = p - rr * (D / 4);
-        *(float4*)&xs[rr * LDX + 4 * kp] = *(const float4*)(xg + 4 * p);
+    {
+        // all residual loads first (clamped to the last piece), then the LDS stores
+        constexpr int NX = (S * (D / 4) + 255) / 256;
+        float4 v[NX];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            const int p = threadIdx.x + 256 * i;
+            v[i] = *(const float4*)(xg + 4 * (p < S * (D / 4) ? p : S * (D / 4) - 1));
+        }
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            const int p = threadIdx.x + 256 * i, rr = p / (D / 4), kp = p - rr * (D / 4);
+            if (p < S * (D / 4)) *(float4*)&xs[rr * LDX + 4 * kp] = v[i];
+        }
     }
     __syncthreads();
 #pragma unroll
@@ -1162,9 +1184,22 @@ __global__ void __launch_bounds__(256, 2) class_pool_ln_f32x3_kernel(const float
     const uint32_t b = blockIdx.x;
     const int C = (int)classes;
     const float* xg = xin + (size_t)b * S * D;
-    for (int p = threadIdx.x; p < 64 * (D / 4); p += 256) {
-        const int t = p / (D / 4), d0 = 4 * (p - t * (D / 4));
-        *(float4*)&xs[t * LDX + d0] = t < S ? *(const float4*)(xg + (size_t)t * D + d0) : make_float4(0.f, 0.f, 0.f, 0.f);
+    {
+        // every load issued before the first LDS store (a load -> store loop waited a memory round
+        // trip per iteration); rows 62, 63 zero
+        constexpr int N4 = 64 * (D / 4) / 256;
+        static_assert(64 * (D / 4) % 256 == 0, "whole float4s per thread");
+        float4 v[N4];
+#pragma unroll
+        for (int i = 0; i < N4; ++i) {
+            const int p = threadIdx.x + 256 * i, t = p / (D / 4), d0 = 4 * (p - t * (D / 4));
+            v[i] = *(const float4*)(xg + (size_t)(t < S ? t : S - 1) * D + d0);
+        }
+#pragma unroll
+        for (int i = 0; i < N4; ++i) {
+            const int p = threadIdx.x + 256 * i, t = p / (D / 4), d0 = 4 * (p - t * (D / 4));
+            *(float4*)&xs[t * LDX + d0] = t < S ? v[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
     }
     __syncthreads();
     const int CT = C > 32 ? 2 : 1, WPC = 4 / CT;       // class tiles, waves per class tile

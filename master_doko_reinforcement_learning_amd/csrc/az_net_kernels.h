@@ -686,9 +686,26 @@ __global__ void __launch_bounds__(256, HD == 40 ? DK_QKV_WPE : 2) qkv_attn_ln_ke
     unsigned long long t_prev = __builtin_amdgcn_s_memtime();
 #endif
     const uint16_t* hg = h_in + (size_t)b * S * D;
-    for (int p = threadIdx.x; p < 64 * (D / 8); p += 256) {
-        const int rr = p / (D / 8), kp = p - rr * (D / 8);
-        *(uint4*)&ys[rr * LDY + 8 * kp] = rr < S ? *(const uint4*)(hg + 8 * p) : make_uint4(0u, 0u, 0u, 0u);
+    {
+        // every load issued before the first LDS store (a load -> store loop waited a memory
+        // round trip per iteration); rows 62, 63 zero
+        constexpr int NPC = 64 * (D / 8) / 256;
+        static_assert(64 * (D / 8) % 256 == 0, "whole pieces per thread");
+        // (the thread index through an opaque copy: the compiler otherwise kept index terms of
+        // this prologue alive for the epilogue's LDS writes and spilled them)
+        int tid = (int)threadIdx.x;
+        asm volatile("" : "+v"(tid));
+        uint4 v[NPC];
+#pragma unroll
+        for (int i = 0; i < NPC; ++i) {
+            const int p = tid + 256 * i, rr = p / (D / 8), kp = p - rr * (D / 8);
+            v[i] = *(const uint4*)(hg + (size_t)(rr < S ? rr : S - 1) * D + 8 * kp);
+        }
+#pragma unroll
+        for (int i = 0; i < NPC; ++i) {
+            const int p = tid + 256 * i, rr = p / (D / 8), kp = p - rr * (D / 8);
+            *(uint4*)&ys[rr * LDY + 8 * kp] = rr < S ? v[i] : make_uint4(0u, 0u, 0u, 0u);
+        }
     }
     __syncthreads();
     DK_NSTAMP(0);
@@ -786,9 +803,21 @@ __global__ void __launch_bounds__(256, 2) class_pool_ln_kernel(const uint16_t* _
     const uint32_t b = blockIdx.x;                                   // one sample per workgroup
     const int C = (int)classes;
     const uint16_t* xg = xin + (size_t)b * S * D;
-    for (int p = threadIdx.x; p < 64 * (D / 8); p += 256) {
-        const int t = p / (D / 8), d0 = 8 * (p - t * (D / 8));
-        *(uint4*)&xs[t * LDX + d0] = t < S ? *(const uint4*)(xg + (size_t)t * D + d0) : make_uint4(0u, 0u, 0u, 0u);
+    {
+        // every load issued before the first LDS store; rows 62, 63 zero
+        constexpr int NPC = 64 * (D / 8) / 256;
+        static_assert(64 * (D / 8) % 256 == 0, "whole pieces per thread");
+        uint4 v[NPC];
+#pragma unroll
+        for (int i = 0; i < NPC; ++i) {
+            const int p = threadIdx.x + 256 * i, t = p / (D / 8), d0 = 8 * (p - t * (D / 8));
+            v[i] = *(const uint4*)(xg + (size_t)(t < S ? t : S - 1) * D + d0);
+        }
+#pragma unroll
+        for (int i = 0; i < NPC; ++i) {
+            const int p = threadIdx.x + 256 * i, t = p / (D / 8), d0 = 8 * (p - t * (D / 8));
+            *(uint4*)&xs[t * LDX + d0] = t < S ? v[i] : make_uint4(0u, 0u, 0u, 0u);
+        }
     }
     __syncthreads();
     // x^T from the rows in LDS: thread (d, t0) gathers 8 tokens of one dimension (2-B reads, a
