@@ -1209,10 +1209,20 @@ __global__ void __launch_bounds__(256, 2) class_pool_ln_f32x3_kernel(const float
     f32x16_t sc[2];
     sc[0] = f32x16_t{0};
     sc[1] = f32x16_t{0};
-#pragma unroll 2
+    // the query pieces one k-step ahead (loaded in the step that used them, each step waited an
+    // L2 round trip)
+    float4 qa = *(const float4*)qrow, qb = *(const float4*)(qrow + 4);
+#pragma unroll
     for (int ks = 0; ks < KD; ++ks) {
+        float qv[8] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w};
+        if (ks + 1 < KD) {
+            qa = *(const float4*)(qrow + 16 * (ks + 1));
+            qb = *(const float4*)(qrow + 16 * (ks + 1) + 4);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) qv[j] = cls < C ? qv[j] : 0.0f;
         bf16x8_t qh, ql;
-        split_f32x8(qrow + 16 * ks, cls < C, qh, ql);
+        split_bf16x8(qv, qh, ql);
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt) {
             bf16x8_t xh, xl;

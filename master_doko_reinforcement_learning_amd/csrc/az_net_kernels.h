@@ -840,9 +840,16 @@ __global__ void __launch_bounds__(256, 2) class_pool_ln_kernel(const uint16_t* _
     f32x16_t sc[2];
     sc[0] = f32x16_t{0};
     sc[1] = f32x16_t{0};
-#pragma unroll 2
+    // the query fragments one k-step ahead (an L2 round trip per step otherwise)
+    const uint16_t* qrow = queries + (size_t)(cls < C ? cls : 0) * D + 8 * hh;
+    uint4 qn = *(const uint4*)qrow;
+#pragma unroll
     for (int ks = 0; ks < KD; ++ks) {
-        const bf16x8_t qf = load_frag8(queries + (size_t)(cls < C ? cls : 0) * D + 16 * ks + 8 * hh, cls < C);
+        const uint4 qu = qn;
+        if (ks + 1 < KD) qn = *(const uint4*)(qrow + 16 * (ks + 1));
+        union { uint4 u; bf16x8_t v; } qcv;
+        qcv.u = cls < C ? qu : make_uint4(0u, 0u, 0u, 0u);
+        const bf16x8_t qf = qcv.v;
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt) {
             const bf16x8_t xa = *(const bf16x8_t*)&xs[(32 * mt + r) * LDX + 16 * ks + 8 * hh];
