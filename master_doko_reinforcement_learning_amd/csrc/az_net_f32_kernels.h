@@ -1357,8 +1357,10 @@ __global__ void __launch_bounds__(256, 2) class_mlp_f32x3_kernel(const float* __
     const bool ok = row < batch;
     bf16x8_t afh[KS], afl[KS];
     const float* ar = ac + ((size_t)c * batch + (ok ? row : 0u)) * D + 8 * hh;
+    // (unconditional loads -- rows past the batch read row 0 and are never stored: a load under
+    // the row condition waited for each load in turn)
 #pragma unroll
-    for (int kk = 0; kk < KS; ++kk) split_f32x8(ar + 16 * kk, ok, afh[kk], afl[kk]);
+    for (int kk = 0; kk < KS; ++kk) split_f32x8(ar + 16 * kk, true, afh[kk], afl[kk]);
     const uint16_t* wh = w1h + (size_t)c * D * D + (size_t)r * D + 8 * hh;
     const uint16_t* wl = w1l + (size_t)c * D * D + (size_t)r * D + 8 * hh;
     const float* b1c = b1 + (size_t)c * D;
@@ -1377,6 +1379,7 @@ __global__ void __launch_bounds__(256, 2) class_mlp_f32x3_kernel(const float* __
                 nh = load_frag8(wh + o2, true);
                 nl = load_frag8(wl + o2, true);
             }
+            __builtin_amdgcn_sched_barrier(0);   // (the next step's loads stay ahead of this step's MFMAs)
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, afh[ks], acc, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, afl[ks], acc, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, afh[ks], acc, 0, 0, 0);
