@@ -502,8 +502,10 @@ int dk_net_mlp_ln_bf16_async(const void* h, void* x_io, const void* w1, const vo
  * activations and biases, bf16x3 products (each f32 operand split into bf16 hi + lo; three MFMAs
  * per k-step, ~16-bit product accuracy as hipBLASLt's f32 GEMMs at matmul precision "medium"
  * on gfx950).  w1_hi / w1_lo [n_hidden][d] and w2_hi / w2_lo [d][n_hidden] are the weights'
- * bf16 hi / lo parts, W2's columns in the split layout: within every group of 16 hidden units,
- * units 4-7 and 8-11 swapped (az_network.mlp_split_bf16x3 makes all four);
+ * bf16 hi / lo parts, W2's columns in the split layout (az_network.mlp_split_bf16x3 makes all
+ * four): d = 160, within every group of 16 hidden units units 4-7 and 8-11 swapped; d = 256,
+ * within every group of 32 slot q holds unit 4 (q >> 3) + (q & 7) if (q & 7) < 4, else
+ * 12 + 4 (q >> 3) + (q & 7);
  * x += (a W2^T + b2); h_out = LN(x).  d = 160 or 256, n_hidden % 32 == 0, n_hidden <= 1024.  Replaces F.linear + GELU + F.linear + add + LayerNorm of
  * rs-doko-py-bridge/python/az_doko.py:87-145 at f32. */
 int dk_net_mlp_ln_f32x3_async(const float* h, float* x_io, const void* w1_hi, const void* w1_lo, const float* b1,

@@ -275,12 +275,22 @@ def _f32c(t):
 
 
 def mlp_split_bf16x3(w1, w2):
-    """The MLP weights in mlp_ln_f32x3_kernel's split layout: bf16 hi / lo pairs (w = hi + lo to
-    ~16 bits) of W1 [n, d] and of W2 [d, n] with W2's columns permuted within every group of 16
-    hidden units (units 4-7 and 8-11 swapped: a lane's GEMM2 fragment becomes one 16-B piece)."""
+    """The MLP weights in the f32 MLP kernels' split layout: bf16 hi / lo pairs (w = hi + lo to
+    ~16 bits) of W1 [n, d] and of W2 [d, n] with W2's columns permuted so that a lane's GEMM2
+    fragment is one 16-B piece in GEMM1's accumulator order:
+      d = 160 (mlp_ln_f32x3_kernel, 32 x 32 tiles): within every group of 16 hidden units,
+        units 4-7 and 8-11 swapped;
+      d = 256 (mlp16_ln_f32x3_kernel, 16 x 16 tiles): within every group of 32, slot q holds unit
+        4 (q >> 3) + (q & 7) if (q & 7) < 4, else 16 + 4 (q >> 3) + (q & 7) - 4."""
     w2 = w2.float()
-    n = w2.shape[1]
-    w2 = w2.reshape(-1, n // 16, 4, 4)[:, :, [0, 2, 1, 3], :].reshape(-1, n)
+    d, n = w2.shape
+    if d == 256:
+        q = torch.arange(32)
+        kg, j = q // 8, q % 8
+        src = torch.where(j < 4, 4 * kg + j, 16 + 4 * kg + j - 4)
+        w2 = w2.reshape(d, n // 32, 32)[:, :, src.to(w2.device)].reshape(d, n)
+    else:
+        w2 = w2.reshape(-1, n // 16, 4, 4)[:, :, [0, 2, 1, 3], :].reshape(-1, n)
     parts = []
     for w in (w1.float(), w2):
         hi = w.bfloat16().contiguous()

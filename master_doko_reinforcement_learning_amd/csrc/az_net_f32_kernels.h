@@ -630,6 +630,197 @@ __global__ void __launch_bounds__(64 * WAVES, D <= 160 ? 8 / WAVES : 1) mlp_ln_f
 }
 
 // ---------------------------------------------------------------------------
+// The MLP half at d = 256 with 16 rows per wave (v_mfma_f32_16x16x32_bf16): the 32-row form
+// holds 128 registers of h fragments and 128 of output accumulators per wave at d = 256, so it
+// runs one wave per SIMD, and each weight-DMA piece a wave issues (~100-185 cycles) idles the
+// SIMD's MFMA pipe.  At 16 rows a wave holds half of each; eight waves x 16 rows = 128 rows per
+// workgroup (the same weight staging per row), two waves per SIMD.
+//   GEMM1 (per 32-hidden chunk, two 16 x 16 tiles): D1 = W1_c h^T; lane (n = row, kg) then holds
+//     hidden 4 kg + j (tile 0) and 16 + 4 kg + j (tile 1), j < 4: bias + GELU + split in place ARE
+//     the B fragment of GEMM2's 32-wide k-step (slot 8 kg + j), given W2's columns in the matching
+//     order: within every 32-hidden group, slot q <- hidden (q & 7) < 4 ? 4 (q >> 3) + (q & 7) :
+//     16 + 4 (q >> 3) + (q & 7) - 4 (az_network.mlp_split_bf16x3 at d = 256).
+//   GEMM2: D2 = W2_c a^T over 16 output tiles of 16 columns.
+// LDS as mlp_ln_f32x3_kernel: W1 chunk piece-major (a fragment read: 16 rows x 4 pieces, distinct
+// bank quads), W2 chunk rows of 4 pieces with piece p at p ^ ((o & 4) >> 1) (conflict-free for the
+// 16 x 16 x 32 A-fragment groups), double-buffered, DMA spread over GEMM1's k-steps.
+template <int D, int NC>
+__global__ void __launch_bounds__(512, 1) mlp16_ln_f32x3_kernel(const float* __restrict__ h, float* __restrict__ x_io,
+                                                              const uint16_t* __restrict__ w1h, const uint16_t* __restrict__ w1l,
+                                                              const float* __restrict__ b1,
+                                                              const uint16_t* __restrict__ w2h, const uint16_t* __restrict__ w2l,
+                                                              const float* __restrict__ b2, uint32_t rows, uint32_t n_hidden,
+                                                              const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                              float eps, float* __restrict__ h_out) {
+    static_assert(D % 32 == 0 && NC == 32, "d: multiple of 32; chunks of 32 hidden units");
+    constexpr int WAVES = 8;
+    constexpr int KS = D / 32, OT = D / 16;                             // 32-wide k-steps, 16-column output tiles
+    constexpr int W1E = NC * D, W2E = D * NC, BUF = 2 * (W1E + W2E);   // one buffer: W1 hi, W1 lo, W2 hi, W2 lo
+    constexpr int Q1 = D / 8, Q2 = NC / 8;                              // 16-B pieces per row
+    constexpr int NP = BUF / 8, NI = NP / 64, NIW = NI / WAVES;         // pieces, wave instructions (per wave)
+    static_assert(NP % 64 == 0 && NI % WAVES == 0 && (NC * Q1) % 64 == 0 && (D * Q2) % 64 == 0, "whole instructions");
+    __shared__ __attribute__((aligned(16))) uint16_t lds0[BUF];
+    __shared__ __attribute__((aligned(16))) uint16_t lds1[BUF];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, n = lane & 15, kg = lane >> 4;
+    const uint32_t row = blockIdx.x * (16u * WAVES) + (uint32_t)wave * 16u + (uint32_t)n;
+    const bool ok = row < rows;
+    // the row's h, split: lane (n, kg) holds k = 32 ks + 8 kg .. + 7 (rows past the end: row 0, never stored)
+    bf16x8_t hfh[KS], hfl[KS];
+    {
+        const float* hr = h + (size_t)(ok ? row : 0u) * D + 8 * kg;
+        float4 va[KS], vb[KS];
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            va[ks] = *(const float4*)(hr + 32 * ks);
+            vb[ks] = *(const float4*)(hr + 32 * ks + 4);
+        }
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            float v[8] = {va[ks].x, va[ks].y, va[ks].z, va[ks].w, vb[ks].x, vb[ks].y, vb[ks].z, vb[ks].w};
+            split_bf16x8(v, hfh[ks], hfl[ks]);
+        }
+    }
+    typedef __attribute__((address_space(3))) void lds_void;
+    // per-lane DMA source offsets: W1 (row lane & 31, piece lane >> 5 of the instruction's pair);
+    // W2 (row lane >> 2 of the instruction's 16, piece lane & 3 swizzled by the row's bit 2)
+    const int dma1 = (lane & 31) * D + 8 * (lane >> 5);
+    const int dma2 = (lane >> 2) * (int)n_hidden + 8 * ((lane & 3) ^ (((lane >> 2) & 4) >> 1));
+    auto stage_one = [&](uint32_t c, uint16_t* dst, int ui) {
+        const int u = wave + WAVES * ui;   // wave-uniform
+        const uint16_t* g;
+        if (u < 2 * (NC * Q1 / 64)) {
+            const int lo = u >= NC * Q1 / 64, v = lo ? u - NC * Q1 / 64 : u;
+            g = (lo ? w1l : w1h) + (size_t)c * NC * D + 16 * v + dma1;
+        } else {
+            const int u2 = u - 2 * (NC * Q1 / 64), lo = u2 >= D * Q2 / 64, v = lo ? u2 - D * Q2 / 64 : u2;
+            g = (lo ? w2l : w2h) + (size_t)(16 * v) * n_hidden + (size_t)c * NC + dma2;
+        }
+        __builtin_amdgcn_global_load_lds(g, (lds_void*)&dst[512 * u], 16, 0, 0);
+    };
+    f32x4_t acc2[OT];
+#pragma unroll
+    for (int t = 0; t < OT; ++t) acc2[t] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
+    const uint32_t chunks = n_hidden / NC;
+#pragma unroll
+    for (int ui = 0; ui < NIW; ++ui) stage_one(0u, lds0, ui);
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    const int sw2 = (n & 4) >> 1;   // W2 piece swizzle of rows 16 t + n
+    auto chunk = [&](uint32_t c, const uint16_t* cur, uint16_t* nxt) {
+        // GEMM1 onto the chunk's biases (scalar loads: lgkmcnt, not behind the DMA), lane kg's four
+        float bb[NC];
+#pragma unroll
+        for (int m = 0; m < NC; ++m) bb[m] = b1[c * NC + m];
+        f32x4_t acc1[2];
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int base = 16 * tt + j;
+                acc1[tt][j] = kg == 0 ? bb[base] : kg == 1 ? bb[base + 4] : kg == 2 ? bb[base + 8] : bb[base + 12];
+            }
+        const uint32_t cn = c + 1 < chunks ? c + 1 : c;
+        // W1 fragment of tile tt, k-step ks: row 16 tt + n, piece 4 ks + kg (piece-major: (p NC + row) x 8)
+        auto w1f = [&](const uint16_t* base, int tt, int ks) {
+            return *(const bf16x8_t*)(base + 8 * ((4 * ks + kg) * NC + 16 * tt + n));
+        };
+        bf16x8_t nh0 = w1f(cur, 0, 0), nl0 = w1f(cur + W1E, 0, 0), nh1 = w1f(cur, 1, 0), nl1 = w1f(cur + W1E, 1, 0);
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            const bf16x8_t ah0 = nh0, al0 = nl0, ah1 = nh1, al1 = nl1;
+            if (ks + 1 < KS) {
+                nh0 = w1f(cur, 0, ks + 1); nl0 = w1f(cur + W1E, 0, ks + 1);
+                nh1 = w1f(cur, 1, ks + 1); nl1 = w1f(cur + W1E, 1, ks + 1);
+            }
+            acc1[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al0, hfh[ks], acc1[0], 0, 0, 0);
+            acc1[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al1, hfh[ks], acc1[1], 0, 0, 0);
+            acc1[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah0, hfl[ks], acc1[0], 0, 0, 0);
+            acc1[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah1, hfl[ks], acc1[1], 0, 0, 0);
+            acc1[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah0, hfh[ks], acc1[0], 0, 0, 0);
+            acc1[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah1, hfh[ks], acc1[1], 0, 0, 0);
+            // the next chunk's DMA, one piece per k-step (issue cost under the MFMAs)
+            __builtin_amdgcn_sched_barrier(0);
+            if (ks < NIW) stage_one(cn, nxt, ks);
+            if (ks == KS - 1)
+#pragma unroll
+                for (int ui = KS; ui < NIW; ++ui) stage_one(cn, nxt, ui);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // GELU (f32) -> the split B fragment of GEMM2's k-step: slots 0..3 tile 0, 4..7 tile 1
+        bf16x8_t afh, afl;
+        {
+            float g[8];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                g[j] = gelu_poly(acc1[0][j]);
+                g[4 + j] = gelu_poly(acc1[1][j]);
+            }
+            split_bf16x8(g, afh, afl);
+        }
+        // GEMM2: D2 += W2_c a^T; W2 fragment of tile t: row 16 t + n, piece kg ^ sw2
+        const uint16_t* a2 = cur + 2 * W1E + n * NC + 8 * (kg ^ sw2);
+        bf16x8_t ph = *(const bf16x8_t*)a2, pl = *(const bf16x8_t*)(a2 + W2E);
+#pragma unroll
+        for (int t = 0; t < OT; ++t) {
+            const bf16x8_t wh = ph, wl = pl;
+            if (t + 1 < OT) {
+                ph = *(const bf16x8_t*)(a2 + 16 * (t + 1) * NC);
+                pl = *(const bf16x8_t*)(a2 + W2E + 16 * (t + 1) * NC);
+            }
+            acc2[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl, afh, acc2[t], 0, 0, 0);
+            acc2[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, afl, acc2[t], 0, 0, 0);
+            acc2[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, afh, acc2[t], 0, 0, 0);
+        }
+        __builtin_amdgcn_s_waitcnt(0);   // this wave's pieces of the next chunk have landed
+        __syncthreads();                 // ... and every wave's; every wave is done with `cur`
+    };
+    for (uint32_t c = 0; c < chunks; c += 2) {
+        chunk(c, lds0, lds1);
+        if (c + 1 < chunks) chunk(c + 1, lds1, lds0);
+    }
+    // epilogue: acc2[t][j] = delta of row `row`, column 16 t + 4 kg + j; x += (delta + b2), then LN
+    // over the row's four lanes (n, n + 16, n + 32, n + 48)
+    float* xr = x_io + (size_t)(ok ? row : 0u) * D;
+    float s1 = 0.0f;
+#pragma unroll
+    for (int t = 0; t < OT; ++t) {
+        const int col = 16 * t + 4 * kg;
+        const float4 xv = *(const float4*)(xr + col);
+        const float4 bv = *(const float4*)(b2 + col);
+        acc2[t][0] = xv.x + (acc2[t][0] + bv.x);
+        acc2[t][1] = xv.y + (acc2[t][1] + bv.y);
+        acc2[t][2] = xv.z + (acc2[t][2] + bv.z);
+        acc2[t][3] = xv.w + (acc2[t][3] + bv.w);
+        s1 += (acc2[t][0] + acc2[t][1]) + (acc2[t][2] + acc2[t][3]);
+    }
+    s1 += __shfl_xor(s1, 16);
+    s1 += __shfl_xor(s1, 32);
+    const float mean = s1 / (float)D;
+    float s2 = 0.0f;
+#pragma unroll
+    for (int t = 0; t < OT; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float dv = acc2[t][j] - mean;
+            s2 += dv * dv;
+        }
+    s2 += __shfl_xor(s2, 16);
+    s2 += __shfl_xor(s2, 32);
+    const float rstd = rsqrtf(s2 / (float)D + eps);
+    float* hr = h_out + (size_t)(ok ? row : 0u) * D;
+    if (ok) {
+#pragma unroll
+        for (int t = 0; t < OT; ++t) {
+            const int col = 16 * t + 4 * kg;
+            const float4 gv = *(const float4*)(gamma + col), bv = *(const float4*)(beta + col);
+            *(float4*)(xr + col) = make_float4(acc2[t][0], acc2[t][1], acc2[t][2], acc2[t][3]);
+            *(float4*)(hr + col) = make_float4((acc2[t][0] - mean) * rstd * gv.x + bv.x, (acc2[t][1] - mean) * rstd * gv.y + bv.y,
+                                               (acc2[t][2] - mean) * rstd * gv.z + bv.z, (acc2[t][3] - mean) * rstd * gv.w + bv.w);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // The whole attention half of a block at the reference's precision (round 5), one 256-thread
 // workgroup per sample (as qkv_attn_ln_kernel at bf16):
 //   Q, K, V = W h^T + b            (head w on wave w; bf16x3 products, f32 accumulators)

@@ -2236,7 +2236,8 @@ int dk_net_mlp_ln_f32x3_async(const float* h, float* x_io, const void* w1_hi, co
                            (const uint16_t*)w1_hi, (const uint16_t*)w1_lo, b1, (const uint16_t*)w2_hi, (const uint16_t*)w2_lo,
                            b2, rows, n_hidden, gamma, beta, eps, h_out);
     else
-        hipLaunchKernelGGL((dk::net::mlp_ln_f32x3_kernel<256, 32, 4>), grid, block, 0, (hipStream_t)stream, h, x_io,
+        // d = 256: 16 rows per wave, eight waves, two per SIMD (mlp16_ln_f32x3_kernel; W2 in its split layout)
+        hipLaunchKernelGGL((dk::net::mlp16_ln_f32x3_kernel<256, 32>), grid, dim3(512u), 0, (hipStream_t)stream, h, x_io,
                            (const uint16_t*)w1_hi, (const uint16_t*)w1_lo, b1, (const uint16_t*)w2_hi, (const uint16_t*)w2_lo,
                            b2, rows, n_hidden, gamma, beta, eps, h_out);
     DK_HIP(hipGetLastError());
