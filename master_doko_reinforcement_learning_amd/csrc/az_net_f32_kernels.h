@@ -847,9 +847,11 @@ __device__ __forceinline__ void head_tiles_x3(const uint16_t* hsh, const uint16_
 #pragma unroll
         for (int si = 0; si < 2; ++si) acc[dt][si] = f32x16_t{0};
     const size_t o0 = (size_t)r * D, o1 = (size_t)(32 + r < HD ? 32 + r : 0) * D;
-    // W fragments one k-step ahead
-    bf16x8_t nw[2][2];
-    auto wfr = [&](int ks) {
+    // W fragments PF k-steps ahead in a register ring (HD = 64, two waves per SIMD: two steps;
+    // HD = 40 keeps one and its third wave per SIMD)
+    constexpr int PF = HD == 64 ? 2 : 1;
+    bf16x8_t ring[PF][2][2];
+    auto wfr = [&](int ks, bf16x8_t (&nw)[2][2]) {
         const int k0 = 16 * ks + 8 * hh;
         nw[0][0] = load_frag8(wh + o0 + k0, true);
         nw[0][1] = load_frag8(wl + o0 + k0, true);
@@ -863,11 +865,13 @@ __device__ __forceinline__ void head_tiles_x3(const uint16_t* hsh, const uint16_
             nw[1][1] = nw[0][1];
         }
     };
-    wfr(0);
+#pragma unroll
+    for (int p = 0; p < PF; ++p) wfr(p, ring[p]);
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
+        auto& nw = ring[ks % PF];
         const bf16x8_t a0h = nw[0][0], a0l = nw[0][1], a1h = nw[1][0], a1l = nw[1][1];
-        if (ks + 1 < NKS) wfr(ks + 1);
+        if (ks + PF < NKS) wfr(ks + PF, nw);
         // (the next k-step's loads stay at the top: left to the scheduler they sank to the end of
         // the step, reusing the current operands' registers, and the next step waited for them)
         __builtin_amdgcn_sched_barrier(0);
