@@ -536,6 +536,11 @@ int dk_net_class_pool_ln_f32_async(const float* x, uint32_t batch, uint32_t d, c
 int dk_net_class_mlp_f32x3_async(const float* pooled, uint32_t batch, uint32_t d, uint32_t classes, const void* w1_hi,
                                  const void* w1_lo, const float* b1, const float* w2, const float* b2, float* out,
                                  void* stream);
+/* dk_net_class_mlp_bf16_async: the bf16 network's class MLPs in one launch: pooled [C, B, d]
+ * (dk_net_class_pool_ln_bf16_async's output) -> out [B, C] bf16 = w2[c] . GELU(W1[c] a + b1[c])
+ * + b2[c] (f32 accumulation, exact erf GELU); w1 [C, d, d], b1 / w2 [C, d], b2 [C] bf16. */
+int dk_net_class_mlp_bf16_async(const void* pooled, uint32_t batch, uint32_t d, uint32_t classes, const void* w1,
+                                const void* b1, const void* w2, const void* b2, void* out, void* stream);
 /* dk_net_class_pool_ln_bf16_async: PerClassAttentionMLPHead's attention pooling and each class
  * MLP's opening LayerNorm (az_doko.py:42-50): x [batch][62][d], queries [classes][d] (classes
  * <= 64), w = softmax(queries x^T * scale) over the 62 tokens, a = w x, out[c][b][:] =

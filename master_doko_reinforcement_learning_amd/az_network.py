@@ -154,9 +154,27 @@ class ClassHead(nn.Module):
                 raise RuntimeError("doko_amd f32 head kernel error %d" % rc)
         return out
 
+    def bf16_fused_ok(self, x):
+        B, S, d = x.shape
+        return (x.is_cuda and x.dtype == torch.bfloat16 and S == SEQ and d in (160, 256) and self.queries.shape[0] <= 64
+                and not torch.is_grad_enabled()
+                and all(p.dtype == torch.bfloat16 and p.is_contiguous() for p in self.parameters()))
+
     def forward(self, x, fused=True):                            # x [B, S, d]
         if fused and self.f32_fused_ok(x):
             return self.forward_f32(x)
+        if fused and self.bf16_fused_ok(x):
+            # pooling + class LayerNorms, then every class's MLP in one launch (class_mlp_bf16_kernel)
+            from . import _native
+            ac = self.pooled(x)
+            B, C = x.shape[0], self.queries.shape[0]
+            out = torch.empty((B, C), dtype=torch.bfloat16, device=x.device)
+            rc = _native.lib().dk_net_class_mlp_bf16_async(ac.data_ptr(), B, x.shape[2], C, self.w1.data_ptr(),
+                                                           self.b1.data_ptr(), self.w2.data_ptr(), self.b2.data_ptr(),
+                                                           out.data_ptr(), torch.cuda.current_stream(x.device).cuda_stream)
+            if rc != 0:
+                raise RuntimeError("doko_amd class MLP kernel error %d" % rc)
+            return out
         ac = self.pooled(x)
         h = F.gelu(torch.bmm(ac, self.w1.transpose(1, 2)) + self.b1[:, None, :])   # [C, B, d]
         return ((h * self.w2[:, None, :]).sum(-1) + self.b2[:, None]).transpose(0, 1)   # [B, C]

@@ -1591,5 +1591,54 @@ __global__ void __launch_bounds__(256, 2) class_mlp_f32x3_kernel(const float* __
     if (ok && hh == 0) out[(size_t)row * classes + c] = part + b2[c];
 }
 
+// The bf16 network's class MLPs in one launch (the bf16 form of class_mlp_f32x3_kernel):
+// out[b][c] = bf16(w2[c] . GELU(W1[c] a[c][b] + b1[c]) + b2[c]), bf16 operands, one product per
+// k-step, f32 accumulation, the exact erf GELU in f32 -- replacing the class-batched bmm, the bias
+// and GELU passes and the w2 product + sum of ClassHead.forward (each rounding to bf16).
+template <int D>
+__global__ void __launch_bounds__(256, 2) class_mlp_bf16_kernel(const uint16_t* __restrict__ ac, uint32_t batch, uint32_t classes,
+                                                                const uint16_t* __restrict__ w1, const uint16_t* __restrict__ b1,
+                                                                const uint16_t* __restrict__ w2, const uint16_t* __restrict__ b2,
+                                                                uint16_t* __restrict__ out) {
+    constexpr int KS = D / 16, OT = D / 32;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
+    const uint32_t c = blockIdx.y;
+    const uint32_t row = blockIdx.x * 128u + (uint32_t)wave * 32u + (uint32_t)r;
+    const bool ok = row < batch;
+    // (unconditional loads: rows past the batch read row 0 and are never stored)
+    bf16x8_t af[KS];
+    const uint16_t* ar = ac + ((size_t)c * batch + (ok ? row : 0u)) * D + 8 * hh;
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) af[kk] = *(const bf16x8_t*)(ar + 16 * kk);
+    const uint16_t* wr = w1 + (size_t)c * D * D + (size_t)r * D + 8 * hh;
+    const uint16_t* b1c = b1 + (size_t)c * D;
+    const uint16_t* w2c = w2 + (size_t)c * D;
+    float part = 0.0f;
+    bf16x8_t nw = *(const bf16x8_t*)wr;
+#pragma unroll 1
+    for (int ot = 0; ot < OT; ++ot) {
+        f32x16_t acc = f32x16_t{0};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            const bf16x8_t a = nw;
+            if (ks + 1 < KS || ot + 1 < OT) {
+                const int o2 = ks + 1 < KS ? 32 * ot * D + 16 * (ks + 1) : 32 * (ot + 1) * D;
+                nw = *(const bf16x8_t*)(wr + o2);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, af[ks], acc, 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+            const int i = 32 * ot + (g & 3) + 8 * (g >> 2) + 4 * hh;
+            const float v = acc[g] + bf2f(b1c[i]);
+            part += 0.5f * v * (1.0f + erff(v * 0.70710678118654752f)) * bf2f(w2c[i]);
+        }
+    }
+    part += __shfl_xor(part, 32);
+    if (ok && hh == 0) out[(size_t)row * classes + c] = f2bf(part + bf2f(b2[c]));
+}
+
 }  // namespace net
 }  // namespace dk

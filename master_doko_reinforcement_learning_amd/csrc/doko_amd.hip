@@ -2282,6 +2282,24 @@ int dk_net_class_pool_ln_f32_async(const float* x, uint32_t batch, uint32_t d, c
     return DK_OK;
 }
 
+int dk_net_class_mlp_bf16_async(const void* pooled, uint32_t batch, uint32_t d, uint32_t classes, const void* w1,
+                                const void* b1, const void* w2, const void* b2, void* out, void* stream) {
+    if (!pooled || !w1 || !b1 || !w2 || !b2 || !out || classes == 0 || classes > 65535u || (d != 160u && d != 256u))
+        return DK_E_INVALID;
+    if (batch == 0) return DK_OK;
+    const dim3 grid((batch + 127u) / 128u, classes);
+    if (d == 160u)
+        hipLaunchKernelGGL((dk::net::class_mlp_bf16_kernel<160>), grid, dim3(256), 0, (hipStream_t)stream,
+                           (const uint16_t*)pooled, batch, classes, (const uint16_t*)w1, (const uint16_t*)b1,
+                           (const uint16_t*)w2, (const uint16_t*)b2, (uint16_t*)out);
+    else
+        hipLaunchKernelGGL((dk::net::class_mlp_bf16_kernel<256>), grid, dim3(256), 0, (hipStream_t)stream,
+                           (const uint16_t*)pooled, batch, classes, (const uint16_t*)w1, (const uint16_t*)b1,
+                           (const uint16_t*)w2, (const uint16_t*)b2, (uint16_t*)out);
+    DK_HIP(hipGetLastError());
+    return DK_OK;
+}
+
 int dk_net_class_mlp_f32x3_async(const float* pooled, uint32_t batch, uint32_t d, uint32_t classes, const void* w1_hi,
                                  const void* w1_lo, const float* b1, const float* w2, const float* b2, float* out,
                                  void* stream) {

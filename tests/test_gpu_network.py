@@ -395,6 +395,32 @@ def test_class_pool_ln_matches_torch(d, C):
     torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=4e-2)
 
 
+@pytest.mark.parametrize("d,C", [(160, 39), (256, 33)])
+def test_class_mlp_bf16_matches_fp32(d, C):
+    """The bf16 class MLPs (class_mlp_bf16_kernel) on the bf16 pooled operand against the same
+    MLPs in fp32 on the same bf16 operands: only the final bf16 rounding apart (B = 300: a
+    partial row block); the whole bf16 head against its torch bf16 form within bf16 noise."""
+    import torch.nn.functional as F
+    from master_doko_reinforcement_learning_amd.az_network import ClassHead
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(6)
+    head = ClassHead(d, C).to(dev).to(torch.bfloat16).eval()
+    x = torch.randn(300, 62, d, device=dev).to(torch.bfloat16)
+    with torch.inference_mode():
+        assert head.bf16_fused_ok(x)
+        got = head(x)
+        tor = head(x, fused=False)
+        ac = head.pooled(x).float()
+        h = F.gelu(torch.bmm(ac, head.w1.float().transpose(1, 2)) + head.b1.float()[:, None, :])
+        ref = ((h * head.w2.float()[:, None, :]).sum(-1) + head.b2.float()[:, None]).transpose(0, 1)
+    assert got.dtype == torch.bfloat16 and got.shape == ref.shape == (300, C)
+    scale = ref.abs().max().item()
+    e = (got.float() - ref).abs().max().item() / scale
+    assert e < 8e-3, e
+    e2 = (got.float() - tor.float()).abs().max().item() / scale
+    assert e2 < 5e-2, e2
+
+
 @pytest.mark.parametrize("d,C", [(160, 39), (160, 4), (256, 33)])
 def test_class_head_f32_matches_torch(d, C):
     """The f32 heads (class_pool_ln_f32x3_kernel + class_mlp_f32x3_kernel, bf16x3 products)
