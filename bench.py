@@ -576,9 +576,9 @@ def net_precision(args, torch):
         return (torch.float32, "f32 network (reference precision: f32 activations, matmul precision 'medium')", 2500.0 / 3,
                 "f32 activations; GEMM products from bf16 pieces (bf16x3: three MFMAs per k-step, ~16-bit "
                 "products, as hipBLASLt's 'medium' f32 GEMMs measured, profiles/r04/fp32_gemm_probe.json): at d = 160 "
-                "every block as two HIP kernels (qkv_attn_ln_f32x3_kernel, mlp_ln_f32x3_kernel) and the heads as two "
-                "(class_pool_ln_f32x3_kernel, class_mlp_f32x3_kernel), no hipBLASLt; at d = 256 the MLP half likewise, "
-                "the attention projections on hipBLASLt at 'medium': peak = bf16 dense / 3")
+                "and d = 256 every block as two HIP kernels (qkv_attn_ln_f32x3_kernel, mlp_ln_f32x3_kernel / "
+                "mlp16_ln_f32x3_kernel) and the heads as two (class_pool_ln_f32x3_kernel, class_mlp_f32x3_kernel), "
+                "no hipBLASLt: peak = bf16 dense / 3")
     return torch.bfloat16, "bf16 network", 2500.0, "bf16 dense peak"
 
 
