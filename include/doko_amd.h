@@ -506,7 +506,7 @@ int dk_net_mlp_ln_bf16_async(const void* h, void* x_io, const void* w1, const vo
  * four): d = 160, within every group of 16 hidden units units 4-7 and 8-11 swapped; d = 256,
  * within every group of 32 slot q holds unit 4 (q >> 3) + (q & 7) if (q & 7) < 4, else
  * 12 + 4 (q >> 3) + (q & 7);
- * x += (a W2^T + b2); h_out = LN(x).  d = 160 or 256, n_hidden % 32 == 0, n_hidden <= 1024.  Replaces F.linear + GELU + F.linear + add + LayerNorm of
+ * x += (a W2^T + b2); h_out = LN(x).  d = 160 or 256, n_hidden % 32 == 0 (d = 256: % 64), n_hidden <= 1024.  Replaces F.linear + GELU + F.linear + add + LayerNorm of
  * rs-doko-py-bridge/python/az_doko.py:87-145 at f32. */
 int dk_net_mlp_ln_f32x3_async(const float* h, float* x_io, const void* w1_hi, const void* w1_lo, const float* b1,
                               const void* w2_hi, const void* w2_lo, const float* b2, uint32_t rows, uint32_t d,

@@ -401,7 +401,7 @@ class FusedTrunkF32(FusedTrunk):
 
     def mlp_ln(self, x, blk, h, ln):
         n = blk.fc.weight.shape[0]
-        if self.d in (160, 256) and n % 32 == 0 and n <= 1024 and blk.fc.bias is not None and blk.proj.bias is not None:
+        if self.d in (160, 256) and n % (64 if self.d == 256 else 32) == 0 and n <= 1024 and blk.fc.bias is not None and blk.proj.bias is not None:
             # the whole MLP half in one kernel, bf16x3 products (mlp_ln_f32x3_kernel)
             w1h, w1l, w2h, w2l = split_bf16x3(blk)
             ho = torch.empty_like(x)

@@ -445,8 +445,25 @@ __global__ void __launch_bounds__(64 * WAVES, D <= 160 ? 8 / WAVES : 1) mlp_ln_f
     // W2 (row lane >> 2 of the instruction's 16, swizzled piece); uniform parts added per call
     const int dma1 = (lane & 31) * D + 8 * (lane >> 5);
     const int dma2 = (lane >> 2) * (int)n_hidden + 8 * ((lane & 3) ^ ((lane >> 4) & 3));
+    constexpr int NIW = NI / WAVES;   // DMA instructions per wave and chunk
+    // Four waves, each matrix a wave's share (d = 160: 10 instructions each): wave m stages all of
+    // matrix m (W1 hi, W1 lo, W2 hi, W2 lo) through ONE buffer resource, with buffer_load ... lds
+    // (MUBUF: vmcnt only).  The FLAT-encoded global_load_lds also counts in lgkmcnt, and while
+    // one is in flight the compiler can only wait lgkmcnt(0) for an LDS read, so a W fragment
+    // read ahead was waited on together with every read issued after it.  (Four resident
+    // resources, one per matrix, pushed the biases' SGPRs into spills.)
+    constexpr bool PER_MATRIX = WAVES == 4 && NC * Q1 / 64 == NIW && D * Q2 / 64 == NIW;
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    const bool w1side = wv < 2;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(wv == 0 ? w1h : wv == 1 ? w1l : wv == 2 ? w2h : w2l), (short)0, (int)(2u * n_hidden * D), 0x00020000);
+    const int dmav = 2 * (w1side ? dma1 : dma2);                                  // bytes
+    const uint32_t cstride = w1side ? 2u * NC * D : 2u * NC, ustride = w1side ? 32u : 32u * n_hidden;
     auto stage_one = [&](uint32_t c, uint16_t* dst, int ui) {
-        {
+        if constexpr (PER_MATRIX) {
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)&dst[512 * (wv * NIW + ui)], 16, dmav,
+                                                     (int)(c * cstride + (uint32_t)ui * ustride), 0, 0);
+        } else {
             const int u = wave + WAVES * ui;   // wave-uniform
             const uint16_t* g;
             if (u < 2 * (NC * Q1 / 64)) {
@@ -459,7 +476,6 @@ __global__ void __launch_bounds__(64 * WAVES, D <= 160 ? 8 / WAVES : 1) mlp_ln_f
             __builtin_amdgcn_global_load_lds(g, (lds_void*)&dst[512 * u], 16, 0, 0);
         }
     };
-    constexpr int NIW = NI / WAVES;   // DMA instructions per wave and chunk
 #ifndef DK_MLPF32_DMA_STEP
 #define DK_MLPF32_DMA_STEP 1
 #endif
@@ -509,6 +525,7 @@ __global__ void __launch_bounds__(64 * WAVES, D <= 160 ? 8 / WAVES : 1) mlp_ln_f
         for (int kk = 0; kk < KS; ++kk) {
             const bf16x8_t ah = nh, al = nl;
             if (kk + 1 < KS) { nh = w1f(a1, kk + 1); nl = w1f(a1 + W1E, kk + 1); }
+            if (PER_MATRIX) __builtin_amdgcn_sched_barrier(0);   // the next reads stay a k-step ahead
 #ifndef DK_SOL_NOGEMM1
             acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, hfh[kk], acc1, 0, 0, 0);
             acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, hfl[kk], acc1, 0, 0, 0);
@@ -558,6 +575,7 @@ __global__ void __launch_bounds__(64 * WAVES, D <= 160 ? 8 / WAVES : 1) mlp_ln_f
             const int s2 = q / OT, t = q % OT;
             const bf16x8_t wh = ph, wl = pl;
             if (q + 1 < GS * OT) { ph = w2f(a2h, q + 1); pl = w2f(a2l, q + 1); }
+            if (PER_MATRIX) __builtin_amdgcn_sched_barrier(0);   // (a tile ahead)
 #ifndef DK_SOL_NOGEMM2
             acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl, afh[s2], acc2[t], 0, 0, 0);
             acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, afl[s2], acc2[t], 0, 0, 0);
@@ -667,7 +685,11 @@ __global__ void __launch_bounds__(512, 1) mlp16_ln_f32x3_kernel(const float* __r
     // the row's h, split: lane (n, kg) holds k = 32 ks + 8 kg .. + 7 (rows past the end: row 0, never stored)
     bf16x8_t hfh[KS], hfl[KS];
     {
+#ifdef DK_SOL_NOIO
+        const float* hr = h + 8 * kg;   // (measurement build: every row reads row 0, no HBM)
+#else
         const float* hr = h + (size_t)(ok ? row : 0u) * D + 8 * kg;
+#endif
         float4 va[KS], vb[KS];
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
@@ -681,22 +703,41 @@ __global__ void __launch_bounds__(512, 1) mlp16_ln_f32x3_kernel(const float* __r
         }
     }
     typedef __attribute__((address_space(3))) void lds_void;
-    // per-lane DMA source offsets: W1 (row lane & 31, piece lane >> 5 of the instruction's pair);
-    // W2 (row lane >> 2 of the instruction's 16, piece lane & 3 swizzled by the row's bit 2)
-    const int dma1 = (lane & 31) * D + 8 * (lane >> 5);
-    const int dma2 = (lane >> 2) * (int)n_hidden + 8 * ((lane & 3) ^ (((lane >> 2) & 4) >> 1));
+    // per-lane DMA source offsets (bytes): W1 (row lane & 31, piece lane >> 5 of the instruction's
+    // pair); W2 (row lane >> 2 of the instruction's 16, piece lane & 3 swizzled by the row's bit 2)
+    const int dma1 = 2 * ((lane & 31) * D + 8 * (lane >> 5));
+    const int dma2 = 2 * ((lane >> 2) * (int)n_hidden + 8 * ((lane & 3) ^ (((lane >> 2) & 4) >> 1)));
+    // The DMA goes through buffer_load ... lds (MUBUF: vmcnt only).  The FLAT-encoded
+    // global_load_lds also counts in lgkmcnt, and while one is in flight the compiler can only
+    // wait lgkmcnt(0) for an LDS read: every W fragment read then waited on the reads issued
+    // after it, the whole point of reading ahead lost.
+    const uint32_t wb1 = 2u * NC * D, wbytes = 2u * n_hidden * D;   // bytes: one chunk of W1, all of W1 / W2
+    const __amdgpu_buffer_rsrc_t r1h = __builtin_amdgcn_make_buffer_rsrc((void*)w1h, (short)0, (int)wbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t r1l = __builtin_amdgcn_make_buffer_rsrc((void*)w1l, (short)0, (int)wbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t r2h = __builtin_amdgcn_make_buffer_rsrc((void*)w2h, (short)0, (int)wbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t r2l = __builtin_amdgcn_make_buffer_rsrc((void*)w2l, (short)0, (int)wbytes, 0x00020000);
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    // instruction u = wv + WAVES ui: which matrix it stages depends on ui alone (each matrix is a
+    // whole number of WAVES-instruction rounds), so after unrolling every branch below is static
+    constexpr int N1 = NC * Q1 / 64, N2 = D * Q2 / 64;
+    static_assert(N1 % WAVES == 0 && N2 % WAVES == 0, "matrix boundaries on instruction rounds");
     auto stage_one = [&](uint32_t c, uint16_t* dst, int ui) {
-        const int u = wave + WAVES * ui;   // wave-uniform
-        const uint16_t* g;
-        if (u < 2 * (NC * Q1 / 64)) {
-            const int lo = u >= NC * Q1 / 64, v = lo ? u - NC * Q1 / 64 : u;
-            g = (lo ? w1l : w1h) + (size_t)c * NC * D + 16 * v + dma1;
+        const int u = wv + WAVES * ui;   // wave-uniform (SGPR)
+        if (WAVES * ui < 2 * N1) {
+            const bool lo = WAVES * ui >= N1;
+            const int v = lo ? u - N1 : u;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(lo ? r1l : r1h, (lds_void*)&dst[512 * u], 16, dma1,
+                                                     (int)(c * wb1 + 32u * v), 0, 0);
         } else {
-            const int u2 = u - 2 * (NC * Q1 / 64), lo = u2 >= D * Q2 / 64, v = lo ? u2 - D * Q2 / 64 : u2;
-            g = (lo ? w2l : w2h) + (size_t)(16 * v) * n_hidden + (size_t)c * NC + dma2;
+            const bool lo = WAVES * ui >= 2 * N1 + N2;
+            const int v = u - 2 * N1 - (lo ? N2 : 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(lo ? r2l : r2h, (lds_void*)&dst[512 * u], 16, dma2,
+                                                     (int)(32u * v * n_hidden + 2u * c * NC), 0, 0);
         }
-        __builtin_amdgcn_global_load_lds(g, (lds_void*)&dst[512 * u], 16, 0, 0);
     };
+    // GEMM1's biases for this lane (hidden 16 tt + 4 kg + j of the chunk), read a chunk ahead
+    // during GEMM2, after the chunk's DMA has been issued (vmcnt retires in order)
+    float4 bn0 = *(const float4*)(b1 + 4 * kg), bn1 = *(const float4*)(b1 + 16 + 4 * kg);
     f32x4_t acc2[OT];
 #pragma unroll
     for (int t = 0; t < OT; ++t) acc2[t] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
@@ -706,19 +747,18 @@ __global__ void __launch_bounds__(512, 1) mlp16_ln_f32x3_kernel(const float* __r
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
     const int sw2 = (n & 4) >> 1;   // W2 piece swizzle of rows 16 t + n
-    auto chunk = [&](uint32_t c, const uint16_t* cur, uint16_t* nxt) {
-        // GEMM1 onto the chunk's biases (scalar loads: lgkmcnt, not behind the DMA), lane kg's four
-        float bb[NC];
-#pragma unroll
-        for (int m = 0; m < NC; ++m) bb[m] = b1[c * NC + m];
-        f32x4_t acc1[2];
-#pragma unroll
-        for (int tt = 0; tt < 2; ++tt)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int base = 16 * tt + j;
-                acc1[tt][j] = kg == 0 ? bb[base] : kg == 1 ? bb[base + 4] : kg == 2 ? bb[base + 8] : bb[base + 12];
-            }
+    // the residual rows of the epilogue: loaded in the last chunk, after its GEMM1 (the h
+    // fragments' registers are free then), in flight under its GELU and GEMM2
+    float4 xpre[OT];
+#ifdef DK_SOL_NOIO
+    float* xr = x_io;
+#else
+    float* xr = x_io + (size_t)(ok ? row : 0u) * D;
+#endif
+    auto chunk = [&](uint32_t c, const uint16_t* cur, uint16_t* nxt, auto last) {
+        constexpr bool LAST = decltype(last)::value;
+        // GEMM1 onto the chunk's biases
+        f32x4_t acc1[2] = {f32x4_t{bn0.x, bn0.y, bn0.z, bn0.w}, f32x4_t{bn1.x, bn1.y, bn1.z, bn1.w}};
         const uint32_t cn = c + 1 < chunks ? c + 1 : c;
         // W1 fragment of tile tt, k-step ks: row 16 tt + n, piece 4 ks + kg (piece-major: (p NC + row) x 8)
         auto w1f = [&](const uint16_t* base, int tt, int ks) {
@@ -732,20 +772,45 @@ __global__ void __launch_bounds__(512, 1) mlp16_ln_f32x3_kernel(const float* __r
                 nh0 = w1f(cur, 0, ks + 1); nl0 = w1f(cur + W1E, 0, ks + 1);
                 nh1 = w1f(cur, 1, ks + 1); nl1 = w1f(cur + W1E, 1, ks + 1);
             }
+            __builtin_amdgcn_sched_barrier(0);   // the next k-step's reads stay a whole k-step ahead
+#ifndef DK_SOL_NOGEMM1
             acc1[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al0, hfh[ks], acc1[0], 0, 0, 0);
             acc1[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al1, hfh[ks], acc1[1], 0, 0, 0);
             acc1[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah0, hfl[ks], acc1[0], 0, 0, 0);
             acc1[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah1, hfl[ks], acc1[1], 0, 0, 0);
             acc1[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah0, hfh[ks], acc1[0], 0, 0, 0);
             acc1[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah1, hfh[ks], acc1[1], 0, 0, 0);
+#else
+            acc1[0][ks & 3] += (float)ah0[0] + (float)al0[1] + (float)ah1[2] + (float)al1[3];
+#endif
             // the next chunk's DMA, one piece per k-step (issue cost under the MFMAs)
             __builtin_amdgcn_sched_barrier(0);
-            if (ks < NIW) stage_one(cn, nxt, ks);
-            if (ks == KS - 1)
+#ifndef DK_SOL_NODMA
+            if (!LAST) {
+                if (ks < NIW) stage_one(cn, nxt, ks);
+                if (ks == KS - 1)
 #pragma unroll
-                for (int ui = KS; ui < NIW; ++ui) stage_one(cn, nxt, ui);
+                    for (int ui = KS; ui < NIW; ++ui) stage_one(cn, nxt, ui);
+            }
+#endif
             __builtin_amdgcn_sched_barrier(0);
         }
+        // GEMM2's W2 fragments ride a ring two tiles deep (tile t: row 16 t + n, piece kg ^ sw2);
+        // the first two are read before the GELU so its VALU work covers their latency, and the
+        // sched_barriers keep each read two tiles ahead of its MFMAs (left to itself the compiler
+        // moved every read next to its use behind an lgkmcnt(0))
+        const uint16_t* a2 = cur + 2 * W1E + n * NC + 8 * (kg ^ sw2);
+        bf16x8_t rh[3], rl[3];
+        rh[0] = *(const bf16x8_t*)a2; rl[0] = *(const bf16x8_t*)(a2 + W2E);
+        rh[1] = *(const bf16x8_t*)(a2 + 16 * NC); rl[1] = *(const bf16x8_t*)(a2 + W2E + 16 * NC);
+        if (!LAST) {
+            bn0 = *(const float4*)(b1 + cn * NC + 4 * kg);
+            bn1 = *(const float4*)(b1 + cn * NC + 16 + 4 * kg);
+        } else {
+#pragma unroll
+            for (int t = 0; t < OT; ++t) xpre[t] = *(const float4*)(xr + 16 * t + 4 * kg);
+        }
+        __builtin_amdgcn_sched_barrier(0);
         // GELU (f32) -> the split B fragment of GEMM2's k-step: slots 0..3 tile 0, 4..7 tile 1
         bf16x8_t afh, afl;
         {
@@ -757,35 +822,46 @@ __global__ void __launch_bounds__(512, 1) mlp16_ln_f32x3_kernel(const float* __r
             }
             split_bf16x8(g, afh, afl);
         }
-        // GEMM2: D2 += W2_c a^T; W2 fragment of tile t: row 16 t + n, piece kg ^ sw2
-        const uint16_t* a2 = cur + 2 * W1E + n * NC + 8 * (kg ^ sw2);
-        bf16x8_t ph = *(const bf16x8_t*)a2, pl = *(const bf16x8_t*)(a2 + W2E);
+        __builtin_amdgcn_sched_barrier(0);
+        // GEMM2: D2 += W2_c a^T
 #pragma unroll
         for (int t = 0; t < OT; ++t) {
-            const bf16x8_t wh = ph, wl = pl;
-            if (t + 1 < OT) {
-                ph = *(const bf16x8_t*)(a2 + 16 * (t + 1) * NC);
-                pl = *(const bf16x8_t*)(a2 + W2E + 16 * (t + 1) * NC);
+            if (t + 2 < OT) {
+                rh[(t + 2) % 3] = *(const bf16x8_t*)(a2 + 16 * (t + 2) * NC);
+                rl[(t + 2) % 3] = *(const bf16x8_t*)(a2 + W2E + 16 * (t + 2) * NC);
             }
+            __builtin_amdgcn_sched_barrier(0);
+            const bf16x8_t wh = rh[t % 3], wl = rl[t % 3];
+#ifndef DK_SOL_NOGEMM2
             acc2[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl, afh, acc2[t], 0, 0, 0);
             acc2[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, afl, acc2[t], 0, 0, 0);
             acc2[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, afh, acc2[t], 0, 0, 0);
+#else
+            acc2[t][0] += (float)wh[0] + (float)wl[1] + (float)afh[2] + (float)afl[3];
+#endif
+            __builtin_amdgcn_sched_barrier(0);
         }
-        __builtin_amdgcn_s_waitcnt(0);   // this wave's pieces of the next chunk have landed
-        __syncthreads();                 // ... and every wave's; every wave is done with `cur`
+#ifndef DK_SOL_NOBAR
+        if (!LAST) {
+            __builtin_amdgcn_s_waitcnt(0);   // this wave's pieces of the next chunk have landed
+            __syncthreads();                 // ... and every wave's; every wave is done with `cur`
+        }
+#endif
     };
-    for (uint32_t c = 0; c < chunks; c += 2) {
-        chunk(c, lds0, lds1);
-        if (c + 1 < chunks) chunk(c + 1, lds1, lds0);
+    // (an even chunk count, checked on the host: the last chunk, peeled, computes from lds1)
+    for (uint32_t c = 0; c + 2 < chunks; c += 2) {
+        chunk(c, lds0, lds1, std::false_type{});
+        chunk(c + 1, lds1, lds0, std::false_type{});
     }
+    chunk(chunks - 2, lds0, lds1, std::false_type{});
+    chunk(chunks - 1, lds1, lds0, std::true_type{});
     // epilogue: acc2[t][j] = delta of row `row`, column 16 t + 4 kg + j; x += (delta + b2), then LN
     // over the row's four lanes (n, n + 16, n + 32, n + 48)
-    float* xr = x_io + (size_t)(ok ? row : 0u) * D;
     float s1 = 0.0f;
 #pragma unroll
     for (int t = 0; t < OT; ++t) {
         const int col = 16 * t + 4 * kg;
-        const float4 xv = *(const float4*)(xr + col);
+        const float4 xv = xpre[t];
         const float4 bv = *(const float4*)(b2 + col);
         acc2[t][0] = xv.x + (acc2[t][0] + bv.x);
         acc2[t][1] = xv.y + (acc2[t][1] + bv.y);
@@ -808,7 +884,11 @@ __global__ void __launch_bounds__(512, 1) mlp16_ln_f32x3_kernel(const float* __r
     s2 += __shfl_xor(s2, 32);
     const float rstd = rsqrtf(s2 / (float)D + eps);
     float* hr = h_out + (size_t)(ok ? row : 0u) * D;
+#ifdef DK_SOL_NOIO
+    if (ok && (rows >> 31)) {
+#else
     if (ok) {
+#endif
 #pragma unroll
         for (int t = 0; t < OT; ++t) {
             const int col = 16 * t + 4 * kg;
@@ -849,7 +929,10 @@ __device__ __forceinline__ void head_tiles_x3(const uint16_t* hsh, const uint16_
     const size_t o0 = (size_t)r * D, o1 = (size_t)(32 + r < HD ? 32 + r : 0) * D;
     // W fragments PF k-steps ahead in a register ring (HD = 64, two waves per SIMD: two steps;
     // HD = 40 keeps one and its third wave per SIMD)
-    constexpr int PF = HD == 64 ? 2 : 1;
+#ifndef DK_ATTN_PF64
+#define DK_ATTN_PF64 2
+#endif
+    constexpr int PF = HD == 64 ? DK_ATTN_PF64 : 1;
     bf16x8_t ring[PF][2][2];
     auto wfr = [&](int ks, bf16x8_t (&nw)[2][2]) {
         const int k0 = 16 * ks + 8 * hh;

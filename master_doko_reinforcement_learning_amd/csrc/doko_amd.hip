@@ -2215,7 +2215,8 @@ int dk_net_mlp_ln_f32x3_async(const float* h, float* x_io, const void* w1_hi, co
                               uint32_t n_hidden, const float* gamma, const float* beta, float eps, float* h_out,
                               void* stream) {
     if (!h || !x_io || !w1_hi || !w1_lo || !b1 || !w2_hi || !w2_lo || !b2 || !gamma || !beta || !h_out ||
-        (d != 160u && d != 256u) || n_hidden == 0 || n_hidden > dk::net::MLP_MAX_HIDDEN || n_hidden % 32u)
+        (d != 160u && d != 256u) || n_hidden == 0 || n_hidden > dk::net::MLP_MAX_HIDDEN || n_hidden % 32u ||
+        (d == 256u && n_hidden % 64u))   // (d = 256: an even number of 32-unit chunks)
         return DK_E_INVALID;
     if (rows == 0) return DK_OK;
     // 4 waves x 32 rows per workgroup, double-buffered weight chunks: two workgroups per CU at

@@ -1,7 +1,7 @@
 """The f32 attention half of a block: qkv_attn_ln_f32x3_kernel (one pass per sample, bf16x3
 products) against the unfused f32 path (hipBLASLt qkv F.linear at matmul precision "medium" +
 attn62_bias_f32 (f32 MFMA) + F.linear of the folded projection + add_bias_ln_f32), alternated.
-usage: python tools/attn_f32x3_bench.py [samples] [reps]"""
+usage: python tools/attn_f32x3_bench.py [samples] [reps] [d]  (d = 160 or 256, four heads)"""
 import os
 import sys
 
@@ -12,12 +12,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def main(B=8192, reps=20):
+def main(B=8192, reps=20, d=160):
     from master_doko_reinforcement_learning_amd import _native
     L = _native.lib()
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
-    d, H, hd = 160, 4, 40
+    H = 4
+    hd = d // H
     h = torch.randn(B, 62, d, device=dev)
     x = torch.randn(B, 62, d, device=dev)
     wq, bq = torch.randn(3 * d, d, device=dev) / d ** 0.5, torch.randn(3 * d, device=dev) * 0.1
