@@ -116,6 +116,10 @@ def lib():
                                                      vp, vp]),
         "dk_net_qkv_attn_ln_f32x3_async": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, u32, u32, u32, vp, vp,
                                                           ctypes.c_float, vp, vp]),
+        "dk_net_qkv_attn_ln_f32x3_ex_async": (ctypes.c_int, [vp, vp, vp, vp, ctypes.c_float, vp, vp, vp, vp, vp, vp, u32, u32,
+                                                             u32, vp, vp, ctypes.c_float, vp, vp]),
+        "dk_net_mlp_ln_f32x3_ex_async": (ctypes.c_int, [vp, vp, vp, vp, ctypes.c_float, vp, vp, vp, vp, vp, vp, u32, u32, u32,
+                                                        vp, vp, ctypes.c_float, vp, vp]),
         "dk_net_class_pool_ln_f32_async": (ctypes.c_int, [vp, u32, u32, vp, u32, ctypes.c_float, vp, vp, ctypes.c_float,
                                                           vp, vp]),
         "dk_net_class_mlp_f32x3_async": (ctypes.c_int, [vp, u32, u32, u32, vp, vp, vp, vp, vp, vp, vp]),
@@ -149,7 +153,7 @@ EXPORTED = [
     "dk_pool_bytes", "dk_legal_actions_async", "dk_env_step_batch_async", "dk_env_random_plies_batch_async",
     "dk_az_begin_async", "dk_az_root_async", "dk_az_rng_async", "dk_az_select_async", "dk_az_backup_async", "dk_az_finish_async",
     "dk_az_records_async", "dk_az_step_async", "dk_az_encode_async", "dk_net_embed_ln_bf16_async",
-    "dk_net_add_ln_bf16_async", "dk_net_attn62_bf16_async", "dk_net_fc_gelu_bf16_async", "dk_net_mlp_ln_bf16_async", "dk_net_mlp_ln_f32x3_async", "dk_net_qkv_attn_ln_f32x3_async", "dk_net_class_pool_ln_f32_async", "dk_net_class_mlp_f32x3_async", "dk_net_class_mlp_bf16_async", "dk_net_attn_ln_bf16_async", "dk_net_qkv_attn_ln_bf16_async", "dk_net_class_pool_ln_bf16_async",
+    "dk_net_add_ln_bf16_async", "dk_net_attn62_bf16_async", "dk_net_fc_gelu_bf16_async", "dk_net_mlp_ln_bf16_async", "dk_net_mlp_ln_f32x3_async", "dk_net_qkv_attn_ln_f32x3_async", "dk_net_qkv_attn_ln_f32x3_ex_async", "dk_net_mlp_ln_f32x3_ex_async", "dk_net_class_pool_ln_f32_async", "dk_net_class_mlp_f32x3_async", "dk_net_class_mlp_bf16_async", "dk_net_attn_ln_bf16_async", "dk_net_qkv_attn_ln_bf16_async", "dk_net_class_pool_ln_bf16_async",
     "dk_net_embed_ln_f32_async", "dk_net_add_ln_f32_async", "dk_net_attn62_f32_async", "dk_net_gelu_f32_async", "dk_net_add_bias_ln_f32_async", "dk_net_gelu_bias_f32_async", "dk_net_attn62_bias_f32_async", "dk_ar_begin_async", "dk_ar_guesses_async", "dk_ar_prepare_async",
     "dk_ar_choose_async", "dk_ar_output_async", "dk_ar_fallback_async", "dk_fuse_accumulate_masked_async",
     "dk_fdo_from_fields", "dk_fdo_to_fields", "dk_do_from_fields", "dk_do_to_fields", "dk_is_consistent_batch",

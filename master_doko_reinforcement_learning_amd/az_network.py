@@ -399,6 +399,38 @@ class FusedTrunkF32(FusedTrunk):
         w, b = blk.folded_proj()
         return self.add_ln(x, _f32c(F.linear(y, w)), ln, b)
 
+    def run(self, h, blocks, final_ln, x=None):
+        if not (self.d == 256 and len(blocks) > 0 and all(self.ex_ok(blk) for blk in blocks)):
+            return super().run(h, blocks, final_ln, x)
+        # d = 256: every half after the first reads the residual stream x and applies the
+        # LayerNorm its producer used to write out as h (the *_ex kernels); only the last half
+        # writes h (the final LayerNorm, for the heads).  Per half, x in and out instead of h in,
+        # x in and out, h out.
+        x = self.x if x is None else x
+        for i, blk in enumerate(blocks):
+            wqh, wql, wph, wpl, bpf = split_attn_bf16x3(blk)
+            lin = None if i == 0 else blk.ln_1
+            self.ck(self.L.dk_net_qkv_attn_ln_f32x3_ex_async(
+                h.data_ptr() if i == 0 else None, x.data_ptr(), lin.weight.data_ptr() if lin else None,
+                lin.bias.data_ptr() if lin else None, lin.eps if lin else 0.0, wqh.data_ptr(), wql.data_ptr(),
+                blk.qkv.bias.data_ptr(), wph.data_ptr(), wpl.data_ptr(), bpf.data_ptr(), x.shape[0], 4, 64, None, None,
+                0.0, None, self.st))
+            last = i + 1 == len(blocks)
+            w1h, w1l, w2h, w2l = split_bf16x3(blk)
+            ho = torch.empty_like(x) if last else None
+            self.ck(self.L.dk_net_mlp_ln_f32x3_ex_async(
+                None, x.data_ptr(), blk.ln_2.weight.data_ptr(), blk.ln_2.bias.data_ptr(), blk.ln_2.eps, w1h.data_ptr(),
+                w1l.data_ptr(), blk.fc.bias.data_ptr(), w2h.data_ptr(), w2l.data_ptr(), blk.proj.bias.data_ptr(), self.rows,
+                self.d, blk.fc.weight.shape[0], final_ln.weight.data_ptr() if last else None,
+                final_ln.bias.data_ptr() if last else None, final_ln.eps if last else 0.0,
+                ho.data_ptr() if last else None, self.st))
+        return ho
+
+    def ex_ok(self, blk):
+        n = blk.fc.weight.shape[0]
+        return (blk.heads == 4 and blk.qkv.bias is not None and n % 64 == 0 and n <= 1024 and blk.fc.bias is not None
+                and blk.proj.bias is not None and blk.ln_1.weight is not None and blk.ln_2.weight is not None)
+
     def mlp_ln(self, x, blk, h, ln):
         n = blk.fc.weight.shape[0]
         if self.d in (160, 256) and n % (64 if self.d == 256 else 32) == 0 and n <= 1024 and blk.fc.bias is not None and blk.proj.bias is not None:

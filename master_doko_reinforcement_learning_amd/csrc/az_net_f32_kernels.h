@@ -662,14 +662,19 @@ __global__ void __launch_bounds__(64 * WAVES, D <= 160 ? 8 / WAVES : 1) mlp_ln_f
 // LDS as mlp_ln_f32x3_kernel: W1 chunk piece-major (a fragment read: 16 rows x 4 pieces, distinct
 // bank quads), W2 chunk rows of 4 pieces with piece p at p ^ ((o & 4) >> 1) (conflict-free for the
 // 16 x 16 x 32 A-fragment groups), double-buffered, DMA spread over GEMM1's k-steps.
-template <int D, int NC>
+// XIN: the input is the residual stream itself (h == nullptr), normalised here with the
+// LayerNorm (gin, bin, eps_in) that its producer no longer applies; h_out == nullptr: x only is
+// written (the next half normalises it) -- two of the four row-sized HBM transfers per half gone.
+template <int D, int NC, bool XIN = false>
 __global__ void __launch_bounds__(512, 1) mlp16_ln_f32x3_kernel(const float* __restrict__ h, float* __restrict__ x_io,
                                                               const uint16_t* __restrict__ w1h, const uint16_t* __restrict__ w1l,
                                                               const float* __restrict__ b1,
                                                               const uint16_t* __restrict__ w2h, const uint16_t* __restrict__ w2l,
                                                               const float* __restrict__ b2, uint32_t rows, uint32_t n_hidden,
                                                               const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                              float eps, float* __restrict__ h_out) {
+                                                              float eps, float* __restrict__ h_out,
+                                                              const float* __restrict__ gin = nullptr,
+                                                              const float* __restrict__ bin = nullptr, float eps_in = 0.0f) {
     static_assert(D % 32 == 0 && NC == 32, "d: multiple of 32; chunks of 32 hidden units");
     constexpr int WAVES = 8;
     constexpr int KS = D / 32, OT = D / 16;                             // 32-wide k-steps, 16-column output tiles
@@ -686,9 +691,9 @@ __global__ void __launch_bounds__(512, 1) mlp16_ln_f32x3_kernel(const float* __r
     bf16x8_t hfh[KS], hfl[KS];
     {
 #ifdef DK_SOL_NOIO
-        const float* hr = h + 8 * kg;   // (measurement build: every row reads row 0, no HBM)
+        const float* hr = (XIN ? x_io : h) + 8 * kg;   // (measurement build: every row reads row 0, no HBM)
 #else
-        const float* hr = h + (size_t)(ok ? row : 0u) * D + 8 * kg;
+        const float* hr = (XIN ? x_io : h) + (size_t)(ok ? row : 0u) * D + 8 * kg;
 #endif
         float4 va[KS], vb[KS];
 #pragma unroll
@@ -696,9 +701,38 @@ __global__ void __launch_bounds__(512, 1) mlp16_ln_f32x3_kernel(const float* __r
             va[ks] = *(const float4*)(hr + 32 * ks);
             vb[ks] = *(const float4*)(hr + 32 * ks + 4);
         }
+        float mu = 0.0f, rs = 1.0f;
+        if constexpr (XIN) {
+            // the row's LayerNorm over its four lanes (n, n + 16, n + 32, n + 48): two-pass
+            float s1 = 0.0f;
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) s1 += ((va[ks].x + va[ks].y) + (va[ks].z + va[ks].w)) + ((vb[ks].x + vb[ks].y) + (vb[ks].z + vb[ks].w));
+            s1 += __shfl_xor(s1, 16);
+            s1 += __shfl_xor(s1, 32);
+            mu = s1 / (float)D;
+            float s2 = 0.0f;
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                const float a0 = va[ks].x - mu, a1 = va[ks].y - mu, a2 = va[ks].z - mu, a3 = va[ks].w - mu;
+                const float c0 = vb[ks].x - mu, c1 = vb[ks].y - mu, c2 = vb[ks].z - mu, c3 = vb[ks].w - mu;
+                s2 += ((a0 * a0 + a1 * a1) + (a2 * a2 + a3 * a3)) + ((c0 * c0 + c1 * c1) + (c2 * c2 + c3 * c3));
+            }
+            s2 += __shfl_xor(s2, 16);
+            s2 += __shfl_xor(s2, 32);
+            rs = rsqrtf(s2 / (float)D + eps_in);
+        }
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
             float v[8] = {va[ks].x, va[ks].y, va[ks].z, va[ks].w, vb[ks].x, vb[ks].y, vb[ks].z, vb[ks].w};
+            if constexpr (XIN) {
+                const int c0 = 32 * ks + 8 * kg;
+                const float4 g0 = *(const float4*)(gin + c0), g1 = *(const float4*)(gin + c0 + 4);
+                const float4 e0 = *(const float4*)(bin + c0), e1 = *(const float4*)(bin + c0 + 4);
+                const float g[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+                const float be[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[j] = (v[j] - mu) * rs * g[j] + be[j];
+            }
             split_bf16x8(v, hfh[ks], hfl[ks]);
         }
     }
@@ -884,6 +918,7 @@ __global__ void __launch_bounds__(512, 1) mlp16_ln_f32x3_kernel(const float* __r
     s2 += __shfl_xor(s2, 32);
     const float rstd = rsqrtf(s2 / (float)D + eps);
     float* hr = h_out + (size_t)(ok ? row : 0u) * D;
+    const bool wh = h_out != nullptr;   // (uniform)
 #ifdef DK_SOL_NOIO
     if (ok && (rows >> 31)) {
 #else
@@ -892,10 +927,12 @@ __global__ void __launch_bounds__(512, 1) mlp16_ln_f32x3_kernel(const float* __r
 #pragma unroll
         for (int t = 0; t < OT; ++t) {
             const int col = 16 * t + 4 * kg;
-            const float4 gv = *(const float4*)(gamma + col), bv = *(const float4*)(beta + col);
             *(float4*)(xr + col) = make_float4(acc2[t][0], acc2[t][1], acc2[t][2], acc2[t][3]);
-            *(float4*)(hr + col) = make_float4((acc2[t][0] - mean) * rstd * gv.x + bv.x, (acc2[t][1] - mean) * rstd * gv.y + bv.y,
-                                               (acc2[t][2] - mean) * rstd * gv.z + bv.z, (acc2[t][3] - mean) * rstd * gv.w + bv.w);
+            if (wh) {
+                const float4 gv = *(const float4*)(gamma + col), bv = *(const float4*)(beta + col);
+                *(float4*)(hr + col) = make_float4((acc2[t][0] - mean) * rstd * gv.x + bv.x, (acc2[t][1] - mean) * rstd * gv.y + bv.y,
+                                                   (acc2[t][2] - mean) * rstd * gv.z + bv.z, (acc2[t][3] - mean) * rstd * gv.w + bv.w);
+            }
         }
     }
 }
@@ -1054,14 +1091,18 @@ __device__ __forceinline__ void split_head(const f32x16_t (&acc)[2][2], bf16x8_t
         }
 }
 
-template <int HD>
+// XIN (as mlp16_ln_f32x3_kernel): the sample's rows come from x_io (h_in unused) and are
+// normalised here with (gin, bin, eps_in); h_out == nullptr: x only is written.
+template <int HD, bool XIN = false>
 __global__ void __launch_bounds__(256, HD == 40 ? 3 : 2) qkv_attn_ln_f32x3_kernel(const float* __restrict__ h_in, float* __restrict__ x_io,
                                                                    const uint16_t* __restrict__ wqh, const uint16_t* __restrict__ wql,
                                                                    const float* __restrict__ bqkv,
                                                                    const uint16_t* __restrict__ wph, const uint16_t* __restrict__ wpl,
                                                                    const float* __restrict__ bp, float scale,
                                                                    const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                                   float eps, float* __restrict__ h_out) {
+                                                                   float eps, float* __restrict__ h_out,
+                                                                   const float* __restrict__ gin = nullptr,
+                                                                   const float* __restrict__ bin = nullptr, float eps_in = 0.0f) {
     constexpr int S = 62, D = HD * 4, LDY = D + 8, LDT = 64 + 4, KS = (HD + 15) / 16, LDX = D + 4;
     constexpr bool TAIL3 = HD == 40;                       // the three projections' dims 32..39 in one tile
     constexpr bool PERDT = HD == 64;                       // Q / K one 32-dim tile at a time
@@ -1075,7 +1116,7 @@ __global__ void __launch_bounds__(256, HD == 40 ? 3 : 2) qkv_attn_ln_f32x3_kerne
     uint16_t* hsh = lds;
     uint16_t* hsl = lds + 64 * LDY;
     // the sample's h rows, split; rows 62, 63 zero
-    const float* hg = h_in + (size_t)b * S * D;
+    const float* hg = (XIN ? x_io : h_in) + (size_t)b * S * D;
     {
         // every load issued before the first split / LDS store (a load -> store loop waited a
         // memory round trip per iteration); rows 62, 63 zero
@@ -1089,11 +1130,36 @@ __global__ void __launch_bounds__(256, HD == 40 ? 3 : 2) qkv_attn_ln_f32x3_kerne
             va[i] = *(const float4*)src;
             vb[i] = *(const float4*)(src + 4);
         }
+        // XIN: each row's D / 8 pieces sit on D / 8 consecutive lanes (the same piece index kp for
+        // every i): the row's LayerNorm reduces over them, two-pass
+        static_assert(!XIN || (D / 8 == 32 && 256 % (D / 8) == 0), "XIN: a row on one half-wave");
+        float4 xg0{}, xg1{}, xe0{}, xe1{};
+        if constexpr (XIN) {
+            const int c0 = 8 * (threadIdx.x & (D / 8 - 1));
+            xg0 = *(const float4*)(gin + c0); xg1 = *(const float4*)(gin + c0 + 4);
+            xe0 = *(const float4*)(bin + c0); xe1 = *(const float4*)(bin + c0 + 4);
+        }
 #pragma unroll
         for (int i = 0; i < NPC; ++i) {
             const int p = threadIdx.x + 256 * i, rr = p / (D / 8), kp = p - rr * (D / 8);
             const bool ok = rr < S;
             float v[8] = {va[i].x, va[i].y, va[i].z, va[i].w, vb[i].x, vb[i].y, vb[i].z, vb[i].w};
+            if constexpr (XIN) {
+                float s1 = ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
+#pragma unroll
+                for (int o = 1; o < D / 8; o <<= 1) s1 += __shfl_xor(s1, o);
+                const float mu = s1 / (float)D;
+                float s2 = 0.0f;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) s2 += (v[j] - mu) * (v[j] - mu);
+#pragma unroll
+                for (int o = 1; o < D / 8; o <<= 1) s2 += __shfl_xor(s2, o);
+                const float rs = rsqrtf(s2 / (float)D + eps_in);
+                const float g[8] = {xg0.x, xg0.y, xg0.z, xg0.w, xg1.x, xg1.y, xg1.z, xg1.w};
+                const float be[8] = {xe0.x, xe0.y, xe0.z, xe0.w, xe1.x, xe1.y, xe1.z, xe1.w};
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[j] = (v[j] - mu) * rs * g[j] + be[j];
+            }
 #pragma unroll
             for (int j = 0; j < 8; ++j) v[j] = ok ? v[j] : 0.0f;
             bf16x8_t fh, fl;
@@ -1412,13 +1478,16 @@ __global__ void __launch_bounds__(256, HD == 40 ? 3 : 2) qkv_attn_ln_f32x3_kerne
         const float rstd = rsqrtf(s2 / (float)D + eps);
         if (row < S) {
             const size_t o = ((size_t)b * S + row) * D;
+            const bool wh = h_out != nullptr;   // (uniform)
 #pragma unroll
             for (int i = 0; i < LP; ++i) {
                 const int c0 = 4 * (q + 4 * i);
-                const float4 g = *(const float4*)(gamma + c0), be = *(const float4*)(beta + c0);
                 *(float4*)(x_io + o + c0) = xv[i];
-                *(float4*)(h_out + o + c0) = make_float4((xv[i].x - mean) * rstd * g.x + be.x, (xv[i].y - mean) * rstd * g.y + be.y,
-                                                         (xv[i].z - mean) * rstd * g.z + be.z, (xv[i].w - mean) * rstd * g.w + be.w);
+                if (wh) {
+                    const float4 g = *(const float4*)(gamma + c0), be = *(const float4*)(beta + c0);
+                    *(float4*)(h_out + o + c0) = make_float4((xv[i].x - mean) * rstd * g.x + be.x, (xv[i].y - mean) * rstd * g.y + be.y,
+                                                             (xv[i].z - mean) * rstd * g.z + be.z, (xv[i].w - mean) * rstd * g.w + be.w);
+                }
             }
         }
     }

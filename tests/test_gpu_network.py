@@ -77,6 +77,80 @@ def test_mlp_ln_f32x3_matches_torch(d, n):
     assert ex < 2e-5 and eh < 2e-5, (ex, eh)
 
 
+@pytest.mark.parametrize("write_h", [False, True])
+def test_ex_halves_normalise_x_input(write_h):
+    """The d = 256 halves with the LayerNorm in the consumer (dk_net_*_f32x3_ex_async, h_in NULL):
+    each against exact f32 torch on LN_in(x) (matmul precision "highest"): x' within 2e-5 of the
+    delta scale; h_out NULL leaves its buffer untouched, otherwise h' = LN(x') within 2e-5."""
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(17)
+    d, n, B, H, hd = 256, 1024, 29, 4, 64
+    x = torch.randn(B, 62, d, device=dev) * 2 + 0.5
+    gi, bi = 1 + 0.1 * torch.randn(d, device=dev), 0.1 * torch.randn(d, device=dev)
+    g, be = 1 + 0.1 * torch.randn(d, device=dev), 0.1 * torch.randn(d, device=dev)
+    wq, bq = torch.randn(3 * d, d, device=dev) / d ** 0.5, torch.randn(3 * d, device=dev) * 0.1
+    wp, bp = torch.randn(d, d, device=dev) / d ** 0.5, torch.randn(d, device=dev) * 0.1
+    w1, b1 = torch.randn(n, d, device=dev) / d ** 0.5, torch.randn(n, device=dev) * 0.1
+    w2, b2 = torch.randn(d, n, device=dev) / n ** 0.5, torch.randn(d, device=dev) * 0.1
+    prev = torch.get_float32_matmul_precision()
+    torch.set_float32_matmul_precision("highest")
+    try:
+        h = F.layer_norm(x, (d,), gi, bi, 1e-5)
+        qkv = F.linear(h, wq, bq)
+        q, k, v = (qkv[..., i * d:(i + 1) * d].reshape(B, 62, H, hd).transpose(1, 2) for i in range(3))
+        p = torch.softmax((q @ k.transpose(-1, -2)) / hd ** 0.5, dim=-1)
+        da = F.linear((p @ v).transpose(1, 2).reshape(B, 62, d), wp, bp)
+        xa = x + da
+        dm = F.linear(F.gelu(F.linear(F.layer_norm(xa, (d,), gi, bi, 1e-5), w1, b1)), w2, b2)
+        xm = xa + dm
+    finally:
+        torch.set_float32_matmul_precision(prev)
+    sp = []
+    for w in (wq, wp):
+        hi = w.bfloat16().contiguous()
+        sp += [hi, (w - hi.float()).bfloat16().contiguous()]
+    from master_doko_reinforcement_learning_amd.az_network import mlp_split_bf16x3
+    sm = mlp_split_bf16x3(w1, w2)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    xo = x.clone()
+    ha = torch.full_like(x, float("nan"))
+    hm = torch.full_like(x, float("nan"))
+    L = _lib()
+    assert L.dk_net_qkv_attn_ln_f32x3_ex_async(None, xo.data_ptr(), gi.data_ptr(), bi.data_ptr(), 1e-5, sp[0].data_ptr(),
+                                               sp[1].data_ptr(), bq.data_ptr(), sp[2].data_ptr(), sp[3].data_ptr(),
+                                               bp.data_ptr(), B, H, hd, g.data_ptr() if write_h else None,
+                                               be.data_ptr() if write_h else None, 1e-5,
+                                               ha.data_ptr() if write_h else None, st) == 0
+    torch.cuda.synchronize()
+    xa_got = xo.clone()
+    assert L.dk_net_mlp_ln_f32x3_ex_async(None, xo.data_ptr(), gi.data_ptr(), bi.data_ptr(), 1e-5, sm[0].data_ptr(),
+                                          sm[1].data_ptr(), b1.data_ptr(), sm[2].data_ptr(), sm[3].data_ptr(), b2.data_ptr(),
+                                          B * 62, d, n, g.data_ptr() if write_h else None,
+                                          be.data_ptr() if write_h else None, 1e-5, hm.data_ptr() if write_h else None,
+                                          st) == 0
+    torch.cuda.synchronize()
+    ea = (xa_got - xa).abs().max().item() / da.abs().max().item()
+    em = (xo - xm).abs().max().item() / dm.abs().max().item()
+    assert ea < 2e-5 and em < 2e-5, (ea, em)
+    if write_h:
+        for got, xr in ((ha, xa), (hm, xm)):
+            ref = F.layer_norm(xr, (d,), g, be, 1e-5)
+            assert (got - ref).abs().max().item() / ref.abs().max().item() < 2e-5
+    else:
+        assert torch.isnan(ha).all() and torch.isnan(hm).all()
+    # the invalid forms: neither h_in nor ln_in; h_out aliasing x; d = 160
+    assert L.dk_net_mlp_ln_f32x3_ex_async(None, xo.data_ptr(), None, None, 1e-5, sm[0].data_ptr(), sm[1].data_ptr(),
+                                          b1.data_ptr(), sm[2].data_ptr(), sm[3].data_ptr(), b2.data_ptr(), B * 62, d, n,
+                                          None, None, 1e-5, None, st) != 0
+    assert L.dk_net_qkv_attn_ln_f32x3_ex_async(None, xo.data_ptr(), gi.data_ptr(), bi.data_ptr(), 1e-5, sp[0].data_ptr(),
+                                               sp[1].data_ptr(), bq.data_ptr(), sp[2].data_ptr(), sp[3].data_ptr(),
+                                               bp.data_ptr(), B, H, hd, g.data_ptr(), be.data_ptr(), 1e-5, xo.data_ptr(),
+                                               st) != 0
+    assert L.dk_net_mlp_ln_f32x3_ex_async(None, xo.data_ptr(), gi.data_ptr(), bi.data_ptr(), 1e-5, sm[0].data_ptr(),
+                                          sm[1].data_ptr(), b1.data_ptr(), sm[2].data_ptr(), sm[3].data_ptr(), b2.data_ptr(),
+                                          B * 62, 160, 640, None, None, 1e-5, None, st) != 0
+
+
 @pytest.mark.parametrize("d", [160, 256])
 def test_qkv_attn_ln_f32x3_matches_torch(d):
     """The f32 attention half with bf16x3 products (qkv_attn_ln_f32x3_kernel, d = 160 / 256, 4 heads of 40 / 64):
