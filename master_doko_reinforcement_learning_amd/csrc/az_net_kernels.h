@@ -1182,6 +1182,9 @@ constexpr uint32_t MLP_MAX_HIDDEN = 1024;
 #ifndef DK_MLP_P2
 #define DK_MLP_P2 1
 #endif
+#ifndef DK_MLP_PIN
+#define DK_MLP_PIN 0
+#endif
 #ifndef DK_MLP_WAVES160
 #define DK_MLP_WAVES160 8
 #endif
@@ -1323,8 +1326,10 @@ __global__ void __launch_bounds__(64 * WAVES, WAVES == 8 ? 1 : DK_MLP_MINB) mlp_
                 for (int j = 0; j < HT; ++j)
                     ring[kk % P1D][j] = *(const bf16x8_t*)&lds[(buf) * W1E + (32 * j + r) * LDW1 + 16 * (kk + P1D) + 8 * hh];
             }
+            if (DK_MLP_PIN) __builtin_amdgcn_sched_barrier(0);   // (the ring's reads stay P1D k-steps ahead)
 #pragma unroll
             for (int j = 0; j < HT; ++j) acc1[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[j], hf[kk], acc1[j], 0, 0, 0);
+            if (DK_MLP_PIN) __builtin_amdgcn_sched_barrier(0);
         }
     };
     auto prefetch_x = [&]() {
@@ -1378,7 +1383,9 @@ __global__ void __launch_bounds__(64 * WAVES, WAVES == 8 ? 1 : DK_MLP_MINB) mlp_
             const int s = q / OT, t = q % OT;
             const bf16x8_t cur = ring2[q % P2D];
             if (q + P2D < GS * OT) ring2[q % P2D] = w2frag((q + P2D) / OT, (q + P2D) % OT);
+            if (DK_MLP_PIN) __builtin_amdgcn_sched_barrier(0);
             acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur, af[s], acc2[t], 0, 0, 0);
+            if (DK_MLP_PIN) __builtin_amdgcn_sched_barrier(0);
         }
     };
     // one code path for all waves: iteration c = [GELU + GEMM2 of chunk c - 1][GEMM1 of chunk c];
