@@ -1182,8 +1182,11 @@ constexpr uint32_t MLP_MAX_HIDDEN = 1024;
 #ifndef DK_MLP_P2
 #define DK_MLP_P2 1
 #endif
+// DK_MLP_PIN: the W fragment rings two deep and pinned by scheduling barriers at d <= 160
+// (left to itself the compiler issued each read one MFMA before its use; -1.5 % at C5's MLP,
+// profiles/r05/bf16_mlp_pin_ab/; d = 256 has no registers for it)
 #ifndef DK_MLP_PIN
-#define DK_MLP_PIN 0
+#define DK_MLP_PIN 1
 #endif
 #ifndef DK_MLP_WAVES160
 #define DK_MLP_WAVES160 8
@@ -1235,6 +1238,7 @@ __global__ void __launch_bounds__(64 * WAVES, WAVES == 8 ? 1 : DK_MLP_MINB) mlp_
     constexpr int T = 64 * WAVES;                    // threads of the workgroup
     constexpr bool SKEW = DK_MLP_SKEW && D <= 160 && WAVES == 8;   // d = 256 has no registers to spare
     constexpr bool WIDE = DK_MLP_WIDE_STORE && D <= 160;           // (d = 256: spills)
+    constexpr bool PIN = DK_MLP_PIN && D <= 160;
     constexpr int NB = SKEW ? 3 : 2;
     constexpr int W1E = NC * LDW1, W2E = D * LDW2;
     __shared__ __attribute__((aligned(16))) uint16_t lds[NB * (W1E + W2E)];
@@ -1309,7 +1313,7 @@ __global__ void __launch_bounds__(64 * WAVES, WAVES == 8 ? 1 : DK_MLP_MINB) mlp_
         for (int j = 0; j < HT; ++j) acc1[j] = f32x16_t{0};
         // software-pipelined P1 k-steps deep: the W1 fragments of k-step kk + P1 are read from
         // LDS while the MFMAs of k-step kk run (an LDS read under load outlasts two MFMAs)
-        constexpr int P1D = DK_MLP_P1;
+        constexpr int P1D = PIN ? 2 : DK_MLP_P1;
         bf16x8_t ring[P1D][HT];
 #pragma unroll
         for (int kk = 0; kk < P1D && kk < KS; ++kk)
@@ -1326,10 +1330,10 @@ __global__ void __launch_bounds__(64 * WAVES, WAVES == 8 ? 1 : DK_MLP_MINB) mlp_
                 for (int j = 0; j < HT; ++j)
                     ring[kk % P1D][j] = *(const bf16x8_t*)&lds[(buf) * W1E + (32 * j + r) * LDW1 + 16 * (kk + P1D) + 8 * hh];
             }
-            if (DK_MLP_PIN) __builtin_amdgcn_sched_barrier(0);   // (the ring's reads stay P1D k-steps ahead)
+            if (PIN) __builtin_amdgcn_sched_barrier(0);   // (the ring's reads stay P1D k-steps ahead)
 #pragma unroll
             for (int j = 0; j < HT; ++j) acc1[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[j], hf[kk], acc1[j], 0, 0, 0);
-            if (DK_MLP_PIN) __builtin_amdgcn_sched_barrier(0);
+            if (PIN) __builtin_amdgcn_sched_barrier(0);
         }
     };
     auto prefetch_x = [&]() {
@@ -1374,7 +1378,7 @@ __global__ void __launch_bounds__(64 * WAVES, WAVES == 8 ? 1 : DK_MLP_MINB) mlp_
             a.u[1] = *(const uint2*)(wr + 8);
             return a.v;
         };
-        constexpr int P2D = DK_MLP_P2;   // W2 fragments read P2D MFMAs ahead
+        constexpr int P2D = PIN ? 2 : DK_MLP_P2;   // W2 fragments read P2D MFMAs ahead
         bf16x8_t ring2[P2D];
 #pragma unroll
         for (int q = 0; q < P2D && q < GS * OT; ++q) ring2[q] = w2frag(q / OT, q % OT);
@@ -1383,9 +1387,9 @@ __global__ void __launch_bounds__(64 * WAVES, WAVES == 8 ? 1 : DK_MLP_MINB) mlp_
             const int s = q / OT, t = q % OT;
             const bf16x8_t cur = ring2[q % P2D];
             if (q + P2D < GS * OT) ring2[q % P2D] = w2frag((q + P2D) / OT, (q + P2D) % OT);
-            if (DK_MLP_PIN) __builtin_amdgcn_sched_barrier(0);
+            if (PIN) __builtin_amdgcn_sched_barrier(0);
             acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur, af[s], acc2[t], 0, 0, 0);
-            if (DK_MLP_PIN) __builtin_amdgcn_sched_barrier(0);
+            if (PIN) __builtin_amdgcn_sched_barrier(0);
         }
     };
     // one code path for all waves: iteration c = [GELU + GEMM2 of chunk c - 1][GEMM1 of chunk c];
