@@ -1,7 +1,7 @@
-# End-of-session check: the GPU suite, smoke, the default bench, the network benches, and a kernel
+# End-of-session check: the GPU suite, smoke, the default bench, the network benches, and a kernel  (usage: bash tools/gpu/final_check.sh [out-dir])
 # trace of the IMPI f32 step.
 set -e
-OUT=gpurun_out/r6final; mkdir -p $OUT
+OUT=gpurun_out/${1:-final}; mkdir -p $OUT
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1
 timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
 timeout -k 10 600 python -u bench.py > $OUT/bench_default.json 2> $OUT/bench_default.err
