@@ -1,5 +1,5 @@
-# End-of-session check: the GPU suite, smoke, the default bench, the network benches, and a kernel  (usage: bash tools/gpu/final_check.sh [out-dir])
-# trace of the IMPI f32 step.
+# End-of-session check: the GPU suite, smoke, the default bench, the network benches, and a
+# kernel trace of the IMPI f32 step.   usage: bash tools/gpu/final_check.sh [out-dir under gpurun_out]
 set -e
 OUT=gpurun_out/${1:-final}; mkdir -p $OUT
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1
