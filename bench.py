@@ -577,8 +577,9 @@ def net_precision(args, torch):
                 "f32 activations; GEMM products from bf16 pieces (bf16x3: three MFMAs per k-step, ~16-bit "
                 "products, as hipBLASLt's 'medium' f32 GEMMs measured, profiles/r04/fp32_gemm_probe.json): at d = 160 "
                 "and d = 256 every block as two HIP kernels (qkv_attn_ln_f32x3_kernel, mlp_ln_f32x3_kernel / "
-                "mlp16_ln_f32x3_kernel) and the heads as two (class_pool_ln_f32x3_kernel, class_mlp_f32x3_kernel), "
-                "no hipBLASLt: peak = bf16 dense / 3")
+                "mlp16_ln_f32x3_kernel; at d = 256 each half normalises the residual stream itself, x-only chain) and "
+                "the heads as two (class_pool_ln_f32x3_kernel, class_mlp_f32x3_kernel), no hipBLASLt: peak = bf16 "
+                "dense / 3")
     return torch.bfloat16, "bf16 network", 2500.0, "bf16 dense peak"
 
 
