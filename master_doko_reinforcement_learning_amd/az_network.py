@@ -29,6 +29,7 @@ load_reference_state_dict maps a reference state_dict onto this module.
 """
 import ctypes
 import math
+import os
 
 import torch
 import torch.nn.functional as F
@@ -400,7 +401,9 @@ class FusedTrunkF32(FusedTrunk):
         return self.add_ln(x, _f32c(F.linear(y, w)), ln, b)
 
     def run(self, h, blocks, final_ln, x=None):
-        if not (self.d == 256 and len(blocks) > 0 and all(self.ex_ok(blk) for blk in blocks)):
+        # (DK_F32_XCHAIN=0: the h-in / h-out chain, a measurement switch)
+        if not (self.d == 256 and len(blocks) > 0 and all(self.ex_ok(blk) for blk in blocks)) or \
+                os.environ.get("DK_F32_XCHAIN", "1") == "0":
             return super().run(h, blocks, final_ln, x)
         # d = 256: every half after the first reads the residual stream x and applies the
         # LayerNorm its producer used to write out as h (the *_ex kernels); only the last half
