@@ -9,7 +9,8 @@ import subprocess
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_DIR = os.path.join(ROOT, "oracle")
-LIB_PATH = os.path.join(ORACLE_DIR, "liboracle_doko.so")
+# ORACLE_LIB: another build of the restatement (the sanitizer build, oracle/_asan/)
+LIB_PATH = os.environ.get("ORACLE_LIB") or os.path.join(ORACLE_DIR, "liboracle_doko.so")
 
 _lib = None
 
