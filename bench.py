@@ -33,6 +33,12 @@ METRIC = "determinized rollouts/sec (48-card full game, 1000 sims/root) at 1/2/4
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
+def simds(dev):
+    """SIMDs of the device (4 per CU on gfx950)."""
+    import torch
+    return 4 * torch.cuda.get_device_properties(dev).multi_processor_count
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -62,11 +68,12 @@ def parse():
     p.add_argument("--games", type=int, default=8192, help="concurrent self-play games per GPU (c5)")
     p.add_argument("--az-iterations", type=int, default=200, help="PUCT iterations per move (c5)")
     p.add_argument("--ar-samples", type=int, default=4, help="AR samples per infostate (impi)")
-    p.add_argument("--net-precision", choices=["bf16", "f32"], default="bf16",
-                   help="c5 / impi / impid network: bf16 = the fused bf16 HIP kernels (default); f32 = the reference's "
-                        "precision: f32 activations, torch.set_float32_matmul_precision('medium') and allow_tf32 as "
-                        "az_doko.py:539-541 / main.py:508 set them (hipBLASLt then computes the f32 GEMMs from bf16 "
-                        "products, ~5e-6 relative error: profiles/r04/fp32_gemm_probe.json)")
+    p.add_argument("--net-precision", choices=["bf16", "f32"], default="f32",
+                   help="c5 / impi / impid network: f32 (default) = the reference's precision (f32 activations at "
+                        "matmul precision 'medium', az_doko.py:539-541 / main.py:508) on the hand-written f32 kernels, "
+                        "GEMM products from bf16 hi / lo pieces (bf16x3, ~16-bit products, as fine as hipBLASLt's "
+                        "'medium' measured: profiles/r04/fp32_gemm_probe.json; no hipBLASLt kernel runs); bf16 = the "
+                        "fused bf16 kernels, NARROWER than the reference (bf16 activations and weights, opt-in)")
     p.add_argument("--ar-temperature", type=float, default=0.4, help="AR sampling temperature (impi; all_policies.rs:30)")
     p.add_argument("--iterations", type=int, default=1000)
     p.add_argument("--infostates", type=int, default=None,
@@ -413,6 +420,7 @@ def main():
     # per-wave clocks of the last timed search launch: how much of it the persistent grid's
     # drain tail costs (the waves that ran out of groups wait for the slowest one)
     waves = eng.last_search_waves()
+    clocks = eng.last_search_clocks()
     if rank == 0 and args.dump_actions and bufs["actions"] is not None:
         np.save(args.dump_actions, bufs["actions"].cpu().numpy())
     if args.dump_acc and bufs["acc"] is not None:
@@ -515,8 +523,16 @@ def main():
             "search_waves": {"waves": waves["waves"], "busy_frac": round(waves["busy_frac"], 4),
                              "first_end_ms": round(waves["first_end_ms"], 2),
                              "median_end_ms": round(waves["median_end_ms"], 2), "span_ms": round(waves["span_ms"], 2),
-                             "note": "each wave of the persistent grid stamps the 100 MHz counter at start and once "
-                                     "the group queue is dry for it; 1 - busy_frac = drain tail + launch ramp"},
+                             "sclk_mhz": round(clocks["sclk_mhz"], 1),
+                             "sclk_range_mhz": [round(clocks["sclk_min_mhz"], 1), round(clocks["sclk_max_mhz"], 1)],
+                             # the launch's SIMD-cycles per simulation: event time x shader clock x SIMDs / simulations
+                             # (comparable across boxes whose clocks differ)
+                             "cycles_per_simulation": round(kernel_ms * 1e-3 * clocks["sclk_mhz"] * 1e6 * simds(dev)
+                                                            / (n_roots * iters), 1),
+                             "note": "each wave of the persistent grid stamps the 100 MHz counter and the shader clock "
+                                     "(s_memtime) at start and once the group queue is dry for it; 1 - busy_frac = "
+                                     "drain tail + launch ramp; sclk_mhz = shader cycles / real time over the waves; "
+                                     "cycles_per_simulation = search_kernel_ms x sclk x SIMDs / simulations"},
             "roofline": {
                 # bound: what binds the launch, measured (round-4 review): latency of the per-lane tree
                 # walks -- neither VALU nor DRAM is saturated (valu below).  achieved/peak/frac stay the
@@ -580,7 +596,8 @@ def net_precision(args, torch):
                 "mlp16_ln_f32x3_kernel; at d = 256 each half normalises the residual stream itself, x-only chain) and "
                 "the heads as two (class_pool_ln_f32x3_kernel, class_mlp_f32x3_kernel), no hipBLASLt: peak = bf16 "
                 "dense / 3")
-    return torch.bfloat16, "bf16 network", 2500.0, "bf16 dense peak"
+    return (torch.bfloat16, "bf16 network (narrower than the reference's f32; opt-in --net-precision bf16)", 2500.0,
+            "bf16 dense peak")
 
 
 def run_c5(args, dk, L, dev, stream, rank, world, local_rank, dist):

@@ -625,6 +625,12 @@ int dk_last_search_ms(dk_ctx* ctx, float* ms);
  * out[3] = the median wave's end (ms after the first start), out[4] = waves.  Measurement
  * only (the reference has no counterpart); waits for the launch. */
 int dk_last_search_waves(dk_ctx* ctx, double* out);
+/* The shader clock of the last search launch, from s_memtime / s_memrealtime stamps taken by
+ * every wave at its start and end (measurement; no reference counterpart): out[0] = mean clock in
+ * MHz (shader cycles / real time over all waves), out[1] / out[2] = the slowest / fastest wave's
+ * clock, out[3] = mean shader cycles a wave was busy.  Makes a launch's time comparable across
+ * boxes whose clocks differ (cycles per simulation). */
+int dk_last_search_clocks(dk_ctx* ctx, double* out);
 /* memory footprint of the node / state pools reserved by dk_create (bytes) */
 uint64_t dk_pool_bytes(const dk_ctx* ctx);
 /* Pool demand since dk_create (waits for `stream`): the most child slots one search used

@@ -65,6 +65,7 @@ def lib():
         "dk_sync": (ctypes.c_int, [vp, vp]),
         "dk_last_search_ms": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_float)]),
         "dk_last_search_waves": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double)]),
+        "dk_last_search_clocks": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double)]),
         "dk_new_game_batch": (ctypes.c_int, [vp, ctypes.c_int, vp, u32, vp]),
         "dk_new_game_batch_async": (ctypes.c_int, [vp, ctypes.c_int, vp, u32, vp, vp]),
         "dk_env_allowed_batch": (ctypes.c_int, [vp, vp, u32, ctypes.c_int, vp]),
@@ -149,7 +150,7 @@ EXPORTED = [
     "dk_new_game_batch_async", "dk_env_allowed_batch", "dk_env_step_batch", "dk_env_rewards_batch",
     "dk_env_rollout_batch", "dk_env_rollout_batch_async", "dk_env_random_plies_batch", "dk_search_batch",
     "dk_search_batch_async", "dk_search_batch_rng", "dk_search_batch_rng_async", "dk_determinize_batch", "dk_determinize_batch_async", "dk_fuse",
-    "dk_fuse_accumulate_async", "dk_fuse_select_async", "dk_decide_batch", "dk_sync", "dk_last_search_ms", "dk_last_search_waves",
+    "dk_fuse_accumulate_async", "dk_fuse_select_async", "dk_decide_batch", "dk_sync", "dk_last_search_ms", "dk_last_search_waves", "dk_last_search_clocks",
     "dk_pool_bytes", "dk_legal_actions_async", "dk_env_step_batch_async", "dk_env_random_plies_batch_async",
     "dk_az_begin_async", "dk_az_root_async", "dk_az_rng_async", "dk_az_select_async", "dk_az_backup_async", "dk_az_finish_async",
     "dk_az_records_async", "dk_az_step_async", "dk_az_encode_async", "dk_net_embed_ln_bf16_async",

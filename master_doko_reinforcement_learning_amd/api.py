@@ -152,6 +152,13 @@ class Engine:
         return {"span_ms": out[0], "busy_frac": out[1], "first_end_ms": out[2], "median_end_ms": out[3],
                 "waves": int(out[4])}
 
+    def last_search_clocks(self):
+        """Shader clock of the last search launch (dk_last_search_clocks): mean / slowest / fastest
+        wave clock in MHz and the mean shader cycles a wave was busy."""
+        out = (ctypes.c_double * 4)()
+        _check(_native.lib().dk_last_search_clocks(self._ctx, out))
+        return {"sclk_mhz": out[0], "sclk_min_mhz": out[1], "sclk_max_mhz": out[2], "wave_busy_cycles": out[3]}
+
     # ---- game construction (FdoState::new_game / DoState::new_game)
     def new_games(self, game, seeds):
         seeds = np.ascontiguousarray(seeds, dtype=np.uint64)

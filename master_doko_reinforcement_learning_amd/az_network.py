@@ -19,8 +19,8 @@ Re-expressed for MI355X rather than translated (forward_fused):
     mlp_ln_kernel, and the heads' class pooling + LayerNorm in class_pool_ln_kernel;
   * the reference's f32 precision (FusedTrunkF32, csrc/az_net_f32_kernels.h) for
     `--net-precision f32`;
-  * the 4 + 39 per-class MLPs of the heads run as ONE batched GEMM per layer
-    (class-stacked weights [C, d, d]) instead of 43 small launches;
+  * the 4 + 39 per-class MLPs of the heads run in ONE kernel launch (class_mlp_bf16_kernel /
+    class_mlp_f32x3_kernel over class-stacked weights [C, d, d]) instead of 43 small module calls;
   * the tokens come straight from the device encoder, no host round trip.
   forward_torch keeps the reference structure (the qkv projection has the
   nn.MultiheadAttention in_proj [q; k; v] layout, see load_reference_state_dict).
@@ -532,9 +532,11 @@ class DokoAzNet(nn.Module):
 
 class AzEvaluator:
     """The network as AlphaZeroSearch's `network` callable: dk_az_state records ->
-    device encoder (az_encode) -> DokoAzNet (bf16) -> (value f32 [n, 4], logits f32 [n, 39])."""
+    device encoder (az_encode) -> DokoAzNet -> (value f32 [n, 4], logits f32 [n, 39]).  dtype
+    float32 (default) is the reference's precision (az_doko.py:379-400, 539-541: f32 activations,
+    matmul precision "medium"); torch.bfloat16 runs the narrower bf16 kernels."""
 
-    def __init__(self, engine, net, dtype=torch.bfloat16):
+    def __init__(self, engine, net, dtype=torch.float32):
         self.engine = engine
         self.net = net.eval().to(dtype)
         self.dtype = dtype

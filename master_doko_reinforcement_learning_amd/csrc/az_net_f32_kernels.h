@@ -1,6 +1,9 @@
-// Row kernels of the networks' f32 forward (az_network.FusedTrunkF32): the reference's
-// precision -- f32 activations everywhere, the GEMMs on hipBLASLt at matmul precision
-// "medium" (az_doko.py:539-541, main.py:508) -- with the memory-bound passes fused:
+// Kernels of the networks' f32 forward (az_network.FusedTrunkF32): the reference's precision --
+// f32 activations everywhere, GEMM products at least as fine as its matmul precision "medium"
+// (az_doko.py:539-541, main.py:508).  At d = 160 / 256 with 4 heads every GEMM runs inside the
+// hand-written bf16x3 kernels below (qkv_attn_ln_f32x3, mlp_ln_f32x3 / mlp16_ln_f32x3, the class
+// heads); only other shapes fall back to torch GEMMs around these row kernels, the memory-bound
+// passes fused:
 //   embed_ln_f32 : x = sum of the six token embeddings (left to right, f32); h = LN(x)
 //   add_ln_f32   : x += delta; h = LN(x)                 (delta may be NULL: h = LN(x))
 //   attn62_f32   : softmax(q k^T / sqrt(hd)) v per (sample, head), q / k / v read from the

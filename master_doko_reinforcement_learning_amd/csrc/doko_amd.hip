@@ -248,7 +248,11 @@ __global__ void __launch_bounds__(WAVE, H::MIN_WAVES) search_kernel(const dk_sta
     // per-wave start / end of the realtime counter (100 MHz), indexed by the wave's first pool
     // lane (dk_last_search_waves): how long each wave had work before the group queue drained
     const uint32_t clock_idx = lane_base + blockIdx.x * rpw;
-    if (wave_clock && lane == 0) wave_clock[2 * clock_idx] = __builtin_amdgcn_s_memrealtime();
+    // (and the shader-clock counter, s_memtime, beside it: cycles per real time = the launch's clock)
+    if (wave_clock && lane == 0) {
+        wave_clock[4 * clock_idx] = __builtin_amdgcn_s_memrealtime();
+        wave_clock[4 * clock_idx + 2] = __builtin_amdgcn_s_memtime();
+    }
     const uint32_t T = iters + 1;
     const uint32_t n_ln = LN_LDS ? T : 0u;
     for (uint32_t i = lane; i < n_ln; i += WAVE) dk_lds[i] = (uint64_t)__double_as_longlong(ln_table[i]);
@@ -328,7 +332,10 @@ __global__ void __launch_bounds__(WAVE, H::MIN_WAVES) search_kernel(const dk_sta
         best[root] = b;
     }
     if (hw) atomicMax(high_water, hw);
-    if (wave_clock && lane == 0) wave_clock[2 * clock_idx + 1] = __builtin_amdgcn_s_memrealtime();
+    if (wave_clock && lane == 0) {
+        wave_clock[4 * clock_idx + 3] = __builtin_amdgcn_s_memtime();
+        wave_clock[4 * clock_idx + 1] = __builtin_amdgcn_s_memrealtime();
+    }
 }
 
 // is_consistent (rs-full-doko/src/matching/is_consistent.rs:38-305) of assumed hands and
@@ -946,7 +953,7 @@ struct dk_ctx {
     bool lds_path_fixed = false;    // DK_LDS_PATH (1..MAX_PATH) fixes it
     bool verbose = false;           // DK_VERBOSE=1: one stderr line per search launch (shape, residency)
     uint64_t* prof = nullptr;       // phase timers (DK_PHASE_PROF builds only)
-    uint64_t* wave_clock = nullptr; // [pool_roots][2] realtime-counter start / end of the search waves (by first lane)
+    uint64_t* wave_clock = nullptr; // [pool_roots][4] realtime start / end, shader-clock start / end of the search waves (by first lane)
     // AlphaZero PUCT search (dk_az_*): per-game node / state regions, allocated on first use
     dk::az::Node* az_nodes = nullptr;
     dk_az_state* az_states = nullptr;
@@ -1393,7 +1400,7 @@ dk_ctx* dk_create(const dk_config* cfg) {
     ok = ok && hipMalloc(&ctx->err, sizeof(int)) == hipSuccess;
     ok = ok && hipMalloc(&ctx->high_water, 4 * sizeof(uint32_t)) == hipSuccess;
     ok = ok && hipMemset(ctx->high_water, 0, 4 * sizeof(uint32_t)) == hipSuccess;
-    ok = ok && hipMalloc(&ctx->wave_clock, (R + 1) * 2 * sizeof(uint64_t)) == hipSuccess;
+    ok = ok && hipMalloc(&ctx->wave_clock, (R + 1) * 4 * sizeof(uint64_t)) == hipSuccess;
     ctx->region_slot.assign((R + dk_ctx::REGION_LANES - 1) / dk_ctx::REGION_LANES, -1);
     if (ok && with_fallback) {
         // 64 waves of 64 roots (fewer when the context is smaller): overflow is rare, and the
@@ -1508,8 +1515,8 @@ int dk_pool_high_water(dk_ctx* ctx, void* stream, uint32_t* slots, uint32_t* cap
     return DK_OK;
 }
 
-int dk_last_search_waves(dk_ctx* ctx, double* out) {
-    if (!ctx || !out) return DK_E_INVALID;
+// the per-wave stamps of the last search launch: [wave][rt0, rt1, clk0, clk1]
+static int last_wave_stamps(dk_ctx* ctx, std::vector<uint64_t>& t, uint32_t* nw_out) {
     uint32_t first, nw, stride;
     hipEvent_t e1;
     {
@@ -1520,13 +1527,26 @@ int dk_last_search_waves(dk_ctx* ctx, double* out) {
     }
     if (nw == 0) return DK_E_INVALID;
     DK_HIP(hipEventSynchronize(e1));
-    std::vector<uint64_t> t((size_t)nw * stride * 2);
-    DK_HIP(hipMemcpy(t.data(), ctx->wave_clock + 2 * (size_t)first, t.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    std::vector<uint64_t> raw((size_t)nw * stride * 4);
+    DK_HIP(hipMemcpy(raw.data(), ctx->wave_clock + 4 * (size_t)first, raw.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    t.resize((size_t)nw * 4);
+    for (uint32_t w = 0; w < nw; ++w)
+        for (int k = 0; k < 4; ++k) t[4 * (size_t)w + k] = raw[4 * (size_t)w * stride + k];
+    *nw_out = nw;
+    return DK_OK;
+}
+
+int dk_last_search_waves(dk_ctx* ctx, double* out) {
+    if (!ctx || !out) return DK_E_INVALID;
+    std::vector<uint64_t> t;
+    uint32_t nw = 0;
+    const int rc = last_wave_stamps(ctx, t, &nw);
+    if (rc != DK_OK) return rc;
     uint64_t t0 = ~0ull, t1 = 0, e_min = ~0ull;
     std::vector<uint64_t> ends(nw);
     double busy = 0.0;
     for (uint32_t w = 0; w < nw; ++w) {
-        const uint64_t a = t[2 * (size_t)w * stride], b = t[2 * (size_t)w * stride + 1];
+        const uint64_t a = t[4 * (size_t)w], b = t[4 * (size_t)w + 1];
         t0 = a < t0 ? a : t0; t1 = b > t1 ? b : t1; e_min = b < e_min ? b : e_min;
         busy += (double)(b - a);
         ends[w] = b;
@@ -1538,6 +1558,26 @@ int dk_last_search_waves(dk_ctx* ctx, double* out) {
     out[2] = (double)(e_min - t0) / 1e5;                   // first wave out of work (ms)
     out[3] = (double)(ends[nw / 2] - t0) / 1e5;            // median wave end (ms)
     out[4] = (double)nw;
+    return DK_OK;
+}
+
+int dk_last_search_clocks(dk_ctx* ctx, double* out) {
+    if (!ctx || !out) return DK_E_INVALID;
+    std::vector<uint64_t> t;
+    uint32_t nw = 0;
+    const int rc = last_wave_stamps(ctx, t, &nw);
+    if (rc != DK_OK) return rc;
+    double rt = 0.0, clk = 0.0, lo = 1e30, hi = 0.0;
+    for (uint32_t w = 0; w < nw; ++w) {
+        const double r = (double)(t[4 * (size_t)w + 1] - t[4 * (size_t)w]);
+        const double c = (double)(t[4 * (size_t)w + 3] - t[4 * (size_t)w + 2]);
+        rt += r; clk += c;
+        if (r > 0) { const double f = c / r * 100.0; lo = f < lo ? f : lo; hi = f > hi ? f : hi; }
+    }
+    out[0] = rt > 0 ? clk / rt * 100.0 : 0.0;   // shader clock (MHz): cycles per 100 MHz tick x 100
+    out[1] = lo < 1e30 ? lo : 0.0;             // slowest / fastest wave's clock (MHz)
+    out[2] = hi;
+    out[3] = clk / (double)nw;                 // mean shader cycles a wave was busy
     return DK_OK;
 }
 
