@@ -81,6 +81,22 @@ class Block(nn.Module):
         x = x + self.attn_delta(self.ln_1(x))
         return x + self.mlp_delta(self.ln_2(x))
 
+    # state_dict names of the reference's TransformerBlock (TransformerBlock.py:5-27, SelfAttention.py:4-36)
+    REF_NAMES = (("ln_1.weight", "ln_1.weight"), ("ln_1.bias", "ln_1.bias"),
+                 ("qkv.weight", "attn.attn.in_proj_weight"), ("qkv.bias", "attn.attn.in_proj_bias"),
+                 ("out.weight", "attn.attn.out_proj.weight"), ("out.bias", "attn.attn.out_proj.bias"),
+                 ("c_proj.weight", "attn.c_proj.weight"), ("c_proj.bias", "attn.c_proj.bias"),
+                 ("ln_2.weight", "ln_2.weight"), ("ln_2.bias", "ln_2.bias"),
+                 ("fc.weight", "mlp.c_fc.weight"), ("fc.bias", "mlp.c_fc.bias"),
+                 ("proj.weight", "mlp.c_proj.weight"), ("proj.bias", "mlp.c_proj.bias"))
+
+    @torch.no_grad()
+    def load_reference(self, sd, prefix=""):
+        """Copy a reference TransformerBlock's parameters (state_dict entries `prefix + name`)."""
+        own = self.state_dict()
+        for mine, ref in self.REF_NAMES:
+            own[mine].copy_(sd[prefix + ref])
+
 
 class ClassHead(nn.Module):
     """PerClassAttentionMLPHead (az_doko.py:28-56) with class-stacked MLP weights."""
@@ -508,17 +524,9 @@ class DokoAzNet(nn.Module):
         for i, n in enumerate(names):
             self.emb[i].weight.copy_(sd["transformer.%s.weight" % n])
 
-        def blk(dst, pre):
-            dst.ln_1.weight.copy_(sd[pre + "ln_1.weight"]); dst.ln_1.bias.copy_(sd[pre + "ln_1.bias"])
-            dst.qkv.weight.copy_(sd[pre + "attn.attn.in_proj_weight"]); dst.qkv.bias.copy_(sd[pre + "attn.attn.in_proj_bias"])
-            dst.out.weight.copy_(sd[pre + "attn.attn.out_proj.weight"]); dst.out.bias.copy_(sd[pre + "attn.attn.out_proj.bias"])
-            dst.c_proj.weight.copy_(sd[pre + "attn.c_proj.weight"]); dst.c_proj.bias.copy_(sd[pre + "attn.c_proj.bias"])
-            dst.ln_2.weight.copy_(sd[pre + "ln_2.weight"]); dst.ln_2.bias.copy_(sd[pre + "ln_2.bias"])
-            dst.fc.weight.copy_(sd[pre + "mlp.c_fc.weight"]); dst.fc.bias.copy_(sd[pre + "mlp.c_fc.bias"])
-            dst.proj.weight.copy_(sd[pre + "mlp.c_proj.weight"]); dst.proj.bias.copy_(sd[pre + "mlp.c_proj.bias"])
         for group, mods in (("h", self.blocks), ("p_h", self.p_blocks), ("v_h", self.v_blocks)):
             for i, m in enumerate(mods):
-                blk(m, "transformer.%s.%d." % (group, i))
+                m.load_reference(sd, "transformer.%s.%d." % (group, i))
         for ln, n in ((self.p_ln, "p_ln_f"), (self.v_ln, "v_ln_f")):
             ln.weight.copy_(sd["transformer.%s.weight" % n]); ln.bias.copy_(sd["transformer.%s.bias" % n])
         for head, n in ((self.value_head, "value_head"), (self.policy_head, "policy_head")):

@@ -58,14 +58,7 @@ class DokoImpiNet(nn.Module):
         for i, n in enumerate(names):
             self.emb[i].weight.copy_(sd["transformer.%s.weight" % n])
         for i, m in enumerate(self.blocks):
-            pre = "transformer.h.%d." % i
-            m.ln_1.weight.copy_(sd[pre + "ln_1.weight"]); m.ln_1.bias.copy_(sd[pre + "ln_1.bias"])
-            m.qkv.weight.copy_(sd[pre + "attn.attn.in_proj_weight"]); m.qkv.bias.copy_(sd[pre + "attn.attn.in_proj_bias"])
-            m.out.weight.copy_(sd[pre + "attn.attn.out_proj.weight"]); m.out.bias.copy_(sd[pre + "attn.attn.out_proj.bias"])
-            m.c_proj.weight.copy_(sd[pre + "attn.c_proj.weight"]); m.c_proj.bias.copy_(sd[pre + "attn.c_proj.bias"])
-            m.ln_2.weight.copy_(sd[pre + "ln_2.weight"]); m.ln_2.bias.copy_(sd[pre + "ln_2.bias"])
-            m.fc.weight.copy_(sd[pre + "mlp.c_fc.weight"]); m.fc.bias.copy_(sd[pre + "mlp.c_fc.bias"])
-            m.proj.weight.copy_(sd[pre + "mlp.c_proj.weight"]); m.proj.bias.copy_(sd[pre + "mlp.c_proj.bias"])
+            m.load_reference(sd, "transformer.h.%d." % i)
         self.ln_f.weight.copy_(sd["transformer.ln_f.weight"]); self.ln_f.bias.copy_(sd["transformer.ln_f.bias"])
         self.head.queries.copy_(sd["lm_head.card_queries"])
         for c in range(IPI_CLASSES):

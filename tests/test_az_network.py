@@ -1,38 +1,23 @@
 """AlphaZero network (az_network.DokoAzNet) against a plain-PyTorch fp32 module with the
-reference's structure and state_dict names (rs-doko-py-bridge/python/az_doko.py:28-138,
-TransformerBlock.py, SelfAttention.py): identical outputs after load_reference_state_dict.
-CPU only."""
+reference's structure and state_dict names (rs-doko-py-bridge/python/az_doko.py:28-138): identical
+outputs after load_reference_state_dict.  Its blocks are RefStructBlock, pinned to the reference's
+own TransformerBlock.py by tests/test_net_fixtures.py; the per-class head (_Head) restates
+az_doko.py:28-55, which cannot be imported here (parity unpinned).  CPU only."""
 import torch
 from torch import nn
 
 from master_doko_reinforcement_learning_amd.az_network import VOCAB, DokoAzNet
+from net_fixtures import RefStructBlock
 
 
 class _Cfg:
     n_embd, n_head, attn_pdrop, resid_pdrop = 32, 4, 0.0, 0.0
 
 
-class _SelfAttention(nn.Module):
-    def __init__(self, c):
-        super().__init__()
-        self.attn = nn.MultiheadAttention(c.n_embd, c.n_head, dropout=0.0, batch_first=True)
-        self.c_proj = nn.Linear(c.n_embd, c.n_embd)
-
-    def forward(self, x):
-        return self.c_proj(self.attn(x, x, x)[0])
-
-
-class _Block(nn.Module):
-    def __init__(self, c):
-        super().__init__()
-        self.ln_1 = nn.LayerNorm(c.n_embd)
-        self.attn = _SelfAttention(c)
-        self.ln_2 = nn.LayerNorm(c.n_embd)
-        self.mlp = nn.ModuleDict(dict(c_fc=nn.Linear(c.n_embd, 4 * c.n_embd), c_proj=nn.Linear(4 * c.n_embd, c.n_embd)))
-
-    def forward(self, x):
-        x = x + self.attn(self.ln_1(x))
-        return x + self.mlp.c_proj(nn.functional.gelu(self.mlp.c_fc(self.ln_2(x))))
+def _Block(c):
+    """The reference block's structure and state_dict names (net_fixtures.RefStructBlock, pinned
+    to the reference's own TransformerBlock.py outputs by tests/test_net_fixtures.py)."""
+    return RefStructBlock(c.n_embd, c.n_head)
 
 
 class _Head(nn.Module):
