@@ -93,6 +93,11 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=0)
     p.add_argument("--cpu-roots-per-thread", type=int, default=96)
     p.add_argument("--dump-actions", default="", help="rank 0 writes the fused actions (.npy) of the last step")
+    p.add_argument("--replica-offset", type=int, default=0,
+                   help="c5: replica index = rank + offset (seeds and network weights), so that a 1-rank run can "
+                        "reproduce any rank of an N-rank run")
+    p.add_argument("--dump-records", default="",
+                   help="c5: every rank writes its games' dk_az_state records after the last step to <path>_r<replica>.npy")
     p.add_argument("--dump-acc", default="", help="rank 0 writes the all-reduced fusion accumulators (.npy) of the last step")
     p.add_argument("--small-infostates", type=int, default=512,
                    help="c3: also time the survey's small decision batch (512 infostates x 64 = 32,768 roots); 0 = skip")
@@ -610,7 +615,8 @@ def run_c5(args, dk, L, dev, stream, rank, world, local_rank, dist):
     independent, so N GPUs run N replicas (weak scaling, no collective)."""
     import torch
     from master_doko_reinforcement_learning_amd.az_network import AzEvaluator, DokoAzNet
-    torch.manual_seed(1234 + rank)
+    rep = rank + args.replica_offset           # the replica's seeds and weights (--replica-offset)
+    torch.manual_seed(1234 + rep)
     G, iters = args.games, args.az_iterations
     eng = dk.Engine(device=local_rank, max_roots=64, max_iterations=max(1, iters))
     sp = stream.cuda_stream
@@ -619,7 +625,7 @@ def run_c5(args, dk, L, dev, stream, rank, world, local_rank, dist):
         if rc != 0:
             raise RuntimeError("doko_amd error %d: %s" % (rc, L.dk_status_string(rc).decode()))
 
-    seeds = np.arange(G, dtype=np.uint64) + np.uint64(0xA2000000 + rank * G)
+    seeds = np.arange(G, dtype=np.uint64) + np.uint64(0xA2000000 + rep * G)
     st = torch.zeros((G, 128), dtype=torch.uint8, device=dev)
     ck(L.dk_new_game_batch_async(eng.ctx, dk.GAME_FULL_DOKO, torch.tensor(seeds.view(np.int64), device=dev).data_ptr(),
                                  G, st.data_ptr(), sp))
@@ -681,10 +687,13 @@ def run_c5(args, dk, L, dev, stream, rank, world, local_rank, dist):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     net_ms = sum(e0.elapsed_time(e1) for e0, e1 in ev_time[1:])
+    if args.dump_records:
+        np.save("%s_r%d.npy" % (args.dump_records, rep), records.cpu().numpy())
     evals = G * (iters + 1) * args.steps
     flop = az_flop_per_eval()
     result = None
     if rank == 0:
+        cpu = cpu_baseline_net(args, "c5") if world == 1 and not args.no_cpu_baseline else None
         achieved = flop * evals / (net_ms / 1e3) / 1e12
         result = {
             "metric": "AlphaZero self-play PUCT simulations/sec (one policy/value network leaf evaluation each)",
@@ -710,7 +719,7 @@ def run_c5(args, dk, L, dev, stream, rank, world, local_rank, dist):
                          "frac": achieved / npeak, "traffic": None,
                          "note": "network GEMMs/attention: %.1f MFLOP per leaf evaluation (algorithmic), %s; achieved "
                                  "over the network's event-timed share of the step" % (flop / 1e6, nnote)},
-            "cpu_baseline": None,
+            "cpu_baseline": cpu,
         }
         print(json.dumps(result))
     if world > 1:
@@ -1131,6 +1140,7 @@ def run_impi(args, dk, L, dev, stream, rank, world, local_rank, dist):
     flop = impi_flop_per_eval()
     result = None
     if rank == 0:
+        cpu = cpu_baseline_net(args, "impi") if world == 1 and not decide and not args.no_cpu_baseline else None
         achieved = flop * stats["rows"] / (net_ms / 1e3) / 1e12
         result = {
             "metric": ("AR-determinized decisions/sec (mcts_ar_maxn_policy: %d AR samples x %d UCT simulations each)"
@@ -1163,13 +1173,107 @@ def run_impi(args, dk, L, dev, stream, rank, world, local_rank, dist):
                                  "(infostates ordered by guess count, each round runs the prefix of lanes still "
                                  "guessing); achieved over the network's event-timed share of the step; %s"
                                  % (flop / 1e6, nnote)},
-            "cpu_baseline": None,
+            "cpu_baseline": cpu,
         }
         print(json.dumps(result))
     if world > 1:
         dist.destroy_process_group()
     eng.close()
     return result
+
+
+def cpu_baseline_net(args, kind, target_s=3.0, batch=256):
+    """CPU baseline of the network workloads (c5: AlphaZero self-play; impi: AR determinization)
+    on this box's host cores, the reference's two parts timed separately on a bounded sample:
+      net  : the reference architecture (DokoAzNet d 160 / DokoImpiNet d 256, random weights) in
+             torch-CPU f32 at matmul precision "medium" (az_doko.py:539-541, main.py:508), batches of
+             `batch` evaluations of random valid tokens -> evaluations/s;
+      tree : the ORACLE's search around the network with its synthetic hash network -- c5:
+             mcts_search (async_mcts.rs:224-406: PUCT, c 4.0, Dirichlet 0.8 / 0.3, T 0.5) on fresh
+             deals; impi: forward_pred_process_with_mask (forward.rs:392-661, T 0.4) on the C3
+             infostates -- one worker thread per usable core -> simulations (or samples) per second
+             and network evaluations per unit.
+    value = units/s with one network evaluation per simulation (c5) / per guess (impi), network and
+    tree work serialised: 1 / (evals_per_unit / net_rate + 1 / tree_rate)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import ctypes
+    from concurrent.futures import ThreadPoolExecutor
+
+    import torch
+
+    import oracle_lib as ol
+    cores, quota = cpu_quota_cores()
+    threads = args.cpu_threads or (min(cores, int(np.ceil(quota))) if quota else cores)
+    prev_threads = torch.get_num_threads()
+    prev_prec = torch.get_float32_matmul_precision()
+    torch.set_num_threads(threads)
+    torch.set_float32_matmul_precision("medium")
+    try:
+        if kind == "c5":
+            from master_doko_reinforcement_learning_amd.az_network import VOCAB as voc, DokoAzNet as Net
+        else:
+            from master_doko_reinforcement_learning_amd.impi_network import VOCAB_IPI as voc, DokoImpiNet as Net
+        torch.manual_seed(99)
+        net = Net().eval()
+        g = torch.Generator().manual_seed(7)
+        tok = torch.cat([torch.randint(0, v, (batch, 62 if i < 5 else 1), generator=g) for i, v in enumerate(voc)], dim=1)
+        with torch.inference_mode():
+            net(tok[:16])                                                   # warm-up
+            n_ev, t0 = 0, time.perf_counter()
+            while time.perf_counter() - t0 < target_s or n_ev == 0:
+                net(tok)
+                n_ev += batch
+            net_secs = time.perf_counter() - t0
+        net_rate = n_ev / net_secs
+    finally:
+        torch.set_num_threads(prev_threads)
+        torch.set_float32_matmul_precision(prev_prec)
+
+    def timed_pool(work, n):
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(threads) as ex:
+            out = list(ex.map(work, range(n)))
+        return out, time.perf_counter() - t0
+
+    if kind == "c5":
+        iters = args.az_iterations
+
+        def work(k):      # one move decision of a fresh deal (ctypes releases the GIL)
+            st = ol.FdoState.new_game(0xA2000000 + k)
+            st.az_search(None, iters, 4.0, 0.3, 10, 2, 0.5, ol.rng_seed(0xA2 ^ k), alpha=0.8)
+            return iters
+
+        _, t1 = timed_pool(work, threads)
+        n = max(threads, int(threads * target_s / max(t1, 1e-3)))
+        done, secs = timed_pool(work, n)
+        tree_rate = sum(done) / secs
+        evals_per_unit = 1.0
+        unit, sample = "simulations/s", "%d searches of %d PUCT iterations on fresh deals" % (n, iters)
+    else:
+        def infostate(j):
+            st = ol.FdoState.new_game(0xC3000000 + j)
+            for _ in range(4):
+                st.play(24)
+            rng = ol.rng_seed(0xC3100000 + j)
+            st.random_plies(rng, [0, 8, 20, 32][j % 4], True)
+            return st
+
+        def work(k):
+            _, _, _, guesses = infostate(k % 4096).ipi_sample(ol.rng_seed(0xA5000000 + k), args.ar_temperature)
+            return guesses
+
+        _, t1 = timed_pool(work, threads)
+        n = max(threads, int(threads * target_s / max(t1, 1e-3)))
+        done, secs = timed_pool(work, n)
+        tree_rate = n / secs
+        evals_per_unit = float(np.mean(done))
+        unit, sample = "samples/s", "%d AR samples of the C3 infostates (%.1f guesses each)" % (n, evals_per_unit)
+    value = 1.0 / (evals_per_unit / net_rate + 1.0 / tree_rate)
+    return {"value": value, "unit": unit, "cores": threads, "kind": "port", "cpu_quota_cores": quota,
+            "network_evals_per_s": net_rate, "tree_units_per_s": tree_rate, "network_evals_per_unit": evals_per_unit,
+            "sample": "network: %d evaluations in batches of %d (torch-CPU f32, matmul precision 'medium', %d threads, "
+                      "%.1f s); tree: the oracle restatement with its hash network, %s on %d threads (%.1f s); "
+                      "combined serially per evaluation" % (n_ev, batch, threads, net_secs, sample, threads, secs)}
 
 
 def cpu_quota_cores():

@@ -119,3 +119,33 @@ def test_bench_many_ranks(tmp_path, partition, ranks):
     r1, a1, acc1 = _bench(tmp_path, 1, total, "maxn", "q1%d%s" % (ranks, partition), partition)
     assert aN.shape == (total,)
     assert np.array_equal(accN, acc1) and np.array_equal(aN, a1)
+
+
+def _bench_c5(tmp_path, gpus, tag, offset=0):
+    env = dict(os.environ)
+    env["DK_DIST_BACKEND"] = "gloo"
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    rec = str(tmp_path / ("rec_%s" % tag))
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--workload", "c5", "--gpus", str(gpus), "--steps", "2",
+           "--warmup", "1", "--no-cpu-baseline", "--games", "96", "--az-iterations", "24",
+           "--replica-offset", str(offset), "--dump-records", rec]
+    out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=150 + 30 * gpus)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
+    line = [l for l in out.stdout.splitlines() if l.startswith("{")][-1]
+    return json.loads(line), rec
+
+
+def test_bench_c5_replicas_two_ranks(tmp_path):
+    """Config 5 on N GPUs runs N independent self-play replicas (games do not interact; only the
+    barriers and the max-over-ranks time are collective).  Two ranks on one GPU (gloo): each rank's
+    games after three moves (every dk_az_state record: state, announcements) equal a 1-rank run of
+    the same replica (--replica-offset), bit for bit, at the reference's f32 network precision."""
+    r2, rec2 = _bench_c5(tmp_path, 2, "two")
+    assert r2["n_gpus"] == 2 and r2["config"]["parallelism"] == "replicas x2"
+    for rep in (0, 1):
+        r1, rec1 = _bench_c5(tmp_path, 1, "one%d" % rep, offset=rep)
+        assert r1["n_gpus"] == 1
+        a, b = np.load("%s_r%d.npy" % (rec2, rep)), np.load("%s_r%d.npy" % (rec1, rep))
+        assert a.shape == b.shape and np.array_equal(a, b), rep
+    assert not np.array_equal(np.load("%s_r0.npy" % rec2), np.load("%s_r1.npy" % rec2))   # distinct replicas
