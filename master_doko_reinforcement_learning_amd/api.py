@@ -612,13 +612,19 @@ class AlphaZeroSearch:
         seeds_t = torch.as_tensor(np.ascontiguousarray(seeds, dtype=np.uint64).view(np.int64), device=dev)
         roots = roots.contiguous()
         noise = None if noise is None else noise.contiguous().float()
+        # every argument is checked before the first launch (a refused call leaves no batch half begun)
+        if not roots.is_cuda or seeds_t.shape[0] != n:
+            raise ValueError("roots: uint8 [n, %d] on the GPU and seeds [n] expected" % AZ_STATE_BYTES)
+        if noise is not None and (noise.device != dev or tuple(noise.shape) != (n, NUM_ACTIONS)):
+            raise ValueError("noise: float32 [n, %d] on the roots' device expected" % NUM_ACTIONS)
+        if rng_states is not None and (rng_states.dtype != torch.int64 or tuple(rng_states.shape) != (n, 4)
+                                       or not rng_states.is_contiguous() or rng_states.device != dev):
+            raise ValueError("rng_states: contiguous int64 [n, 4] on the roots' device expected")
         ev = torch.empty((n, AZ_STATE_BYTES), dtype=torch.uint8, device=dev)
         need = torch.empty(n, dtype=torch.uint8, device=dev)
         _check(L.dk_az_begin_async(ctx, roots.data_ptr(), seeds_t.data_ptr(), n, iterations, self.epoch,
                                    ev.data_ptr(), st))
         if rng_states is not None:
-            if rng_states.dtype != torch.int64 or tuple(rng_states.shape) != (n, 4) or not rng_states.is_contiguous():
-                raise ValueError("rng_states: contiguous int64 [n, 4] expected")
             _check(L.dk_az_rng_async(ctx, rng_states.data_ptr(), 1, st))
         value, logits = network(ev)
         value, logits = value.float().contiguous(), logits.float().contiguous()

@@ -62,8 +62,8 @@ class Block(nn.Module):
         """c_proj(out(y)) = (Wc Wo) y + (Wc bo + bc): the two back-to-back projections of
         the reference's SelfAttention (MultiheadAttention.out_proj, then c_proj) folded
         into one GEMM for inference (products in f64 on the host, cached until the weights change)."""
-        key = (self.out.weight.data_ptr(), self.c_proj.weight.data_ptr(), self.out.weight._version,
-               self.c_proj.weight._version, self.out.weight.dtype)
+        key = tuple((p.data_ptr(), p._version) for p in (self.out.weight, self.out.bias, self.c_proj.weight,
+                                                          self.c_proj.bias)) + (self.out.weight.dtype,)
         if getattr(self, "_fold_key", None) != key:
             # (in f64 on the host, once per weight version: exact to the storage dtype's rounding,
             # and no BLAS kernel on the device)
@@ -347,8 +347,8 @@ def split_bf16x3(blk):
 def split_attn_bf16x3(blk):
     """The attention half's weights as bf16 hi / lo pairs: Wqkv and the folded projection
     (Block.folded_proj, f32), cached on the block until a weight changes; with the folded f32 bias."""
-    key = (blk.qkv.weight.data_ptr(), blk.qkv.weight._version, blk.out.weight._version, blk.c_proj.weight._version,
-           blk.out.bias._version, blk.c_proj.bias._version)
+    key = tuple((p.data_ptr(), p._version) for p in (blk.qkv.weight, blk.out.weight, blk.out.bias, blk.c_proj.weight,
+                                                     blk.c_proj.bias))
     c = getattr(blk, "_attn_bf16x3", None)
     if c is None or c[0] != key:
         wp, bp = blk.folded_proj()

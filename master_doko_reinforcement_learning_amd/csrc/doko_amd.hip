@@ -969,8 +969,11 @@ struct dk_ctx {
     bool az_root_done = false;
     // glibc logf / powf(., 1 / shape) of the 2^23 Open01<f32> values (rand_distr.h), built on first use
     float* rd_ln = nullptr;
-    float* rd_pw = nullptr;
-    float rd_inv_shape = 0.0f;
+    // powf(u, 1/alpha) tables per shape (alpha < 1), most recently built first: a few alphas in use
+    // on one context (e.g. 0.5 for evaluation, 0.8 for training) each keep their table
+    static constexpr int RD_PW_CACHE = 4;
+    float* rd_pw[RD_PW_CACHE] = {};
+    float rd_inv_shape[RD_PW_CACHE] = {};
     std::vector<void*> scratch;
     std::vector<size_t> scratch_size;
     // results of the synchronous (host-pointer) entry points: DMA into this page-locked buffer,
@@ -1236,8 +1239,10 @@ hipError_t launch_search(dk_ctx* ctx, const dk_state* roots, const uint64_t* see
     const bool lng = iters > dk::P24_MAX_ITERS;
     const bool h16 = ctx->hot_layout ? ctx->hot_layout <= 16 : true;
     // 8-B records where their fields hold the search (visits, state index, slots: P8_MAX_ITERS)
+    // (not with child blocks aligned beyond even slots, DK_BLOCK_ALIGN > 2: the padding could push a
+    // slot index past the 13-bit child_base / 2 field that P8_SLOT_BOUND is proven against)
     const bool h8 = h16 && iters <= dk::P8_MAX_ITERS && ctx->hot_layout != 16 && ctx->p8_ok &&
-                    (ctx->hot_layout == 8 || multi);
+                    ctx->block_align <= 2u && (ctx->hot_layout == 8 || multi);
     if (ctx->wide)   // per-wave pool regions of >= 4 GiB: 64-bit offsets (never with ln in LDS: iterations > 2047)
         return launch_search_t<E, false, dk::NodeHot32W>(ctx, roots, seeds, n, iters, c, visits, values, best, st, 0, rpw, sl, err, rng_io);
     // lane pairs where a single wave per SIMD holds at most 32 roots (DK_PAIR=0 / 1 forces)
@@ -1352,20 +1357,7 @@ dk_ctx* dk_create(const dk_config* cfg) {
     if (pool > cfg->max_roots) pool = cfg->max_roots;
     const uint32_t rpw = ctx->roots_per_wave;
     ctx->pool_roots = (uint32_t)((pool + rpw - 1) / rpw * rpw);   // whole regions of rpw roots
-    if (cap_default) {
-        size_t free_b = 0, total_b = 0;
-        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
-            const uint32_t floor_cap = ((64u + 4u * cfg->max_iterations) + 255u) & ~255u;
-            const size_t per_slot = (getenv("DK_HOT_RECORD") && atoi(getenv("DK_HOT_RECORD")) == 32 ? sizeof(dk::NodeHot32)
-                                                                                                  : sizeof(dk::NodeHot16)) +
-                                    sizeof(dk::NodeCold);
-            while (ctx->cap_slots > floor_cap && (size_t)ctx->pool_roots * ctx->cap_slots * per_slot > free_b / 2)
-                ctx->cap_slots = (ctx->cap_slots / 2 + 255u) & ~255u;
-            if (ctx->cap_slots < floor_cap) ctx->cap_slots = floor_cap < proven ? floor_cap : proven;
-        }
-    }
-    const bool with_fallback = ctx->cap_slots < proven;
-    const size_t R = ctx->pool_roots, S = ctx->cap_slots, T = (size_t)cfg->max_iterations + 1;
+    const size_t T = (size_t)cfg->max_iterations + 1;
     // node states per lane region (>= T): DK_STATE_STRIDE, else T
     size_t ST = T;
     if (const char* e = getenv("DK_STATE_STRIDE")) {
@@ -1373,21 +1365,39 @@ dk_ctx* dk_create(const dk_config* cfg) {
         if (v >= (long long)T) ST = (size_t)v;
     }
     ctx->state_stride = (uint32_t)ST;
-    // Hot records per slot: 16 B (the 8-B, 16-B and long 16-B layouts all fit; rounds 1-4 always
-    // allocated 32 B), 32 B only when DK_HOT_RECORD=32 forces the cached-mean layout or a wave's
-    // regions reach 4 GiB (NodeHot32W, 64-bit offsets).  32-bit pool offsets (GpuMem::at) cover a
-    // wave's region only below 4 GiB: 64 lanes x the capacity x the record, in the main and the
-    // fallback pools, and the node states.
-    {
+    // Hot records per slot for a capacity of S slots: 16 B (the 8-B, 16-B and long 16-B layouts all
+    // fit; rounds 1-4 always allocated 32 B), 32 B only when DK_HOT_RECORD=32 forces the cached-mean
+    // layout or a wave's regions reach 4 GiB (NodeHot32W, 64-bit offsets).  32-bit pool offsets
+    // (GpuMem::at) cover a wave's region only below 4 GiB: 64 lanes x the capacity x the record, in
+    // the main and the fallback pools, and the node states.  The default sizing below prices a slot
+    // with the record this rule then picks.
+    auto hot_rec_for = [&](uint64_t S_, bool* wide) {
         const uint64_t lim = 1ULL << 32, lanes = WAVE;
-        const uint64_t slots = with_fallback ? std::max<uint64_t>(S, proven) : S;
+        const uint64_t slots = S_ < proven ? std::max<uint64_t>(S_, proven) : S_;
         auto wide_at = [&](uint64_t rec) {
             return lanes * slots * rec >= lim || lanes * slots * sizeof(dk::NodeCold) >= lim ||
                    lanes * ST * STATE_SLOT_BYTES >= lim;
         };
-        ctx->hot_rec = ctx->hot_layout == 32 ? sizeof(dk::NodeHot32) : sizeof(dk::NodeHot16);
-        ctx->wide = wide_at(ctx->hot_rec);
-        if (ctx->wide) ctx->hot_rec = sizeof(dk::NodeHot32);
+        size_t rec = ctx->hot_layout == 32 ? sizeof(dk::NodeHot32) : sizeof(dk::NodeHot16);
+        *wide = wide_at(rec);
+        return *wide ? sizeof(dk::NodeHot32) : rec;
+    };
+    if (cap_default) {
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
+            const uint32_t floor_cap = ((64u + 4u * cfg->max_iterations) + 255u) & ~255u;
+            auto per_slot = [&](uint32_t S_) { bool w; return hot_rec_for(S_, &w) + sizeof(dk::NodeCold); };
+            while (ctx->cap_slots > floor_cap && (size_t)ctx->pool_roots * ctx->cap_slots * per_slot(ctx->cap_slots) > free_b / 2)
+                ctx->cap_slots = (ctx->cap_slots / 2 + 255u) & ~255u;
+            if (ctx->cap_slots < floor_cap) ctx->cap_slots = floor_cap < proven ? floor_cap : proven;
+        }
+    }
+    const bool with_fallback = ctx->cap_slots < proven;
+    const size_t R = ctx->pool_roots, S = ctx->cap_slots;
+    {
+        bool wide = false;
+        ctx->hot_rec = hot_rec_for(S, &wide);
+        ctx->wide = wide;
     }
     const size_t HR = ctx->hot_rec;
     bool ok = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) == hipSuccess;
@@ -1485,7 +1495,8 @@ void dk_destroy(dk_ctx* ctx) {
     if (ctx->az_states) (void)hipFree(ctx->az_states);
     if (ctx->az_games) (void)hipFree(ctx->az_games);
     if (ctx->rd_ln) (void)hipFree(ctx->rd_ln);
-    if (ctx->rd_pw) (void)hipFree(ctx->rd_pw);
+    for (float* p : ctx->rd_pw)
+        if (p) (void)hipFree(p);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -2009,24 +2020,54 @@ int dk_az_begin_async(dk_ctx* ctx, const dk_az_state* d_roots, const uint64_t* d
 // The Open01<f32> tables of rand_distr.h: u_k = (1 + k 2^-23) - (1 - 2^-24), k < 2^23, and glibc's
 // logf(u_k) / powf(u_k, inv_shape) -- what Rust's f32::ln / f32::powf call.  Built on the host like
 // the ln(N) table of the UCT search (64 MB at most; rebuilt when the shape changes).
-static int rd_tables(dk_ctx* ctx, float alpha, hipStream_t st) {
+// A table is published in the context only once its copy has succeeded (a failed build leaves
+// no half-initialised table behind); *pw receives the table of this alpha (nullptr for alpha >= 1).
+static int rd_tables(dk_ctx* ctx, float alpha, hipStream_t st, float** pw) {
     constexpr uint32_t K = 1u << 23;
+    constexpr int NC = dk_ctx::RD_PW_CACHE;
     const bool small = alpha < 1.0f;
     const float inv_shape = 1.0f / alpha;
-    if (ctx->rd_ln && (!small || (ctx->rd_pw && ctx->rd_inv_shape == inv_shape))) return DK_OK;
+    *pw = nullptr;
+    int hit = -1;
+    for (int i = 0; i < NC && small; ++i)
+        if (ctx->rd_pw[i] && ctx->rd_inv_shape[i] == inv_shape) hit = i;
+    if (ctx->rd_ln && (!small || hit >= 0)) {
+        if (hit > 0) {   // most recently used first
+            float* p = ctx->rd_pw[hit]; const float v = ctx->rd_inv_shape[hit];
+            for (int i = hit; i > 0; --i) { ctx->rd_pw[i] = ctx->rd_pw[i - 1]; ctx->rd_inv_shape[i] = ctx->rd_inv_shape[i - 1]; }
+            ctx->rd_pw[0] = p; ctx->rd_inv_shape[0] = v;
+        }
+        if (small) *pw = ctx->rd_pw[0];
+        return DK_OK;
+    }
     std::vector<float> h(K);
     auto u_of = [](uint32_t k) { return __builtin_bit_cast(float, k | 0x3F800000u) - (1.0f - FLT_EPSILON / 2.0f); };
-    if (hipStreamSynchronize(st) != hipSuccess) return DK_E_LAUNCH;   // (a running root kernel may read the table)
+    if (hipStreamSynchronize(st) != hipSuccess) return DK_E_LAUNCH;   // (a running root kernel may read the tables)
+    auto build = [&](float** slot, bool log_table) -> int {
+        for (uint32_t k = 0; k < K; ++k) h[k] = log_table ? logf(u_of(k)) : powf(u_of(k), inv_shape);
+        float* d = nullptr;
+        if (hipMalloc(&d, K * sizeof(float)) != hipSuccess) return DK_E_CAPACITY;
+        if (hipMemcpy(d, h.data(), K * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) {
+            (void)hipFree(d);
+            return DK_E_LAUNCH;
+        }
+        *slot = d;
+        return DK_OK;
+    };
     if (!ctx->rd_ln) {
-        for (uint32_t k = 0; k < K; ++k) h[k] = logf(u_of(k));
-        if (hipMalloc(&ctx->rd_ln, K * sizeof(float)) != hipSuccess) { ctx->rd_ln = nullptr; return DK_E_CAPACITY; }
-        if (hipMemcpy(ctx->rd_ln, h.data(), K * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) return DK_E_LAUNCH;
+        float* d = nullptr;
+        const int rc = build(&d, true);
+        if (rc != DK_OK) return rc;
+        ctx->rd_ln = d;
     }
-    if (small && !(ctx->rd_pw && ctx->rd_inv_shape == inv_shape)) {
-        for (uint32_t k = 0; k < K; ++k) h[k] = powf(u_of(k), inv_shape);
-        if (!ctx->rd_pw && hipMalloc(&ctx->rd_pw, K * sizeof(float)) != hipSuccess) { ctx->rd_pw = nullptr; return DK_E_CAPACITY; }
-        if (hipMemcpy(ctx->rd_pw, h.data(), K * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) return DK_E_LAUNCH;
-        ctx->rd_inv_shape = inv_shape;
+    if (small) {
+        float* d = nullptr;
+        const int rc = build(&d, false);
+        if (rc != DK_OK) return rc;
+        if (ctx->rd_pw[NC - 1]) (void)hipFree(ctx->rd_pw[NC - 1]);   // evict the least recently used shape
+        for (int i = NC - 1; i > 0; --i) { ctx->rd_pw[i] = ctx->rd_pw[i - 1]; ctx->rd_inv_shape[i] = ctx->rd_inv_shape[i - 1]; }
+        ctx->rd_pw[0] = d; ctx->rd_inv_shape[0] = inv_shape;
+        *pw = d;
     }
     return DK_OK;
 }
@@ -2037,10 +2078,11 @@ int dk_az_root_async(dk_ctx* ctx, const float* d_value, const float* d_logits, c
     dk::rd::Open01Tab tab{nullptr, nullptr};
     if (!d_noise) {
         if (!dk::rd::dirichlet_alpha_ok(dirichlet_alpha)) return DK_E_INVALID;
-        const int rc = rd_tables(ctx, dirichlet_alpha, pick(ctx, stream));
+        float* pw = nullptr;
+        const int rc = rd_tables(ctx, dirichlet_alpha, pick(ctx, stream), &pw);
         if (rc) return ctx->last_error = rc;
         tab.ln = ctx->rd_ln;
-        tab.pw = ctx->rd_pw;
+        tab.pw = pw;
     }
     hipLaunchKernelGGL(az_root_kernel, dim3(grid_for(ctx->az_n, 64)), dim3(64), 0, pick(ctx, stream), d_value, d_logits,
                        d_noise, dirichlet_alpha, tab, dirichlet_epsilon, ctx->az_epoch, ctx->az_n, ctx->az_nodes,

@@ -134,9 +134,12 @@ DK_HD float gamma_sample(const GammaF32& g, Rng& r, const Open01Tab& t) {
     return gamma_large(g, r, t);
 }
 
-// Dirichlet<f32, 39>::sample, FromGamma (all alphas equal here).  Alphas <= 0.1 take the
-// crate's Beta construction, which the reference's configurations never use (0.5, 0.8, 1.0):
-// the caller refuses them.
+// Dirichlet<f32, 39>::sample, FromGamma (all alphas equal here).  Alphas <= 0.1 make the crate
+// take its FromBeta stick-breaking construction (Cheng's Beta algorithms, restated in
+// oracle/rand_distr05.hpp); its f32 ln / exp of arbitrary arguments cannot be reproduced
+// glibc-exactly on the device (glibc's logf / expf differ from the correctly rounded value on
+// ~2e-4 / 8e-5 of all inputs, and no table covers them), so the device does not draw it:
+// dk_az_root_async refuses such an alpha without caller noise (DK_E_INVALID).
 DK_HD void dirichlet39(float alpha, Rng& r, const Open01Tab& t, float out[39]) {
     const GammaF32 g = gamma_new(alpha);
     float sum = 0.0f;

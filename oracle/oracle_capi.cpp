@@ -397,6 +397,12 @@ int or_dirichlet(float alpha, int n, uint32_t n_draws, uint64_t* rng_state, floa
     rng_to(r, rng_state);
     return 1;
 }
+void or_beta(float a, float b, uint32_t n, uint64_t* rng_state, float* out) {
+    SmallRng r = rng_from(rng_state);
+    const rdist::Beta g(a, b);
+    for (uint32_t i = 0; i < n; ++i) out[i] = g.sample(r);
+    rng_to(r, rng_state);
+}
 void or_gamma(float shape, uint32_t n, uint64_t* rng_state, float* out) {
     SmallRng r = rng_from(rng_state);
     const rdist::Gamma g(shape);

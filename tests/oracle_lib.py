@@ -87,6 +87,7 @@ def lib():
                                             ctypes.c_int, ctypes.c_int, ctypes.c_float, u64p, u32p, f32p]),
             "or_dirichlet": (ctypes.c_int, [ctypes.c_float, ctypes.c_int, ctypes.c_uint32, u64p, f32p]),
             "or_gamma": (None, [ctypes.c_float, ctypes.c_uint32, u64p, f32p]),
+            "or_beta": (None, [ctypes.c_float, ctypes.c_float, ctypes.c_uint32, u64p, f32p]),
             "or_normal_f64": (None, [ctypes.c_uint32, u64p, f64p]),
             "or_exp1_f64": (None, [ctypes.c_uint32, u64p, f64p]),
             "or_ziggurat_tables": (None, [f64p]),

@@ -20,16 +20,17 @@ def _z(x, mean, var, n):
     return abs(float(np.mean(x)) - mean) / np.sqrt(var / n)
 
 
-@pytest.mark.parametrize("alpha", [0.5, 0.8, 1.0, 2.5])
+@pytest.mark.parametrize("alpha", [0.05, 0.1, 0.5, 0.8, 1.0, 2.5])
 def test_dirichlet_moments(alpha):
     """Dirichlet([alpha; 39]) (async_mcts.rs:111): 10^6 draws; every component has mean 1/39 and
-    variance alpha (a0 - alpha) / (a0^2 (a0 + 1)), a0 = 39 alpha; each draw sums to 1."""
+    variance alpha (a0 - alpha) / (a0^2 (a0 + 1)), a0 = 39 alpha; each draw sums to 1.  alpha <= 0.1
+    takes the crate's FromBeta stick-breaking construction (components may underflow to 0 in f32)."""
     n, k = 1_000_000, 39
     out = np.zeros(n * k, dtype=np.float32)
     rng = _rng(1234 + int(alpha * 10))
     assert ol.lib().or_dirichlet(ctypes.c_float(alpha), k, n, rng, out.ctypes.data_as(ctypes.POINTER(ctypes.c_float))) == 1
     x = out.reshape(n, k).astype(np.float64)
-    assert np.all(x > 0)
+    assert np.all(x > 0) if alpha > 0.1 else np.all(x >= 0)
     assert np.allclose(x.sum(axis=1), 1.0, atol=1e-5)
     a0 = k * alpha
     mean, var = 1.0 / k, alpha * (a0 - alpha) / (a0 * a0 * (a0 + 1.0))
@@ -75,3 +76,18 @@ def test_ziggurat_tables_shape():
         assert np.all(np.diff(x) < 0) and x[-1] == 0.0 and np.all(np.diff(f) > 0) and f[-1] == 1.0
     assert "%.18f" % nx[0] == "3.910757959537090045" and "%.18f" % nx[2] == "3.449278298560964462"
     assert "%.18f" % nf[0] == "0.000477467764586655" and "%.18f" % t[1028] == "3.654152885361008796"
+
+
+@pytest.mark.parametrize("a,b", [(0.1, 3.8), (0.05, 0.05), (0.5, 0.5), (3.0, 0.7), (2.5, 4.0), (1.5, 1.2)])
+def test_beta_moments(a, b):
+    """Beta(a, b) (Cheng's BC for min(a, b) <= 1, BB otherwise; the parameter switch both ways):
+    mean a / (a + b), variance a b / ((a + b)^2 (a + b + 1)) over 10^6 draws."""
+    n = 1_000_000
+    out = np.zeros(n, dtype=np.float32)
+    ol.lib().or_beta(ctypes.c_float(a), ctypes.c_float(b), n, _rng(31), out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)))
+    x = out.astype(np.float64)
+    assert np.all((x >= 0) & (x <= 1))
+    s = a + b
+    mean, var = a / s, a * b / (s * s * (s + 1.0))
+    assert _z(x, mean, var, n) < 5.0
+    assert abs(np.var(x) / var - 1.0) < 0.02
