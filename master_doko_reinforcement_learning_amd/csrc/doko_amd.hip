@@ -1193,7 +1193,8 @@ hipError_t launch_search_t(dk_ctx* ctx, const dk_state* roots, const uint64_t* s
     }
     hipLaunchKernelGGL(kern, dim3(grid), dim3(WAVE), lds_bytes, st, roots, seeds, n, iters, c, ctx->ln_table,
                        ctx->hot, ctx->cold, (typename E::Node*)ctx->states, ctx->ovf, ctx->ovf_st, ctx->cap_slots,
-                       ctx->state_stride, ctx->block_align,
+                       ctx->state_stride,
+                       ctx->block_align == dk::BALIGN_LINE ? dk::BALIGN_LINE | (uint32_t)(128 / sizeof(H)) : ctx->block_align,
                        rpw, lp, visits, values, best, err, sl.queue, ctx->prof,
                        ordered ? (const uint32_t*)sl.order : (const uint32_t*)nullptr,
                        fallback ? sl.retry : (uint32_t*)nullptr, (const uint32_t*)nullptr, ctx->high_water, perm, base,
@@ -1239,10 +1240,11 @@ hipError_t launch_search(dk_ctx* ctx, const dk_state* roots, const uint64_t* see
     const bool lng = iters > dk::P24_MAX_ITERS;
     const bool h16 = ctx->hot_layout ? ctx->hot_layout <= 16 : true;
     // 8-B records where their fields hold the search (visits, state index, slots: P8_MAX_ITERS)
-    // (not with child blocks aligned beyond even slots, DK_BLOCK_ALIGN > 2: the padding could push a
-    // slot index past the 13-bit child_base / 2 field that P8_SLOT_BOUND is proven against)
+    // (with child blocks placed beyond even slots -- DK_BLOCK_ALIGN > 2 or "line" -- only while the main
+    // pool's capacity keeps every slot index within the 13-bit child_base / 2 field: the capacity
+    // check then bounds the padded blocks; the fallback pass packs, P8_SLOT_BOUND)
     const bool h8 = h16 && iters <= dk::P8_MAX_ITERS && ctx->hot_layout != 16 && ctx->p8_ok &&
-                    ctx->block_align <= 2u && (ctx->hot_layout == 8 || multi);
+                    (ctx->block_align <= 2u || ctx->cap_slots <= (1u << 14)) && (ctx->hot_layout == 8 || multi);
     if (ctx->wide)   // per-wave pool regions of >= 4 GiB: 64-bit offsets (never with ln in LDS: iterations > 2047)
         return launch_search_t<E, false, dk::NodeHot32W>(ctx, roots, seeds, n, iters, c, visits, values, best, st, 0, rpw, sl, err, rng_io);
     // lane pairs where a single wave per SIMD holds at most 32 roots (DK_PAIR=0 / 1 forces)
@@ -1338,8 +1340,11 @@ dk_ctx* dk_create(const dk_config* cfg) {
     }
     if (const char* e = getenv("DK_VERBOSE")) ctx->verbose = atoi(e) != 0;
     if (const char* e = getenv("DK_BLOCK_ALIGN")) {
+        // a power of two 1..64: blocks start at multiples of it; "line": blocks kept within one
+        // 128-B line (search_core.h block_base; the launch passes the line's slots per layout)
         const int v = atoi(e);
         if (v >= 1 && v <= 64 && (v & (v - 1)) == 0) ctx->block_align = (uint32_t)v;
+        else if (strcmp(e, "line") == 0) ctx->block_align = dk::BALIGN_LINE;
     }
     if (const char* e = getenv("DK_PAIR")) ctx->pair = atoi(e) != 0 ? 1 : 0;
     if (const char* e = getenv("DK_LN_LDS")) ctx->ln_in_lds = atoi(e) != 0;

@@ -205,6 +205,22 @@ static constexpr uint32_t NI_MAX_STATES = 1u << 22;
 #define DK_DEFER_BACKUP 0
 #endif
 static constexpr int PROF_SLOTS = 40;   // per-root counters of the profiling build (DK_PHASE_PROF)
+// Child-block placement (GpuMem::balign / HostMem::balign): a power of two A >= 1 starts every block
+// at a multiple of A slots; BALIGN_LINE | L (L a power of two: the slots of one 128-B line) packs
+// blocks but moves one that would straddle a line boundary to the next line, so that a block of at
+// most L slots is one line -- one DRAM line per selection level instead of 1.6 on average with
+// 8-B records (a random 8 / 16-B access moves a whole 128-B line) -- and a larger one starts a line.  `pb`: the block's slots (8-B
+// records: rounded up to even).  Placement never changes results, only slot indices.
+static constexpr uint32_t BALIGN_LINE = 0x80000000u;
+DK_HD uint32_t block_base(uint32_t next, uint32_t pb, uint32_t balign) {
+    if (balign & BALIGN_LINE) {
+        const uint32_t line = balign & 0xFFFFu;
+        const uint32_t off = next & (line - 1u);
+        if (pb > line) return off ? next + (line - off) : next;        // (a larger block: whole lines)
+        return off + pb > line ? next + (line - off) : next;
+    }
+    return (next + balign - 1u) & ~(balign - 1u);
+}
 static constexpr int MAX_DEPTH = 512;   // selection path bound (LDS part + global overflow)
 
 DK_HD int sel4i(const int r[4], int p) { return p == 0 ? r[0] : (p == 1 ? r[1] : (p == 2 ? r[2] : r[3])); }
@@ -1039,9 +1055,9 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
             const int a = ctz64(bit);
             const uint32_t block = nch + (uint32_t)popc64(cd.unexpanded);
             if (nch == 0) {
-                // (8-B records: blocks start at even slots, next_slot stays even; mem.balign >= 1 may
-                // align them further, e.g. to whole 128-B lines)
-                const uint32_t base = (next_slot + mem.balign - 1u) & ~(mem.balign - 1u);
+                // (8-B records: blocks start at even slots, next_slot stays even; mem.balign may align
+                // them further or keep them within one 128-B line, block_base)
+                const uint32_t base = block_base(next_slot, P8 ? (block + 1u) & ~1u : block, mem.balign);
                 if (base + block > mem.cap_slots || next_state >= mem.cap_states || next_state >= NI_MAX_STATES) {
                     status = SR_CAPACITY;
                     break;

@@ -6,6 +6,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <vector>
+#include <algorithm>
 
 #include "../../master_doko_reinforcement_learning_amd/csrc/engine/adapters.h"
 #include "../../master_doko_reinforcement_learning_amd/csrc/engine/search_core.h"
@@ -26,10 +27,15 @@ template <class E, class OEnv>
 static void compare(const dk_state& packed, const OEnv& oenv, uint64_t seed, uint32_t iters, double c,
                     const double* ln, uint32_t max_path, int idx, const char* name) {
     typename E::Work w; E::load(packed, w);
+    // DK_BALIGN_LINE=1: blocks kept within 128-B lines (dk::block_base), the padding given room
+    const bool line = getenv("DK_BALIGN_LINE") != nullptr;
 #if DK_HOT8
-    HostMem8<typename E::Node> mem(dk::P8_SLOT_BOUND(iters), iters + 1, max_path);
+    HostMem8<typename E::Node> mem(line ? std::min<uint32_t>(2 * dk::P8_SLOT_BOUND(iters), 1u << 14) : dk::P8_SLOT_BOUND(iters),
+                                   iters + 1, max_path);
+    if (line) mem.balign = dk::BALIGN_LINE | 16u;
 #else
-    HostMem<typename E::Node> mem(40 + 12 * iters, iters + 1, max_path);
+    HostMem<typename E::Node> mem((40 + 12 * iters) * (line ? 2 : 1), iters + 1, max_path);
+    if (line) mem.balign = dk::BALIGN_LINE | 8u;
 #endif
     mem.ln_table = ln;
     dk::Rng rng = dk::Rng::seed_from_u64(seed);

@@ -79,6 +79,15 @@ def test_hot8_variant_exact(native_bins):
     assert _run("search_check8", 4, 1000, 11, 2) > 4
 
 
+def test_line_block_placement_exact(native_bins, monkeypatch):
+    """Child blocks kept within 128-B lines (search_core.h block_base, DK_BLOCK_ALIGN=line): slot
+    placement only, so the searches still equal the oracle's, for 8-B and 16-B records."""
+    monkeypatch.setenv("DK_BALIGN_LINE", "1")
+    assert _run("search_check8", 8, 400, 9) > 10
+    assert _run("search_check8", 4, 1000, 11, 2) > 4
+    assert _run("search_check", 6, 400, 5) > 10
+
+
 def test_engine_cap_vs_oracle(native_bins):
     """cap_engine.h (host build) = oracle card_matching_full; samples always consistent."""
     assert _run("cap_check", 120, 3) > 5000
