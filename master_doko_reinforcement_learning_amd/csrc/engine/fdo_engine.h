@@ -720,6 +720,25 @@ DK_HD int rollout_cards(const Work& w0, Rng& rng, int pts[4]) {
                 draws();
                 play(A3, T3, (s + 3u) & 3u, false, 3u, true);
             } else {
+#if defined(DK_TRICK_DOUBLE) && defined(__HIP_DEVICE_COMPILE__)
+                // measurement builds: a fast-path trick whose wave has at most DK_TRICK_DOUBLE active
+                // lanes is played once more on copies (result discarded, kept alive): the time it adds
+                // prices the rollout's sparse trips (the wave runs its longest lane's tricks)
+                if (popc64(__builtin_amdgcn_ballot_w64(true)) <= DK_TRICK_DOUBLE) {
+                    const Rng rs = rng;
+                    uint32_t a0 = A0, a1 = A1, a2 = A2, a3 = A3, t0 = T0, t1 = T1, t2 = T2, t3 = T3;
+                    const uint32_t sl = lead, sb = best_pos, sw = win_card, se = t_eyes, sd = da_bits, slt = lt;
+                    const int sk = best_key, spl = plies;
+                    play(a0, t0, s, true, 0u, false);
+                    play(a1, t1, (s + 1u) & 3u, false, 1u, false);
+                    play(a2, t2, (s + 2u) & 3u, false, 2u, false);
+                    play(a3, t3, (s + 3u) & 3u, false, 3u, false);
+                    asm volatile("" :: "v"(a0 ^ a1 ^ a2 ^ a3), "v"(t0 ^ t1 ^ t2 ^ t3), "v"(best_pos), "v"(t_eyes), "v"(da_bits),
+                                 "v"(win_card), "v"((uint32_t)rng.s0));
+                    rng = rs; lead = sl; best_pos = sb; win_card = sw; t_eyes = se; da_bits = sd; lt = slt; best_key = sk;
+                    plies = spl;
+                }
+#endif
                 play(A0, T0, s, true, 0u, false);
                 play(A1, T1, (s + 1u) & 3u, false, 1u, false);
                 play(A2, T2, (s + 2u) & 3u, false, 2u, false);

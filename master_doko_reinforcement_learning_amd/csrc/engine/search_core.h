@@ -1086,6 +1086,18 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
             // a forced chain grew: its head now points at the new end
             if (block == 1 && chain_head != 0xFFFFFFFFu) mem.store_child_base(chain_head, child, chain_info);
             DK_STAMP_DRAINED(te0);
+#if defined(DK_EXP_DOUBLE) && defined(__HIP_DEVICE_COMPILE__)
+            {   // measurement builds: the expansion's transition and action set once more on a copy
+                Work w2 = E::unpack_node(packed);
+                const uint64_t al2 = E::allowed(w2, false);
+                E::step(w2, a);
+                const auto n2 = E::pack_node(w2);
+                uint32_t k2 = (uint32_t)al2 ^ (uint32_t)(al2 >> 32), wd[sizeof(n2) / 4];
+                __builtin_memcpy(wd, &n2, sizeof(wd));
+                for (uint32_t i = 0; i < sizeof(n2) / 4; ++i) k2 ^= wd[i];
+                asm volatile("" :: "v"(k2));
+            }
+#endif
             E::step(w, a);
             DK_STAMP_DRAINED(te1);
             DK_PROF(mem, 12, te1 - te0);
@@ -1123,6 +1135,14 @@ DK_HD int search_root(const typename E::Work& root, Rng& rng, uint32_t iters, do
         DK_PROF(mem, 1, t2 - t1);
         // ---------------- rollout
         int r[4];
+#if defined(DK_ROLL_DOUBLE) && defined(__HIP_DEVICE_COMPILE__)
+        {   // measurement builds: the rollout played a second time on copies (result discarded, kept
+            // alive): the VALU instructions / time it adds are the rollout's (profiles/r06/valu_by_phase.json)
+            Rng r2 = rng; int q[4];
+            const int p2 = E::rollout(w, r2, q);
+            asm volatile("" :: "v"(p2), "v"(q[0]), "v"(q[1]), "v"(q[2]), "v"(q[3]), "v"((uint32_t)r2.s0));
+        }
+#endif
         [[maybe_unused]] const int rplies = E::rollout(w, rng, r);
         DK_PROF(mem, 10, (uint64_t)rplies);
         DK_PROF_WAVEMAX(11, rplies);
