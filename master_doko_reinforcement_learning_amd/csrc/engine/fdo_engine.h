@@ -582,6 +582,9 @@ DK_HD int round_draws(const Work& w) {
 #ifndef DK_ROLLOUT_FAST
 #define DK_ROLLOUT_FAST 1   // tricks without announcement offers skip the per-card offer tests
 #endif
+#ifndef DK_FOX_SKIP
+#define DK_FOX_SKIP 0       // (measurement switch) fast tricks skip the fox tracking once no lane holds a Diamond Ace
+#endif
 DK_HD int rollout_cards(const Work& w0, Rng& rng, int pts[4]) {
     uint32_t any0, any1, any2, any3, two0, two1, two2, two3;
     {
@@ -640,7 +643,7 @@ DK_HD int rollout_cards(const Work& w0, Rng& rng, int pts[4]) {
     // one card of player p, whose hand is (a, t2), at position `pos` of the trick; updates the
     // hand and the running trick.  `track` keeps the hand sizes (nb) per card, which only the
     // announcement offers read (draws).
-    auto play = [&](uint32_t& a, uint32_t& t2, uint32_t p, bool first, uint32_t pos, bool track) {
+    auto play = [&](uint32_t& a, uint32_t& t2, uint32_t p, bool first, uint32_t pos, bool track, bool fox = true) {
         const uint32_t f = a & lead;
         const uint32_t legal = f ? f : a;
         const uint32_t r = rng.range_u32((uint32_t)popc32(legal));
@@ -670,7 +673,8 @@ DK_HD int rollout_cards(const Work& w0, Rng& rng, int pts[4]) {
         best_pos = better ? pos : best_pos;
         win_card = better ? card : win_card;
         t_eyes = (first ? 0u : t_eyes) + ((ci.x >> 24) & 15u);
-        da_bits = (first ? 0u : da_bits) | (card == (uint32_t)DIAMOND_ACE ? 1u << p : 0u);
+        // (fox = false: no lane of the wave holds a Diamond Ace, so none is played: nothing to track)
+        da_bits = fox ? (first ? 0u : da_bits) | (card == (uint32_t)DIAMOND_ACE ? 1u << p : 0u) : 0u;
         plies += 1;
     };
     // collapsed announcement round after a card: one forced draw per offered player
@@ -739,10 +743,21 @@ DK_HD int rollout_cards(const Work& w0, Rng& rng, int pts[4]) {
                     plies = spl;
                 }
 #endif
-                play(A0, T0, s, true, 0u, false);
-                play(A1, T1, (s + 1u) & 3u, false, 1u, false);
-                play(A2, T2, (s + 2u) & 3u, false, 2u, false);
-                play(A3, T3, (s + 3u) & 3u, false, 3u, false);
+#if DK_FOX_SKIP
+                // once no lane of the wave holds a Diamond Ace (the fox, stats/**), its per-card tracking is skipped
+                if (!wave_any((((A0 | A1 | A2 | A3) >> (uint32_t)DIAMOND_ACE) & 1u) != 0u)) {
+                    play(A0, T0, s, true, 0u, false, false);
+                    play(A1, T1, (s + 1u) & 3u, false, 1u, false, false);
+                    play(A2, T2, (s + 2u) & 3u, false, 2u, false, false);
+                    play(A3, T3, (s + 3u) & 3u, false, 3u, false, false);
+                } else
+#endif
+                {
+                    play(A0, T0, s, true, 0u, false);
+                    play(A1, T1, (s + 1u) & 3u, false, 1u, false);
+                    play(A2, T2, (s + 2u) & 3u, false, 2u, false);
+                    play(A3, T3, (s + 3u) & 3u, false, 3u, false);
+                }
                 nb -= 0x01010101u;
             }
             const uint32_t bp = best_pos;
