@@ -475,6 +475,9 @@ DK_HD void play_action(Work& w, int a) {
 }
 
 // ---- DKV scoring (stats/stats.rs:46-243 and stats/**) -------------------------
+#ifndef DK_SCORE_FAST
+#define DK_SCORE_FAST 0     // (measurement switch) score() without announcements takes a short path
+#endif
 struct Flags { bool ann, u90, u60, u30, black, none, o_ann, o_90, o_60, o_30, o_black; };
 DK_HD Flags ann_flags(uint32_t prev) {
     Flags f;
@@ -497,6 +500,38 @@ DK_HD void score(const Work& w, int pts[4]) {
     }
     const bool re_all = re_t == 12, ko_all = ko_t == 12;
     const uint32_t rp = all_higher_than(w.re_lowest), kp = all_higher_than(w.contra_lowest);
+#if DK_SCORE_FAST
+    // Neither team announced (every lane of the wave: the rollouts' usual case, nobody announces
+    // in them): of the winning conditions only `eyes >= 121 && R.none && K.none` (Re) and
+    // `eyes >= 120 && ...` (Kontra) remain, and as re_eyes + ko_eyes = 240 exactly one holds; the
+    // game value is the loser's thresholds plus "schwarz" -- the general path below gives the same.
+    if (!wave_any(rp != 0u || kp != 0u)) {
+        const bool rw = re_eyes >= 121;
+        const bool is_solo = popc32(re) == 1;
+        int ra = 0, ka = 0;
+        if (!is_solo) {
+            if (!rw) { ka += 1; ra -= 1; }                      // team_win == Kontra
+            ra += doko_re - doko_ko; ka += doko_ko - doko_re;
+            int fre = 0, fko = 0;
+            for (int i = 0; i < 2; ++i) {
+                if (i >= w.fox_n) break;
+                const uint8_t ev = i == 0 ? w.fox0 : w.fox1;
+                const bool by_re = (re >> (ev >> 2)) & 1, win_re = (re >> (ev & 3)) & 1;
+                if (by_re != win_re) { if (win_re) fre++; else fko++; }
+            }
+            ra += fre - fko; ka += fko - fre;
+            if (w.karl) { if ((re >> (w.karl - 1)) & 1) { ra += 1; ka -= 1; } else { ra -= 1; ka += 1; } }
+        }
+        const uint32_t loser = rw ? ko_eyes : re_eyes;
+        const int v = 1 + (loser < 90) + (loser < 60) + (loser < 30) + ((rw ? re_all : ko_all) ? 1 : 0);
+        int re_pts = (rw ? v : -v) + ra;
+        const int ko_pts = (rw ? -v : v) + ka;
+        if (is_solo) re_pts *= 3;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) pts[p] = ((re >> p) & 1) ? re_pts : ko_pts;
+        return;
+    }
+#endif
     const Flags R = ann_flags(rp), K = ann_flags(kp);
     const bool rw =
         (re_eyes >= 121 && R.none && K.none) || (re_eyes >= 121 && R.o_ann && !K.ann) || (re_eyes >= 121 && R.o_ann && K.o_ann) ||
