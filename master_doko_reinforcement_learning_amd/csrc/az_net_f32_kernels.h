@@ -560,7 +560,11 @@ __global__ void __launch_bounds__(64 * WAVES, D <= 160 ? 8 / WAVES : 1) mlp_ln_f
         for (int s2 = 0; s2 < GS; ++s2) {
             float g[8];
 #pragma unroll
+#ifndef DK_SOL_NOGELU
             for (int t = 0; t < 8; ++t) g[t] = gelu_poly(acc1[8 * s2 + t]);
+#else
+            for (int t = 0; t < 8; ++t) g[t] = acc1[8 * s2 + t];   // (speed-of-light measurement build)
+#endif
             split_bf16x8(g, afh[s2], afl[s2]);
         }
         DK_FSTAMP(2);
