@@ -416,25 +416,29 @@ class FusedTrunkF32(FusedTrunk):
         w, b = blk.folded_proj()
         return self.add_ln(x, _f32c(F.linear(y, w)), ln, b)
 
+    def chain(self, blocks):
+        """True when `run` takes the x-only chain over these blocks (DK_F32_XCHAIN=0: the h-in / h-out
+        chain, a measurement switch)."""
+        return (self.d in (160, 256) and len(blocks) > 0 and all(self.ex_ok(blk) for blk in blocks)
+                and os.environ.get("DK_F32_XCHAIN", "1") != "0")
+
     def run(self, h, blocks, final_ln, x=None):
-        # (DK_F32_XCHAIN=0: the h-in / h-out chain, a measurement switch)
-        if not (self.d == 256 and len(blocks) > 0 and all(self.ex_ok(blk) for blk in blocks)) or \
-                os.environ.get("DK_F32_XCHAIN", "1") == "0":
+        if not self.chain(blocks):
             return super().run(h, blocks, final_ln, x)
-        # d = 256: every half after the first reads the residual stream x and applies the
-        # LayerNorm its producer used to write out as h (the *_ex kernels); only the last half
-        # writes h (the final LayerNorm, for the heads).  Per half, x in and out instead of h in,
-        # x in and out, h out.
+        # d = 256 (round 5) and d = 160 (round 6): every half reads the residual stream x and applies
+        # the LayerNorm its producer used to write out as h (the *_ex kernels; at d = 160 also the
+        # first half, from x and ln_1); only the last half writes h (the final LayerNorm, for the
+        # heads).  Per half, x in and out instead of h in, x in and out, h out.
         x = self.x if x is None else x
         for i, blk in enumerate(blocks):
             wqh, wql, wph, wpl, bpf = split_attn_bf16x3(blk)
-            lin = None if i == 0 else blk.ln_1
+            lin = None if (i == 0 and self.d == 256) else blk.ln_1
             self.ck(self.L.dk_net_qkv_attn_ln_f32x3_ex_async(
-                h.data_ptr() if i == 0 else None, x.data_ptr(), lin.weight.data_ptr() if lin else None,
+                h.data_ptr() if lin is None else None, x.data_ptr(), lin.weight.data_ptr() if lin else None,
                 lin.bias.data_ptr() if lin else None, lin.eps if lin else 0.0, wqh.data_ptr(), wql.data_ptr(),
-                blk.qkv.bias.data_ptr(), wph.data_ptr(), wpl.data_ptr(), bpf.data_ptr(), x.shape[0], 4, 64, None, None,
-                0.0, None, self.st))
-            last = i + 1 == len(blocks)
+                blk.qkv.bias.data_ptr(), wph.data_ptr(), wpl.data_ptr(), bpf.data_ptr(), x.shape[0], 4, self.d // 4, None,
+                None, 0.0, None, self.st))
+            last = i + 1 == len(blocks) and final_ln is not None   # (final_ln None: no h at all)
             w1h, w1l, w2h, w2l = split_bf16x3(blk)
             ho = torch.empty_like(x) if last else None
             self.ck(self.L.dk_net_mlp_ln_f32x3_ex_async(
@@ -509,9 +513,12 @@ class DokoAzNet(nn.Module):
         if not (self.blocks and self.p_blocks and self.v_blocks):
             raise ValueError("the fused forward needs shared, policy and value blocks")
         f = (trunk or FusedTrunk)(tokens, self.emb, self.blocks[0].ln_1)
-        hp = f.run(f.h, self.blocks, self.p_blocks[0].ln_1)       # f.x now holds the shared trunk's output
+        # (f32 at d = 160: every half normalises x itself, so the branch inputs need no h)
+        x_only = isinstance(f, FusedTrunkF32) and f.d == 160 and all(f.chain(b) for b in (self.blocks, self.p_blocks,
+                                                                                          self.v_blocks))
+        hp = f.run(f.h, self.blocks, None if x_only else self.p_blocks[0].ln_1)   # f.x: the shared trunk's output
         xv = f.x.clone()
-        hv = f.add_ln(xv, None, self.v_blocks[0].ln_1)
+        hv = None if x_only else f.add_ln(xv, None, self.v_blocks[0].ln_1)
         hp = f.run(hp, self.p_blocks, self.p_ln)
         hv = f.run(hv, self.v_blocks, self.v_ln, x=xv)
         return self.value_head(hv), self.policy_head(hp)

@@ -383,14 +383,20 @@ __device__ __forceinline__ void split_bf16x8(const float (&v)[8], bf16x8_t& hi, 
     lo = b.v;
 }
 
-template <int D, int NC, int WAVES = 4>
+// XIN (round 6, the d = 160 x-only chain; as mlp16_ln_f32x3_kernel at d = 256): the input is the
+// residual stream x_io itself (h unused), normalised here with (gin, bin, eps_in) -- the lane pair
+// (r, r + 32) holds the row, so the LayerNorm reduces over one xor-32 exchange; h_out == nullptr:
+// x only is written.
+template <int D, int NC, int WAVES = 4, bool XIN = false>
 __global__ void __launch_bounds__(64 * WAVES, D <= 160 ? 8 / WAVES : 1) mlp_ln_f32x3_kernel(const float* __restrict__ h, float* __restrict__ x_io,
                                                                 const uint16_t* __restrict__ w1h, const uint16_t* __restrict__ w1l,
                                                                 const float* __restrict__ b1,
                                                                 const uint16_t* __restrict__ w2h, const uint16_t* __restrict__ w2l,
                                                                 const float* __restrict__ b2, uint32_t rows, uint32_t n_hidden,
                                                                 const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                                float eps, float* __restrict__ h_out) {
+                                                                float eps, float* __restrict__ h_out,
+                                                                const float* __restrict__ gin = nullptr,
+                                                                const float* __restrict__ bin = nullptr, float eps_in = 0.0f) {
     static_assert(D % 32 == 0 && NC == 32, "d: multiple of 32; chunks of 32 hidden units");
     // WAVES x 32 rows per workgroup; the chunks' weights double-buffered (one barrier per chunk)
     // in two LDS arrays: the chunk loop runs in pairs (compute from lds0 while staging into lds1,
@@ -427,7 +433,41 @@ __global__ void __launch_bounds__(64 * WAVES, D <= 160 ? 8 / WAVES : 1) mlp_ln_f
 #endif
     // the row's h, split: lane (r, hh) holds k = 16 kk + 8 hh .. + 7 of row r
     bf16x8_t hfh[KS], hfl[KS];
-    {
+    if constexpr (XIN) {
+        // the row's x (this lane: k = 16 kk + 8 hh .. + 7), its LayerNorm over the lane pair
+        // (two-pass: mean, then the biased variance), normalised and split
+        const float* xr0 = x_io + (size_t)(ok ? row : 0u) * D + 8 * hh;
+        float4 xa[KS], xb[KS];
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk) { xa[kk] = *(const float4*)(xr0 + 16 * kk); xb[kk] = *(const float4*)(xr0 + 16 * kk + 4); }
+        float s1 = 0.0f;
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk) s1 += ((xa[kk].x + xa[kk].y) + (xa[kk].z + xa[kk].w)) + ((xb[kk].x + xb[kk].y) + (xb[kk].z + xb[kk].w));
+        s1 += __shfl_xor(s1, 32);
+        const float mu = s1 / (float)D;
+        float s2 = 0.0f;
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk) {
+            const float v[8] = {xa[kk].x, xa[kk].y, xa[kk].z, xa[kk].w, xb[kk].x, xb[kk].y, xb[kk].z, xb[kk].w};
+#pragma unroll
+            for (int j = 0; j < 8; ++j) s2 += (v[j] - mu) * (v[j] - mu);
+        }
+        s2 += __shfl_xor(s2, 32);
+        const float rs = rsqrtf(s2 / (float)D + eps_in);
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk) {
+            const int c0 = 16 * kk + 8 * hh;
+            const float4 g0 = *(const float4*)(gin + c0), g1 = *(const float4*)(gin + c0 + 4);
+            const float4 e0 = *(const float4*)(bin + c0), e1 = *(const float4*)(bin + c0 + 4);
+            const float g[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+            const float be[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
+            const float x8[8] = {xa[kk].x, xa[kk].y, xa[kk].z, xa[kk].w, xb[kk].x, xb[kk].y, xb[kk].z, xb[kk].w};
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = (x8[j] - mu) * rs * g[j] + be[j];
+            split_bf16x8(v, hfh[kk], hfl[kk]);
+        }
+    } else {
         const float* hr = h + (size_t)(ok ? row : 0u) * D + 8 * hh;
 #pragma unroll
         for (int kk = 0; kk < KS; ++kk) {
@@ -632,7 +672,16 @@ __global__ void __launch_bounds__(64 * WAVES, D <= 160 ? 8 / WAVES : 1) mlp_ln_f
     s2 += __shfl_xor(s2, 32);
     const float rstd = rsqrtf(s2 / (float)D + eps);
     float* hr = h_out + (size_t)(ok ? row : 0u) * D;
-    if (ok) {
+    const bool wh = !XIN || h_out != nullptr;   // (uniform; XIN with h_out == nullptr: x only)
+    if (ok && !wh) {
+#pragma unroll
+        for (int t = 0; t < OT; ++t)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                *(float4*)(xr + 32 * t + 8 * q + 4 * hh) =
+                    make_float4(acc2[t][4 * q], acc2[t][4 * q + 1], acc2[t][4 * q + 2], acc2[t][4 * q + 3]);
+    }
+    if (ok && wh) {
 #pragma unroll
         for (int t = 0; t < OT; ++t)
 #pragma unroll
@@ -1124,7 +1173,50 @@ __global__ void __launch_bounds__(256, HD == 40 ? 3 : 2) qkv_attn_ln_f32x3_kerne
     uint16_t* hsl = lds + 64 * LDY;
     // the sample's h rows, split; rows 62, 63 zero
     const float* hg = (XIN ? x_io : h_in) + (size_t)b * S * D;
-    {
+    if constexpr (XIN && D == 160) {
+        // XIN at d = 160 (round 6): four threads per row (64 rows), thread q of a row holds its
+        // pieces 5 q .. 5 q + 4 (40 values), so the row's LayerNorm reduces over lanes ^1, ^2;
+        // every load issued first; rows 62, 63 zero
+        constexpr int PPT = D / 8 / 4;                     // pieces per thread
+        const int rr = threadIdx.x >> 2, q4 = threadIdx.x & 3;
+        const bool ok = rr < S;
+        const float* src = hg + (size_t)(ok ? rr : S - 1) * D + 8 * PPT * q4;
+        float4 va[PPT], vb[PPT];
+#pragma unroll
+        for (int i = 0; i < PPT; ++i) { va[i] = *(const float4*)(src + 8 * i); vb[i] = *(const float4*)(src + 8 * i + 4); }
+        float s1 = 0.0f;
+#pragma unroll
+        for (int i = 0; i < PPT; ++i) s1 += ((va[i].x + va[i].y) + (va[i].z + va[i].w)) + ((vb[i].x + vb[i].y) + (vb[i].z + vb[i].w));
+        s1 += __shfl_xor(s1, 1);
+        s1 += __shfl_xor(s1, 2);
+        const float mu = s1 / (float)D;
+        float s2 = 0.0f;
+#pragma unroll
+        for (int i = 0; i < PPT; ++i) {
+            const float v[8] = {va[i].x, va[i].y, va[i].z, va[i].w, vb[i].x, vb[i].y, vb[i].z, vb[i].w};
+#pragma unroll
+            for (int j = 0; j < 8; ++j) s2 += (v[j] - mu) * (v[j] - mu);
+        }
+        s2 += __shfl_xor(s2, 1);
+        s2 += __shfl_xor(s2, 2);
+        const float rs = rsqrtf(s2 / (float)D + eps_in);
+#pragma unroll
+        for (int i = 0; i < PPT; ++i) {
+            const int kp = PPT * q4 + i, c0 = 8 * kp;
+            const float4 g0 = *(const float4*)(gin + c0), g1 = *(const float4*)(gin + c0 + 4);
+            const float4 e0 = *(const float4*)(bin + c0), e1 = *(const float4*)(bin + c0 + 4);
+            const float g[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+            const float be[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
+            const float x8[8] = {va[i].x, va[i].y, va[i].z, va[i].w, vb[i].x, vb[i].y, vb[i].z, vb[i].w};
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = ok ? (x8[j] - mu) * rs * g[j] + be[j] : 0.0f;
+            bf16x8_t fh, fl;
+            split_bf16x8(v, fh, fl);
+            *(bf16x8_t*)&hsh[rr * LDY + c0] = fh;
+            *(bf16x8_t*)&hsl[rr * LDY + c0] = fl;
+        }
+    } else {
         // every load issued before the first split / LDS store (a load -> store loop waited a
         // memory round trip per iteration); rows 62, 63 zero
         constexpr int NPC = 64 * (D / 8) / 256;
@@ -1139,7 +1231,7 @@ __global__ void __launch_bounds__(256, HD == 40 ? 3 : 2) qkv_attn_ln_f32x3_kerne
         }
         // XIN: each row's D / 8 pieces sit on D / 8 consecutive lanes (the same piece index kp for
         // every i): the row's LayerNorm reduces over them, two-pass
-        static_assert(!XIN || (D / 8 == 32 && 256 % (D / 8) == 0), "XIN: a row on one half-wave");
+        static_assert(!XIN || (D / 8 == 32 && 256 % (D / 8) == 0), "XIN here: a row on one half-wave (d = 160 above)");
         float4 xg0{}, xg1{}, xe0{}, xe1{};
         if constexpr (XIN) {
             const int c0 = 8 * (threadIdx.x & (D / 8 - 1));

@@ -2355,9 +2355,9 @@ int dk_net_qkv_attn_ln_f32x3_async(const float* h, float* x_io, const void* wqkv
     return DK_OK;
 }
 
-// The d = 256 halves with the LayerNorm moved to the consumer (round 6): the input is either h
-// (h_in given, ln_in_* unused) or the residual stream normalised in the kernel with ln_in (h_in
-// NULL); h_out NULL writes x only (gamma / beta / eps then unused).
+// The halves with the LayerNorm moved to the consumer (d = 256: round 5; d = 160: round 6): the
+// input is either h (h_in given, ln_in_* unused) or the residual stream normalised in the kernel
+// with ln_in (h_in NULL); h_out NULL writes x only (gamma / beta / eps then unused).
 int dk_net_qkv_attn_ln_f32x3_ex_async(const float* h_in, float* x_io, const float* ln_in_gamma, const float* ln_in_beta,
                                       float ln_in_eps, const void* wqkv_hi, const void* wqkv_lo, const float* bqkv,
                                       const void* wp_hi, const void* wp_lo, const float* bp, uint32_t batch, uint32_t heads,
@@ -2366,11 +2366,16 @@ int dk_net_qkv_attn_ln_f32x3_ex_async(const float* h_in, float* x_io, const floa
     const bool xin = h_in == nullptr;
     if (!x_io || !wqkv_hi || !wqkv_lo || !bqkv || !wp_hi || !wp_lo || !bp || (xin && (!ln_in_gamma || !ln_in_beta)) ||
         (h_out && (!gamma || !beta || h_out == h_in || h_out == x_io)) || (h_in && h_in == x_io) || heads != 4u ||
-        head_dim != 64u)
+        (head_dim != 64u && head_dim != 40u) || (head_dim == 40u && !xin))
         return DK_E_INVALID;
     if (batch == 0) return DK_OK;
     const float scale = 1.0f / sqrtf((float)head_dim);
-    if (xin)
+    if (xin && head_dim == 40u)
+        hipLaunchKernelGGL((dk::net::qkv_attn_ln_f32x3_kernel<40, true>), dim3(batch), dim3(256), 0, (hipStream_t)stream,
+                           (const float*)nullptr, x_io, (const uint16_t*)wqkv_hi, (const uint16_t*)wqkv_lo, bqkv,
+                           (const uint16_t*)wp_hi, (const uint16_t*)wp_lo, bp, scale, gamma, beta, eps, h_out, ln_in_gamma,
+                           ln_in_beta, ln_in_eps);
+    else if (xin)
         hipLaunchKernelGGL((dk::net::qkv_attn_ln_f32x3_kernel<64, true>), dim3(batch), dim3(256), 0, (hipStream_t)stream,
                            (const float*)nullptr, x_io, (const uint16_t*)wqkv_hi, (const uint16_t*)wqkv_lo, bqkv,
                            (const uint16_t*)wp_hi, (const uint16_t*)wp_lo, bp, scale, gamma, beta, eps, h_out, ln_in_gamma,
@@ -2390,12 +2395,18 @@ int dk_net_mlp_ln_f32x3_ex_async(const float* h_in, float* x_io, const float* ln
                                  const float* gamma, const float* beta, float eps, float* h_out, void* stream) {
     const bool xin = h_in == nullptr;
     if (!x_io || !w1_hi || !w1_lo || !b1 || !w2_hi || !w2_lo || !b2 || (xin && (!ln_in_gamma || !ln_in_beta)) ||
-        (h_out && (!gamma || !beta || h_out == h_in || h_out == x_io)) || (h_in && h_in == x_io) || d != 256u ||
-        n_hidden == 0 || n_hidden > dk::net::MLP_MAX_HIDDEN || n_hidden % 64u)
+        (h_out && (!gamma || !beta || h_out == h_in || h_out == x_io)) || (h_in && h_in == x_io) ||
+        (d != 256u && d != 160u) || (d == 160u && !xin) || n_hidden == 0 || n_hidden > dk::net::MLP_MAX_HIDDEN ||
+        n_hidden % 64u)
         return DK_E_INVALID;
     if (rows == 0) return DK_OK;
     const dim3 grid((rows + 127u) / 128u);
-    if (xin)
+    if (d == 160u)   // (4 waves x 32 rows, mlp_ln_f32x3_kernel; the input normalised in the kernel)
+        hipLaunchKernelGGL((dk::net::mlp_ln_f32x3_kernel<160, 32, 4, true>), grid, dim3(256u), 0, (hipStream_t)stream,
+                           (const float*)nullptr, x_io, (const uint16_t*)w1_hi, (const uint16_t*)w1_lo, b1,
+                           (const uint16_t*)w2_hi, (const uint16_t*)w2_lo, b2, rows, n_hidden, gamma, beta, eps, h_out,
+                           ln_in_gamma, ln_in_beta, ln_in_eps);
+    else if (xin)
         hipLaunchKernelGGL((dk::net::mlp16_ln_f32x3_kernel<256, 32, true>), grid, dim3(512u), 0, (hipStream_t)stream,
                            (const float*)nullptr, x_io, (const uint16_t*)w1_hi, (const uint16_t*)w1_lo, b1,
                            (const uint16_t*)w2_hi, (const uint16_t*)w2_lo, b2, rows, n_hidden, gamma, beta, eps, h_out,
