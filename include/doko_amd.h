@@ -524,21 +524,28 @@ int dk_net_qkv_attn_ln_f32x3_async(const float* h, float* x_io, const void* wqkv
                                    uint32_t head_dim, const float* gamma, const float* beta, float eps, float* h_out,
                                    void* stream);
 
-/* dk_net_qkv_attn_ln_f32x3_ex_async / dk_net_mlp_ln_f32x3_ex_async (d = 256, 4 heads of 64): the
- * two halves above with the LayerNorm moved into the consumer, so that a chain of halves moves the
- * residual stream x only.  Input: h_in [rows, d] as above, or h_in NULL and the kernel normalises x
- * itself with (ln_in_gamma, ln_in_beta, ln_in_eps) -- the LayerNorm the producer used to apply.
- * h_out NULL: only x is updated (gamma / beta / eps unused); otherwise h_out = LN(x) as above.
- * The same weights, split layouts and validity rules (n_hidden % 64 == 0); DK_E_INVALID otherwise. */
+/* dk_net_qkv_attn_ln_f32x3_ex_async / dk_net_mlp_ln_f32x3_ex_async (d = 256, 4 heads of 64; and
+ * since round 6 d = 160, 4 heads of 40, x-input form only): the two halves above with the LayerNorm
+ * moved into the consumer, so that a chain of halves moves the residual stream x only.  Input: h_in
+ * [rows, d] as above, or h_in NULL and the kernel normalises x itself with (ln_in_gamma,
+ * ln_in_beta, ln_in_eps) -- the LayerNorm the producer used to apply.  h_out NULL: only x is
+ * updated (gamma / beta unused); otherwise h_out = LN(x) as above.
+ * Row statistics (d = 160 only; NULL at d = 256): stats_out [rows][2] receives each new x row's
+ * LayerNorm mean and 1 / sqrt(var + eps) (eps: the LayerNorm the next half applies); stats_in gives
+ * the x-input form those statistics instead of reducing over the row (the d = 160 MLP half
+ * requires them; the attention half computes them itself when stats_in is NULL).  stats_in and
+ * stats_out may be the same buffer.  The same weights, split layouts and validity rules
+ * (n_hidden % 64 == 0); DK_E_INVALID otherwise. */
 int dk_net_qkv_attn_ln_f32x3_ex_async(const float* h_in, float* x_io, const float* ln_in_gamma, const float* ln_in_beta,
                                       float ln_in_eps, const void* wqkv_hi, const void* wqkv_lo, const float* bqkv,
                                       const void* wp_hi, const void* wp_lo, const float* bp, uint32_t batch, uint32_t heads,
                                       uint32_t head_dim, const float* gamma, const float* beta, float eps, float* h_out,
-                                      void* stream);
+                                      const float* stats_in, float* stats_out, void* stream);
 int dk_net_mlp_ln_f32x3_ex_async(const float* h_in, float* x_io, const float* ln_in_gamma, const float* ln_in_beta,
                                  float ln_in_eps, const void* w1_hi, const void* w1_lo, const float* b1, const void* w2_hi,
                                  const void* w2_lo, const float* b2, uint32_t rows, uint32_t d, uint32_t n_hidden,
-                                 const float* gamma, const float* beta, float eps, float* h_out, void* stream);
+                                 const float* gamma, const float* beta, float eps, float* h_out, const float* stats_in,
+                                 float* stats_out, void* stream);
 /* The heads at the reference's precision (round 5; PerClassAttentionMLPHead,
  * rs-doko-py-bridge/python/az_doko.py:28-56), f32 activations, bf16x3 MFMA products:
  * dk_net_class_pool_ln_f32_async: x [B, 62, d] -> out [C, B, d] (class-major) =

@@ -430,6 +430,11 @@ class FusedTrunkF32(FusedTrunk):
         # first half, from x and ln_1); only the last half writes h (the final LayerNorm, for the
         # heads).  Per half, x in and out instead of h in, x in and out, h out.
         x = self.x if x is None else x
+        # d = 160: the halves pass each other the new x rows' LayerNorm statistics (mean, 1/std), so
+        # that the consumer does not reduce over the row (8 B per row; one buffer, used in place)
+        st = torch.empty((x.shape[0] * SEQ, 2), dtype=torch.float32, device=x.device) if self.d == 160 else None
+        stp = st.data_ptr() if st is not None else None
+        ho = None
         for i, blk in enumerate(blocks):
             wqh, wql, wph, wpl, bpf = split_attn_bf16x3(blk)
             lin = None if (i == 0 and self.d == 256) else blk.ln_1
@@ -437,16 +442,18 @@ class FusedTrunkF32(FusedTrunk):
                 h.data_ptr() if lin is None else None, x.data_ptr(), lin.weight.data_ptr() if lin else None,
                 lin.bias.data_ptr() if lin else None, lin.eps if lin else 0.0, wqh.data_ptr(), wql.data_ptr(),
                 blk.qkv.bias.data_ptr(), wph.data_ptr(), wpl.data_ptr(), bpf.data_ptr(), x.shape[0], 4, self.d // 4, None,
-                None, 0.0, None, self.st))
-            last = i + 1 == len(blocks) and final_ln is not None   # (final_ln None: no h at all)
+                None, blk.ln_2.eps, None, stp if i > 0 else None, stp, self.st))
+            last = i + 1 == len(blocks)
             w1h, w1l, w2h, w2l = split_bf16x3(blk)
-            ho = torch.empty_like(x) if last else None
+            wh = last and final_ln is not None   # (final_ln None: no h at all)
+            ho = torch.empty_like(x) if wh else None
+            nxt_eps = blocks[i + 1].ln_1.eps if not last else (final_ln.eps if final_ln is not None else 1e-5)
             self.ck(self.L.dk_net_mlp_ln_f32x3_ex_async(
                 None, x.data_ptr(), blk.ln_2.weight.data_ptr(), blk.ln_2.bias.data_ptr(), blk.ln_2.eps, w1h.data_ptr(),
                 w1l.data_ptr(), blk.fc.bias.data_ptr(), w2h.data_ptr(), w2l.data_ptr(), blk.proj.bias.data_ptr(), self.rows,
-                self.d, blk.fc.weight.shape[0], final_ln.weight.data_ptr() if last else None,
-                final_ln.bias.data_ptr() if last else None, final_ln.eps if last else 0.0,
-                ho.data_ptr() if last else None, self.st))
+                self.d, blk.fc.weight.shape[0], final_ln.weight.data_ptr() if wh else None,
+                final_ln.bias.data_ptr() if wh else None, final_ln.eps if wh else nxt_eps,
+                ho.data_ptr() if wh else None, stp, stp if not last else None, self.st))
         return ho
 
     def ex_ok(self, blk):

@@ -383,10 +383,12 @@ __device__ __forceinline__ void split_bf16x8(const float (&v)[8], bf16x8_t& hi, 
     lo = b.v;
 }
 
-// XIN (round 6, the d = 160 x-only chain; as mlp16_ln_f32x3_kernel at d = 256): the input is the
-// residual stream x_io itself (h unused), normalised here with (gin, bin, eps_in) -- the lane pair
-// (r, r + 32) holds the row, so the LayerNorm reduces over one xor-32 exchange; h_out == nullptr:
-// x only is written.
+// XIN (round 6, the d = 160 x-only chain): the input is the residual stream x_io itself (h unused),
+// normalised here with (gin, bin) and the row statistics its producer wrote (stats_in: mean and
+// 1 / sqrt(var + eps_in) per row, the producer's two-pass LayerNorm statistics -- so the h this
+// computes equals the h the producer would have written); h_out == nullptr: x only is written;
+// stats_out != nullptr: the new x's row statistics (with `eps`) for the next half.  (Reducing over
+// the row here instead kept 80 values per lane live beside the split fragments and spilled.)
 template <int D, int NC, int WAVES = 4, bool XIN = false>
 __global__ void __launch_bounds__(64 * WAVES, D <= 160 ? 8 / WAVES : 1) mlp_ln_f32x3_kernel(const float* __restrict__ h, float* __restrict__ x_io,
                                                                 const uint16_t* __restrict__ w1h, const uint16_t* __restrict__ w1l,
@@ -396,7 +398,9 @@ __global__ void __launch_bounds__(64 * WAVES, D <= 160 ? 8 / WAVES : 1) mlp_ln_f
                                                                 const float* __restrict__ gamma, const float* __restrict__ beta,
                                                                 float eps, float* __restrict__ h_out,
                                                                 const float* __restrict__ gin = nullptr,
-                                                                const float* __restrict__ bin = nullptr, float eps_in = 0.0f) {
+                                                                const float* __restrict__ bin = nullptr,
+                                                                const float2* __restrict__ stats_in = nullptr,
+                                                                float2* __restrict__ stats_out = nullptr) {
     static_assert(D % 32 == 0 && NC == 32, "d: multiple of 32; chunks of 32 hidden units");
     // WAVES x 32 rows per workgroup; the chunks' weights double-buffered (one barrier per chunk)
     // in two LDS arrays: the chunk loop runs in pairs (compute from lds0 while staging into lds1,
@@ -434,38 +438,26 @@ __global__ void __launch_bounds__(64 * WAVES, D <= 160 ? 8 / WAVES : 1) mlp_ln_f
     // the row's h, split: lane (r, hh) holds k = 16 kk + 8 hh .. + 7 of row r
     bf16x8_t hfh[KS], hfl[KS];
     if constexpr (XIN) {
-        // the row's x (this lane: k = 16 kk + 8 hh .. + 7), its LayerNorm over the lane pair
-        // (two-pass: mean, then the biased variance), normalised and split
+        // the row's x (this lane: k = 16 kk + 8 hh .. + 7), normalised with the producer's row
+        // statistics and the consumer's weights, then split (as the h loads below: no reduction)
         const float* xr0 = x_io + (size_t)(ok ? row : 0u) * D + 8 * hh;
-        float4 xa[KS], xb[KS];
-#pragma unroll
-        for (int kk = 0; kk < KS; ++kk) { xa[kk] = *(const float4*)(xr0 + 16 * kk); xb[kk] = *(const float4*)(xr0 + 16 * kk + 4); }
-        float s1 = 0.0f;
-#pragma unroll
-        for (int kk = 0; kk < KS; ++kk) s1 += ((xa[kk].x + xa[kk].y) + (xa[kk].z + xa[kk].w)) + ((xb[kk].x + xb[kk].y) + (xb[kk].z + xb[kk].w));
-        s1 += __shfl_xor(s1, 32);
-        const float mu = s1 / (float)D;
-        float s2 = 0.0f;
-#pragma unroll
-        for (int kk = 0; kk < KS; ++kk) {
-            const float v[8] = {xa[kk].x, xa[kk].y, xa[kk].z, xa[kk].w, xb[kk].x, xb[kk].y, xb[kk].z, xb[kk].w};
-#pragma unroll
-            for (int j = 0; j < 8; ++j) s2 += (v[j] - mu) * (v[j] - mu);
-        }
-        s2 += __shfl_xor(s2, 32);
-        const float rs = rsqrtf(s2 / (float)D + eps_in);
+        const float2 st = stats_in[ok ? row : 0u];
 #pragma unroll
         for (int kk = 0; kk < KS; ++kk) {
             const int c0 = 16 * kk + 8 * hh;
+            const float4 xa = *(const float4*)(xr0 + 16 * kk), xb = *(const float4*)(xr0 + 16 * kk + 4);
             const float4 g0 = *(const float4*)(gin + c0), g1 = *(const float4*)(gin + c0 + 4);
             const float4 e0 = *(const float4*)(bin + c0), e1 = *(const float4*)(bin + c0 + 4);
+            const float x8[8] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w};
             const float g[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
             const float be[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
-            const float x8[8] = {xa[kk].x, xa[kk].y, xa[kk].z, xa[kk].w, xb[kk].x, xb[kk].y, xb[kk].z, xb[kk].w};
             float v[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = (x8[j] - mu) * rs * g[j] + be[j];
+            for (int j = 0; j < 8; ++j) v[j] = (x8[j] - st.x) * st.y * g[j] + be[j];
             split_bf16x8(v, hfh[kk], hfl[kk]);
+            // (materialised here, a k-step at a time: sunk to their first use in the chunk loop,
+            // with every load left at the top, they spilled)
+            asm volatile("" : "+v"(hfh[kk]), "+v"(hfl[kk]));
         }
     } else {
         const float* hr = h + (size_t)(ok ? row : 0u) * D + 8 * hh;
@@ -640,6 +632,9 @@ __global__ void __launch_bounds__(64 * WAVES, D <= 160 ? 8 / WAVES : 1) mlp_ln_f
         chunk(c, lds0, lds1);
         if (c + 1 < chunks) chunk(c + 1, lds1, lds0);
     }
+    // (XIN: the epilogue reads x again instead of the compiler keeping the prologue's x values
+    // alive through the chunk loop, which spilled them)
+    if constexpr (XIN) asm volatile("" ::: "memory");
     // epilogue: acc2[t][g] = delta of row `row`, column 32 t + 8 (g >> 2) + 4 hh + (g & 3);
     // x += (delta + b2) (the GEMM's bias first: F.linear's epilogue order), then LN
     // (all loads first, the stores under one branch: per-store branches kept every x load
@@ -673,6 +668,9 @@ __global__ void __launch_bounds__(64 * WAVES, D <= 160 ? 8 / WAVES : 1) mlp_ln_f
     const float rstd = rsqrtf(s2 / (float)D + eps);
     float* hr = h_out + (size_t)(ok ? row : 0u) * D;
     const bool wh = !XIN || h_out != nullptr;   // (uniform; XIN with h_out == nullptr: x only)
+    if constexpr (XIN) {
+        if (stats_out != nullptr && ok && hh == 0) stats_out[row] = make_float2(mean, rstd);
+    }
     if (ok && !wh) {
 #pragma unroll
         for (int t = 0; t < OT; ++t)
@@ -1158,7 +1156,9 @@ __global__ void __launch_bounds__(256, HD == 40 ? 3 : 2) qkv_attn_ln_f32x3_kerne
                                                                    const float* __restrict__ gamma, const float* __restrict__ beta,
                                                                    float eps, float* __restrict__ h_out,
                                                                    const float* __restrict__ gin = nullptr,
-                                                                   const float* __restrict__ bin = nullptr, float eps_in = 0.0f) {
+                                                                   const float* __restrict__ bin = nullptr, float eps_in = 0.0f,
+                                                                   const float2* __restrict__ stats_in = nullptr,
+                                                                   float2* __restrict__ stats_out = nullptr) {
     constexpr int S = 62, D = HD * 4, LDY = D + 8, LDT = 64 + 4, KS = (HD + 15) / 16, LDX = D + 4;
     constexpr bool TAIL3 = HD == 40;                       // the three projections' dims 32..39 in one tile
     constexpr bool PERDT = HD == 64;                       // Q / K one 32-dim tile at a time
@@ -1184,22 +1184,29 @@ __global__ void __launch_bounds__(256, HD == 40 ? 3 : 2) qkv_attn_ln_f32x3_kerne
         float4 va[PPT], vb[PPT];
 #pragma unroll
         for (int i = 0; i < PPT; ++i) { va[i] = *(const float4*)(src + 8 * i); vb[i] = *(const float4*)(src + 8 * i + 4); }
-        float s1 = 0.0f;
+        // the row statistics: the producer's (stats_in), else a two-pass reduction over the 4 lanes
+        float mu, rs;
+        if (stats_in != nullptr) {   // (uniform)
+            const float2 st = stats_in[(size_t)b * S + (ok ? rr : S - 1)];
+            mu = st.x; rs = st.y;
+        } else {
+            float s1 = 0.0f;
 #pragma unroll
-        for (int i = 0; i < PPT; ++i) s1 += ((va[i].x + va[i].y) + (va[i].z + va[i].w)) + ((vb[i].x + vb[i].y) + (vb[i].z + vb[i].w));
-        s1 += __shfl_xor(s1, 1);
-        s1 += __shfl_xor(s1, 2);
-        const float mu = s1 / (float)D;
-        float s2 = 0.0f;
+            for (int i = 0; i < PPT; ++i) s1 += ((va[i].x + va[i].y) + (va[i].z + va[i].w)) + ((vb[i].x + vb[i].y) + (vb[i].z + vb[i].w));
+            s1 += __shfl_xor(s1, 1);
+            s1 += __shfl_xor(s1, 2);
+            mu = s1 / (float)D;
+            float s2 = 0.0f;
 #pragma unroll
-        for (int i = 0; i < PPT; ++i) {
-            const float v[8] = {va[i].x, va[i].y, va[i].z, va[i].w, vb[i].x, vb[i].y, vb[i].z, vb[i].w};
+            for (int i = 0; i < PPT; ++i) {
+                const float v[8] = {va[i].x, va[i].y, va[i].z, va[i].w, vb[i].x, vb[i].y, vb[i].z, vb[i].w};
 #pragma unroll
-            for (int j = 0; j < 8; ++j) s2 += (v[j] - mu) * (v[j] - mu);
+                for (int j = 0; j < 8; ++j) s2 += (v[j] - mu) * (v[j] - mu);
+            }
+            s2 += __shfl_xor(s2, 1);
+            s2 += __shfl_xor(s2, 2);
+            rs = rsqrtf(s2 / (float)D + eps_in);
         }
-        s2 += __shfl_xor(s2, 1);
-        s2 += __shfl_xor(s2, 2);
-        const float rs = rsqrtf(s2 / (float)D + eps_in);
 #pragma unroll
         for (int i = 0; i < PPT; ++i) {
             const int kp = PPT * q4 + i, c0 = 8 * kp;
@@ -1577,6 +1584,7 @@ __global__ void __launch_bounds__(256, HD == 40 ? 3 : 2) qkv_attn_ln_f32x3_kerne
         const float rstd = rsqrtf(s2 / (float)D + eps);
         if (row < S) {
             const size_t o = ((size_t)b * S + row) * D;
+            if (stats_out != nullptr && q == 0) stats_out[(size_t)b * S + row] = make_float2(mean, rstd);
             const bool wh = h_out != nullptr;   // (uniform)
 #pragma unroll
             for (int i = 0; i < LP; ++i) {

@@ -2362,29 +2362,30 @@ int dk_net_qkv_attn_ln_f32x3_ex_async(const float* h_in, float* x_io, const floa
                                       float ln_in_eps, const void* wqkv_hi, const void* wqkv_lo, const float* bqkv,
                                       const void* wp_hi, const void* wp_lo, const float* bp, uint32_t batch, uint32_t heads,
                                       uint32_t head_dim, const float* gamma, const float* beta, float eps, float* h_out,
-                                      void* stream) {
+                                      const float* stats_in, float* stats_out, void* stream) {
     const bool xin = h_in == nullptr;
     if (!x_io || !wqkv_hi || !wqkv_lo || !bqkv || !wp_hi || !wp_lo || !bp || (xin && (!ln_in_gamma || !ln_in_beta)) ||
         (h_out && (!gamma || !beta || h_out == h_in || h_out == x_io)) || (h_in && h_in == x_io) || heads != 4u ||
-        (head_dim != 64u && head_dim != 40u) || (head_dim == 40u && !xin))
+        (head_dim != 64u && head_dim != 40u) || (head_dim == 40u && !xin) ||
+        (head_dim == 64u && (stats_in || stats_out)))   // (row statistics: the d = 160 chain only)
         return DK_E_INVALID;
     if (batch == 0) return DK_OK;
     const float scale = 1.0f / sqrtf((float)head_dim);
-    if (xin && head_dim == 40u)
+    if (head_dim == 40u)
         hipLaunchKernelGGL((dk::net::qkv_attn_ln_f32x3_kernel<40, true>), dim3(batch), dim3(256), 0, (hipStream_t)stream,
                            (const float*)nullptr, x_io, (const uint16_t*)wqkv_hi, (const uint16_t*)wqkv_lo, bqkv,
                            (const uint16_t*)wp_hi, (const uint16_t*)wp_lo, bp, scale, gamma, beta, eps, h_out, ln_in_gamma,
-                           ln_in_beta, ln_in_eps);
+                           ln_in_beta, ln_in_eps, (const float2*)stats_in, (float2*)stats_out);
     else if (xin)
         hipLaunchKernelGGL((dk::net::qkv_attn_ln_f32x3_kernel<64, true>), dim3(batch), dim3(256), 0, (hipStream_t)stream,
                            (const float*)nullptr, x_io, (const uint16_t*)wqkv_hi, (const uint16_t*)wqkv_lo, bqkv,
                            (const uint16_t*)wp_hi, (const uint16_t*)wp_lo, bp, scale, gamma, beta, eps, h_out, ln_in_gamma,
-                           ln_in_beta, ln_in_eps);
+                           ln_in_beta, ln_in_eps, (const float2*)nullptr, (float2*)nullptr);
     else
         hipLaunchKernelGGL((dk::net::qkv_attn_ln_f32x3_kernel<64, false>), dim3(batch), dim3(256), 0, (hipStream_t)stream,
                            h_in, x_io, (const uint16_t*)wqkv_hi, (const uint16_t*)wqkv_lo, bqkv, (const uint16_t*)wp_hi,
                            (const uint16_t*)wp_lo, bp, scale, gamma, beta, eps, h_out, (const float*)nullptr,
-                           (const float*)nullptr, 0.0f);
+                           (const float*)nullptr, 0.0f, (const float2*)nullptr, (float2*)nullptr);
     DK_HIP(hipGetLastError());
     return DK_OK;
 }
@@ -2392,20 +2393,21 @@ int dk_net_qkv_attn_ln_f32x3_ex_async(const float* h_in, float* x_io, const floa
 int dk_net_mlp_ln_f32x3_ex_async(const float* h_in, float* x_io, const float* ln_in_gamma, const float* ln_in_beta,
                                  float ln_in_eps, const void* w1_hi, const void* w1_lo, const float* b1, const void* w2_hi,
                                  const void* w2_lo, const float* b2, uint32_t rows, uint32_t d, uint32_t n_hidden,
-                                 const float* gamma, const float* beta, float eps, float* h_out, void* stream) {
+                                 const float* gamma, const float* beta, float eps, float* h_out, const float* stats_in,
+                                 float* stats_out, void* stream) {
     const bool xin = h_in == nullptr;
     if (!x_io || !w1_hi || !w1_lo || !b1 || !w2_hi || !w2_lo || !b2 || (xin && (!ln_in_gamma || !ln_in_beta)) ||
         (h_out && (!gamma || !beta || h_out == h_in || h_out == x_io)) || (h_in && h_in == x_io) ||
-        (d != 256u && d != 160u) || (d == 160u && !xin) || n_hidden == 0 || n_hidden > dk::net::MLP_MAX_HIDDEN ||
-        n_hidden % 64u)
+        (d != 256u && d != 160u) || (d == 160u && (!xin || !stats_in)) || (d == 256u && (stats_in || stats_out)) ||
+        n_hidden == 0 || n_hidden > dk::net::MLP_MAX_HIDDEN || n_hidden % 64u)
         return DK_E_INVALID;
     if (rows == 0) return DK_OK;
     const dim3 grid((rows + 127u) / 128u);
-    if (d == 160u)   // (4 waves x 32 rows, mlp_ln_f32x3_kernel; the input normalised in the kernel)
+    if (d == 160u)   // (4 waves x 32 rows, mlp_ln_f32x3_kernel: x normalised with the producer's row statistics)
         hipLaunchKernelGGL((dk::net::mlp_ln_f32x3_kernel<160, 32, 4, true>), grid, dim3(256u), 0, (hipStream_t)stream,
                            (const float*)nullptr, x_io, (const uint16_t*)w1_hi, (const uint16_t*)w1_lo, b1,
                            (const uint16_t*)w2_hi, (const uint16_t*)w2_lo, b2, rows, n_hidden, gamma, beta, eps, h_out,
-                           ln_in_gamma, ln_in_beta, ln_in_eps);
+                           ln_in_gamma, ln_in_beta, (const float2*)stats_in, (float2*)stats_out);
     else if (xin)
         hipLaunchKernelGGL((dk::net::mlp16_ln_f32x3_kernel<256, 32, true>), grid, dim3(512u), 0, (hipStream_t)stream,
                            (const float*)nullptr, x_io, (const uint16_t*)w1_hi, (const uint16_t*)w1_lo, b1,

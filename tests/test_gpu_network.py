@@ -119,22 +119,29 @@ def test_ex_halves_normalise_x_input(write_h, d):
     ha = torch.full_like(x, float("nan"))
     hm = torch.full_like(x, float("nan"))
     L = _lib()
+    # d = 160: the attention half hands the MLP half the new rows' LayerNorm statistics
+    stats = torch.full((B * 62, 2), float("nan"), device=dev) if d == 160 else None
+    sptr = stats.data_ptr() if stats is not None else None
     assert L.dk_net_qkv_attn_ln_f32x3_ex_async(None, xo.data_ptr(), gi.data_ptr(), bi.data_ptr(), 1e-5, sp[0].data_ptr(),
                                                sp[1].data_ptr(), bq.data_ptr(), sp[2].data_ptr(), sp[3].data_ptr(),
                                                bp.data_ptr(), B, H, hd, g.data_ptr() if write_h else None,
                                                be.data_ptr() if write_h else None, 1e-5,
-                                               ha.data_ptr() if write_h else None, st) == 0
+                                               ha.data_ptr() if write_h else None, None, sptr, st) == 0
     torch.cuda.synchronize()
     xa_got = xo.clone()
     assert L.dk_net_mlp_ln_f32x3_ex_async(None, xo.data_ptr(), gi.data_ptr(), bi.data_ptr(), 1e-5, sm[0].data_ptr(),
                                           sm[1].data_ptr(), b1.data_ptr(), sm[2].data_ptr(), sm[3].data_ptr(), b2.data_ptr(),
                                           B * 62, d, n, g.data_ptr() if write_h else None,
                                           be.data_ptr() if write_h else None, 1e-5, hm.data_ptr() if write_h else None,
-                                          st) == 0
+                                          sptr, None, st) == 0
     torch.cuda.synchronize()
     ea = (xa_got - xa).abs().max().item() / da.abs().max().item()
     em = (xo - xm).abs().max().item() / dm.abs().max().item()
     assert ea < 2e-5 and em < 2e-5, (ea, em)
+    if stats is not None:   # the statistics the attention half wrote: those of x' = xa
+        mu = xa.reshape(-1, d).mean(-1)
+        rs = torch.rsqrt(xa.reshape(-1, d).var(-1, unbiased=False) + 1e-5)
+        assert torch.allclose(stats[:, 0], mu, rtol=1e-5, atol=1e-5) and torch.allclose(stats[:, 1], rs, rtol=1e-5)
     if write_h:
         for got, xr in ((ha, xa), (hm, xm)):
             ref = F.layer_norm(xr, (d,), g, be, 1e-5)
@@ -145,18 +152,23 @@ def test_ex_halves_normalise_x_input(write_h, d):
     # exist only in the x-input form); a width without kernels
     assert L.dk_net_mlp_ln_f32x3_ex_async(None, xo.data_ptr(), None, None, 1e-5, sm[0].data_ptr(), sm[1].data_ptr(),
                                           b1.data_ptr(), sm[2].data_ptr(), sm[3].data_ptr(), b2.data_ptr(), B * 62, d, n,
-                                          None, None, 1e-5, None, st) != 0
+                                          None, None, 1e-5, None, sptr, None, st) != 0
     assert L.dk_net_qkv_attn_ln_f32x3_ex_async(None, xo.data_ptr(), gi.data_ptr(), bi.data_ptr(), 1e-5, sp[0].data_ptr(),
                                                sp[1].data_ptr(), bq.data_ptr(), sp[2].data_ptr(), sp[3].data_ptr(),
                                                bp.data_ptr(), B, H, hd, g.data_ptr(), be.data_ptr(), 1e-5, xo.data_ptr(),
-                                               st) != 0
+                                               None, None, st) != 0
     hdummy = torch.zeros_like(x)
     assert L.dk_net_mlp_ln_f32x3_ex_async(hdummy.data_ptr(), xo.data_ptr(), None, None, 1e-5, sm[0].data_ptr(),
                                           sm[1].data_ptr(), b1.data_ptr(), sm[2].data_ptr(), sm[3].data_ptr(), b2.data_ptr(),
-                                          B * 62, 160, 640, None, None, 1e-5, None, st) != 0
+                                          B * 62, 160, 640, None, None, 1e-5, None, sptr, None, st) != 0
     assert L.dk_net_mlp_ln_f32x3_ex_async(None, xo.data_ptr(), gi.data_ptr(), bi.data_ptr(), 1e-5, sm[0].data_ptr(),
                                           sm[1].data_ptr(), b1.data_ptr(), sm[2].data_ptr(), sm[3].data_ptr(), b2.data_ptr(),
-                                          B * 62, 192, 768, None, None, 1e-5, None, st) != 0
+                                          B * 62, 192, 768, None, None, 1e-5, None, None, None, st) != 0
+    # the MLP half at d = 160 needs the statistics; at d = 256 none are accepted
+    assert L.dk_net_mlp_ln_f32x3_ex_async(None, xo.data_ptr(), gi.data_ptr(), bi.data_ptr(), 1e-5, sm[0].data_ptr(),
+                                          sm[1].data_ptr(), b1.data_ptr(), sm[2].data_ptr(), sm[3].data_ptr(), b2.data_ptr(),
+                                          B * 62, d, n, None, None, 1e-5, None, None if d == 160 else xo.data_ptr(), None,
+                                          st) != 0
 
 
 @pytest.mark.parametrize("d", [160, 256])
