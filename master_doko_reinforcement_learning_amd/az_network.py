@@ -371,7 +371,7 @@ class FusedTrunkF32(FusedTrunk):
     them and the GEMMs on hipBLASLt at "medium", the attention half's out_proj and c_proj folded
     into one GEMM (Block.folded_proj, f32).  The heads: ClassHead.forward_f32."""
 
-    def __init__(self, tokens, emb, ln0):
+    def __init__(self, tokens, emb, ln0, need_h=True):
         from . import _native
         self.L = _native.lib()
         self.st = torch.cuda.current_stream(tokens.device).cuda_stream
@@ -379,10 +379,12 @@ class FusedTrunkF32(FusedTrunk):
         B, d = tok.shape[0], emb[0].weight.shape[1]
         self.rows, self.d = B * SEQ, d
         self.x = torch.empty((B, SEQ, d), dtype=torch.float32, device=tok.device)
-        self.h = torch.empty_like(self.x)
+        # (need_h False: the embedding sum only; the x-only chain normalises x in its first half)
+        self.h = torch.empty_like(self.x) if need_h else None
         tables = (ctypes_vp * 6)(*[e.weight.data_ptr() for e in emb])
         self.ck(self.L.dk_net_embed_ln_f32_async(tok.data_ptr(), B, tables, d, ln0.weight.data_ptr(), ln0.bias.data_ptr(),
-                                                 ln0.eps, self.x.data_ptr(), self.h.data_ptr(), self.st))
+                                                 ln0.eps, self.x.data_ptr(), self.h.data_ptr() if need_h else None,
+                                                 self.st))
 
     # The GEMMs run without their bias (hipBLASLt's f32 GEMMs at "medium" take about twice as long
     # with the bias epilogue, profiles/r04/fp32_bias_probe.log); each bias is added, in the
@@ -416,11 +418,15 @@ class FusedTrunkF32(FusedTrunk):
         w, b = blk.folded_proj()
         return self.add_ln(x, _f32c(F.linear(y, w)), ln, b)
 
-    def chain(self, blocks):
-        """True when `run` takes the x-only chain over these blocks (DK_F32_XCHAIN=0: the h-in / h-out
-        chain, a measurement switch)."""
-        return (self.d in (160, 256) and len(blocks) > 0 and all(self.ex_ok(blk) for blk in blocks)
+    @classmethod
+    def chain_ok(cls, d, blocks):
+        """True when `run` takes the x-only chain over these blocks of width d (DK_F32_XCHAIN=0: the
+        h-in / h-out chain, a measurement switch)."""
+        return (d in (160, 256) and len(blocks) > 0 and all(cls.ex_ok(blk) for blk in blocks)
                 and os.environ.get("DK_F32_XCHAIN", "1") != "0")
+
+    def chain(self, blocks):
+        return self.chain_ok(self.d, blocks)
 
     def run(self, h, blocks, final_ln, x=None):
         if not self.chain(blocks):
@@ -456,7 +462,8 @@ class FusedTrunkF32(FusedTrunk):
                 ho.data_ptr() if wh else None, stp, stp if not last else None, self.st))
         return ho
 
-    def ex_ok(self, blk):
+    @staticmethod
+    def ex_ok(blk):
         n = blk.fc.weight.shape[0]
         return (blk.heads == 4 and blk.qkv.bias is not None and n % 64 == 0 and n <= 1024 and blk.fc.bias is not None
                 and blk.proj.bias is not None and blk.ln_1.weight is not None and blk.ln_2.weight is not None)
@@ -519,10 +526,13 @@ class DokoAzNet(nn.Module):
         f32 forward (reference precision)."""
         if not (self.blocks and self.p_blocks and self.v_blocks):
             raise ValueError("the fused forward needs shared, policy and value blocks")
-        f = (trunk or FusedTrunk)(tokens, self.emb, self.blocks[0].ln_1)
-        # (f32 at d = 160: every half normalises x itself, so the branch inputs need no h)
-        x_only = isinstance(f, FusedTrunkF32) and f.d == 160 and all(f.chain(b) for b in (self.blocks, self.p_blocks,
-                                                                                          self.v_blocks))
+        # (f32 at d = 160: every half normalises x itself, so neither the embedding nor the branch
+        # inputs need an h)
+        d = self.emb[0].weight.shape[1]
+        x_only = trunk is FusedTrunkF32 and d == 160 and all(FusedTrunkF32.chain_ok(d, b) for b in
+                                                             (self.blocks, self.p_blocks, self.v_blocks))
+        f = trunk(tokens, self.emb, self.blocks[0].ln_1, need_h=False) if x_only else \
+            (trunk or FusedTrunk)(tokens, self.emb, self.blocks[0].ln_1)
         hp = f.run(f.h, self.blocks, None if x_only else self.p_blocks[0].ln_1)   # f.x: the shared trunk's output
         xv = f.x.clone()
         hv = None if x_only else f.add_ln(xv, None, self.v_blocks[0].ln_1)

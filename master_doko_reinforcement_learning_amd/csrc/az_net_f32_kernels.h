@@ -88,7 +88,9 @@ __global__ void embed_ln_f32_kernel(const int32_t* __restrict__ tokens, uint32_t
             xo[j] = a;
         }
     }
-    ln_row_f32<P4>(x, d, lane, (const float4*)gamma, (const float4*)beta, eps, (float4*)(h_out + (size_t)row * d));
+    // (h_out NULL: x only -- the d = 160 x-only chain normalises x in its first half)
+    if (h_out != nullptr)
+        ln_row_f32<P4>(x, d, lane, (const float4*)gamma, (const float4*)beta, eps, (float4*)(h_out + (size_t)row * d));
 }
 
 template <int P4>

@@ -2571,7 +2571,8 @@ int p4_of(uint32_t d) { return (d % 4u == 0u && d >= 4u && d <= 128u * (uint32_t
 int dk_net_embed_ln_f32_async(const int32_t* d_tokens, uint32_t batch, const void* const* tables, uint32_t d,
                               const void* gamma, const void* beta, float eps, void* x_out, void* h_out, void* stream) {
     const int p4 = p4_of(d);
-    if (!tables || !d_tokens || !x_out || !h_out || !gamma || !beta || p4 == 0) return DK_E_INVALID;
+    // (h_out NULL: x only)
+    if (!tables || !d_tokens || !x_out || (h_out && (!gamma || !beta)) || p4 == 0) return DK_E_INVALID;
     if (batch == 0) return DK_OK;
     const uint32_t rows = batch * 62u;
     const dim3 grid((rows + 7u) / 8u), block(256);
