@@ -1205,7 +1205,10 @@ def cpu_baseline_net(args, kind, target_s=3.0, batch=256):
     cores, quota = cpu_quota_cores()
     threads = args.cpu_threads or (min(cores, int(np.ceil(quota))) if quota else cores)
     prev_threads = torch.get_num_threads()
-    prev_prec = torch.get_float32_matmul_precision()
+    try:
+        prev_prec = torch.get_float32_matmul_precision()
+    except RuntimeError:   # (the GPU leg set allow_tf32 through the legacy API: leave "medium" set after)
+        prev_prec = "medium"
     torch.set_num_threads(threads)
     torch.set_float32_matmul_precision("medium")
     try:
