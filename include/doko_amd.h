@@ -377,8 +377,10 @@ int dk_decide_batch(dk_ctx* ctx, const dk_state* infostates, uint32_t n_info, ui
  *                       restricted to the root's allowed actions and renormalised; announcements are
  *                       offered at the root iff epoch >= 10.  d_noise == NULL (the reference's way):
  *                       each game draws Dirichlet([dirichlet_alpha; 39]) from its own SmallRng
- *                       (rand_distr 0.5.1, async_mcts.rs:111-113; alpha must be > 0.1, the crate's
- *                       Gamma construction); otherwise d_noise[n][39] is used and nothing is drawn
+ *                       (rand_distr 0.5.1, async_mcts.rs:111-113; alpha > 0 and finite, as the
+ *                       crate requires: alpha <= 0.1 takes its Beta stick-breaking construction,
+ *                       larger alphas its Gamma one); otherwise d_noise[n][39] is used and nothing
+ *                       is drawn
  *                                                                        (expand_root_node, async_mcts.rs:71-196)
  *   repeat `iterations` times:
  *     dk_az_select_async  PUCT descent, leaf expansion; d_eval[g] = leaf state,
@@ -404,6 +406,11 @@ int dk_az_begin_async(dk_ctx* ctx, const dk_az_state* d_roots, const uint64_t* d
 int dk_az_root_async(dk_ctx* ctx, const float* d_value, const float* d_logits, const float* d_noise, float dirichlet_alpha,
                      float dirichlet_epsilon, void* stream);
 int dk_az_rng_async(dk_ctx* ctx, uint64_t* d_rng, int set, void* stream);
+/* glibc's logf (fn 0) / expf (fn 1) as the device computes them for the root noise's Beta draws
+ * (engine/libm_f32.h; Rust's f32::ln / f32::exp call the platform libm): d_y[i] = fn(x_i) for the
+ * f32 whose bits are first + i * stride (mod 2^32), i < n.  Exported so that the restatement can be
+ * checked against the host's glibc across the whole f32 range (tests/test_gpu_parity.py). */
+int dk_f32_libm_async(int fn, uint32_t first, uint32_t stride, uint64_t n, float* d_y, void* stream);
 int dk_az_select_async(dk_ctx* ctx, float c, dk_az_state* d_eval, uint8_t* d_need_eval, void* stream);
 int dk_az_backup_async(dk_ctx* ctx, const float* d_value, const float* d_logits, void* stream);
 int dk_az_finish_async(dk_ctx* ctx, int temperature_mode, float temperature, uint32_t* d_visits, uint8_t* d_action,

@@ -90,6 +90,7 @@ def lib():
         "dk_az_begin_async": (ctypes.c_int, [vp, vp, vp, u32, u32, ctypes.c_int, vp, vp]),
         "dk_az_root_async": (ctypes.c_int, [vp, vp, vp, vp, ctypes.c_float, ctypes.c_float, vp]),
         "dk_az_rng_async": (ctypes.c_int, [vp, vp, ctypes.c_int, vp]),
+        "dk_f32_libm_async": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64, vp, vp]),
         "dk_az_select_async": (ctypes.c_int, [vp, ctypes.c_float, vp, vp, vp]),
         "dk_az_backup_async": (ctypes.c_int, [vp, vp, vp, vp]),
         "dk_az_finish_async": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_float, vp, vp, vp]),
@@ -152,7 +153,7 @@ EXPORTED = [
     "dk_search_batch_async", "dk_search_batch_rng", "dk_search_batch_rng_async", "dk_determinize_batch", "dk_determinize_batch_async", "dk_fuse",
     "dk_fuse_accumulate_async", "dk_fuse_select_async", "dk_decide_batch", "dk_sync", "dk_last_search_ms", "dk_last_search_waves", "dk_last_search_clocks",
     "dk_pool_bytes", "dk_legal_actions_async", "dk_env_step_batch_async", "dk_env_random_plies_batch_async",
-    "dk_az_begin_async", "dk_az_root_async", "dk_az_rng_async", "dk_az_select_async", "dk_az_backup_async", "dk_az_finish_async",
+    "dk_az_begin_async", "dk_az_root_async", "dk_az_rng_async", "dk_f32_libm_async", "dk_az_select_async", "dk_az_backup_async", "dk_az_finish_async",
     "dk_az_records_async", "dk_az_step_async", "dk_az_encode_async", "dk_net_embed_ln_bf16_async",
     "dk_net_add_ln_bf16_async", "dk_net_attn62_bf16_async", "dk_net_fc_gelu_bf16_async", "dk_net_mlp_ln_bf16_async", "dk_net_mlp_ln_f32x3_async", "dk_net_qkv_attn_ln_f32x3_async", "dk_net_qkv_attn_ln_f32x3_ex_async", "dk_net_mlp_ln_f32x3_ex_async", "dk_net_class_pool_ln_f32_async", "dk_net_class_mlp_f32x3_async", "dk_net_class_mlp_bf16_async", "dk_net_attn_ln_bf16_async", "dk_net_qkv_attn_ln_bf16_async", "dk_net_class_pool_ln_bf16_async",
     "dk_net_embed_ln_f32_async", "dk_net_add_ln_f32_async", "dk_net_attn62_f32_async", "dk_net_gelu_f32_async", "dk_net_add_bias_ln_f32_async", "dk_net_gelu_bias_f32_async", "dk_net_attn62_bias_f32_async", "dk_ar_begin_async", "dk_ar_guesses_async", "dk_ar_prepare_async",

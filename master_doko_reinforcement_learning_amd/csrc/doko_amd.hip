@@ -2081,8 +2081,8 @@ int dk_az_root_async(dk_ctx* ctx, const float* d_value, const float* d_logits, c
                      float dirichlet_epsilon, void* stream) {
     if (!ctx || !ctx->az_n || !d_value || !d_logits) return DK_E_INVALID;
     dk::rd::Open01Tab tab{nullptr, nullptr};
-    if (!d_noise) {
-        if (!dk::rd::dirichlet_alpha_ok(dirichlet_alpha)) return DK_E_INVALID;
+    if (!d_noise && !dk::rd::dirichlet_alpha_ok(dirichlet_alpha)) return DK_E_INVALID;
+    if (!d_noise && dk::rd::dirichlet_needs_tables(dirichlet_alpha)) {   // (FromBeta reads none)
         float* pw = nullptr;
         const int rc = rd_tables(ctx, dirichlet_alpha, pick(ctx, stream), &pw);
         if (rc) return ctx->last_error = rc;
@@ -2094,6 +2094,22 @@ int dk_az_root_async(dk_ctx* ctx, const float* d_value, const float* d_logits, c
                        ctx->az_states, ctx->az_games, ctx->az_cap_nodes, ctx->az_cap_states, ctx->err);
     DK_HIP(hipGetLastError());
     ctx->az_root_done = true;
+    return DK_OK;
+}
+
+__global__ void f32_libm_kernel(int fn, uint32_t first, uint32_t stride, uint64_t n, float* y) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const float x = __builtin_bit_cast(float, (uint32_t)(first + (uint32_t)i * stride));
+        y[i] = fn ? dk::lm::expf_glibc(x) : dk::lm::logf_glibc(x);
+    }
+}
+
+int dk_f32_libm_async(int fn, uint32_t first, uint32_t stride, uint64_t n, float* d_y, void* stream) {
+    if ((fn != 0 && fn != 1) || (n && !d_y)) return DK_E_INVALID;
+    if (!n) return DK_OK;
+    const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, 8192);
+    hipLaunchKernelGGL(f32_libm_kernel, dim3((uint32_t)blocks), dim3(256), 0, (hipStream_t)stream, fn, first, stride, n, d_y);
+    DK_HIP(hipGetLastError());
     return DK_OK;
 }
 

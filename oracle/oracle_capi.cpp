@@ -397,6 +397,16 @@ int or_dirichlet(float alpha, int n, uint32_t n_draws, uint64_t* rng_state, floa
     rng_to(r, rng_state);
     return 1;
 }
+// glibc logf (fn 0) / expf (fn 1) of the f32 with bits first + i * stride (the values the device's
+// restatement, engine/libm_f32.h, must reproduce)
+void or_libm_f32(int fn, uint32_t first, uint32_t stride, uint64_t n, float* out) {
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint32_t b = first + (uint32_t)i * stride;
+        float x;
+        std::memcpy(&x, &b, 4);
+        out[i] = fn ? expf(x) : logf(x);
+    }
+}
 void or_beta(float a, float b, uint32_t n, uint64_t* rng_state, float* out) {
     SmallRng r = rng_from(rng_state);
     const rdist::Beta g(a, b);

@@ -4,7 +4,7 @@
 // the RNG stream position must be identical, for greedy, infinite and T = 1
 // temperatures, with caller-supplied root noise and with the noise the search draws
 // from its own SmallRng (rand_distr.h as az_root_kernel runs it; alphas 0.8 / 1.0 / 0.5:
-// the three Gamma paths).  The batch is driven exactly as the GPU drives it: init ->
+// the three Gamma paths; 0.1 / 0.05: the FromBeta construction).  The batch is driven exactly as the GPU drives it: init ->
 // network(root) -> root_expand -> iterations x {select -> network(leaves) ->
 // backup} -> finish, over all games at once.
 // Usage: az_check <positions> <iterations> <seed>
@@ -76,11 +76,11 @@ int main(int argc, char** argv) {
     std::vector<float> ln01(K), pw01(K);
     auto u_of = [](uint32_t k) { return __builtin_bit_cast(float, k | 0x3F800000u) - (1.0f - FLT_EPSILON / 2.0f); };
     for (uint32_t k = 0; k < K; ++k) ln01[k] = logf(u_of(k));
-    for (int run = 0; run < 6; ++run) {
-        const int mode = run % 3;
+    for (int run = 0; run < 8; ++run) {
+        const int mode = run < 6 ? run % 3 : (run == 6 ? 2 : 0);
         const bool drawn = run >= 3;
-        const float alpha = mode == 0 ? 0.8f : (mode == 1 ? 1.0f : 0.5f);
-        if (drawn && alpha < 1.0f)
+        const float alpha = run >= 6 ? (run == 6 ? 0.1f : 0.05f) : (mode == 0 ? 0.8f : (mode == 1 ? 1.0f : 0.5f));
+        if (drawn && alpha < 1.0f && alpha > 0.1f)
             for (uint32_t k = 0; k < K; ++k) pw01[k] = powf(u_of(k), 1.0f / alpha);
         const dk::rd::Open01Tab tab{pw01.data(), ln01.data()};
         const int epoch = mode == 1 ? 3 : 12;

@@ -4,7 +4,8 @@
 //      the ones the oracle recomputes by the crate's generator, bit for bit;
 //   2. StandardNormal / Exp1 f64 streams, Gamma<f32> and Dirichlet<f32, 39> draws are
 //      identical value for value, and so is the RNG stream position after every draw, for
-//      shapes on all three Gamma paths (< 1, == 1, > 1).  The engine runs with the Open01
+//      shapes on all three Gamma paths (< 1, == 1, > 1), Beta<f32> draws on both of Cheng's
+//      algorithms (BB, BC), and the FromBeta Dirichlet (alpha <= 0.1).  The engine runs with the Open01
 //      tables the context builds (glibc logf / powf of the 2^23 Open01 values) and its own
 //      ln v = (float)log((double)v); the oracle calls glibc throughout.
 // Usage: dirichlet_check <draws per alpha> <seed>
@@ -50,8 +51,24 @@ int main(int argc, char** argv) {
             checked += 2;
         }
     }
-    // 2b. Gamma and Dirichlet on every path
-    const float alphas[] = {0.3f, 0.5f, 0.8f, 1.0f, 1.5f, 3.0f};
+    // 2b. Beta on both algorithms (the FromBeta Dirichlet's pairs among them: (0.1, 3.8), (0.05, 0.05))
+    const float pairs[][2] = {{0.1f, 3.8f}, {0.05f, 0.05f}, {0.05f, 1.9f}, {0.5f, 0.5f}, {3.0f, 0.7f}, {2.5f, 4.0f}};
+    for (const auto& pr : pairs) {
+        SmallRng o = SmallRng::seed_from_u64(seed * 613 + (uint64_t)(pr[0] * 1000) * 7 + (uint64_t)(pr[1] * 1000));
+        dk::Rng d = to_dk(o);
+        const rdist::Beta ob(pr[0], pr[1]);
+        const dk::rd::BetaF32 db = dk::rd::beta_new(pr[0], pr[1]);
+        for (long i = 0; i < 10 * draws; ++i) {
+            const float a = ob.sample(o), b = dk::rd::beta_sample(db, d);
+            if (memcmp(&a, &b, 4) || !same(d, o)) {
+                printf("MISMATCH beta (%g, %g) draw %ld: %a vs %a\n", pr[0], pr[1], i, a, b);
+                return 1;
+            }
+            checked++;
+        }
+    }
+    // 2c. Gamma and Dirichlet on every path (alpha <= 0.1: the FromBeta construction)
+    const float alphas[] = {0.05f, 0.1f, 0.3f, 0.5f, 0.8f, 1.0f, 1.5f, 3.0f};
     for (float alpha : alphas) {
         const float inv_shape = 1.0f / alpha;
         if (alpha < 1.0f)

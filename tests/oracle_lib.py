@@ -88,6 +88,7 @@ def lib():
             "or_dirichlet": (ctypes.c_int, [ctypes.c_float, ctypes.c_int, ctypes.c_uint32, u64p, f32p]),
             "or_gamma": (None, [ctypes.c_float, ctypes.c_uint32, u64p, f32p]),
             "or_beta": (None, [ctypes.c_float, ctypes.c_float, ctypes.c_uint32, u64p, f32p]),
+            "or_libm_f32": (None, [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64, f32p]),
             "or_normal_f64": (None, [ctypes.c_uint32, u64p, f64p]),
             "or_exp1_f64": (None, [ctypes.c_uint32, u64p, f64p]),
             "or_ziggurat_tables": (None, [f64p]),

@@ -103,16 +103,24 @@ def test_engine_assignment_vs_oracle(native_bins):
 def test_dirichlet_vs_oracle(native_bins):
     """engine/rand_distr.h (the root noise the GPU draws, host build) = the oracle's rand_distr
     0.5.1 restatement: ziggurat tables, StandardNormal / Exp1 streams, Gamma on all three paths
-    and Dirichlet<f32, 39>, value for value with the RNG stream position (parity unpinned:
-    no reference vector exists for these draws)."""
-    assert _run("dirichlet_check", 20000, 3) == 2120000
+    Beta<f32> on Cheng's BB and BC, and Dirichlet<f32, 39> on FromGamma and FromBeta (alpha 0.05,
+    0.1), value for value with the RNG stream position (parity unpinned: no reference vector
+    exists for these draws)."""
+    assert _run("dirichlet_check", 20000, 3) == 3760000
+
+
+def test_libm_f32_vs_glibc(native_bins):
+    """engine/libm_f32.h -- glibc's logf / expf restated for the device (the FromBeta noise's
+    Beta draws call them on arbitrary arguments; Rust's f32::ln / f32::exp are the platform libm)
+    -- equals the host's glibc on all 2^32 f32 inputs, bit for bit."""
+    assert _run("libm_check", 1, max(1, min(16, os.cpu_count() or 1))) == 1 << 32
 
 
 def test_az_core_vs_oracle(native_bins):
     """az_core.h (host build, driven batch-wise like the GPU) = oracle AlphaZero
     mcts_search: root priors, visits, chosen action and RNG position, three temperature modes,
     with caller-supplied noise and with the Dirichlet noise the search draws itself."""
-    assert _run("az_check", 120, 300, 5) == 720
+    assert _run("az_check", 120, 300, 5) == 960
 
 
 def test_fusion_kats():

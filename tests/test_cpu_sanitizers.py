@@ -36,7 +36,8 @@ CASES = [
     ("fdo_engine_check", (40, 11), 1000),
     ("do_engine_check", (30, 7), 1000),
     ("az_check", (20, 100, 5), 120),
-    ("dirichlet_check", (2000, 3), 212000),
+    ("dirichlet_check", (2000, 3), 376000),
+    ("libm_check", (65537, 8), 65536),
     ("assign_check", (30, 3), 1000),
     ("ar_check", (30, 3, 9), 200),
 ]
