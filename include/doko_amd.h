@@ -541,13 +541,15 @@ int dk_net_qkv_attn_ln_f32x3_async(const float* h, float* x_io, const void* wqkv
  * LayerNorm mean and 1 / sqrt(var + eps) (eps: the LayerNorm the next half applies); stats_in gives
  * the x-input form those statistics instead of reducing over the row (the d = 160 MLP half
  * requires them; the attention half computes them itself when stats_in is NULL).  stats_in and
- * stats_out may be the same buffer.  The same weights, split layouts and validity rules
- * (n_hidden % 64 == 0); DK_E_INVALID otherwise. */
+ * stats_out may be the same buffer.  x_out (attention half only; NULL or x_io: in place): the new
+ * x rows are written there and x_io is only read -- a branch that starts from a shared trunk's x
+ * (the AlphaZero network's policy and value branches) without copying it first.  The same weights,
+ * split layouts and validity rules (n_hidden % 64 == 0); DK_E_INVALID otherwise. */
 int dk_net_qkv_attn_ln_f32x3_ex_async(const float* h_in, float* x_io, const float* ln_in_gamma, const float* ln_in_beta,
                                       float ln_in_eps, const void* wqkv_hi, const void* wqkv_lo, const float* bqkv,
                                       const void* wp_hi, const void* wp_lo, const float* bp, uint32_t batch, uint32_t heads,
                                       uint32_t head_dim, const float* gamma, const float* beta, float eps, float* h_out,
-                                      const float* stats_in, float* stats_out, void* stream);
+                                      const float* stats_in, float* stats_out, float* x_out, void* stream);
 int dk_net_mlp_ln_f32x3_ex_async(const float* h_in, float* x_io, const float* ln_in_gamma, const float* ln_in_beta,
                                  float ln_in_eps, const void* w1_hi, const void* w1_lo, const float* b1, const void* w2_hi,
                                  const void* w2_lo, const float* b2, uint32_t rows, uint32_t d, uint32_t n_hidden,

@@ -119,7 +119,7 @@ def lib():
         "dk_net_qkv_attn_ln_f32x3_async": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, u32, u32, u32, vp, vp,
                                                           ctypes.c_float, vp, vp]),
         "dk_net_qkv_attn_ln_f32x3_ex_async": (ctypes.c_int, [vp, vp, vp, vp, ctypes.c_float, vp, vp, vp, vp, vp, vp, u32, u32,
-                                                             u32, vp, vp, ctypes.c_float, vp, vp, vp, vp]),
+                                                             u32, vp, vp, ctypes.c_float, vp, vp, vp, vp, vp]),
         "dk_net_mlp_ln_f32x3_ex_async": (ctypes.c_int, [vp, vp, vp, vp, ctypes.c_float, vp, vp, vp, vp, vp, vp, u32, u32, u32,
                                                         vp, vp, ctypes.c_float, vp, vp, vp, vp]),
         "dk_net_class_pool_ln_f32_async": (ctypes.c_int, [vp, u32, u32, vp, u32, ctypes.c_float, vp, vp, ctypes.c_float,

@@ -428,8 +428,13 @@ class FusedTrunkF32(FusedTrunk):
     def chain(self, blocks):
         return self.chain_ok(self.d, blocks)
 
-    def run(self, h, blocks, final_ln, x=None):
+    def run(self, h, blocks, final_ln, x=None, x_out=None):
+        """x_out (x-only chain): the first half reads x and writes the new x to x_out, the rest
+        continue in place on x_out -- a branch from a shared trunk's x without copying it."""
         if not self.chain(blocks):
+            if x_out is not None:
+                x_out.copy_(self.x if x is None else x)
+                x = x_out
             return super().run(h, blocks, final_ln, x)
         # d = 256 (round 5) and d = 160 (round 6): every half reads the residual stream x and applies
         # the LayerNorm its producer used to write out as h (the *_ex kernels; at d = 160 also the
@@ -448,7 +453,10 @@ class FusedTrunkF32(FusedTrunk):
                 h.data_ptr() if lin is None else None, x.data_ptr(), lin.weight.data_ptr() if lin else None,
                 lin.bias.data_ptr() if lin else None, lin.eps if lin else 0.0, wqh.data_ptr(), wql.data_ptr(),
                 blk.qkv.bias.data_ptr(), wph.data_ptr(), wpl.data_ptr(), bpf.data_ptr(), x.shape[0], 4, self.d // 4, None,
-                None, blk.ln_2.eps, None, stp if i > 0 else None, stp, self.st))
+                None, blk.ln_2.eps, None, stp if i > 0 else None, stp,
+                x_out.data_ptr() if (i == 0 and x_out is not None) else None, self.st))
+            if i == 0 and x_out is not None:
+                x = x_out
             last = i + 1 == len(blocks)
             w1h, w1l, w2h, w2l = split_bf16x3(blk)
             wh = last and final_ln is not None   # (final_ln None: no h at all)
@@ -534,8 +542,14 @@ class DokoAzNet(nn.Module):
         f = trunk(tokens, self.emb, self.blocks[0].ln_1, need_h=False) if x_only else \
             (trunk or FusedTrunk)(tokens, self.emb, self.blocks[0].ln_1)
         hp = f.run(f.h, self.blocks, None if x_only else self.p_blocks[0].ln_1)   # f.x: the shared trunk's output
+        if x_only:
+            # the value branch first, its first half writing a new x (the trunk's x stays for the
+            # policy branch, no copy); then the policy branch in place on the trunk's x
+            hv = f.run(None, self.v_blocks, self.v_ln, x_out=torch.empty_like(f.x))
+            hp = f.run(hp, self.p_blocks, self.p_ln)
+            return self.value_head(hv), self.policy_head(hp)
         xv = f.x.clone()
-        hv = None if x_only else f.add_ln(xv, None, self.v_blocks[0].ln_1)
+        hv = f.add_ln(xv, None, self.v_blocks[0].ln_1)
         hp = f.run(hp, self.p_blocks, self.p_ln)
         hv = f.run(hv, self.v_blocks, self.v_ln, x=xv)
         return self.value_head(hv), self.policy_head(hp)

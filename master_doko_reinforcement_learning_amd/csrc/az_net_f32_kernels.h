@@ -93,6 +93,33 @@ __global__ void embed_ln_f32_kernel(const int32_t* __restrict__ tokens, uint32_t
         ln_row_f32<P4>(x, d, lane, (const float4*)gamma, (const float4*)beta, eps, (float4*)(h_out + (size_t)row * d));
 }
 
+// The embedding sum alone (h_out NULL: the x-only chain normalises x in its first half), one lane
+// per float4 of a row: lanes fully used at any d % 4 == 0 (the row-per-half-wave form above left
+// 24 of 32 lanes idle in its second group at d = 160) and x stored contiguously across the wave.
+// The six token reads of a row are shared by its d / 4 lanes (cache hits).
+__global__ void embed_f32_kernel(const int32_t* __restrict__ tokens, uint32_t B, int d, const float* __restrict__ e0,
+                                 const float* __restrict__ e1, const float* __restrict__ e2, const float* __restrict__ e3,
+                                 const float* __restrict__ e4, const float* __restrict__ e5, float* __restrict__ x_out) {
+    const uint32_t n4 = (uint32_t)d / 4u;
+    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i >= (uint64_t)B * 62u * n4) return;
+    const uint32_t row = (uint32_t)(i / n4), j = (uint32_t)(i % n4);
+    const uint32_t b = row / 62u, s = row % 62u;
+    const int32_t* t = tokens + (size_t)b * 311;
+    const int32_t k0 = t[s], k1 = t[62 + s], k2 = t[124 + s], k3 = t[186 + s], k4 = t[248 + s], k5 = t[310];
+    float4 a = ((const float4*)(e0 + (size_t)k0 * d))[j];
+    const float4 v1 = ((const float4*)(e1 + (size_t)k1 * d))[j], v2 = ((const float4*)(e2 + (size_t)k2 * d))[j],
+                 v3 = ((const float4*)(e3 + (size_t)k3 * d))[j], v4 = ((const float4*)(e4 + (size_t)k4 * d))[j],
+                 v5 = ((const float4*)(e5 + (size_t)k5 * d))[j];
+    // torch: ((((e0 + e1) + e2) + e3) + e4) + e5
+    a.x += v1.x; a.y += v1.y; a.z += v1.z; a.w += v1.w;
+    a.x += v2.x; a.y += v2.y; a.z += v2.z; a.w += v2.w;
+    a.x += v3.x; a.y += v3.y; a.z += v3.z; a.w += v3.w;
+    a.x += v4.x; a.y += v4.y; a.z += v4.z; a.w += v4.w;
+    a.x += v5.x; a.y += v5.y; a.z += v5.z; a.w += v5.w;
+    ((float4*)x_out)[i] = a;
+}
+
 template <int P4>
 __global__ void add_ln_f32_kernel(float* __restrict__ x_io, const float* __restrict__ delta, uint32_t rows, int d,
                                   const float* gamma, const float* beta, float eps, float* __restrict__ h_out,
@@ -433,12 +460,19 @@ __global__ void __launch_bounds__(64 * WAVES, D <= 160 ? 8 / WAVES : 1) mlp_ln_f
 #ifdef DK_NET_PROF
     // phase clocks of wave 0 (profiling builds): drained stamps, sums in registers, atomics at the end
     unsigned long long f_prev = __builtin_amdgcn_s_memtime(), facc[6] = {0, 0, 0, 0, 0, 0};
+    const unsigned long long f_t0 = f_prev, f_r0 = __builtin_amdgcn_s_memrealtime();
 #define DK_FSTAMP(k) do { __builtin_amdgcn_s_waitcnt(0); const unsigned long long t_ = __builtin_amdgcn_s_memtime(); facc[k] += t_ - f_prev; f_prev = t_; } while (0)
 #else
 #define DK_FSTAMP(k) ((void)0)
 #endif
+#if DK_MLPF32_PRIO == 1
+    if (blockIdx.x & 1) __builtin_amdgcn_s_setprio(1);
+#elif DK_MLPF32_PRIO == 2
+    if ((blockIdx.x >> 8) & 1) __builtin_amdgcn_s_setprio(1);
+#endif
     // the row's h, split: lane (r, hh) holds k = 16 kk + 8 hh .. + 7 of row r
     bf16x8_t hfh[KS], hfl[KS];
+    auto prologue = [&]() {
     if constexpr (XIN) {
         // the row's x (this lane: k = 16 kk + 8 hh .. + 7), normalised with the producer's row
         // statistics and the consumer's weights, then split (as the h loads below: no reduction)
@@ -473,6 +507,10 @@ __global__ void __launch_bounds__(64 * WAVES, D <= 160 ? 8 / WAVES : 1) mlp_ln_f
             split_bf16x8(v, hfh[kk], hfl[kk]);
         }
     }
+    };
+#if !DK_MLPF32_STAGE_FIRST
+    prologue();
+#endif
     typedef __attribute__((address_space(3))) void lds_void;
     // (a compile-time count of DMA instructions per wave: the loads issued before a stage -- the
     // chunk's biases -- then wait on a counted vmcnt, not on the stage itself)
@@ -516,6 +554,18 @@ __global__ void __launch_bounds__(64 * WAVES, D <= 160 ? 8 / WAVES : 1) mlp_ln_f
 #ifndef DK_MLPF32_DMA_STEP
 #define DK_MLPF32_DMA_STEP 1
 #endif
+#ifndef DK_MLPF32_PKGELU
+#define DK_MLPF32_PKGELU 0
+#endif
+#ifndef DK_MLPF32_EARLY_BIAS
+#define DK_MLPF32_EARLY_BIAS 0
+#endif
+#ifndef DK_MLPF32_PRIO
+#define DK_MLPF32_PRIO 0
+#endif
+#ifndef DK_MLPF32_STAGE_FIRST
+#define DK_MLPF32_STAGE_FIRST 0
+#endif
     constexpr int DMA_PER_STEP = DK_MLPF32_DMA_STEP;
     auto stage = [&](uint32_t c, uint16_t* dst) {
 #pragma unroll
@@ -531,16 +581,25 @@ __global__ void __launch_bounds__(64 * WAVES, D <= 160 ? 8 / WAVES : 1) mlp_ln_f
 #ifdef DK_SOL_NODMA
     stage(0u, lds1);   // (speed-of-light measurement build: every chunk computes on chunk 0's weights)
 #endif
+#if DK_MLPF32_STAGE_FIRST
+    prologue();        // (the first chunk's DMA in flight under the row loads)
+#endif
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
     DK_FSTAMP(0);
+    float bb[NC];   // (DK_MLPF32_EARLY_BIAS: loaded before the previous chunk's closing wait)
+#if DK_MLPF32_EARLY_BIAS
+#pragma unroll
+    for (int m = 0; m < NC; ++m) bb[m] = b1[m];
+#endif
     auto chunk = [&](uint32_t c, const uint16_t* cur, uint16_t* nxt) {
         // GEMM1 accumulates onto the chunk's biases (acc1[4 j + e] = b1[32 c + 8 j + 4 hh + e]),
         // read with uniform addresses (scalar loads: counted by lgkmcnt, so that waiting for them
         // does not wait for the stage's DMA, which vmcnt counts), each lane taking its half
-        float bb[NC];
+#if !DK_MLPF32_EARLY_BIAS
 #pragma unroll
         for (int m = 0; m < NC; ++m) bb[m] = b1[c * NC + m];
+#endif
         f32x16_t acc1;
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -595,7 +654,15 @@ __global__ void __launch_bounds__(64 * WAVES, D <= 160 ? 8 / WAVES : 1) mlp_ln_f
             float g[8];
 #pragma unroll
 #ifndef DK_SOL_NOGELU
+#if DK_MLPF32_PKGELU
+            for (int t = 0; t < 8; t += 2) {
+                const f32x2_t gg = gelu_poly_pk(f32x2_t{acc1[8 * s2 + t], acc1[8 * s2 + t + 1]});
+                g[t] = gg.x;
+                g[t + 1] = gg.y;
+            }
+#else
             for (int t = 0; t < 8; ++t) g[t] = gelu_poly(acc1[8 * s2 + t]);
+#endif
 #else
             for (int t = 0; t < 8; ++t) g[t] = acc1[8 * s2 + t];   // (speed-of-light measurement build)
 #endif
@@ -626,6 +693,10 @@ __global__ void __launch_bounds__(64 * WAVES, D <= 160 ? 8 / WAVES : 1) mlp_ln_f
 #endif
         }
         DK_FSTAMP(3);
+#if DK_MLPF32_EARLY_BIAS
+#pragma unroll
+        for (int m = 0; m < NC; ++m) bb[m] = b1[cn * NC + m];   // (their latency under the wait below)
+#endif
         __builtin_amdgcn_s_waitcnt(0);   // this wave's pieces of the next chunk have landed
         __syncthreads();                 // ... and every wave's; every wave is done with `cur`
         DK_FSTAMP(4);
@@ -697,8 +768,12 @@ __global__ void __launch_bounds__(64 * WAVES, D <= 160 ? 8 / WAVES : 1) mlp_ln_f
     }
     DK_FSTAMP(5);
 #ifdef DK_NET_PROF
-    if (lane == 0 && wave == 0)
+    if (lane == 0 && wave == 0) {
         for (int q = 0; q < 6; ++q) atomicAdd(&dk_mlp_prof_acc[q], facc[q]);
+        // the shader clock over the workgroup's life: cycles (s_memtime) and 100 MHz ticks
+        atomicAdd(&dk_mlp_prof_acc[6], __builtin_amdgcn_s_memtime() - f_t0);
+        atomicAdd(&dk_mlp_prof_acc[7], __builtin_amdgcn_s_memrealtime() - f_r0);
+    }
 #endif
 #undef DK_FSTAMP
 }
@@ -1148,7 +1223,9 @@ __device__ __forceinline__ void split_head(const f32x16_t (&acc)[2][2], bf16x8_t
 }
 
 // XIN (as mlp16_ln_f32x3_kernel): the sample's rows come from x_io (h_in unused) and are
-// normalised here with (gin, bin, eps_in); h_out == nullptr: x only is written.
+// normalised here with (gin, bin, eps_in); h_out == nullptr: x only is written.  x_out != nullptr:
+// the new x goes there and x_io is only read (a branch starting from a shared trunk's x without a
+// copy of it).
 template <int HD, bool XIN = false>
 __global__ void __launch_bounds__(256, HD == 40 ? 3 : 2) qkv_attn_ln_f32x3_kernel(const float* __restrict__ h_in, float* __restrict__ x_io,
                                                                    const uint16_t* __restrict__ wqh, const uint16_t* __restrict__ wql,
@@ -1160,7 +1237,8 @@ __global__ void __launch_bounds__(256, HD == 40 ? 3 : 2) qkv_attn_ln_f32x3_kerne
                                                                    const float* __restrict__ gin = nullptr,
                                                                    const float* __restrict__ bin = nullptr, float eps_in = 0.0f,
                                                                    const float2* __restrict__ stats_in = nullptr,
-                                                                   float2* __restrict__ stats_out = nullptr) {
+                                                                   float2* __restrict__ stats_out = nullptr,
+                                                                   float* __restrict__ x_out = nullptr) {
     constexpr int S = 62, D = HD * 4, LDY = D + 8, LDT = 64 + 4, KS = (HD + 15) / 16, LDX = D + 4;
     constexpr bool TAIL3 = HD == 40;                       // the three projections' dims 32..39 in one tile
     constexpr bool PERDT = HD == 64;                       // Q / K one 32-dim tile at a time
@@ -1591,7 +1669,7 @@ __global__ void __launch_bounds__(256, HD == 40 ? 3 : 2) qkv_attn_ln_f32x3_kerne
 #pragma unroll
             for (int i = 0; i < LP; ++i) {
                 const int c0 = 4 * (q + 4 * i);
-                *(float4*)(x_io + o + c0) = xv[i];
+                *(float4*)((x_out != nullptr ? x_out : x_io) + o + c0) = xv[i];
                 if (wh) {
                     const float4 g = *(const float4*)(gamma + c0), be = *(const float4*)(beta + c0);
                     *(float4*)(h_out + o + c0) = make_float4((xv[i].x - mean) * rstd * g.x + be.x, (xv[i].y - mean) * rstd * g.y + be.y,

@@ -1168,6 +1168,24 @@ __device__ __forceinline__ float gelu_poly(float v) {
     return fmaf(-fabsf(v), fabsf(v) > 5.5f ? 0.0f : e, fmaxf(v, 0.0f));
 }
 
+// gelu_poly on a pair, its fma chain on packed f32 (v_pk_fma_f32: two lanes' values per
+// instruction), the same operations per element: bit-identical to two gelu_poly calls.
+__device__ __forceinline__ f32x2_t gelu_poly_pk(f32x2_t v) {
+    const float a0 = fminf(fabsf(v.x), 5.5f), a1 = fminf(fabsf(v.y), 5.5f);
+    const f32x2_t a = {a0, a1};
+    f32x2_t q = {3.236920019844547e-05f, 3.236920019844547e-05f};
+    q = __builtin_elementwise_fma(q, a, f32x2_t{-0.0007541869999840856f, -0.0007541869999840856f});
+    q = __builtin_elementwise_fma(q, a, f32x2_t{0.008001405745744705f, 0.008001405745744705f});
+    q = __builtin_elementwise_fma(q, a, f32x2_t{-0.05324144661426544f, -0.05324144661426544f});
+    q = __builtin_elementwise_fma(q, a, f32x2_t{-0.45893436670303345f, -0.45893436670303345f});
+    q = __builtin_elementwise_fma(q, a, f32x2_t{-1.1511378288269043f, -1.1511378288269043f});
+    q = __builtin_elementwise_fma(q, a, f32x2_t{-1.0f, -1.0f});
+    const f32x2_t e = {fabsf(v.x) > 5.5f ? 0.0f : __builtin_amdgcn_exp2f(q.x), fabsf(v.y) > 5.5f ? 0.0f : __builtin_amdgcn_exp2f(q.y)};
+    const f32x2_t m = {fmaxf(v.x, 0.0f), fmaxf(v.y, 0.0f)};
+    const f32x2_t na = {-fabsf(v.x), -fabsf(v.y)};
+    return __builtin_elementwise_fma(na, e, m);
+}
+
 // f32 pair -> two bf16 (round to nearest even, NaN kept), one v_cvt_pk_bf16_f32
 constexpr uint32_t MLP_MAX_HIDDEN = 1024;
 #ifndef DK_MLP_SKEW

@@ -2378,10 +2378,12 @@ int dk_net_qkv_attn_ln_f32x3_ex_async(const float* h_in, float* x_io, const floa
                                       float ln_in_eps, const void* wqkv_hi, const void* wqkv_lo, const float* bqkv,
                                       const void* wp_hi, const void* wp_lo, const float* bp, uint32_t batch, uint32_t heads,
                                       uint32_t head_dim, const float* gamma, const float* beta, float eps, float* h_out,
-                                      const float* stats_in, float* stats_out, void* stream) {
+                                      const float* stats_in, float* stats_out, float* x_out, void* stream) {
     const bool xin = h_in == nullptr;
+    if (x_out == x_io) x_out = nullptr;   // (in place)
     if (!x_io || !wqkv_hi || !wqkv_lo || !bqkv || !wp_hi || !wp_lo || !bp || (xin && (!ln_in_gamma || !ln_in_beta)) ||
-        (h_out && (!gamma || !beta || h_out == h_in || h_out == x_io)) || (h_in && h_in == x_io) || heads != 4u ||
+        (h_out && (!gamma || !beta || h_out == h_in || h_out == x_io || h_out == x_out)) || (h_in && h_in == x_io) ||
+        (x_out && x_out == h_in) || heads != 4u ||
         (head_dim != 64u && head_dim != 40u) || (head_dim == 40u && !xin) ||
         (head_dim == 64u && (stats_in || stats_out)))   // (row statistics: the d = 160 chain only)
         return DK_E_INVALID;
@@ -2391,17 +2393,17 @@ int dk_net_qkv_attn_ln_f32x3_ex_async(const float* h_in, float* x_io, const floa
         hipLaunchKernelGGL((dk::net::qkv_attn_ln_f32x3_kernel<40, true>), dim3(batch), dim3(256), 0, (hipStream_t)stream,
                            (const float*)nullptr, x_io, (const uint16_t*)wqkv_hi, (const uint16_t*)wqkv_lo, bqkv,
                            (const uint16_t*)wp_hi, (const uint16_t*)wp_lo, bp, scale, gamma, beta, eps, h_out, ln_in_gamma,
-                           ln_in_beta, ln_in_eps, (const float2*)stats_in, (float2*)stats_out);
+                           ln_in_beta, ln_in_eps, (const float2*)stats_in, (float2*)stats_out, x_out);
     else if (xin)
         hipLaunchKernelGGL((dk::net::qkv_attn_ln_f32x3_kernel<64, true>), dim3(batch), dim3(256), 0, (hipStream_t)stream,
                            (const float*)nullptr, x_io, (const uint16_t*)wqkv_hi, (const uint16_t*)wqkv_lo, bqkv,
                            (const uint16_t*)wp_hi, (const uint16_t*)wp_lo, bp, scale, gamma, beta, eps, h_out, ln_in_gamma,
-                           ln_in_beta, ln_in_eps, (const float2*)nullptr, (float2*)nullptr);
+                           ln_in_beta, ln_in_eps, (const float2*)nullptr, (float2*)nullptr, x_out);
     else
         hipLaunchKernelGGL((dk::net::qkv_attn_ln_f32x3_kernel<64, false>), dim3(batch), dim3(256), 0, (hipStream_t)stream,
                            h_in, x_io, (const uint16_t*)wqkv_hi, (const uint16_t*)wqkv_lo, bqkv, (const uint16_t*)wp_hi,
                            (const uint16_t*)wp_lo, bp, scale, gamma, beta, eps, h_out, (const float*)nullptr,
-                           (const float*)nullptr, 0.0f, (const float2*)nullptr, (float2*)nullptr);
+                           (const float*)nullptr, 0.0f, (const float2*)nullptr, (float2*)nullptr, x_out);
     DK_HIP(hipGetLastError());
     return DK_OK;
 }
@@ -2591,9 +2593,16 @@ int dk_net_embed_ln_f32_async(const int32_t* d_tokens, uint32_t batch, const voi
     if (!tables || !d_tokens || !x_out || (h_out && (!gamma || !beta)) || p4 == 0) return DK_E_INVALID;
     if (batch == 0) return DK_OK;
     const uint32_t rows = batch * 62u;
-    const dim3 grid((rows + 7u) / 8u), block(256);
     hipStream_t st = (hipStream_t)stream;
     const float* const* t = (const float* const*)tables;
+    if (!h_out) {   // x only: one lane per float4
+        const uint64_t n = (uint64_t)rows * (d / 4u);
+        hipLaunchKernelGGL(dk::net::embed_f32_kernel, dim3((uint32_t)((n + 255u) / 256u)), dim3(256), 0, st, d_tokens, batch,
+                           (int)d, t[0], t[1], t[2], t[3], t[4], t[5], (float*)x_out);
+        DK_HIP(hipGetLastError());
+        return DK_OK;
+    }
+    const dim3 grid((rows + 7u) / 8u), block(256);
     switch (p4) {
 #define M(P) case P: hipLaunchKernelGGL(dk::net::embed_ln_f32_kernel<P>, grid, block, 0, st, d_tokens, batch, (int)d, t[0], t[1], \
                                         t[2], t[3], t[4], t[5], (const float*)gamma, (const float*)beta, eps, (float*)x_out,      \

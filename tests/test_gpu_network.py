@@ -126,9 +126,17 @@ def test_ex_halves_normalise_x_input(write_h, d):
                                                sp[1].data_ptr(), bq.data_ptr(), sp[2].data_ptr(), sp[3].data_ptr(),
                                                bp.data_ptr(), B, H, hd, g.data_ptr() if write_h else None,
                                                be.data_ptr() if write_h else None, 1e-5,
-                                               ha.data_ptr() if write_h else None, None, sptr, st) == 0
+                                               ha.data_ptr() if write_h else None, None, sptr, None, st) == 0
     torch.cuda.synchronize()
     xa_got = xo.clone()
+    # x_out: the same half from the same x into another buffer, x left as it was
+    xsrc, xdst = x.clone(), torch.full_like(x, float("nan"))
+    assert L.dk_net_qkv_attn_ln_f32x3_ex_async(None, xsrc.data_ptr(), gi.data_ptr(), bi.data_ptr(), 1e-5, sp[0].data_ptr(),
+                                               sp[1].data_ptr(), bq.data_ptr(), sp[2].data_ptr(), sp[3].data_ptr(),
+                                               bp.data_ptr(), B, H, hd, None, None, 1e-5, None, None, None,
+                                               xdst.data_ptr(), st) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(xsrc, x) and torch.equal(xdst, xa_got)
     assert L.dk_net_mlp_ln_f32x3_ex_async(None, xo.data_ptr(), gi.data_ptr(), bi.data_ptr(), 1e-5, sm[0].data_ptr(),
                                           sm[1].data_ptr(), b1.data_ptr(), sm[2].data_ptr(), sm[3].data_ptr(), b2.data_ptr(),
                                           B * 62, d, n, g.data_ptr() if write_h else None,
@@ -156,7 +164,7 @@ def test_ex_halves_normalise_x_input(write_h, d):
     assert L.dk_net_qkv_attn_ln_f32x3_ex_async(None, xo.data_ptr(), gi.data_ptr(), bi.data_ptr(), 1e-5, sp[0].data_ptr(),
                                                sp[1].data_ptr(), bq.data_ptr(), sp[2].data_ptr(), sp[3].data_ptr(),
                                                bp.data_ptr(), B, H, hd, g.data_ptr(), be.data_ptr(), 1e-5, xo.data_ptr(),
-                                               None, None, st) != 0
+                                               None, None, None, st) != 0
     hdummy = torch.zeros_like(x)
     assert L.dk_net_mlp_ln_f32x3_ex_async(hdummy.data_ptr(), xo.data_ptr(), None, None, 1e-5, sm[0].data_ptr(),
                                           sm[1].data_ptr(), b1.data_ptr(), sm[2].data_ptr(), sm[3].data_ptr(), b2.data_ptr(),
@@ -585,6 +593,10 @@ def test_f32_row_kernels_match_torch(d):
     torch.cuda.synchronize()
     assert torch.equal(x, xr)                               # the same left-to-right f32 sum
     torch.testing.assert_close(h, F.layer_norm(xr, (d,), g, b, 1e-5), rtol=1e-5, atol=1e-5)
+    x1 = torch.full_like(x, float("nan"))                   # x only (h_out NULL): embed_f32_kernel
+    assert _lib().dk_net_embed_ln_f32_async(tok.data_ptr(), B, tp, d, None, None, 1e-5, x1.data_ptr(), None, st) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(x1, xr)
     delta = torch.randn_like(x)
     x2 = x.clone()
     assert _lib().dk_net_add_ln_f32_async(x2.data_ptr(), delta.data_ptr(), B * 62, d, g.data_ptr(), b.data_ptr(), 1e-5,
