@@ -448,7 +448,7 @@ class FusedTrunkF32(FusedTrunk):
         ho = None
         for i, blk in enumerate(blocks):
             wqh, wql, wph, wpl, bpf = split_attn_bf16x3(blk)
-            lin = None if (i == 0 and self.d == 256) else blk.ln_1
+            lin = None if (i == 0 and self.d == 256 and h is not None) else blk.ln_1   # (h None: x only)
             self.ck(self.L.dk_net_qkv_attn_ln_f32x3_ex_async(
                 h.data_ptr() if lin is None else None, x.data_ptr(), lin.weight.data_ptr() if lin else None,
                 lin.bias.data_ptr() if lin else None, lin.eps if lin else 0.0, wqh.data_ptr(), wql.data_ptr(),

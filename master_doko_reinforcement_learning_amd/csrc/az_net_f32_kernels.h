@@ -1873,6 +1873,120 @@ __global__ void __launch_bounds__(256, 2) class_pool_ln_f32x3_kernel(const float
     }
 }
 
+// The same pooling + class LayerNorm for a few classes (C <= 8: the AlphaZero value head's 4), in
+// f32 FMAs: a 32-class MFMA tile would be 7/8 padding there, and its four waves each recomputed the
+// whole score tile.  One 256-thread workgroup per sample:
+//   x rows -> LDS (f32, rows padded to d + 1 words: the score phase reads a column, one row per
+//   lane, on distinct banks), the queries -> LDS;
+//   scores: lane t of wave w holds token t of class w (+ 4), q . x_t in k order, * scale
+//   (torch: einsum, then * scale); softmax over the wave's 62 tokens (max, exp, sum, divide);
+//   attended[c][k] = sum over t of p[c][t] x[t][k] (t ascending), one (c, k) per lane;
+//   LayerNorm of each class row (two-pass, biased variance) * w[c] + b[c], class-major output.
+template <int D>
+__global__ void __launch_bounds__(256) class_pool_small_ln_f32_kernel(const float* __restrict__ xin, uint32_t batch,
+                                                                      const float* __restrict__ queries, uint32_t classes,
+                                                                      float scale, const float* __restrict__ lnw,
+                                                                      const float* __restrict__ lnb, float eps,
+                                                                      float* __restrict__ out) {
+    constexpr int S = 62, LDX = D + 1, CM = 8;
+    static_assert(D % 4 == 0, "whole float4 pieces per row");
+    __shared__ float xs[S * LDX];
+    __shared__ float qs[CM * D];      // the queries, then the attended rows
+    __shared__ float ps[CM * 64];     // softmax weights [c][t]
+    const int tid = threadIdx.x, wave = tid >> 6, t = tid & 63, C = (int)classes;
+    const uint32_t b = blockIdx.x;
+    const float4* xg = (const float4*)(xin + (size_t)b * S * D);
+    {
+        constexpr int N4 = S * D / 4, PER = (N4 + 255) / 256;
+        float4 v[PER];
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int p = tid + 256 * i;
+            v[i] = xg[p < N4 ? p : N4 - 1];   // (every load issued before the stores)
+        }
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int p = tid + 256 * i;
+            if (p < N4) {
+                const int row = (4 * p) / D, k = 4 * p - row * D;
+                float* dst = &xs[row * LDX + k];
+                dst[0] = v[i].x; dst[1] = v[i].y; dst[2] = v[i].z; dst[3] = v[i].w;
+            }
+        }
+        for (int p = tid; p < C * D; p += 256) qs[p] = queries[p];
+    }
+    __syncthreads();
+    for (int c = wave; c < C; c += 4) {
+        float sc = 0.0f;
+        if (t < S) {
+            const float* xr = &xs[t * LDX];
+            const float* qr = &qs[c * D];
+#pragma unroll 8
+            for (int k = 0; k < D; ++k) sc = fmaf(qr[k], xr[k], sc);
+        }
+        sc *= scale;
+        float m = t < S ? sc : -INFINITY;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+        const float e = t < S ? expf(sc - m) : 0.0f;
+        float l = e;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) l += __shfl_xor(l, o);
+        ps[c * 64 + t] = e / l;
+    }
+    __syncthreads();
+    // (the queries are read: their LDS takes the attended rows)
+    float av[(CM * D + 255) / 256];
+#pragma unroll
+    for (int i = 0; i < (CM * D + 255) / 256; ++i) {
+        const int o = tid + 256 * i;
+        av[i] = 0.0f;
+        if (o < C * D) {
+            const int c = o / D, k = o - c * D;
+            float a = 0.0f;
+            for (int s2 = 0; s2 < S; ++s2) a = fmaf(ps[c * 64 + s2], xs[s2 * LDX + k], a);
+            av[i] = a;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < (CM * D + 255) / 256; ++i) {
+        const int o = tid + 256 * i;
+        if (o < C * D) qs[o] = av[i];
+    }
+    __syncthreads();
+    constexpr int KP = (D + 63) / 64;   // a row's values per lane
+    for (int c = wave; c < C; c += 4) {
+        float v[KP];
+        float s1 = 0.0f;
+#pragma unroll
+        for (int j = 0; j < KP; ++j) {
+            const int k = t + 64 * j;
+            v[j] = k < D ? qs[c * D + k] : 0.0f;
+            s1 += v[j];
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) s1 += __shfl_xor(s1, o);
+        const float mean = s1 / (float)D;
+        float s2 = 0.0f;
+#pragma unroll
+        for (int j = 0; j < KP; ++j) {
+            const int k = t + 64 * j;
+            const float dv = k < D ? v[j] - mean : 0.0f;
+            s2 += dv * dv;
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) s2 += __shfl_xor(s2, o);
+        const float rstd = rsqrtf(s2 / (float)D + eps);
+        float* orow = out + ((size_t)c * batch + b) * D;
+#pragma unroll
+        for (int j = 0; j < KP; ++j) {
+            const int k = t + 64 * j;
+            if (k < D) orow[k] = (v[j] - mean) * rstd * lnw[(size_t)c * D + k] + lnb[(size_t)c * D + k];
+        }
+    }
+}
+
 // Each class's MLP, out[b][c] = w2[c] . GELU(W1[c] a[c][b] + b1[c]) + b2[c] (the exact erf GELU
 // of nn.GELU), grid (row blocks of 128, classes), 4 waves x 32 rows: the row's pooled vector split
 // in registers, W1[c] hi / lo fragments straight from L2 one k-step ahead (a class's W1 is 2 d^2

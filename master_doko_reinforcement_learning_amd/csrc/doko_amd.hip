@@ -2445,7 +2445,15 @@ int dk_net_class_pool_ln_f32_async(const float* x, uint32_t batch, uint32_t d, c
     if (!x || !queries || !ln_w || !ln_b || !out || classes == 0 || classes > 64u || (d != 160u && d != 256u))
         return DK_E_INVALID;
     if (batch == 0) return DK_OK;
-    if (d == 160u)
+    static const bool small_off = getenv("DK_POOL_SMALL") && atoi(getenv("DK_POOL_SMALL")) == 0;   // (measurement switch)
+    if (classes <= 8u && !small_off) {   // (few classes: f32 FMAs, class_pool_small_ln_f32_kernel)
+        if (d == 160u)
+            hipLaunchKernelGGL((dk::net::class_pool_small_ln_f32_kernel<160>), dim3(batch), dim3(256), 0, (hipStream_t)stream,
+                               x, batch, queries, classes, scale, ln_w, ln_b, eps, out);
+        else
+            hipLaunchKernelGGL((dk::net::class_pool_small_ln_f32_kernel<256>), dim3(batch), dim3(256), 0, (hipStream_t)stream,
+                               x, batch, queries, classes, scale, ln_w, ln_b, eps, out);
+    } else if (d == 160u)
         hipLaunchKernelGGL((dk::net::class_pool_ln_f32x3_kernel<160>), dim3(batch), dim3(256), 0, (hipStream_t)stream, x,
                            batch, queries, classes, scale, ln_w, ln_b, eps, out);
     else

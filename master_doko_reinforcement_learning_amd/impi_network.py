@@ -47,6 +47,11 @@ class DokoImpiNet(nn.Module):
         return self.head(self.ln_f(x), fused=False)
 
     def forward_fused(self, tokens, trunk=None):
+        d = self.emb[0].weight.shape[1]
+        if trunk is FusedTrunkF32 and FusedTrunkF32.chain_ok(d, self.blocks):
+            # x-only chain: the embedding writes x alone and the first half normalises it itself
+            f = trunk(tokens, self.emb, self.blocks[0].ln_1, need_h=False)
+            return self.head(f.run(None, self.blocks, self.ln_f))
         f = (trunk or FusedTrunk)(tokens, self.emb, self.blocks[0].ln_1)
         return self.head(f.run(f.h, self.blocks, self.ln_f))
 

@@ -523,11 +523,12 @@ def test_class_mlp_bf16_matches_fp32(d, C):
     assert e2 < 5e-2, e2
 
 
-@pytest.mark.parametrize("d,C", [(160, 39), (160, 4), (256, 33)])
+@pytest.mark.parametrize("d,C", [(160, 39), (160, 4), (256, 33), (256, 4), (160, 8), (160, 9)])
 def test_class_head_f32_matches_torch(d, C):
-    """The f32 heads (class_pool_ln_f32x3_kernel + class_mlp_f32x3_kernel, bf16x3 products)
-    against ClassHead's torch forward at matmul precision "highest": within 2e-5 of the output
-    scale (B = 300: a partial row block of the class MLP grid)."""
+    """The f32 heads (class_pool_ln_f32x3_kernel -- C <= 8: class_pool_small_ln_f32_kernel, f32
+    FMAs -- + class_mlp_f32x3_kernel, bf16x3 products) against ClassHead's torch forward at matmul
+    precision "highest": within 2e-5 of the output scale (B = 300: a partial row block of the class
+    MLP grid)."""
     from master_doko_reinforcement_learning_amd.az_network import ClassHead
     dev = torch.device("cuda", 0)
     torch.manual_seed(5)
