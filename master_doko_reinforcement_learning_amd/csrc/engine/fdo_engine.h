@@ -617,6 +617,9 @@ DK_HD int round_draws(const Work& w) {
 #ifndef DK_ROLLOUT_FAST
 #define DK_ROLLOUT_FAST 1   // tricks without announcement offers skip the per-card offer tests
 #endif
+#ifndef DK_TRICK_SPEC
+#define DK_TRICK_SPEC 2     // fast tricks drawn speculatively as one block, replayed on a rejection
+#endif
 #ifndef DK_FOX_SKIP
 #define DK_FOX_SKIP 0       // (measurement switch) fast tricks skip the fox tracking once no lane holds a Diamond Ace
 #endif
@@ -678,10 +681,21 @@ DK_HD int rollout_cards(const Work& w0, Rng& rng, int pts[4]) {
     // one card of player p, whose hand is (a, t2), at position `pos` of the trick; updates the
     // hand and the running trick.  `track` keeps the hand sizes (nb) per card, which only the
     // announcement offers read (draws).
-    auto play = [&](uint32_t& a, uint32_t& t2, uint32_t p, bool first, uint32_t pos, bool track, bool fox = true) {
+    // `rej` (speculative tricks): the draw skips range_u32's rejection test and records instead
+    // whether this lane's draw fell into the rejection zone (then the trick is replayed exactly).
+    auto play = [&](uint32_t& a, uint32_t& t2, uint32_t p, bool first, uint32_t pos, bool track, bool fox = true,
+                    uint32_t* rej = nullptr) {
         const uint32_t f = a & lead;
         const uint32_t legal = f ? f : a;
-        const uint32_t r = rng.range_u32((uint32_t)popc32(legal));
+        uint32_t r;
+        if (rej) {
+            const uint32_t n = (uint32_t)popc32(legal);
+            const uint64_t m = (uint64_t)rng.next_u32() * (uint64_t)n;
+            r = (uint32_t)(m >> 32);
+            *rej |= (uint32_t)m > 0u - n ? 1u : 0u;
+        } else {
+            r = rng.range_u32((uint32_t)popc32(legal));
+        }
         const uint32_t card = nth_set_bit24(legal, (uint32_t)popc32(legal) - 1u - r), bit = 1u << card;
 #if DK_ROLLOUT_FAST
         // the second copy goes first: t2 loses the bit if it holds it, a otherwise (no selects)
@@ -787,12 +801,94 @@ DK_HD int rollout_cards(const Work& w0, Rng& rng, int pts[4]) {
                     play(A3, T3, (s + 3u) & 3u, false, 3u, false, false);
                 } else
 #endif
+#if DK_TRICK_SPEC >= 2
+                {
+                    // The four plies in dependency order, as one straight-line block.  The draws
+                    // are taken up front, skipping range_u32's rejection branch (a lane's draw falls
+                    // into its zone with probability < 12 / 2^32 per ply; a wave with any such lane
+                    // replays the trick exactly from the saved generator).  The led class comes from
+                    // the first card by arithmetic, so the three followers' legal sets, ranks and
+                    // table lookups are independent of each other and issue together.
+                    Rng q = rng;
+                    const uint32_t x0 = q.next_u32(), x1 = q.next_u32(), x2 = q.next_u32(), x3 = q.next_u32();
+                    const uint32_t n0 = (uint32_t)popc32(A0);
+                    const uint64_t m0 = (uint64_t)x0 * (uint64_t)n0;
+                    const uint32_t c0 = nth_set_bit24(A0, n0 - 1u - (uint32_t)(m0 >> 32));
+                    const uint32_t ld = class_mask(c0, tm);
+                    const uint32_t f1 = A1 & ld, f2 = A2 & ld, f3 = A3 & ld;
+                    const uint32_t l1 = f1 ? f1 : A1, l2 = f2 ? f2 : A2, l3 = f3 ? f3 : A3;
+                    const uint32_t n1 = (uint32_t)popc32(l1), n2 = (uint32_t)popc32(l2), n3 = (uint32_t)popc32(l3);
+                    const uint64_t m1 = (uint64_t)x1 * (uint64_t)n1, m2 = (uint64_t)x2 * (uint64_t)n2,
+                                   m3 = (uint64_t)x3 * (uint64_t)n3;
+                    const bool rej = (uint32_t)m0 > 0u - n0 || (uint32_t)m1 > 0u - n1 || (uint32_t)m2 > 0u - n2 ||
+                                     (uint32_t)m3 > 0u - n3;
+#ifdef DK_TRICK_REPLAY_ALL
+                    if (!wave_any(rej || true)) {   // (test builds: every trick takes the exact replay)
+#else
+                    if (!wave_any(rej)) {
+#endif
+                        const uint32_t c1 = nth_set_bit24(l1, n1 - 1u - (uint32_t)(m1 >> 32));
+                        const uint32_t c2 = nth_set_bit24(l2, n2 - 1u - (uint32_t)(m2 >> 32));
+                        const uint32_t c3 = nth_set_bit24(l3, n3 - 1u - (uint32_t)(m3 >> 32));
+                        const CardInfo i0 = card_info(gt, c0), i1 = card_info(gt, c1), i2 = card_info(gt, c2),
+                                       i3 = card_info(gt, c3);
+                        rng = q;
+                        const uint32_t b0 = 1u << c0, b1 = 1u << c1, b2 = 1u << c2, b3 = 1u << c3;
+                        const uint32_t d0 = T0 & b0, d1 = T1 & b1, d2 = T2 & b2, d3 = T3 & b3;
+                        T0 ^= d0; A0 ^= b0 ^ d0; T1 ^= d1; A1 ^= b1 ^ d1;
+                        T2 ^= d2; A2 ^= b2 ^ d2; T3 ^= d3; A3 ^= b3 ^ d3;
+                        lead = ld; lt = ld | tm;
+                        const int k1 = ((lt >> c1) & 1u) ? (int)i1.y : -1;
+                        const int k2 = ((lt >> c2) & 1u) ? (int)i2.y : -1;
+                        const int k3 = ((lt >> c3) & 1u) ? (int)i3.y : -1;
+                        best_key = (int)i0.y; best_pos = 0u; win_card = c0;
+                        if (k1 > best_key) { best_key = k1; best_pos = 1u; win_card = c1; }
+                        if (k2 > best_key) { best_key = k2; best_pos = 2u; win_card = c2; }
+                        if (k3 > best_key) { best_key = k3; best_pos = 3u; win_card = c3; }
+                        t_eyes = ((i0.x >> 24) & 15u) + ((i1.x >> 24) & 15u) + ((i2.x >> 24) & 15u) + ((i3.x >> 24) & 15u);
+                        da_bits = (c0 == (uint32_t)DIAMOND_ACE ? 1u << s : 0u) |
+                                  (c1 == (uint32_t)DIAMOND_ACE ? 1u << ((s + 1u) & 3u) : 0u) |
+                                  (c2 == (uint32_t)DIAMOND_ACE ? 1u << ((s + 2u) & 3u) : 0u) |
+                                  (c3 == (uint32_t)DIAMOND_ACE ? 1u << ((s + 3u) & 3u) : 0u);
+                        plies += 4;
+                    } else {
+                        play(A0, T0, s, true, 0u, false);
+                        play(A1, T1, (s + 1u) & 3u, false, 1u, false);
+                        play(A2, T2, (s + 2u) & 3u, false, 2u, false);
+                        play(A3, T3, (s + 3u) & 3u, false, 3u, false);
+                    }
+                }
+#elif DK_TRICK_SPEC
+                {
+                    // The four plies as one straight-line block: the draws skip range_u32's
+                    // rejection branch (a lane falls into its zone with probability < 12 / 2^32
+                    // per ply), so plies 2-4, which depend on ply 1 only through the led class,
+                    // overlap their table lookups.  A wave with any rejecting lane replays the
+                    // trick exactly from the saved hands and generator.
+                    const Rng rs = rng;
+                    const uint32_t a0 = A0, a1 = A1, a2 = A2, a3 = A3, t0 = T0, t1 = T1, t2 = T2, t3 = T3;
+                    uint32_t rej = 0;
+                    play(A0, T0, s, true, 0u, false, true, &rej);
+                    play(A1, T1, (s + 1u) & 3u, false, 1u, false, true, &rej);
+                    play(A2, T2, (s + 2u) & 3u, false, 2u, false, true, &rej);
+                    play(A3, T3, (s + 3u) & 3u, false, 3u, false, true, &rej);
+                    if (wave_any(rej != 0u)) {
+                        rng = rs; A0 = a0; A1 = a1; A2 = a2; A3 = a3; T0 = t0; T1 = t1; T2 = t2; T3 = t3;
+                        plies -= 4;
+                        play(A0, T0, s, true, 0u, false);
+                        play(A1, T1, (s + 1u) & 3u, false, 1u, false);
+                        play(A2, T2, (s + 2u) & 3u, false, 2u, false);
+                        play(A3, T3, (s + 3u) & 3u, false, 3u, false);
+                    }
+                }
+#else
                 {
                     play(A0, T0, s, true, 0u, false);
                     play(A1, T1, (s + 1u) & 3u, false, 1u, false);
                     play(A2, T2, (s + 2u) & 3u, false, 2u, false);
                     play(A3, T3, (s + 3u) & 3u, false, 3u, false);
                 }
+#endif
                 nb -= 0x01010101u;
             }
             const uint32_t bp = best_pos;

@@ -37,6 +37,12 @@ def test_engine_rules_vs_oracle(native_bins):
     assert _run("fdo_engine_check", 300, 11) > 20000
 
 
+def test_engine_rules_vs_oracle_trick_replay(native_bins):
+    """The same checks with every speculative fast-path trick of rollout_cards replayed through
+    the exact per-ply draws (DK_TRICK_REPLAY_ALL): the replay path a rejected draw takes."""
+    assert _run("fdo_engine_check_replay", 300, 11) > 20000
+
+
 def test_do_engine_vs_oracle(native_bins):
     """do_engine.h (host build) = oracle rs-doko: legal masks, wire-format steps, and
     rollouts (fast card phase and stepwise; rewards + RNG stream position), weddings included."""
