@@ -237,10 +237,30 @@ DK_HD int rollout_cards(const Work& w0, Rng& rng, int pts[4]) {
         uint32_t T0 = fdo::sel4u(two0, two1, two2, two3, s0), T1 = fdo::sel4u(two0, two1, two2, two3, (s0 + 1u) & 3u);
         uint32_t T2 = fdo::sel4u(two0, two1, two2, two3, (s0 + 2u) & 3u), T3 = fdo::sel4u(two0, two1, two2, two3, (s0 + 3u) & 3u);
         for (;;) {
-            play(A0, T0, true, 0u);
-            play(A1, T1, false, 1u);
-            play(A2, T2, false, 2u);
-            play(A3, T3, false, 3u);
+            fdo::TrickDraw td;
+            if (DK_TRICK_SPEC && fdo::draw_trick(A0, A1, A2, A3, rng, fdo::GT_NORMAL, tm, td)) {
+                // the four plies as one block (fdo::draw_trick); the exact per-ply path on a rejection
+                const uint32_t b0 = 1u << td.c[0], b1 = 1u << td.c[1], b2 = 1u << td.c[2], b3 = 1u << td.c[3];
+                const uint32_t d0 = T0 & b0, d1 = T1 & b1, d2 = T2 & b2, d3 = T3 & b3;
+                T0 ^= d0; A0 ^= b0 ^ d0; T1 ^= d1; A1 ^= b1 ^ d1;
+                T2 ^= d2; A2 ^= b2 ^ d2; T3 ^= d3; A3 ^= b3 ^ d3;
+                lead = td.ld; lt = td.ld | tm;
+                const int k1 = ((lt >> td.c[1]) & 1u) ? (int)td.i[1].y : -1;
+                const int k2 = ((lt >> td.c[2]) & 1u) ? (int)td.i[2].y : -1;
+                const int k3 = ((lt >> td.c[3]) & 1u) ? (int)td.i[3].y : -1;
+                best_key = (int)td.i[0].y; best_pos = 0u;
+                if (k1 > best_key) { best_key = k1; best_pos = 1u; }
+                if (k2 > best_key) { best_key = k2; best_pos = 2u; }
+                if (k3 > best_key) { best_key = k3; best_pos = 3u; }
+                t_eyes = ((td.i[0].x >> 24) & 15u) + ((td.i[1].x >> 24) & 15u) + ((td.i[2].x >> 24) & 15u) +
+                         ((td.i[3].x >> 24) & 15u);
+                plies += 4;
+            } else {
+                play(A0, T0, true, 0u);
+                play(A1, T1, false, 1u);
+                play(A2, T2, false, 2u);
+                play(A3, T3, false, 3u);
+            }
             const uint32_t bp = best_pos;
             const uint32_t winner = (trick_start + bp) & 3u;
             complete(winner);

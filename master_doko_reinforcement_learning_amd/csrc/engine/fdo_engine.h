@@ -604,6 +604,45 @@ DK_HD int round_draws(const Work& w) {
     return d;
 }
 
+// ---- speculative trick draw (DK_TRICK_SPEC) ------------------------------------------
+// The four plies of a trick whose hands (relative to the leader) are a0..a3, as one
+// straight-line block: the four draws are taken up front, skipping range_u32's rejection
+// branch, the led class comes from the first card by arithmetic, so the three followers'
+// legal sets, ranks and table lookups are independent of each other and issue together.
+// Returns false -- generator untouched -- when any lane of the wave drew into a rejection
+// zone (probability < 12 / 2^32 per ply); the caller then plays the trick by the exact
+// per-ply path.  On true, rng has advanced by the trick's four draws, exactly as the per-ply
+// path would have.
+struct TrickDraw { uint32_t c[4]; CardInfo i[4]; uint32_t ld; };
+DK_HD bool draw_trick(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, Rng& rng, uint32_t gt, uint32_t tm,
+                      TrickDraw& t) {
+    Rng q = rng;
+    const uint32_t x0 = q.next_u32(), x1 = q.next_u32(), x2 = q.next_u32(), x3 = q.next_u32();
+    const uint32_t n0 = (uint32_t)popc32(a0);
+    const uint64_t m0 = (uint64_t)x0 * (uint64_t)n0;
+    const uint32_t c0 = nth_set_bit24(a0, n0 - 1u - (uint32_t)(m0 >> 32));
+    const uint32_t ld = class_mask(c0, tm);
+    const uint32_t f1 = a1 & ld, f2 = a2 & ld, f3 = a3 & ld;
+    const uint32_t l1 = f1 ? f1 : a1, l2 = f2 ? f2 : a2, l3 = f3 ? f3 : a3;
+    const uint32_t n1 = (uint32_t)popc32(l1), n2 = (uint32_t)popc32(l2), n3 = (uint32_t)popc32(l3);
+    const uint64_t m1 = (uint64_t)x1 * (uint64_t)n1, m2 = (uint64_t)x2 * (uint64_t)n2, m3 = (uint64_t)x3 * (uint64_t)n3;
+    const bool rej = (uint32_t)m0 > 0u - n0 || (uint32_t)m1 > 0u - n1 || (uint32_t)m2 > 0u - n2 || (uint32_t)m3 > 0u - n3;
+#ifdef DK_TRICK_REPLAY_ALL
+    if (wave_any(rej || true)) return false;   // (test builds: every trick takes the exact path)
+#else
+    if (wave_any(rej)) return false;
+#endif
+    t.c[0] = c0;
+    t.c[1] = nth_set_bit24(l1, n1 - 1u - (uint32_t)(m1 >> 32));
+    t.c[2] = nth_set_bit24(l2, n2 - 1u - (uint32_t)(m2 >> 32));
+    t.c[3] = nth_set_bit24(l3, n3 - 1u - (uint32_t)(m3 >> 32));
+#pragma unroll
+    for (int k = 0; k < 4; ++k) t.i[k] = card_info(gt, t.c[k]);
+    t.ld = ld;
+    rng = q;
+    return true;
+}
+
 // Card phase to the end (w.phase == PH_PLAYCARD).  Returns plies played.
 // The trick is evaluated incrementally as its cards are played (running best key = first
 // strict maximum, eyes, Diamond-Ace players).  Hands are kept relative to the leader: after
@@ -618,7 +657,7 @@ DK_HD int round_draws(const Work& w) {
 #define DK_ROLLOUT_FAST 1   // tricks without announcement offers skip the per-card offer tests
 #endif
 #ifndef DK_TRICK_SPEC
-#define DK_TRICK_SPEC 2     // fast tricks drawn speculatively as one block, replayed on a rejection
+#define DK_TRICK_SPEC 1     // fast tricks drawn speculatively as one block, replayed on a rejection
 #endif
 #ifndef DK_FOX_SKIP
 #define DK_FOX_SKIP 0       // (measurement switch) fast tricks skip the fox tracking once no lane holds a Diamond Ace
@@ -681,21 +720,10 @@ DK_HD int rollout_cards(const Work& w0, Rng& rng, int pts[4]) {
     // one card of player p, whose hand is (a, t2), at position `pos` of the trick; updates the
     // hand and the running trick.  `track` keeps the hand sizes (nb) per card, which only the
     // announcement offers read (draws).
-    // `rej` (speculative tricks): the draw skips range_u32's rejection test and records instead
-    // whether this lane's draw fell into the rejection zone (then the trick is replayed exactly).
-    auto play = [&](uint32_t& a, uint32_t& t2, uint32_t p, bool first, uint32_t pos, bool track, bool fox = true,
-                    uint32_t* rej = nullptr) {
+    auto play = [&](uint32_t& a, uint32_t& t2, uint32_t p, bool first, uint32_t pos, bool track, bool fox = true) {
         const uint32_t f = a & lead;
         const uint32_t legal = f ? f : a;
-        uint32_t r;
-        if (rej) {
-            const uint32_t n = (uint32_t)popc32(legal);
-            const uint64_t m = (uint64_t)rng.next_u32() * (uint64_t)n;
-            r = (uint32_t)(m >> 32);
-            *rej |= (uint32_t)m > 0u - n ? 1u : 0u;
-        } else {
-            r = rng.range_u32((uint32_t)popc32(legal));
-        }
+        const uint32_t r = rng.range_u32((uint32_t)popc32(legal));
         const uint32_t card = nth_set_bit24(legal, (uint32_t)popc32(legal) - 1u - r), bit = 1u << card;
 #if DK_ROLLOUT_FAST
         // the second copy goes first: t2 loses the bit if it holds it, a otherwise (no selects)
@@ -801,38 +829,13 @@ DK_HD int rollout_cards(const Work& w0, Rng& rng, int pts[4]) {
                     play(A3, T3, (s + 3u) & 3u, false, 3u, false, false);
                 } else
 #endif
-#if DK_TRICK_SPEC >= 2
+#if DK_TRICK_SPEC
                 {
-                    // The four plies in dependency order, as one straight-line block.  The draws
-                    // are taken up front, skipping range_u32's rejection branch (a lane's draw falls
-                    // into its zone with probability < 12 / 2^32 per ply; a wave with any such lane
-                    // replays the trick exactly from the saved generator).  The led class comes from
-                    // the first card by arithmetic, so the three followers' legal sets, ranks and
-                    // table lookups are independent of each other and issue together.
-                    Rng q = rng;
-                    const uint32_t x0 = q.next_u32(), x1 = q.next_u32(), x2 = q.next_u32(), x3 = q.next_u32();
-                    const uint32_t n0 = (uint32_t)popc32(A0);
-                    const uint64_t m0 = (uint64_t)x0 * (uint64_t)n0;
-                    const uint32_t c0 = nth_set_bit24(A0, n0 - 1u - (uint32_t)(m0 >> 32));
-                    const uint32_t ld = class_mask(c0, tm);
-                    const uint32_t f1 = A1 & ld, f2 = A2 & ld, f3 = A3 & ld;
-                    const uint32_t l1 = f1 ? f1 : A1, l2 = f2 ? f2 : A2, l3 = f3 ? f3 : A3;
-                    const uint32_t n1 = (uint32_t)popc32(l1), n2 = (uint32_t)popc32(l2), n3 = (uint32_t)popc32(l3);
-                    const uint64_t m1 = (uint64_t)x1 * (uint64_t)n1, m2 = (uint64_t)x2 * (uint64_t)n2,
-                                   m3 = (uint64_t)x3 * (uint64_t)n3;
-                    const bool rej = (uint32_t)m0 > 0u - n0 || (uint32_t)m1 > 0u - n1 || (uint32_t)m2 > 0u - n2 ||
-                                     (uint32_t)m3 > 0u - n3;
-#ifdef DK_TRICK_REPLAY_ALL
-                    if (!wave_any(rej || true)) {   // (test builds: every trick takes the exact replay)
-#else
-                    if (!wave_any(rej)) {
-#endif
-                        const uint32_t c1 = nth_set_bit24(l1, n1 - 1u - (uint32_t)(m1 >> 32));
-                        const uint32_t c2 = nth_set_bit24(l2, n2 - 1u - (uint32_t)(m2 >> 32));
-                        const uint32_t c3 = nth_set_bit24(l3, n3 - 1u - (uint32_t)(m3 >> 32));
-                        const CardInfo i0 = card_info(gt, c0), i1 = card_info(gt, c1), i2 = card_info(gt, c2),
-                                       i3 = card_info(gt, c3);
-                        rng = q;
+                    // the four plies as one block (draw_trick); the exact per-ply path on a rejection
+                    TrickDraw td;
+                    if (draw_trick(A0, A1, A2, A3, rng, gt, tm, td)) {
+                        const uint32_t c0 = td.c[0], c1 = td.c[1], c2 = td.c[2], c3 = td.c[3], ld = td.ld;
+                        const CardInfo i0 = td.i[0], i1 = td.i[1], i2 = td.i[2], i3 = td.i[3];
                         const uint32_t b0 = 1u << c0, b1 = 1u << c1, b2 = 1u << c2, b3 = 1u << c3;
                         const uint32_t d0 = T0 & b0, d1 = T1 & b1, d2 = T2 & b2, d3 = T3 & b3;
                         T0 ^= d0; A0 ^= b0 ^ d0; T1 ^= d1; A1 ^= b1 ^ d1;
@@ -852,29 +855,6 @@ DK_HD int rollout_cards(const Work& w0, Rng& rng, int pts[4]) {
                                   (c3 == (uint32_t)DIAMOND_ACE ? 1u << ((s + 3u) & 3u) : 0u);
                         plies += 4;
                     } else {
-                        play(A0, T0, s, true, 0u, false);
-                        play(A1, T1, (s + 1u) & 3u, false, 1u, false);
-                        play(A2, T2, (s + 2u) & 3u, false, 2u, false);
-                        play(A3, T3, (s + 3u) & 3u, false, 3u, false);
-                    }
-                }
-#elif DK_TRICK_SPEC
-                {
-                    // The four plies as one straight-line block: the draws skip range_u32's
-                    // rejection branch (a lane falls into its zone with probability < 12 / 2^32
-                    // per ply), so plies 2-4, which depend on ply 1 only through the led class,
-                    // overlap their table lookups.  A wave with any rejecting lane replays the
-                    // trick exactly from the saved hands and generator.
-                    const Rng rs = rng;
-                    const uint32_t a0 = A0, a1 = A1, a2 = A2, a3 = A3, t0 = T0, t1 = T1, t2 = T2, t3 = T3;
-                    uint32_t rej = 0;
-                    play(A0, T0, s, true, 0u, false, true, &rej);
-                    play(A1, T1, (s + 1u) & 3u, false, 1u, false, true, &rej);
-                    play(A2, T2, (s + 2u) & 3u, false, 2u, false, true, &rej);
-                    play(A3, T3, (s + 3u) & 3u, false, 3u, false, true, &rej);
-                    if (wave_any(rej != 0u)) {
-                        rng = rs; A0 = a0; A1 = a1; A2 = a2; A3 = a3; T0 = t0; T1 = t1; T2 = t2; T3 = t3;
-                        plies -= 4;
                         play(A0, T0, s, true, 0u, false);
                         play(A1, T1, (s + 1u) & 3u, false, 1u, false);
                         play(A2, T2, (s + 2u) & 3u, false, 2u, false);

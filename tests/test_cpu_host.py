@@ -49,6 +49,11 @@ def test_do_engine_vs_oracle(native_bins):
     assert _run("do_engine_check", 200, 7) > 30000
 
 
+def test_do_engine_vs_oracle_trick_replay(native_bins):
+    """do_engine.h with every speculative trick replayed through the exact per-ply draws."""
+    assert _run("do_engine_check_replay", 200, 7) > 30000
+
+
 def test_engine_search_vs_oracle(native_bins):
     """search_core.h (host build) = oracle UCT: visits, f64 values bitwise, best, RNG stream."""
     assert _run("search_check", 6, 400, 5) > 10

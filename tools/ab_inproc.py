@@ -7,6 +7,7 @@ A B B A ... over the same determinized roots.  Prints the per-launch HIP-event t
 mean / median ratio.  Both builds must produce identical visits (checked).
 
 usage: python tools/ab_inproc.py A.so B.so [infostates] [reps]
+       python tools/ab_inproc.py A.so B.so c2 [reps]     (C2: 32,768 rs-doko roots after 4x Healthy, as bench.py)
 """
 import ctypes
 import os
@@ -38,7 +39,8 @@ def main(a, b, infostates=12288, reps=6):
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     sp = stream.cuda_stream
-    I, S, iters = infostates, 64, 1000
+    c2 = infostates == "c2"
+    I, S, iters = (512 if c2 else int(infostates)), 64, 1000
     n = I * S
     ctxs = []
     for L in libs:
@@ -61,7 +63,19 @@ def main(a, b, infostates=12288, reps=6):
     d_samp = torch.tensor((np.uint64(0xC3200000) + j * np.uint64(S) + s).reshape(-1).view(np.int64), device=dev)
     d_srch = torch.tensor((np.uint64(0xC3300000) + j * np.uint64(S) + s).reshape(-1).view(np.int64), device=dev)
     roots = torch.zeros((n, 128), dtype=torch.uint8, device=dev)
-    assert L0.dk_determinize_batch_async(c0, info.data_ptr(), I, S, d_samp.data_ptr(), roots.data_ptr(), sp) == 0
+    game = dk.GAME_FULL_DOKO
+    if c2:
+        # bench.py's C2 roots and search seeds (rs-doko deals SmallRng::seed_from_u64(0xD0C00000 + i), 4x Healthy)
+        game = dk.GAME_DOKO
+        gidx = np.arange(n, dtype=np.uint64)
+        d_rs = torch.tensor((gidx + np.uint64(0xD0C00000)).view(np.int64), device=dev)
+        assert L0.dk_new_game_batch_async(c0, dk.GAME_DOKO, d_rs.data_ptr(), n, roots.data_ptr(), sp) == 0
+        h = torch.full((n,), 1 << 24, dtype=torch.int64, device=dev)
+        for _ in range(4):
+            assert L0.dk_env_step_batch_async(c0, roots.data_ptr(), h.data_ptr(), n, sp) == 0
+        d_srch = torch.tensor((gidx * np.uint64(0x9E3779B97F4A7C15) + np.uint64(1)).view(np.int64), device=dev)
+    else:
+        assert L0.dk_determinize_batch_async(c0, info.data_ptr(), I, S, d_samp.data_ptr(), roots.data_ptr(), sp) == 0
     outs = []
     for _ in libs:
         outs.append((torch.zeros((n, 39), dtype=torch.int32, device=dev), torch.zeros((n, 39), dtype=torch.float64, device=dev),
@@ -71,7 +85,7 @@ def main(a, b, infostates=12288, reps=6):
     for r in range(reps + 1):
         for k in order:
             v, q, bst = outs[k]
-            assert libs[k].dk_search_batch_async(ctxs[k], 0, roots.data_ptr(), d_srch.data_ptr(), n, iters, 2.5,
+            assert libs[k].dk_search_batch_async(ctxs[k], game, roots.data_ptr(), d_srch.data_ptr(), n, iters, 2.5,
                                                  v.data_ptr(), q.data_ptr(), bst.data_ptr(), sp) == 0
             assert libs[k].dk_sync(ctxs[k], sp) == 0
             ms = ctypes.c_float()
@@ -90,4 +104,4 @@ def main(a, b, infostates=12288, reps=6):
 
 if __name__ == "__main__":
     args = sys.argv[1:]
-    main(args[0], args[1], *(int(x) for x in args[2:]))
+    main(args[0], args[1], *((x if x == "c2" else int(x)) for x in args[2:]))
