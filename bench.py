@@ -67,6 +67,10 @@ def parse():
                         "root that outgrows them is searched again in the fallback pool, results unchanged)")
     p.add_argument("--games", type=int, default=8192, help="concurrent self-play games per GPU (c5)")
     p.add_argument("--az-iterations", type=int, default=200, help="PUCT iterations per move (c5)")
+    p.add_argument("--c5-streams", type=int, default=8,
+                   help="c5: split the games into this many independent searches (one engine and HIP stream each) "
+                        "whose iterations are issued interleaved, so one part's kernels fill the others' tails "
+                        "(8: +4 %% against 1 and 16, profiles/r06/c5_streams/)")
     p.add_argument("--ar-samples", type=int, default=4, help="AR samples per infostate (impi)")
     p.add_argument("--net-precision", choices=["bf16", "f32"], default="f32",
                    help="c5 / impi / impid network: f32 (default) = the reference's precision (f32 activations at "
@@ -652,9 +656,64 @@ def run_c5(args, dk, L, dev, stream, rank, world, local_rank, dist):
     rng_states = torch.from_numpy(dk.splitmix_rng_states(np.asarray(seeds, dtype=np.uint64) ^ np.uint64(0xA2))
                                   .view(np.int64).copy()).to(dev)
 
+    from master_doko_reinforcement_learning_amd.api import AZ_STATE_BYTES
+    H = max(1, args.c5_streams)
+    if G % H:
+        raise SystemExit("--games must be divisible by --c5-streams")
+    parts = None
+    if H > 1:
+        # H independent searches over G/H games each: own engine (search state), own stream, own
+        # evaluator (token buffer); the network weights are shared.  Games are independent and the
+        # network is row-wise, so every game's search is the one-batch search (checked by the tests).
+        parts = [(dk.Engine(device=local_rank, max_roots=64, max_iterations=max(1, iters)), torch.cuda.Stream(dev))
+                 for _ in range(H)]
+        part_evals = [TimedEval(e, net, dtype=ndt) for e, _ in parts]
+
+    def search_parts(srch):
+        """api.AlphaZeroSearch._search for the H parts, their launches interleaved per iteration."""
+        Gh = G // H
+        main = torch.cuda.current_stream(dev)
+        st = []
+        for h, (e, s) in enumerate(parts):
+            s.wait_stream(main)
+            sl = slice(h * Gh, (h + 1) * Gh)
+            with torch.cuda.stream(s):
+                seeds_t = torch.tensor(np.ascontiguousarray(srch[sl]).view(np.int64), device=dev)
+                ev = torch.empty((Gh, AZ_STATE_BYTES), dtype=torch.uint8, device=dev)
+                need = torch.empty(Gh, dtype=torch.uint8, device=dev)
+                rs = rng_states[sl]
+                ck(L.dk_az_begin_async(e.ctx, records[sl].data_ptr(), seeds_t.data_ptr(), Gh, iters, search.epoch,
+                                       ev.data_ptr(), s.cuda_stream))
+                ck(L.dk_az_rng_async(e.ctx, rs.data_ptr(), 1, s.cuda_stream))
+                v, lg = part_evals[h](ev)
+                v, lg = v.float().contiguous(), lg.float().contiguous()
+                ck(L.dk_az_root_async(e.ctx, v.data_ptr(), lg.data_ptr(), None, search.alpha, search.eps, s.cuda_stream))
+            st.append((e, s, ev, need, rs, seeds_t))
+        for _ in range(iters):
+            for h, (e, s, ev, need, rs, _) in enumerate(st):
+                with torch.cuda.stream(s):
+                    ck(L.dk_az_select_async(e.ctx, search.c, ev.data_ptr(), need.data_ptr(), s.cuda_stream))
+                    v, lg = part_evals[h](ev)
+                    v, lg = v.float().contiguous(), lg.float().contiguous()
+                    ck(L.dk_az_backup_async(e.ctx, v.data_ptr(), lg.data_ptr(), s.cuda_stream))
+        actions = torch.empty(G, dtype=torch.uint8, device=dev)
+        visits = torch.empty((G, dk.NUM_ACTIONS), dtype=torch.int32, device=dev)
+        for h, (e, s, ev, need, rs, _) in enumerate(st):
+            with torch.cuda.stream(s):
+                ck(L.dk_az_finish_async(e.ctx, 2, float(search.temperature), visits[h * Gh:(h + 1) * Gh].data_ptr(),
+                                        actions[h * Gh:(h + 1) * Gh].data_ptr(), s.cuda_stream))
+                ck(L.dk_az_rng_async(e.ctx, rs.data_ptr(), 0, s.cuda_stream))
+            main.wait_stream(s)
+        for e, s, *_ in st:
+            ck(L.dk_sync(e.ctx, s.cuda_stream))
+        return actions
+
     def step():
         srch = np.arange(G, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15) + np.uint64(next_seed[0])
-        actions, _ = search.mcts_search(records, evaluator, None, iters, srch, rng_states=rng_states)
+        if parts is None:
+            actions, _ = search.mcts_search(records, evaluator, None, iters, srch, rng_states=rng_states)
+        else:
+            actions = search_parts(srch)
         dk.az_step(eng, records, actions)
         fin = (records[:, 99] == 3).nonzero().flatten()      # phase byte: Finished -> a fresh deal
         moves[0] += int((actions != 255).sum().item())
@@ -687,6 +746,12 @@ def run_c5(args, dk, L, dev, stream, rank, world, local_rank, dist):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     net_ms = sum(e0.elapsed_time(e1) for e0, e1 in ev_time[1:])
+    if parts is not None:
+        # the parts' network calls overlap each other: their event times do not add up to the
+        # network's share of the step, so the whole step is charged to the network (an upper bound)
+        net_ms = elapsed * 1e3
+        for e, _ in parts:
+            e.close()
     if args.dump_records:
         np.save("%s_r%d.npy" % (args.dump_records, rep), records.cpu().numpy())
     evals = G * (iters + 1) * args.steps
@@ -714,7 +779,8 @@ def run_c5(args, dk, L, dev, stream, rank, world, local_rank, dist):
                        "c_puct": 4.0, "dirichlet": [0.8, 0.3], "temperature": 0.5,
                        "moves_per_step": G, "games_finished": moves[1], "parallelism": "replicas x%d" % world},
             "network_ms_per_step": net_ms / args.steps,
-            "search_ms_per_step": elapsed / args.steps * 1e3 - net_ms / args.steps,
+            "search_ms_per_step": elapsed / args.steps * 1e3 - net_ms / args.steps if parts is None else None,
+            "c5_streams": H,
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": npeak, "unit": "TFLOP/s",
                          "frac": achieved / npeak, "traffic": None,
                          "note": "network GEMMs/attention: %.1f MFLOP per leaf evaluation (algorithmic), %s; achieved "

@@ -121,7 +121,7 @@ def test_bench_many_ranks(tmp_path, partition, ranks):
     assert np.array_equal(accN, acc1) and np.array_equal(aN, a1)
 
 
-def _bench_c5(tmp_path, gpus, tag, offset=0):
+def _bench_c5(tmp_path, gpus, tag, offset=0, extra=()):
     env = dict(os.environ)
     env["DK_DIST_BACKEND"] = "gloo"
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
@@ -129,7 +129,7 @@ def _bench_c5(tmp_path, gpus, tag, offset=0):
     rec = str(tmp_path / ("rec_%s" % tag))
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--workload", "c5", "--gpus", str(gpus), "--steps", "2",
            "--warmup", "1", "--no-cpu-baseline", "--games", "96", "--az-iterations", "24",
-           "--replica-offset", str(offset), "--dump-records", rec]
+           "--replica-offset", str(offset), "--dump-records", rec] + list(extra)
     out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=150 + 30 * gpus)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
     line = [l for l in out.stdout.splitlines() if l.startswith("{")][-1]
@@ -149,3 +149,14 @@ def test_bench_c5_replicas_two_ranks(tmp_path):
         a, b = np.load("%s_r%d.npy" % (rec2, rep)), np.load("%s_r%d.npy" % (rec1, rep))
         assert a.shape == b.shape and np.array_equal(a, b), rep
     assert not np.array_equal(np.load("%s_r0.npy" % rec2), np.load("%s_r1.npy" % rec2))   # distinct replicas
+
+
+def test_bench_c5_streams_equal_one_batch(tmp_path):
+    """--c5-streams 8 (the default): the games split into eight searches on their own engines and
+    streams, their iterations interleaved; every game's record after three moves equals the
+    one-batch run (--c5-streams 1)."""
+    r1, rec1 = _bench_c5(tmp_path, 1, "s1", extra=("--c5-streams", "1"))
+    r2, rec2 = _bench_c5(tmp_path, 1, "s2", extra=("--c5-streams", "8"))
+    assert r2["c5_streams"] == 8 and r1["c5_streams"] == 1
+    a, b = np.load("%s_r0.npy" % rec1), np.load("%s_r0.npy" % rec2)
+    assert a.shape == b.shape and np.array_equal(a, b)
