@@ -67,6 +67,9 @@ def parse():
                         "root that outgrows them is searched again in the fallback pool, results unchanged)")
     p.add_argument("--games", type=int, default=8192, help="concurrent self-play games per GPU (c5)")
     p.add_argument("--az-iterations", type=int, default=200, help="PUCT iterations per move (c5)")
+    p.add_argument("--impi-streams", type=int, default=8,
+                   help="impi: split the infostates into this many independent AR samplings (one engine and HIP "
+                        "stream each) whose network rounds are issued interleaved (api.sample_interleaved)")
     p.add_argument("--c5-streams", type=int, default=8,
                    help="c5: split the games into this many independent searches (one engine and HIP stream each) "
                         "whose iterations are issued interleaved, so one part's kernels fill the others' tails "
@@ -1167,6 +1170,17 @@ def run_impi(args, dk, L, dev, stream, rank, world, local_rank, dist):
 
     ar = dk.ARSampling(eng, network, args.ar_temperature)
     seeds = np.arange(I * S, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15) + np.uint64(0xA5000000 + rank)
+    P = max(1, args.impi_streams) if not decide else 1
+    if I % P:
+        raise SystemExit("--infostates must be divisible by --impi-streams")
+    parts = None
+    if P > 1:
+        # P independent samplings over I/P infostates each (own engine: the AR state; own stream);
+        # every lane's sample equals the one-batch sampling (tests/test_gpu_impi.py)
+        Ip = I // P
+        parts = [(dk.ARSampling(dk.Engine(device=local_rank, max_roots=64, max_iterations=1), network, args.ar_temperature),
+                  torch.cuda.Stream(dev), records[k * Ip:(k + 1) * Ip], S, seeds[k * Ip * S:(k + 1) * Ip * S])
+                 for k in range(P)]
     policy = dk.ArImpiPolicy(eng, network, args.c, args.iterations, S, dk.FUSE_MAXN, args.ar_temperature) if decide else None
     pol_seeds = np.arange(2 * I * S + I, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15) + np.uint64(0xA6000000 + rank)
     stats = {"rows": 0, "consistent": 0, "lanes": 0}
@@ -1177,10 +1191,14 @@ def run_impi(args, dk, L, dev, stream, rank, world, local_rank, dist):
                 _, succ, _ = policy.execute(records, pol_seeds)
                 stats["rows"] += policy.sampler.rows
                 stats["consistent"] += int(succ.sum().item())
-            else:
+            elif parts is None:
                 _, status, _ = ar.sample(records, S, seeds)
                 stats["rows"] += ar.rows
                 stats["consistent"] += int((status == 0).sum().item())
+            else:
+                outs = dk.sample_interleaved(parts)
+                stats["rows"] += sum(p[0].rows for p in parts)
+                stats["consistent"] += sum(int((o[1] == 0).sum().item()) for o in outs)
         stats["lanes"] += I * S
 
     for _ in range(args.warmup):
@@ -1203,6 +1221,11 @@ def run_impi(args, dk, L, dev, stream, rank, world, local_rank, dist):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     net_ms = sum(e0.elapsed_time(e1) for e0, e1 in ev)
+    if parts is not None:
+        # the parts' network calls overlap: the whole step is charged to the network (an upper bound)
+        net_ms = elapsed * 1e3
+        for p in parts:
+            p[0].engine.close()
     flop = impi_flop_per_eval()
     result = None
     if rank == 0:
@@ -1226,7 +1249,10 @@ def run_impi(args, dk, L, dev, stream, rank, world, local_rank, dist):
                     "random-initialised DokoImpiNet (d 256, 4 blocks, 4 heads)",
             "config": {"workload": ("IMPI AR decision: %d infostates x %d AR samples x %d sims per GPU" % (I, S, args.iterations))
                                    if decide else "IMPI AR determinization: %d infostates x %d samples per GPU" % (I, S),
-                       "temperature": args.ar_temperature, "network_rounds": ar.rounds if not decide else policy.sampler.rounds,
+                       "temperature": args.ar_temperature,
+                       "network_rounds": (policy.sampler.rounds if decide else
+                                          ar.rounds if parts is None else max(p[0].rounds for p in parts)),
+                       "impi_streams": P,
                        "network_rows_per_step": stats["rows"] // args.steps,
                        "consistent_fraction": stats["consistent"] / max(1, stats["lanes"]),
                        "parallelism": "replicas x%d" % world},

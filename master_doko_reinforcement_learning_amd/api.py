@@ -673,6 +673,16 @@ class ARSampling:
         return _run_on_stream(infostates.device, self._sample, infostates, samples, seeds)
 
     def _sample(self, infostates, samples, seeds, st):
+        rounds = self._sample_rounds(infostates, samples, seeds, st)
+        while True:
+            try:
+                next(rounds)
+            except StopIteration as done:
+                return done.value
+
+    def _sample_rounds(self, infostates, samples, seeds, st, sync=True):
+        """_sample as a generator that yields after each network round's launches (sample_interleaved,
+        which synchronises the parts itself: sync=False)."""
         import torch
         L = _native.lib()
         ctx = self.engine.ctx
@@ -705,6 +715,7 @@ class ARSampling:
             logits = self.network(tokens[:rows]).float().contiguous()
             _check(L.dk_ar_choose_async(ctx, logits.data_ptr(), self.temperature, st))
             self.rows += rows
+            yield r
         _check(L.dk_ar_prepare_async(ctx, tokens.data_ptr(), st))
         out_s = torch.empty((n, STATE_BYTES), dtype=torch.uint8, device=dev)
         status_s = torch.empty(n, dtype=torch.uint8, device=dev)
@@ -714,8 +725,43 @@ class ARSampling:
         out = out_s.view(n_info, samples, STATE_BYTES)[inv].reshape(n, STATE_BYTES)
         status = status_s.view(n_info, samples)[inv].reshape(n)
         reason = reason_s.view(n_info, samples)[inv].reshape(n)
-        _check(L.dk_sync(ctx, st))
+        if sync:
+            _check(L.dk_sync(ctx, st))
         return out, status, reason
+
+
+def sample_interleaved(parts):
+    """Several independent ARSampling.sample calls whose network rounds are issued interleaved:
+    parts = [(sampler, stream, infostates, samples, seeds)], each sampler on its own Engine (the
+    AR state lives in the engine) and its own torch stream, so one part's kernels fill the tails
+    of the others'.  Every part's result equals its sampler.sample(...) alone (lanes are
+    independent and the networks row-wise).  The caller's stream waits for every part.
+    Returns [(states, status, reason)] in part order."""
+    import torch
+    if not parts:
+        return []
+    dev = parts[0][2].device
+    caller = torch.cuda.current_stream(dev)
+    gens, outs = [], [None] * len(parts)
+    for sampler, stream, info, samples, seeds in parts:
+        stream.wait_stream(caller)
+        with torch.cuda.stream(stream):
+            gens.append(sampler._sample_rounds(info, samples, seeds, stream.cuda_stream, sync=False))
+    live = list(range(len(parts)))
+    while live:
+        for k in list(live):
+            with torch.cuda.stream(parts[k][1]):
+                try:
+                    next(gens[k])
+                except StopIteration as done:
+                    outs[k] = done.value
+                    live.remove(k)
+    for k, (sampler, stream, *_r) in enumerate(parts):
+        _check(_native.lib().dk_sync(sampler.engine.ctx, stream.cuda_stream))
+        caller.wait_stream(stream)
+        for t in outs[k]:
+            t.record_stream(caller)
+    return outs
 
 
 def _stream(t):

@@ -215,3 +215,38 @@ def test_ar_fallback_random_action(eng):
         else:
             bit = ol.random_single(int(allowed[j]) & ~ann, ol.rng_seed(int(seeds[j])))
             assert int(act[j]) == bit.bit_length() - 1
+
+
+def test_ar_sampling_interleaved_parts_equal_one_batch(eng):
+    """sample_interleaved (bench.py --impi-streams): the infostates split into four samplings, each
+    on its own Engine and stream, their network rounds issued interleaved, give every lane the
+    sample, status and reason of the one-batch ARSampling (f32 IMPI network, d 256)."""
+    import torch
+    import master_doko_reinforcement_learning_amd as dk
+    from master_doko_reinforcement_learning_amd.impi_network import DokoImpiNet
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(3)
+    net = DokoImpiNet().to(dev).eval()
+    n, S, P = 1024, 4, 4
+    seeds = np.arange(n, dtype=np.uint64) + 991
+    roots = eng.new_games(0, seeds)
+    env = dk.McEnv(eng)
+    for _ in range(4):
+        roots = env.by_action(roots, np.full(n, np.uint64(1) << np.uint64(24)))
+    rng_states = dk.splitmix_rng_states(seeds + np.uint64(9))
+    roots, _ = env.random_plies(roots, rng_states, np.array([0, 8, 20, 32] * (n // 4), dtype=np.uint32))
+    recs = dk.az_records(eng, torch.from_numpy(roots).to(dev))
+    lane_seeds = np.arange(n * S, dtype=np.uint64) * 5 + 3
+    network = lambda t: net(t)   # noqa: E731
+    with torch.inference_mode():
+        o1, s1, r1 = dk.ARSampling(eng, network, 0.4).sample(recs, S, lane_seeds)
+        m = n // P
+        engines = [dk.Engine(device=0, max_roots=64, max_iterations=1) for _ in range(P)]
+        parts = [(dk.ARSampling(engines[k], network, 0.4), torch.cuda.Stream(dev), recs[k * m:(k + 1) * m], S,
+                  lane_seeds[k * m * S:(k + 1) * m * S]) for k in range(P)]
+        outs = dk.sample_interleaved(parts)
+    assert torch.equal(torch.cat([o[0] for o in outs]), o1)
+    assert torch.equal(torch.cat([o[1] for o in outs]), s1)
+    assert torch.equal(torch.cat([o[2] for o in outs]), r1)
+    for e in engines:
+        e.close()
