@@ -202,9 +202,9 @@ class FusedTrunk:
     kernels (csrc/az_net_kernels.h) for the embedding sum + first LayerNorm, every
     residual add fused with the LayerNorm that follows it, (4 heads of 40 or 64) the whole
     attention half (qkv projection + attention core + folded projection + residual +
-    LayerNorm in one kernel), and (d = 160 or 256) the whole MLP half; the heads' GEMMs are
-    torch (hipBLASLt).  `x` is the residual stream, `h` the
-    current LayerNorm output."""
+    LayerNorm in one kernel), and (d = 160 or 256) the whole MLP half; the heads run
+    class_pool_ln_kernel and class_mlp_bf16_kernel (ClassHead).  Other shapes fall back to torch
+    GEMMs (hipBLASLt).  `x` is the residual stream, `h` the current LayerNorm output."""
 
     def __init__(self, tokens, emb, ln0):
         from . import _native
