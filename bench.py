@@ -1170,7 +1170,7 @@ def run_impi(args, dk, L, dev, stream, rank, world, local_rank, dist):
 
     ar = dk.ARSampling(eng, network, args.ar_temperature)
     seeds = np.arange(I * S, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15) + np.uint64(0xA5000000 + rank)
-    P = max(1, args.impi_streams) if not decide else 1
+    P = max(1, args.impi_streams) if not decide else 1   # (impid: the policy splits its sampling itself)
     if I % P:
         raise SystemExit("--infostates must be divisible by --impi-streams")
     parts = None
@@ -1181,7 +1181,8 @@ def run_impi(args, dk, L, dev, stream, rank, world, local_rank, dist):
         parts = [(dk.ARSampling(dk.Engine(device=local_rank, max_roots=64, max_iterations=1), network, args.ar_temperature),
                   torch.cuda.Stream(dev), records[k * Ip:(k + 1) * Ip], S, seeds[k * Ip * S:(k + 1) * Ip * S])
                  for k in range(P)]
-    policy = dk.ArImpiPolicy(eng, network, args.c, args.iterations, S, dk.FUSE_MAXN, args.ar_temperature) if decide else None
+    policy = dk.ArImpiPolicy(eng, network, args.c, args.iterations, S, dk.FUSE_MAXN, args.ar_temperature,
+                             sampler_streams=max(1, args.impi_streams)) if decide else None
     pol_seeds = np.arange(2 * I * S + I, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15) + np.uint64(0xA6000000 + rank)
     stats = {"rows": 0, "consistent": 0, "lanes": 0}
 

@@ -521,13 +521,17 @@ class ArImpiPolicy:
     from_os_rng, so only the seeding scheme differs, not the distribution)."""
 
     def __init__(self, engine, network, uct_exploration_constant=2.5, iterations=1000, num_samples=64,
-                 fusion=FUSE_MAXN, temperature=0.4):
+                 fusion=FUSE_MAXN, temperature=0.4, sampler_streams=1):
+        """sampler_streams > 1: the AR sampling runs as that many interleaved parts, each on its own
+        Engine and stream (sample_interleaved); results are those of one sampling."""
         self.engine = engine
         self.c = float(uct_exploration_constant)
         self.iterations = iterations
         self.num_samples = num_samples
         self.fusion = fusion
         self.sampler = ARSampling(engine, network, temperature)
+        self.sampler_streams = int(sampler_streams)
+        self._parts = None   # [(ARSampling on its own Engine, torch stream)], made on first use
 
     def execute(self, infostates, seeds):
         """infostates: uint8 [n, 160] dk_az_state records (GPU); seeds: uint64, n*S sampling seeds,
@@ -544,7 +548,21 @@ class ArImpiPolicy:
         if seeds.shape[0] != 2 * n * S + n:
             raise ValueError("need 2*n*num_samples + n seeds")
         dev = infostates.device
-        samples, status, _ = self.sampler.sample(infostates, S, seeds[:n * S])
+        if self.sampler_streams > 1 and n >= self.sampler_streams:
+            P = self.sampler_streams
+            if self._parts is None:
+                self._parts = [(ARSampling(Engine(device=dev.index or 0, max_roots=64, max_iterations=1), self.sampler.network,
+                                           self.sampler.temperature, self.sampler.log_chance), torch.cuda.Stream(dev))
+                               for _ in range(P)]
+            cut = [n * k // P for k in range(P + 1)]
+            outs = sample_interleaved([(smp, stm, infostates[cut[k]:cut[k + 1]], S, seeds[cut[k] * S:cut[k + 1] * S])
+                                       for k, (smp, stm) in enumerate(self._parts)])
+            samples = torch.cat([o[0] for o in outs])
+            status = torch.cat([o[1] for o in outs])
+            self.sampler.rounds = max(smp.rounds for smp, _ in self._parts)
+            self.sampler.rows = sum(smp.rows for smp, _ in self._parts)
+        else:
+            samples, status, _ = self.sampler.sample(infostates, S, seeds[:n * S])
         srch = torch.as_tensor(seeds[n * S:2 * n * S].view(np.int64), device=dev)
         fb = torch.as_tensor(seeds[2 * n * S:].view(np.int64), device=dev)
         visits = torch.empty((n * S, NUM_ACTIONS), dtype=torch.int32, device=dev)

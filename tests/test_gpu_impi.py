@@ -141,7 +141,8 @@ def test_impi_network_fused_matches_fp32_module():
 
 
 @pytest.mark.parametrize("fusion", ["maxn", "avg"])
-def test_ar_decide_end_to_end(eng, fusion):
+@pytest.mark.parametrize("streams", [1, 3])
+def test_ar_decide_end_to_end(eng, fusion, streams):
     """mcts_ar_maxn/avg_policy (all_policies.rs:78-127 -> DefaultImpiPolicy::execute,
     compare_impi.rs:212-371): AR samples (hash network) -> UCT on each -> fusion over the
     consistent samples, against the oracle pipeline (visits of every consistent sample,
@@ -158,7 +159,7 @@ def test_ar_decide_end_to_end(eng, fusion):
         return torch.from_numpy(ol.ipi_hash_eval_np(tokens.cpu().numpy())).to(dev)
 
     mode = dk.FUSE_MAXN if fusion == "maxn" else dk.FUSE_AVG
-    pol = dk.ArImpiPolicy(eng, network, 2.5, iters, S, mode, 0.4)
+    pol = dk.ArImpiPolicy(eng, network, 2.5, iters, S, mode, 0.4, sampler_streams=streams)
     actions, successes, visits = pol.execute(torch.from_numpy(_records(info)).to(dev), seeds)
     actions, successes, visits = actions.cpu().numpy(), successes.cpu().numpy(), visits.cpu().numpy()
     for j, s in enumerate(info):
