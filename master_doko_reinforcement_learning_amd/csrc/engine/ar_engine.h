@@ -93,11 +93,15 @@ DK_HD uint32_t init(const dk_az_state& r, uint64_t seed, Lane& L) {
     L.rem_a = ua; L.rem_b = ub;
     const int rc = real_res(s, cp);
     L.res[cp] = rc < 0 ? DK_NONE : (uint8_t)rc;
-    int pq[4]; uint32_t imp[4];
+    uint32_t pq, imp;   // one byte per player (cap::byte4)
     cap::history_facts(s, pq, imp);
     L.imp = 0; L.played_q = 0;
-    for (int p = 0; p < 4; ++p) { L.imp |= imp[p] << (5 * p); L.played_q |= (uint8_t)((pq[p] & 3) << (2 * p)); }
-    cap::visible_reservations(s, cp, L.vis);
+    for (int p = 0; p < 4; ++p) {
+        L.imp |= cap::byte4(imp, p) << (5 * p);
+        L.played_q |= (uint8_t)((cap::byte4(pq, p) & 3) << (2 * p));
+    }
+    const uint32_t vis = cap::visible_reservations(s, cp);
+    for (int p = 0; p < 4; ++p) L.vis[p] = (uint8_t)cap::byte4(vis, p);
     uint32_t n = 0;
     for (int i = 1; i <= 3; ++i) {
         const int p = (cp + i) & 3;
