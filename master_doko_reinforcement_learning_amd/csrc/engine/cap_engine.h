@@ -48,6 +48,16 @@ struct CM {
         }
     }
     DK_HD void rule1() {
+        // No available card with exactly one possible taker: nothing to assign (the loop below
+        // assigns only such cards, and nothing changes until it does), so skip the scan.
+        uint32_t k1 = 0, k2 = 0;   // card kinds possible for >= 1 / >= 2 of the hidden players
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const uint32_t kp = p != observing ? (uint32_t)(possible[p] | (possible[p] >> 24)) & 0xFFFFFFu : 0u;
+            k2 |= k1 & kp;
+            k1 |= kp;
+        }
+        if ((k1 & ~k2 & ((uint32_t)(available | (available >> 24)) & 0xFFFFFFu)) == 0u) return;
         uint64_t snap = available;
         while (snap) {
             const int c = occ_card(ctz64(snap));
