@@ -93,10 +93,11 @@ struct CM {
         return changed;
     }
     DK_HD void rule4(Rng& rng) {
-        uint64_t snap = available;
-        const int idx = choose_unsized(popc64(snap), rng);
-        for (int i = 0; i < idx; ++i) snap &= snap - 1;
-        const int c = occ_card(ctz64(snap));
+        const uint64_t snap = available;
+        const int cnt = popc64(snap);
+        const int idx = choose_unsized(cnt, rng);
+        // the idx-th available position from the lowest (select by rank, no per-lane loop)
+        const int c = occ_card(ctz64(select_msb_rank(snap, (uint32_t)(cnt - 1 - idx))));
         int taker = -1;
 #pragma unroll
         for (int p = 0; p < 4; ++p)

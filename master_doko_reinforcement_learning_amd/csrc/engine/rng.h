@@ -130,24 +130,22 @@ DK_HD void shuffle48(uint8_t* a, Rng& rng) {
 struct CoinFlipper {
     uint32_t chunk = 0, remaining = 0;
 
+    // coin_flipper.rs flip_c_heads: the refill (too few bits left and no tail among them) is the
+    // only loop; the outcome is then computed by selects, so a wave whose lanes take different
+    // outcomes does not run both branches (the CAP sampler calls this once per remaining card)
     DK_HD bool flip_c_heads(uint32_t c, Rng& rng) {
-        for (;;) {
-            const uint32_t zeros = (uint32_t)clz32(chunk);
-            if (zeros < c) {
-                const uint32_t sh = zeros + 1;
-                chunk = chunk << (sh & 31);
-                remaining = remaining > sh ? remaining - sh : 0;
-                return false;
-            }
-            if (remaining >= c) {
-                remaining -= c;
-                chunk = chunk << (c & 31);
-                return true;
-            }
+        uint32_t zeros = (uint32_t)clz32(chunk);
+        while (zeros >= c && remaining < c) {
             c -= remaining;
             chunk = rng.next_u32();
             remaining = 32;
+            zeros = (uint32_t)clz32(chunk);
         }
+        const bool tails = zeros < c;
+        const uint32_t sh = tails ? zeros + 1 : c;
+        chunk = chunk << (sh & 31);
+        remaining = tails ? (remaining > sh ? remaining - sh : 0) : remaining - c;
+        return !tails;
     }
     DK_HD bool random_ratio(uint64_t n, uint64_t d, Rng& rng) {
         while (n < d) {
