@@ -95,7 +95,11 @@ struct CM {
     DK_HD void rule4(Rng& rng) {
         const uint64_t snap = available;
         const int cnt = popc64(snap);
+#ifdef DK_CAP_SOL_NOCOIN
+        const int idx = (int)(rng.next_u32() % (uint32_t)cnt);   // (speed-of-light measurement build: no CoinFlipper)
+#else
         const int idx = choose_unsized(cnt, rng);
+#endif
         // the idx-th available position from the lowest (select by rank, no per-lane loop)
         const int c = occ_card(ctz64(select_msb_rank(snap, (uint32_t)(cnt - 1 - idx))));
         int taker = -1;
