@@ -175,12 +175,55 @@ struct CoinFlipper {
     }
 };
 
-// Reservoir choice over `count` items in iteration order (CoinFlipper path).
-DK_HD int choose_unsized(int count, Rng& rng) {
+// Reservoir choice over `count` items in iteration order (CoinFlipper path), item by item: the
+// reference's loop (the host check compares choose_unsized with it).
+DK_HD int choose_unsized_ref(int count, Rng& rng) {
     CoinFlipper cf;
     int result = -1;
     for (int i = 0; i < count; ++i)
         if (cf.random_ratio_one_over((uint64_t)(i + 1), rng)) result = i;
+    return result;
+}
+
+// The same choice with runs of "tails" consumed per chunk.  Item i (d = i + 1, c = floor(log2 d))
+// is a tail -- not chosen, no draw -- when the chunk's next 1 bit comes after fewer than c zeros;
+// it consumes those zeros and the 1.  So from the chunk alone: the item starts are offset 0 and the
+// offset after every 1 bit; the first start followed by c zeros (R & S) ends the run of tails, and
+// the 1 bits before it are the tails.  Items that are not plain tails inside the chunk (heads, a
+// refill) take the item-by-item step above.  Results and generator state equal choose_unsized_ref
+// (tests/native/coin_check.cpp).
+DK_HD int choose_unsized(int count, Rng& rng) {
+    if (count <= 0) return -1;
+    CoinFlipper cf;
+    int result = 0;   // item 0 (d = 1, c = 0): always chosen, no bits consumed
+    int i = 1;
+    while (i < count) {
+        const uint32_t d = (uint32_t)i + 1u;
+        const uint32_t c = 31u - (uint32_t)clz32(d);                 // 1 <= c <= 31 here
+        const int end = count < (int)((2u << c) - 1u) ? count : (int)((2u << c) - 1u);   // items sharing c
+        const uint32_t x = cf.chunk;
+        int take = 0;
+        if (x != 0u) {
+            uint32_t w = x, span = 1;                                  // OR over windows of c bits
+            while (span * 2u <= c) { w |= w << span; span *= 2u; }
+            if (span < c) w |= w << (c - span);
+            const uint32_t starts = (x >> 1) | 0x80000000u;
+            const uint32_t f = ~w & starts;
+            const int tails = f ? (clz32(f) == 0 ? 0 : popc32(x >> (32 - clz32(f)))) : popc32(x);
+            take = tails < end - i ? tails : end - i;
+        }
+        if (take > 0) {
+            // consume through the take-th 1 bit from the top
+            const uint32_t pos = (uint32_t)ctz64(select_msb_rank((uint64_t)x, (uint32_t)(take - 1)));
+            const uint32_t sh = 32u - pos;
+            cf.chunk = sh >= 32u ? 0u : x << sh;
+            cf.remaining -= sh;
+            i += take;
+        } else {
+            if (cf.random_ratio_one_over((uint64_t)d, rng)) result = i;
+            ++i;
+        }
+    }
     return result;
 }
 

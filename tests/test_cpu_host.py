@@ -37,6 +37,12 @@ def test_engine_rules_vs_oracle(native_bins):
     assert _run("fdo_engine_check", 300, 11) > 20000
 
 
+def test_coin_flipper_runs_equal_item_by_item(native_bins):
+    """rng.h choose_unsized (runs of tails per chunk, the CAP sampler's rule 4) == the item-by-item
+    CoinFlipper reservoir: chosen index and generator state, 1.5 M random cases."""
+    assert _run("coin_check", 1500000, 3) > 40000000
+
+
 def test_engine_rules_vs_oracle_trick_replay(native_bins):
     """The same checks with every speculative fast-path trick of rollout_cards replayed through
     the exact per-ply draws (DK_TRICK_REPLAY_ALL): the replay path a rejected draw takes."""
